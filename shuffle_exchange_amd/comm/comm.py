@@ -1,0 +1,428 @@
+"""Communication facade over torch.distributed (RCCL over xGMI on MI355X; gloo for CPU tests).
+
+Parity: reference deepspeed/comm/comm.py (ops :177-640, ``init_distributed`` :643-709, comms
+logger via ``timed_op`` :102-135) and deepspeed/comm/torch.py (``TorchBackend`` :96-421, the
+``DS_COMM_*_OFF`` debug toggles :16-88). Differences that matter on MI355X:
+
+* ``isend``/``irecv`` are truly asynchronous (the reference facade calls the blocking send/recv,
+  comm/comm.py:380-389 -- a known quirk).
+* a **group cache** keyed by the member-rank tuple: RCCL communicator creation costs ~100 ms,
+  so the Shuffle-exchange reshuffle (reference stage_1_and_2.py:698-711 destroys and recreates
+  every communicator) reuses groups it has seen before.
+* a **collective fingerprint**: every collective folds (op, group, numel, dtype) into a per-rank
+  running hash; ``verify_fingerprints()`` all-gathers the hashes and raises on divergence. This is
+  the race/ordering detector SURVEY §5.2 asks for (it catches e.g. ranks whose shuffle RNG
+  diverged, which deadlocks or silently mis-averages in the reference).
+* a comms logger reporting per-op latency, algbw and busbw (busbw uses the ring factors of each
+  collective, so it is directly comparable to the per-link xGMI bandwidth).
+"""
+import datetime
+import hashlib
+import os
+import time
+from collections import defaultdict
+
+import torch
+import torch.distributed as tdist
+
+from ..utils.logging import logger, log_dist
+
+ReduceOp = tdist.ReduceOp
+
+_COMM_OFF = {k: os.environ.get(f"SXE_COMM_{k}_OFF", os.environ.get(f"DS_COMM_{k}_OFF", "0")) == "1"
+             for k in ("ALL_GATHER", "REDUCE_SCATTER", "BROADCAST", "ALL_REDUCE", "REDUCE", "ALL_TO_ALL")}
+
+
+class _State:
+    initialized = False
+    backend = None
+    group_cache = {}
+    fingerprint = hashlib.sha1()
+    fp_count = 0
+    fingerprint_enabled = os.environ.get("SXE_COMM_FINGERPRINT", "0") == "1"
+    logger_enabled = False
+    logger_verbose = False
+    logger_prof_all = True
+    logger_prof_ops = []
+    comms = defaultdict(lambda: defaultdict(list))  # op -> msg_size -> [latency_ms...]
+
+
+# ------------------------------------------------------------------------------------------------
+# init / identity
+def init_distributed(dist_backend=None, auto_mpi_discovery=True, distributed_port=29500, verbose=True,
+                     timeout=None, init_method=None, dist_init_required=None, config=None, rank=-1,
+                     world_size=-1):
+    """Initialise the default process group from the torchrun/launcher env (RANK, WORLD_SIZE,
+    LOCAL_RANK, MASTER_ADDR, MASTER_PORT); falls back to OpenMPI env discovery; a single process
+    without env becomes a world of one (rendezvous on 127.0.0.1)."""
+    from ..accelerator import get_accelerator
+    if config is not None:
+        configure(config)
+    if tdist.is_initialized():
+        _State.initialized = True
+        _State.backend = tdist.get_backend()
+        return
+    if dist_init_required is False:
+        return
+    env = os.environ
+    if "RANK" not in env and auto_mpi_discovery and "OMPI_COMM_WORLD_RANK" in env:
+        env["RANK"] = env["OMPI_COMM_WORLD_RANK"]
+        env["WORLD_SIZE"] = env["OMPI_COMM_WORLD_SIZE"]
+        env["LOCAL_RANK"] = env.get("OMPI_COMM_WORLD_LOCAL_RANK", "0")
+    if rank >= 0:
+        env["RANK"] = str(rank)
+    if world_size > 0:
+        env["WORLD_SIZE"] = str(world_size)
+    env.setdefault("RANK", "0")
+    env.setdefault("WORLD_SIZE", "1")
+    env.setdefault("LOCAL_RANK", "0")
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    env.setdefault("MASTER_PORT", str(distributed_port))
+    backend = dist_backend or get_accelerator().communication_backend_name()
+    if timeout is None:
+        timeout = datetime.timedelta(minutes=int(env.get("SXE_TIMEOUT_MIN", env.get("DEEPSPEED_TIMEOUT", "30"))))
+    kw = {}
+    if backend == "nccl":
+        local_rank = int(env["LOCAL_RANK"])
+        torch.cuda.set_device(local_rank)
+        # binding the device lets RCCL split sub-communicators from the world comm (cheap new_group)
+        kw["device_id"] = torch.device("cuda", local_rank)
+    tdist.init_process_group(backend=backend, init_method=init_method, timeout=timeout,
+                             rank=int(env["RANK"]), world_size=int(env["WORLD_SIZE"]), **kw)
+    _State.initialized = True
+    _State.backend = backend
+    if verbose:
+        log_dist(f"initialized {backend} world_size={tdist.get_world_size()}", ranks=[0])
+
+
+def is_initialized():
+    return tdist.is_available() and tdist.is_initialized()
+
+
+def get_rank(group=None):
+    return tdist.get_rank(group) if is_initialized() else 0
+
+
+def get_world_size(group=None):
+    return tdist.get_world_size(group) if is_initialized() else 1
+
+
+def get_local_rank():
+    return int(os.environ.get("LOCAL_RANK", 0))
+
+
+def get_global_rank(group, group_rank):
+    return tdist.get_global_rank(group, group_rank) if group is not None else group_rank
+
+
+def get_backend(group=None):
+    return tdist.get_backend(group) if is_initialized() else None
+
+
+def get_world_group():
+    return tdist.group.WORLD
+
+
+def destroy_process_group(group=None):
+    if group is None:
+        _State.group_cache.clear()
+    else:
+        for k, v in list(_State.group_cache.items()):
+            if v is group:
+                del _State.group_cache[k]
+    tdist.destroy_process_group(group)
+
+
+def new_group(ranks, cache=True):
+    """Collective over the world (every rank must call with the same `ranks`, in the same order).
+    Cached per rank tuple so repeated topologies do not re-create RCCL communicators."""
+    key = tuple(sorted(int(r) for r in ranks))
+    if cache and key in _State.group_cache:
+        return _State.group_cache[key]
+    if not is_initialized():
+        return None
+    g = tdist.new_group(list(key))
+    if cache:
+        _State.group_cache[key] = g
+    return g
+
+
+def group_ranks(group):
+    if group is None or group is tdist.group.WORLD:
+        return list(range(get_world_size()))
+    return tdist.get_process_group_ranks(group)
+
+
+# ------------------------------------------------------------------------------------------------
+# logging / fingerprint
+def configure(config=None, enabled=None, prof_all=None, prof_ops=None, verbose=None):
+    if config is not None and getattr(config, "comms_logger", None) is not None:
+        cl = config.comms_logger
+        _State.logger_enabled = cl.enabled
+        _State.logger_prof_all = cl.prof_all
+        _State.logger_prof_ops = list(cl.prof_ops)
+        _State.logger_verbose = cl.verbose
+    if enabled is not None:
+        _State.logger_enabled = enabled
+    if prof_all is not None:
+        _State.logger_prof_all = prof_all
+    if prof_ops is not None:
+        _State.logger_prof_ops = list(prof_ops)
+    if verbose is not None:
+        _State.logger_verbose = verbose
+
+
+def enable_fingerprint(on=True):
+    _State.fingerprint_enabled = on
+
+
+def _fp(op, group, t):
+    if not _State.fingerprint_enabled:
+        return
+    ranks = tuple(group_ranks(group)) if is_initialized() else (0,)
+    numel = t.numel() if isinstance(t, torch.Tensor) else sum(x.numel() for x in t)
+    dtype = t.dtype if isinstance(t, torch.Tensor) else t[0].dtype
+    _State.fingerprint.update(f"{op}|{ranks}|{numel}|{dtype};".encode())
+    _State.fp_count += 1
+
+
+def fingerprint_digest():
+    return _State.fingerprint.hexdigest(), _State.fp_count
+
+
+def verify_fingerprints(group=None):
+    """All-gather every rank's collective fingerprint; raise if any rank issued a different
+    sequence of collectives (op/group/shape/dtype) since the last reset."""
+    if not is_initialized() or get_world_size(group) == 1:
+        return True
+    digest, count = fingerprint_digest()
+    objs = [None] * get_world_size(group)
+    tdist.all_gather_object(objs, (digest, count), group=group)
+    if len(set(objs)) != 1:
+        raise RuntimeError(f"sxe: collective fingerprint mismatch across ranks: {objs}")
+    return True
+
+
+def reset_fingerprint():
+    _State.fingerprint = hashlib.sha1()
+    _State.fp_count = 0
+
+
+def _bus_factor(op, n):
+    if n <= 1:
+        return 1.0
+    if op in ("all_reduce", "all_reduce_coalesced"):
+        return 2.0 * (n - 1) / n
+    if op in ("all_gather_into_tensor", "all_gather", "reduce_scatter_tensor", "reduce_scatter", "all_to_all_single"):
+        return (n - 1) / n
+    return 1.0
+
+
+def _timed(op, fn, tensor, group, async_op):
+    _fp(op, group, tensor)
+    if not _State.logger_enabled or async_op or (not _State.logger_prof_all and op not in _State.logger_prof_ops):
+        return fn()
+    from ..accelerator import get_accelerator
+    acc = get_accelerator()
+    acc.synchronize()
+    t0 = time.perf_counter()
+    r = fn()
+    acc.synchronize()
+    ms = (time.perf_counter() - t0) * 1000.0
+    size = (tensor.numel() * tensor.element_size()) if isinstance(tensor, torch.Tensor) else \
+        sum(x.numel() * x.element_size() for x in tensor)
+    if op in ("all_gather_into_tensor", "all_gather"):
+        size *= get_world_size(group)
+    _State.comms[op][size].append(ms)
+    if _State.logger_verbose:
+        n = get_world_size(group)
+        algbw = size / (ms / 1000.0) / 1e9 if ms > 0 else 0.0
+        log_dist(f"comm op: {op} | time (ms): {ms:.3f} | msg size: {size} | algbw (GB/s): {algbw:.2f} | "
+                 f"busbw (GB/s): {algbw * _bus_factor(op, n):.2f}", ranks=[0])
+    return r
+
+
+def log_summary(show_straggler=False):
+    """Print the per-op table: count, total/avg latency, algbw/busbw (reference
+    utils/comms_logging.py:67)."""
+    n = get_world_size()
+    lines = [f"{'op':<24}{'msg size':>14}{'count':>8}{'total ms':>12}{'avg ms':>10}{'algbw GB/s':>12}{'busbw GB/s':>12}"]
+    for op, d in sorted(_State.comms.items()):
+        for size, lat in sorted(d.items()):
+            avg = sum(lat) / len(lat)
+            algbw = size / (avg / 1000.0) / 1e9 if avg > 0 else 0.0
+            lines.append(f"{op:<24}{size:>14}{len(lat):>8}{sum(lat):>12.3f}{avg:>10.3f}{algbw:>12.2f}"
+                         f"{algbw * _bus_factor(op, n):>12.2f}")
+    log_dist("\n" + "\n".join(lines), ranks=[0])
+    return lines
+
+
+def get_comms_stats():
+    return {op: {s: list(v) for s, v in d.items()} for op, d in _State.comms.items()}
+
+
+def reset_comms_stats():
+    _State.comms.clear()
+
+
+# ------------------------------------------------------------------------------------------------
+# collectives
+def _skip(kind):
+    return _COMM_OFF.get(kind, False)
+
+
+def all_reduce(tensor, op=ReduceOp.SUM, group=None, async_op=False, prof=False, log_name="all_reduce"):
+    if _skip("ALL_REDUCE") or get_world_size(group) == 1:
+        return None
+    return _timed("all_reduce", lambda: tdist.all_reduce(tensor, op=op, group=group, async_op=async_op), tensor,
+                  group, async_op)
+
+
+def inference_all_reduce(tensor, op=ReduceOp.SUM, group=None):
+    return all_reduce(tensor, op, group)
+
+
+def all_reduce_coalesced(tensors, op=ReduceOp.SUM, group=None, async_op=False):
+    if _skip("ALL_REDUCE") or get_world_size(group) == 1:
+        return None
+    return _timed("all_reduce_coalesced",
+                  lambda: tdist.all_reduce_coalesced(tensors, op=op, group=group, async_op=async_op), tensors, group,
+                  async_op)
+
+
+def reduce(tensor, dst, op=ReduceOp.SUM, group=None, async_op=False):
+    if _skip("REDUCE") or get_world_size(group) == 1:
+        return None
+    return _timed("reduce", lambda: tdist.reduce(tensor, dst, op=op, group=group, async_op=async_op), tensor, group,
+                  async_op)
+
+
+def reduce_scatter_tensor(output, input, op=ReduceOp.SUM, group=None, async_op=False):
+    if _skip("REDUCE_SCATTER"):
+        return None
+    if get_world_size(group) == 1:
+        if output.data_ptr() != input.data_ptr():
+            output.copy_(input.view_as(output))
+        return None
+    if get_backend(group) == "gloo":
+        # gloo lacks reduce_scatter_tensor: all_reduce + slice (plumbing tests only)
+        def fn():
+            buf = input.clone()
+            tdist.all_reduce(buf, op=op, group=group)
+            r = get_rank(group)
+            output.copy_(buf.view(get_world_size(group), -1)[r].view_as(output))
+        return _timed("reduce_scatter_tensor", fn, input, group, False)
+    return _timed("reduce_scatter_tensor",
+                  lambda: tdist.reduce_scatter_tensor(output, input, op=op, group=group, async_op=async_op), input,
+                  group, async_op)
+
+
+reduce_scatter_fn = reduce_scatter_tensor
+
+
+def all_gather_into_tensor(output, input, group=None, async_op=False):
+    if _skip("ALL_GATHER"):
+        return None
+    if get_world_size(group) == 1:
+        if output.data_ptr() != input.data_ptr():
+            output.copy_(input.view_as(output))
+        return None
+    if get_backend(group) == "gloo":
+        def fn():
+            parts = list(output.view(get_world_size(group), -1).unbind(0))
+            tdist.all_gather(parts, input.reshape(-1), group=group)
+        return _timed("all_gather_into_tensor", fn, input, group, False)
+    return _timed("all_gather_into_tensor",
+                  lambda: tdist.all_gather_into_tensor(output, input, group=group, async_op=async_op), input, group,
+                  async_op)
+
+
+allgather_fn = all_gather_into_tensor
+
+
+def all_gather(tensor_list, tensor, group=None, async_op=False):
+    if _skip("ALL_GATHER"):
+        return None
+    return _timed("all_gather", lambda: tdist.all_gather(tensor_list, tensor, group=group, async_op=async_op), tensor,
+                  group, async_op)
+
+
+def all_gather_object(obj_list, obj, group=None):
+    return tdist.all_gather_object(obj_list, obj, group=group)
+
+
+def broadcast(tensor, src, group=None, async_op=False):
+    if _skip("BROADCAST") or get_world_size(group) == 1:
+        return None
+    return _timed("broadcast", lambda: tdist.broadcast(tensor, src, group=group, async_op=async_op), tensor, group,
+                  async_op)
+
+
+def broadcast_object_list(objs, src, group=None):
+    if get_world_size(group) == 1:
+        return
+    tdist.broadcast_object_list(objs, src, group=group)
+
+
+def all_to_all_single(output, input, output_split_sizes=None, input_split_sizes=None, group=None, async_op=False):
+    if _skip("ALL_TO_ALL"):
+        return None
+    if get_world_size(group) == 1:
+        output.copy_(input)
+        return None
+    return _timed("all_to_all_single",
+                  lambda: tdist.all_to_all_single(output, input, output_split_sizes, input_split_sizes, group=group,
+                                                  async_op=async_op), input, group, async_op)
+
+
+def all_to_all(output_tensor_list, input_tensor_list, group=None, async_op=False):
+    return tdist.all_to_all(output_tensor_list, input_tensor_list, group=group, async_op=async_op)
+
+
+def send(tensor, dst, group=None, tag=0):
+    _fp("send", None, tensor)
+    return tdist.send(tensor, dst, group=group, tag=tag)
+
+
+def recv(tensor, src=None, group=None, tag=0):
+    _fp("recv", None, tensor)
+    return tdist.recv(tensor, src, group=group, tag=tag)
+
+
+def isend(tensor, dst, group=None, tag=0):
+    _fp("isend", None, tensor)
+    return tdist.isend(tensor, dst, group=group, tag=tag)
+
+
+def irecv(tensor, src=None, group=None, tag=0):
+    _fp("irecv", None, tensor)
+    return tdist.irecv(tensor, src, group=group, tag=tag)
+
+
+def batch_isend_irecv(p2p_op_list):
+    return tdist.batch_isend_irecv(p2p_op_list)
+
+
+P2POp = tdist.P2POp
+
+
+def barrier(group=None, async_op=False, device_ids=None):
+    if not is_initialized():
+        return None
+    return tdist.barrier(group=group, async_op=async_op)
+
+
+def monitored_barrier(group=None, timeout=None, wait_all_ranks=False):
+    if not is_initialized():
+        return None
+    if get_backend(group) == "gloo":
+        return tdist.monitored_barrier(group=group, timeout=timeout, wait_all_ranks=wait_all_ranks)
+    return tdist.barrier(group=group)
+
+
+def has_reduce_scatter_tensor():
+    return True
+
+
+def has_all_gather_into_tensor():
+    return True

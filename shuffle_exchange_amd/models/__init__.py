@@ -1,0 +1,2 @@
+from .llama import LlamaConfig, LlamaForCausalLM, llama_config  # noqa: F401
+from .gpt2 import GPT2Config, GPT2LMHeadModel, gpt2_config  # noqa: F401

@@ -1,0 +1,190 @@
+"""Llama-family decoder (Llama-2/3, Mistral-style GQA) built on this repo's HIP ops.
+
+MI355X-first layer anatomy (all hot elementwise work in HIP kernels, all GEMMs as large single
+hipBLASLt calls):
+  a, h   = rmsnorm(x + res)            fused residual-add + RMSNorm          (ops/norm.py)
+  qkv    = a @ Wqkv^T                  ONE GEMM for q, k, v  -> [B, S, Hq+2Hkv, D]
+  rope_(qkv[:, :, :Hq+Hkv])            in place, no transposes               (ops/rope.py)
+  o      = attention(q, k, v)          [B, S, H, D] strided views, GQA       (ops/attention.py)
+  m, h2  = rmsnorm(o @ Wo^T + h)
+  out    = swiglu(m @ Wgu^T) @ Wd^T    ONE GEMM for gate|up                  (ops/activation.py)
+  loss   = fused_linear_cross_entropy(final_norm(...), Wlm)                  (ops/cross_entropy.py)
+
+Reference counterparts: the inference-v2 Llama implementation
+(deepspeed/inference/v2/model_implementations/llama_v2/model.py:133-199) and the HF models the
+reference trains through ``deepspeed.initialize``. Config presets match Llama-3 8B / 70B.
+"""
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.utils.checkpoint import checkpoint
+
+from ..ops.activation import swiglu
+from ..ops.attention import attention
+from ..ops.cross_entropy import fused_linear_cross_entropy
+from ..ops.norm import RMSNorm
+from ..ops.rope import RopeCache, apply_rope_qkv_
+
+
+@dataclass
+class LlamaConfig:
+    vocab_size: int = 128256
+    hidden_size: int = 4096
+    intermediate_size: int = 14336
+    num_hidden_layers: int = 32
+    num_attention_heads: int = 32
+    num_key_value_heads: int = 8
+    head_dim: Optional[int] = None
+    rope_theta: float = 500000.0
+    rms_norm_eps: float = 1e-5
+    max_position_embeddings: int = 8192
+    tie_word_embeddings: bool = False
+    initializer_range: float = 0.02
+    activation_checkpointing: bool = False
+    loss_chunk_tokens: Optional[int] = None
+    extra: dict = field(default_factory=dict)
+
+    def __post_init__(self):
+        if self.head_dim is None:
+            self.head_dim = self.hidden_size // self.num_attention_heads
+
+    def num_params(self):
+        h, i, v, L = self.hidden_size, self.intermediate_size, self.vocab_size, self.num_hidden_layers
+        d = self.head_dim
+        qkv = h * (self.num_attention_heads + 2 * self.num_key_value_heads) * d
+        per_layer = qkv + self.num_attention_heads * d * h + 3 * h * i + 2 * h
+        emb = v * h * (1 if self.tie_word_embeddings else 2)
+        return L * per_layer + emb + h
+
+    def flops_per_token(self, seq_len):
+        """Training FLOPs per token: 6 * non-embedding-params + causal attention (fwd 2*S*h per
+        layer for QK^T and PV, halved by causality, x3 for fwd+bwd)."""
+        n = self.num_params() - self.vocab_size * self.hidden_size  # exclude input embedding (lookup)
+        attn = 3 * 2 * 2 * self.num_hidden_layers * seq_len * self.num_attention_heads * self.head_dim / 2
+        return 6 * n + attn
+
+
+PRESETS = {
+    "llama3-8b": dict(),
+    "llama3-70b": dict(hidden_size=8192, intermediate_size=28672, num_hidden_layers=80, num_attention_heads=64,
+                       num_key_value_heads=8),
+    "llama2-7b": dict(vocab_size=32000, hidden_size=4096, intermediate_size=11008, num_hidden_layers=32,
+                      num_attention_heads=32, num_key_value_heads=32, rope_theta=10000.0, rms_norm_eps=1e-5,
+                      max_position_embeddings=4096),
+    "llama-tiny": dict(vocab_size=512, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+                       num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=256),
+}
+
+
+def llama_config(name, **overrides):
+    d = dict(PRESETS[name])
+    d.update(overrides)
+    return LlamaConfig(**d)
+
+
+class LlamaAttention(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.nq, self.nkv, self.d = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+        self.qkv_proj = nn.Linear(cfg.hidden_size, (self.nq + 2 * self.nkv) * self.d, bias=False)
+        self.o_proj = nn.Linear(self.nq * self.d, cfg.hidden_size, bias=False)
+
+    def forward(self, x, rope: RopeCache, position_ids=None):
+        B, S, _ = x.shape
+        qkv = F.linear(x, self.qkv_proj.weight).view(B, S, self.nq + 2 * self.nkv, self.d)
+        qkv = apply_rope_qkv_(qkv, rope, self.nq + self.nkv, position_ids)
+        q = qkv[:, :, :self.nq]
+        k = qkv[:, :, self.nq:self.nq + self.nkv]
+        v = qkv[:, :, self.nq + self.nkv:]
+        o = attention(q, k, v, causal=True)
+        return F.linear(o.reshape(B, S, self.nq * self.d), self.o_proj.weight)
+
+
+class LlamaMLP(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.gate_up_proj = nn.Linear(cfg.hidden_size, 2 * cfg.intermediate_size, bias=False)
+        self.down_proj = nn.Linear(cfg.intermediate_size, cfg.hidden_size, bias=False)
+
+    def forward(self, x):
+        return F.linear(swiglu(F.linear(x, self.gate_up_proj.weight)), self.down_proj.weight)
+
+
+class LlamaDecoderLayer(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.input_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
+        self.self_attn = LlamaAttention(cfg)
+        self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
+        self.mlp = LlamaMLP(cfg)
+
+    def forward(self, x, residual, rope, position_ids=None):
+        """(x, residual) -> (mlp_out, new_residual); the true hidden state is x + residual."""
+        if residual is None:
+            a, h = self.input_layernorm(x), x
+        else:
+            a, h = self.input_layernorm(x, residual)
+        attn = self.self_attn(a, rope, position_ids)
+        m, h2 = self.post_attention_layernorm(attn, h)
+        return self.mlp(m), h2
+
+
+class LMHeadLoss(nn.Module):
+    """LM head as a module (so ZeRO-3 fetch hooks see it); returns the mean CE loss when labels are
+    given (labels are the input ids, shifted here: position t predicts t+1), else logits."""
+
+    def __init__(self, cfg: LlamaConfig, weight=None):
+        super().__init__()
+        self.cfg = cfg
+        if weight is None:
+            self.weight = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden_size))
+        else:
+            self.weight = weight
+
+    def forward(self, h, labels=None, ignore_index=-100):
+        if labels is None:
+            return F.linear(h, self.weight)
+        tgt = torch.cat([labels[:, 1:], torch.full_like(labels[:, :1], ignore_index)], dim=1)
+        return fused_linear_cross_entropy(h, self.weight, tgt, ignore_index, self.cfg.loss_chunk_tokens)
+
+
+class LlamaForCausalLM(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.embed_tokens = nn.Embedding(cfg.vocab_size, cfg.hidden_size)
+        self.layers = nn.ModuleList([LlamaDecoderLayer(cfg) for _ in range(cfg.num_hidden_layers)])
+        self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
+        self.lm_head = LMHeadLoss(cfg, self.embed_tokens.weight if cfg.tie_word_embeddings else None)
+        self._rope = None
+        self.reset_parameters()
+
+    @torch.no_grad()
+    def reset_parameters(self):
+        std = self.cfg.initializer_range
+        for m in self.modules():
+            if isinstance(m, (nn.Linear, nn.Embedding)):
+                m.weight.normal_(0.0, std)
+        if not self.cfg.tie_word_embeddings:
+            self.lm_head.weight.normal_(0.0, std)
+
+    def rope(self, device):
+        if self._rope is None or self._rope.cos.device != device:
+            self._rope = RopeCache(self.cfg.head_dim, self.cfg.max_position_embeddings, self.cfg.rope_theta, device)
+        return self._rope
+
+    def forward(self, input_ids, labels=None, position_ids=None):
+        x = self.embed_tokens(input_ids)
+        rope = self.rope(x.device)
+        res = None
+        for layer in self.layers:
+            if self.cfg.activation_checkpointing and self.training and torch.is_grad_enabled():
+                x, res = checkpoint(layer, x, res, rope, position_ids, use_reentrant=False)
+            else:
+                x, res = layer(x, res, rope, position_ids)
+        h = self.norm(x, res)[0] if res is not None else self.norm(x)
+        return self.lm_head(h, labels)

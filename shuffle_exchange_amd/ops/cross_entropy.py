@@ -1,0 +1,95 @@
+"""Softmax cross-entropy for LM heads (HIP kernels).
+
+``cross_entropy(logits, target)`` -- standard autograd op (fwd saves lse; bwd writes grads).
+``fused_linear_cross_entropy(h, W, target)`` -- LM head + loss in one autograd node: the logits
+buffer is overwritten in place with d(loss)/d(logits) during the forward (loss is the graph's
+terminal node, so the gradient is known up to the scalar upstream factor), the backward is just two
+GEMMs. Peak memory is one bf16 [T, V] buffer instead of logits + fp32 softmax + grad, and
+``chunk_tokens`` bounds even that (ALST's TiledLoss, reference
+runtime/sequence_parallel/ulysses_sp.py:915, plays the same role).
+"""
+import torch
+import torch.nn.functional as F
+
+from . import native
+
+
+class _XEnt(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, ignore_index):
+        logits2 = logits.contiguous().view(-1, logits.shape[-1])
+        loss, lse = torch.ops.sxe.xent_fwd(logits2, target.reshape(-1).contiguous(), int(ignore_index), False, None, 1.0)
+        ctx.save_for_backward(logits2, target.reshape(-1).contiguous(), lse)
+        ctx.ignore_index = ignore_index
+        ctx.shape = logits.shape
+        return loss.view(logits.shape[:-1])
+
+    @staticmethod
+    def backward(ctx, dloss):
+        logits2, target, lse = ctx.saved_tensors
+        g = torch.ops.sxe.xent_bwd(logits2, target, lse, dloss.reshape(-1).float().contiguous(), int(ctx.ignore_index),
+                                   False)
+        return g.view(ctx.shape), None, None
+
+
+def cross_entropy(logits, target, ignore_index=-100, reduction="mean"):
+    if native.use_hip(logits):
+        per_tok = _XEnt.apply(logits, target, ignore_index)
+    else:
+        per_tok = F.cross_entropy(logits.float().reshape(-1, logits.shape[-1]), target.reshape(-1),
+                                  ignore_index=ignore_index, reduction="none").view(target.shape)
+    if reduction == "none":
+        return per_tok
+    if reduction == "sum":
+        return per_tok.sum()
+    n = (target != ignore_index).sum().clamp_min(1)
+    return per_tok.sum() / n
+
+
+class _FusedLinearXEnt(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, weight, target, ignore_index, chunk_tokens):
+        H = h.shape[-1]
+        h2 = h.reshape(-1, H)
+        tgt = target.reshape(-1).contiguous()
+        T = h2.shape[0]
+        n_valid = (tgt != ignore_index).sum().clamp_min(1).float()
+        inv_n = (1.0 / n_valid).reshape(1)
+        need_grad = torch.is_grad_enabled() or h.requires_grad or weight.requires_grad
+        chunk = T if not chunk_tokens else min(int(chunk_tokens), T)
+        loss_sum = torch.zeros((), device=h.device, dtype=torch.float32)
+        dh = torch.empty_like(h2) if need_grad else None
+        dW = None
+        for s in range(0, T, chunk):
+            e = min(T, s + chunk)
+            logits = torch.matmul(h2[s:e], weight.t())
+            loss, _ = torch.ops.sxe.xent_fwd(logits, tgt[s:e], int(ignore_index), need_grad, inv_n, 1.0)
+            loss_sum = loss_sum + loss.sum()
+            if need_grad:
+                torch.matmul(logits, weight, out=dh[s:e])
+                part = torch.matmul(logits.t(), h2[s:e])
+                if dW is None:
+                    dW = part if chunk == T else part.float()
+                else:
+                    dW.add_(part.float())
+            del logits
+        ctx.save_for_backward(dh, dW)
+        ctx.wdtype = weight.dtype
+        ctx.hshape = h.shape
+        return loss_sum / n_valid
+
+    @staticmethod
+    def backward(ctx, gout):
+        dh, dW = ctx.saved_tensors
+        g = gout.to(torch.float32)
+        dh = (dh * g.to(dh.dtype)).view(ctx.hshape)
+        dW = (dW * g.to(dW.dtype)).to(ctx.wdtype)
+        return dh, dW, None, None, None
+
+
+def fused_linear_cross_entropy(h, weight, target, ignore_index=-100, chunk_tokens=None):
+    """mean-reduced CE of ``h @ weight.T`` against ``target`` (ignore_index excluded)."""
+    if native.use_hip(h):
+        return _FusedLinearXEnt.apply(h, weight, target, ignore_index, chunk_tokens)
+    logits = torch.matmul(h, weight.t()).float()
+    return F.cross_entropy(logits.reshape(-1, logits.shape[-1]), target.reshape(-1), ignore_index=ignore_index)

@@ -1,0 +1,555 @@
+"""Training engine: ``initialize()`` returns one of these; ``forward / backward / step`` drive it.
+
+Parity: reference runtime/engine.py:195 ``DeepSpeedEngine`` -- init :198-411, distributed model
+:1278-1352, optimizer selection :1423-1569, ZeRO wiring :1687-1833, forward :2103, backward
+:2270, step :2404 / _take_model_step :2338, checkpoint save :3343 / load :2997, ``no_sync`` :2250,
+including the fork's ``rings / shuffle_step / method / slice_count`` kwargs (:212-215, :1754-1757).
+
+What happens where on MI355X:
+* gradients never touch the host: ZeRO optimizers reduce-scatter them during backward on a side
+  HIP stream and the whole step (norm, clip, skip, fused Adam + bit16 write-back) is device-side;
+* timers are HIP events (no sync until read); tokens/s and TFLOPs are reported (the reference only
+  reports samples/s);
+* the Shuffle-exchange hooks (``shuffle_exchange()``, ``synchronization()``, ``reset_rings()``) are
+  exposed on the engine and can be driven automatically from config (the reference never calls them,
+  SURVEY §0.1).
+"""
+import os
+import time
+from contextlib import contextmanager
+
+import torch
+import torch.nn as nn
+
+from .. import comm as dist
+from ..accelerator import get_accelerator
+from ..ops import optim as fused
+from ..parallel import groups
+from ..utils.logging import log_dist, logger
+from ..utils.timer import NoopTimer, SynchronizedWallClockTimer, ThroughputTimer
+from .checkpoint_engine import AsyncCheckpointEngine, TorchCheckpointEngine
+from .config import SXEConfig
+from .dataloader import RepeatingLoader, SXEDataLoader
+from .fp16.loss_scaler import make_scaler
+from .lr_schedules import build_scheduler
+from .zero.stage12 import ZeroStage12Optimizer
+from .zero.stage3 import ZeroStage3Optimizer
+
+FORWARD_MICRO_TIMER = "fwd_microstep"
+BACKWARD_MICRO_TIMER = "bwd_microstep"
+STEP_MICRO_TIMER = "step_microstep"
+FORWARD_GLOBAL_TIMER = "fwd"
+BACKWARD_GLOBAL_TIMER = "bwd"
+STEP_GLOBAL_TIMER = "step"
+
+_DTYPE = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16, "float32": torch.float32,
+          "float16": torch.float16, "bfloat16": torch.bfloat16}
+
+
+class SXEEngine(nn.Module):
+    def __init__(self, args=None, model=None, optimizer=None, model_parameters=None, training_data=None,
+                 lr_scheduler=None, mpu=None, dist_init_required=None, collate_fn=None, config=None,
+                 config_class=None, mesh_device=None, dont_change_device=False, rings=None, shuffle_step=None,
+                 method=None, slice_count=None):
+        super().__init__()
+        self.client_optimizer = optimizer
+        self.client_lr_scheduler = lr_scheduler
+        self.collate_fn = collate_fn
+        self.mpu = mpu
+        self.global_steps = 0
+        self.global_samples = 0
+        self.micro_steps = 0
+        self.skipped_steps = 0
+        self.gradient_average = True
+        self._in_no_sync = False
+        acc = get_accelerator()
+        dist.init_distributed(dist_init_required=dist_init_required)
+        self.world_size = dist.get_world_size()
+        self.global_rank = dist.get_rank()
+        self.local_rank = dist.get_local_rank()
+        if acc.gpu:
+            acc.set_device(self.local_rank)
+        self.device = torch.device(acc.current_device_name())
+        if config is None and args is not None:
+            config = getattr(args, "deepspeed_config", None) or getattr(args, "sxe_config", None)
+        self._config = config_class if config_class is not None else SXEConfig(config, world_size=self.world_size,
+                                                                                 mpu=mpu)
+        cfg = self._config
+        groups.initialize(tensor_parallel_size=cfg.tensor_parallel_size,
+                          pipeline_parallel_size=cfg.pipeline_parallel_size,
+                          sequence_parallel_size=cfg.sequence_parallel_size, mpu=mpu)
+        dist.configure(cfg)
+        # fork kwargs override the JSON block (reference __init__.py:82-85)
+        se = cfg.shuffle_exchange
+        if any(v is not None for v in (rings, shuffle_step, method, slice_count)):
+            se = se.model_copy(update={k: v for k, v in dict(enabled=True, rings=rings, shuffle_step=shuffle_step,
+                                                              method=method, slice_count=slice_count).items()
+                                       if v is not None})
+        self.shuffle_exchange_config = se
+        self.timers = SynchronizedWallClockTimer() if cfg.wall_clock_breakdown else NoopTimer()
+        self.module = model
+        self._configure_distributed_model(model, dont_change_device)
+        self.tput_timer = ThroughputTimer(batch_size=cfg.train_batch_size, steps_per_output=cfg.steps_per_print,
+                                          seq_len=None)
+        self.training_dataloader = self.deepspeed_io(training_data) if training_data is not None else None
+        self.optimizer = None
+        self.basic_optimizer = None
+        self.lr_scheduler = None
+        if model_parameters is None:
+            model_parameters = [p for p in model.parameters() if p.requires_grad]
+        if optimizer is not None or cfg.optimizer_name is not None:
+            self._configure_optimizer(optimizer, model_parameters)
+            self._configure_lr_scheduler(lr_scheduler)
+        ckpt = cfg.model.checkpoint
+        self.checkpoint_engine = AsyncCheckpointEngine() if ckpt.async_save else TorchCheckpointEngine()
+        self.monitor = None
+        try:
+            from ..monitor.monitor import MonitorMaster
+            self.monitor = MonitorMaster(cfg.model)
+        except Exception as e:  # monitors are optional
+            logger.debug(f"monitor disabled: {e}")
+        self._auto_se_steps = 0
+
+    # ------------------------------------------------------------------------------------ config
+    @property
+    def config(self):
+        return self._config
+
+    def train_batch_size(self):
+        return self._config.train_batch_size
+
+    def train_micro_batch_size_per_gpu(self):
+        return self._config.train_micro_batch_size_per_gpu
+
+    def gradient_accumulation_steps(self):
+        return self._config.gradient_accumulation_steps
+
+    def zero_optimization_stage(self):
+        return self._config.zero_optimization_stage
+
+    def zero_optimization(self):
+        return self._config.zero_enabled
+
+    def fp16_enabled(self):
+        return self._config.fp16_enabled
+
+    def bfloat16_enabled(self):
+        return self._config.bfloat16_enabled
+
+    def gradient_clipping(self):
+        return self._config.gradient_clipping
+
+    def steps_per_print(self):
+        return self._config.steps_per_print
+
+    def wall_clock_breakdown(self):
+        return self._config.wall_clock_breakdown
+
+    @property
+    def communication_data_type(self):
+        t = self._config.model.communication_data_type
+        return _DTYPE[t] if t else None
+
+    def get_data_parallel_group(self):
+        return groups.get_sequence_data_parallel_group()
+
+    @property
+    def dp_world_size(self):
+        return groups.get_data_parallel_world_size()
+
+    @property
+    def mp_world_size(self):
+        return groups.get_tensor_model_parallel_world_size()
+
+    def model_dtype(self):
+        if self.fp16_enabled():
+            return torch.float16
+        if self.bfloat16_enabled():
+            return torch.bfloat16
+        return torch.float32
+
+    # ----------------------------------------------------------------------------------- model
+    def _configure_distributed_model(self, model, dont_change_device):
+        dtype = self.model_dtype()
+        zero_init = any(hasattr(p, "ds_tensor") for p in model.parameters())
+        if not zero_init:
+            if dtype != torch.float32:
+                model.to(dtype)
+            if not dont_change_device:
+                model.to(self.device)
+            self._broadcast_model()
+
+    def _broadcast_model(self):
+        """Identical initial weights on every data-parallel replica (reference engine.py:1242-1261).
+        Coalesced per dtype into one flat broadcast to avoid per-parameter collectives."""
+        if self.world_size == 1:
+            return
+        group = groups.get_sequence_data_parallel_group()
+        ranks = groups.group_ranks("seq_data")
+        if len(ranks) == 1:
+            return
+        src = ranks[0]
+        tensors = [p.data for p in self.module.parameters()] + [b for b in self.module.buffers()]
+        by_dtype = {}
+        for t in tensors:
+            by_dtype.setdefault(t.dtype, []).append(t)
+        for dt, ts in by_dtype.items():
+            flat = torch.cat([t.reshape(-1) for t in ts])
+            dist.broadcast(flat, src=src, group=group)
+            o = 0
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[o:o + n].view_as(t))
+                o += n
+
+    # ------------------------------------------------------------------------------- optimizer
+    def _configure_basic_optimizer(self, model_parameters):
+        cfg = self._config
+        name = cfg.optimizer_name
+        p = dict(cfg.optimizer_params)
+        p.pop("torch_adam", None)
+        p.pop("fused", None)
+        if "betas" in p:
+            p["betas"] = tuple(p["betas"])
+        if name in ("adam", "adamw", "fusedadam"):
+            adam_w_mode = p.pop("adam_w_mode", True) if name != "adamw" else True
+            return fused.FusedAdam(model_parameters, adam_w_mode=adam_w_mode, **p)
+        if name == "lion":
+            return fused.FusedLion(model_parameters, **p)
+        if name == "adagrad":
+            return fused.FusedAdagrad(model_parameters, **p)
+        if name == "lamb":
+            return fused.FusedLamb(model_parameters, **p)
+        if name == "sgd":
+            return torch.optim.SGD(model_parameters, **p)
+        if name in ("onebitadam", "zerooneadam", "onebitlamb"):
+            from .fp16.onebit import OnebitAdam
+            return OnebitAdam(model_parameters, **p)
+        raise ValueError(f"unsupported optimizer type {name}")
+
+    def _configure_optimizer(self, client_optimizer, model_parameters):
+        cfg = self._config
+        if client_optimizer is not None and not callable(client_optimizer) or isinstance(client_optimizer,
+                                                                                        torch.optim.Optimizer):
+            basic = client_optimizer
+        elif callable(client_optimizer):
+            basic = client_optimizer(model_parameters)
+        else:
+            basic = self._configure_basic_optimizer(model_parameters)
+        self.basic_optimizer = basic
+        dtype = self.model_dtype()
+        scaler = make_scaler(cfg.model.fp16, dtype)
+        stage = cfg.zero_optimization_stage
+        zc = cfg.zero_config
+        dp_ranks = groups.group_ranks("seq_data")
+        dp_group = groups.get_sequence_data_parallel_group()
+        mp_group = groups.get_tensor_model_parallel_group() if groups.get_tensor_model_parallel_world_size() > 1 else None
+        se = self.shuffle_exchange_config
+        off = zc.offload_optimizer
+        if off is not None and off.device in ("cpu", "nvme"):
+            from .zero.offload import OffloadOptimizer
+            self.optimizer = OffloadOptimizer(basic, stage=stage, module=self.module, loss_scaler=scaler,
+                                              clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks, dp_group=dp_group,
+                                              offload_config=off, zero_config=zc, aio_config=cfg.model.aio)
+        elif stage == 3:
+            self.optimizer = ZeroStage3Optimizer(
+                self.module, basic, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks,
+                dp_group=dp_group, prefetch_depth=zc.prefetch_depth,
+                param_persistence_threshold=zc.param_persistence_threshold,
+                communication_data_type=self.communication_data_type, unit_classes=zc.fetch_units,
+                shuffle_exchange_cfg=se, mp_group=mp_group, timers=self.timers, mics_shard_size=zc.mics_shard_size)
+        elif stage in (1, 2):
+            self.optimizer = ZeroStage12Optimizer(
+                basic, stage=stage, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks,
+                dp_group=dp_group, reduce_bucket_size=zc.reduce_bucket_size,
+                communication_data_type=self.communication_data_type, overlap_comm=True, shuffle_exchange_cfg=se,
+                mp_group=mp_group, timers=self.timers)
+        else:
+            from .zero.stage0 import DataParallelOptimizer
+            self.optimizer = DataParallelOptimizer(
+                basic, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks, dp_group=dp_group,
+                bucket_size=zc.reduce_bucket_size, mp_group=mp_group, shuffle_exchange_cfg=se)
+
+    def _configure_lr_scheduler(self, client_lr_scheduler):
+        if client_lr_scheduler is not None:
+            if callable(client_lr_scheduler) and not hasattr(client_lr_scheduler, "step"):
+                self.lr_scheduler = client_lr_scheduler(self.basic_optimizer)
+            else:
+                self.lr_scheduler = client_lr_scheduler
+            return
+        if self._config.scheduler_name:
+            self.lr_scheduler = build_scheduler(self._config.scheduler_name, self.optimizer,
+                                                self._config.scheduler_params)
+
+    # ------------------------------------------------------------------------------------- data
+    def deepspeed_io(self, dataset, batch_size=None, route=None, pin_memory=True, data_sampler=None,
+                     collate_fn=None, num_local_io_workers=None):
+        return SXEDataLoader(dataset, batch_size=batch_size or self.train_micro_batch_size_per_gpu(),
+                             pin_memory=pin_memory and get_accelerator().gpu, collate_fn=collate_fn or self.collate_fn,
+                             num_workers=num_local_io_workers or 0, data_parallel_world_size=groups.get_data_parallel_world_size(),
+                             data_parallel_rank=groups.get_data_parallel_rank(), data_sampler=data_sampler)
+
+    # --------------------------------------------------------------------------------- train loop
+    def is_gradient_accumulation_boundary(self):
+        return (self.micro_steps + 1) % self.gradient_accumulation_steps() == 0
+
+    def set_gradient_accumulation_boundary(self, is_boundary):
+        self._boundary_override = is_boundary
+
+    def forward(self, *inputs, **kwargs):
+        self.timers(FORWARD_MICRO_TIMER).start()
+        if self.optimizer is not None and hasattr(self.optimizer, "forward_prologue"):
+            self.optimizer.forward_prologue()
+        if self.fp16_enabled() and self._config.model.fp16.auto_cast:
+            with torch.autocast(device_type=self.device.type, dtype=torch.float16):
+                out = self.module(*inputs, **kwargs)
+        else:
+            out = self.module(*inputs, **kwargs)
+        self.timers(FORWARD_MICRO_TIMER).stop()
+        return out
+
+    __call__ = nn.Module.__call__
+
+    def backward(self, loss, retain_graph=False, scale_wrt_gas=True):
+        assert self.optimizer is not None, "backward() requires an optimizer"
+        self.timers(BACKWARD_MICRO_TIMER).start()
+        gas = self.gradient_accumulation_steps()
+        if scale_wrt_gas and gas > 1:
+            loss = loss / gas
+        boundary = getattr(self, "_boundary_override", None)
+        boundary = self.is_gradient_accumulation_boundary() if boundary is None else boundary
+        opt = self.optimizer
+        opt.set_gradient_accumulation_boundary(boundary and not self._in_no_sync)
+        opt.backward_prologue()
+        scaled = loss * opt.loss_scale if self.fp16_enabled() else loss
+        scaled.backward(retain_graph=retain_graph)
+        if not self._in_no_sync:
+            opt.reduce_gradients()
+        self.timers(BACKWARD_MICRO_TIMER).stop()
+        return loss
+
+    @contextmanager
+    def no_sync(self):
+        """Skip gradient reduction (ZeRO-0/1 only, as in the reference engine.py:2250)."""
+        assert self.zero_optimization_stage() < 2, "no_sync is incompatible with ZeRO stage >= 2"
+        self._in_no_sync = True
+        try:
+            yield
+        finally:
+            self._in_no_sync = False
+
+    def step(self, lr_kwargs=None):
+        self.timers(STEP_MICRO_TIMER).start()
+        boundary = getattr(self, "_boundary_override", None)
+        boundary = self.is_gradient_accumulation_boundary() if boundary is None else boundary
+        if boundary:
+            self._take_model_step(lr_kwargs)
+        self.micro_steps += 1
+        self._boundary_override = None
+        self.timers(STEP_MICRO_TIMER).stop()
+        if boundary and self.wall_clock_breakdown() and self.global_steps % self.steps_per_print() == 0:
+            self.timers.log([FORWARD_MICRO_TIMER, BACKWARD_MICRO_TIMER, STEP_MICRO_TIMER])
+
+    def _take_model_step(self, lr_kwargs=None):
+        self.optimizer.step()
+        overflow = bool(getattr(self.optimizer, "overflow", False))
+        self.optimizer.zero_grad()
+        if overflow:
+            self.skipped_steps += 1
+        elif self.lr_scheduler is not None:
+            self.lr_scheduler.step(**(lr_kwargs or {}))
+        self.global_steps += 1
+        self.global_samples += self.train_batch_size()
+        se = self.shuffle_exchange_config
+        if se.enabled and se.auto_shuffle:
+            self.shuffle_exchange()
+        if se.enabled and se.sync_period > 0 and self.global_steps % se.sync_period == 0:
+            self.synchronization()
+        if self.monitor is not None and self.monitor.enabled and self.global_rank == 0:
+            self.monitor.write_events([("Train/Samples/lr", self.get_lr()[0], self.global_samples)])
+
+    def train(self, mode=True):
+        self.module.train(mode)
+        return self
+
+    def eval(self):
+        self.module.eval()
+        return self
+
+    def zero_grad(self):
+        self.optimizer.zero_grad()
+
+    def get_lr(self):
+        return [g["lr"] for g in self.optimizer.param_groups] if self.optimizer is not None else []
+
+    def get_global_grad_norm(self):
+        return self.optimizer.get_global_grad_norm() if self.optimizer is not None else None
+
+    @property
+    def loss_scale(self):
+        return self.optimizer.loss_scale
+
+    # ---- Shuffle-exchange user hooks (reference stage_1_and_2.py:692-734) ----------------------
+    def shuffle_exchange(self):
+        if hasattr(self.optimizer, "shuffle_exchange"):
+            self.optimizer.shuffle_exchange()
+
+    def synchronization(self):
+        if hasattr(self.optimizer, "synchronization"):
+            self.optimizer.synchronization()
+
+    def reset_rings(self, rings):
+        if hasattr(self.optimizer, "reset_rings"):
+            self.optimizer.reset_rings(rings)
+
+    # ---------------------------------------------------------------------------- checkpointing
+    def _param_names(self):
+        return {p: n for n, p in self.module.named_parameters()}
+
+    def _ckpt_names(self, save_dir, tag):
+        mp = groups.get_tensor_model_parallel_rank()
+        dp = groups.get_sequence_data_parallel_rank()
+        d = os.path.join(save_dir, str(tag))
+        stage = self.zero_optimization_stage()
+        if stage == 3:
+            model = os.path.join(d, f"zero_pp_rank_{dp}_mp_rank_{mp:02d}_model_states.pt")
+        else:
+            model = os.path.join(d, f"mp_rank_{mp:02d}_model_states.pt")
+        prefix = "bf16_" if (self.bfloat16_enabled() and stage == 0) else ""
+        optim = os.path.join(d, f"{prefix}zero_pp_rank_{dp}_mp_rank_{mp:02d}_optim_states.pt")
+        return d, model, optim
+
+    def module_state_dict(self, exclude_frozen_parameters=False):
+        if self.zero_optimization_stage() == 3:
+            if self._config.zero_config.gather_16bit_weights_on_model_save:
+                return self._zero3_consolidated_16bit_state_dict()
+            return None
+        sd = self.module.state_dict()
+        if exclude_frozen_parameters:
+            names = {n for n, p in self.module.named_parameters() if not p.requires_grad}
+            sd = {k: v for k, v in sd.items() if k not in names}
+        return sd
+
+    def _zero3_consolidated_16bit_state_dict(self):
+        opt = self.optimizer
+        sd = {}
+        names = self._param_names()
+        for fg in opt.fgroups:
+            opt._fetch(fg, wait=True)
+            for u in fg.units:
+                for p in u.params:
+                    sd[names[p]] = p.detach().cpu().clone()
+            opt._release(fg)
+        for n, b in self.module.named_buffers():
+            sd[n] = b.detach().cpu().clone()
+        return sd
+
+    def save_checkpoint(self, save_dir, tag=None, client_state=None, save_latest=True,
+                        exclude_frozen_parameters=False):
+        client_state = client_state or {}
+        if tag is None:
+            tag = f"global_step{self.global_steps}"
+        tag = str(tag)
+        d, model_path, optim_path = self._ckpt_names(save_dir, tag)
+        if self.global_rank == 0:
+            os.makedirs(d, exist_ok=True)
+        dist.barrier()
+        os.makedirs(d, exist_ok=True)
+        names = self._param_names()
+        stage = self.zero_optimization_stage()
+        write_model = stage == 3 or groups.get_sequence_data_parallel_rank() == 0
+        if write_model:
+            state = dict(
+                module=self.module_state_dict(exclude_frozen_parameters),
+                buffer_names=[n for n, _ in self.module.named_buffers()],
+                optimizer=None,
+                param_shapes=[{names[p]: tuple(p.shape) for p in pg["params_orig"]}
+                              for pg in self._orig_param_groups()],
+                frozen_param_shapes={n: tuple(p.shape) for n, p in self.module.named_parameters() if not p.requires_grad},
+                lr_scheduler=self.lr_scheduler.state_dict() if self.lr_scheduler is not None else None,
+                sparse_tensor_module_names=[],
+                skipped_steps=self.skipped_steps,
+                global_steps=self.global_steps,
+                global_samples=self.global_samples,
+                dp_world_size=groups.get_sequence_data_parallel_world_size(),
+                mp_world_size=groups.get_tensor_model_parallel_world_size(),
+                ds_config=self._config._param_dict,
+                ds_version="sxe-0.1",
+            )
+            state.update(client_state)
+            self.checkpoint_engine.save(state, model_path)
+        if self.optimizer is not None:
+            osd = self.optimizer.state_dict()
+            if hasattr(self.optimizer, "unit_layout"):
+                osd["unit_layout"] = self.optimizer.unit_layout(names)
+            self.checkpoint_engine.save({"optimizer_state_dict": osd, "ds_config": self._config._param_dict,
+                                         "ds_version": "sxe-0.1"}, optim_path)
+        self.checkpoint_engine.commit(tag)
+        dist.barrier()
+        if save_latest and self.global_rank == 0:
+            with open(os.path.join(save_dir, "latest"), "w") as f:
+                f.write(tag)
+        dist.barrier()
+        return True
+
+    def _orig_param_groups(self):
+        if not hasattr(self, "_orig_groups_cache"):
+            groups_ = []
+            if self.optimizer is not None and hasattr(self.optimizer, "units"):
+                for units in self.optimizer.units:
+                    groups_.append({"params_orig": [p for u in units for p in u.params]})
+            else:
+                groups_.append({"params_orig": [p for p in self.module.parameters() if p.requires_grad]})
+            self._orig_groups_cache = groups_
+        return self._orig_groups_cache
+
+    def load_checkpoint(self, load_dir, tag=None, load_module_strict=True, load_optimizer_states=True,
+                        load_lr_scheduler_states=True, load_module_only=False, custom_load_fn=None):
+        if tag is None:
+            latest = os.path.join(load_dir, "latest")
+            if not os.path.isfile(latest):
+                logger.warning(f"no 'latest' file in {load_dir}; nothing loaded")
+                return None, None
+            with open(latest) as f:
+                tag = f.read().strip()
+        d, model_path, optim_path = self._ckpt_names(load_dir, tag)
+        ce = self.checkpoint_engine
+        state = ce.load(model_path, map_location="cpu")
+        if state.get("module") is not None:
+            if custom_load_fn is not None:
+                custom_load_fn(src=state["module"], dst=self.module)
+            elif self.zero_optimization_stage() == 3:
+                self._zero3_load_16bit(state["module"], strict=load_module_strict)
+            else:
+                self.module.load_state_dict(state["module"], strict=load_module_strict)
+        if not load_module_only:
+            if self.optimizer is not None and os.path.exists(optim_path):
+                osd = ce.load(optim_path, map_location="cpu")["optimizer_state_dict"]
+                self.optimizer.load_state_dict(osd, load_optimizer_states=load_optimizer_states)
+            if load_lr_scheduler_states and self.lr_scheduler is not None and state.get("lr_scheduler"):
+                self.lr_scheduler.load_state_dict(state["lr_scheduler"])
+            self.global_steps = state.get("global_steps", 0)
+            self.global_samples = state.get("global_samples", 0)
+            self.skipped_steps = state.get("skipped_steps", 0)
+        dist.barrier()
+        skip = {"module", "buffer_names", "optimizer", "param_shapes", "frozen_param_shapes", "lr_scheduler",
+                "sparse_tensor_module_names", "skipped_steps", "global_steps", "global_samples", "dp_world_size",
+                "mp_world_size", "ds_config", "ds_version"}
+        client = {k: v for k, v in state.items() if k not in skip}
+        return os.path.join(load_dir, str(tag)), client
+
+    def _zero3_load_16bit(self, sd, strict=True):
+        opt = self.optimizer
+        names = self._param_names()
+        for fg in opt.fgroups:
+            opt._fetch(fg, wait=True)
+            with torch.no_grad():
+                for u in fg.units:
+                    for p in u.params:
+                        n = names[p]
+                        if n in sd:
+                            p.copy_(sd[n].to(p.device, p.dtype))
+                        elif strict:
+                            raise KeyError(f"missing key {n} in checkpoint")
+            opt.commit_modified_units(fg.units)
+            opt._release(fg)

@@ -1,0 +1,204 @@
+"""Shared machinery of the ZeRO optimizers: fp32 master chunks, fused optimizer step, device-side
+clipping/overflow, state dicts.
+
+Parity: the step half of reference runtime/zero/stage_1_and_2.py:2058-2268 (norm :1941, clip
+:2018-2032, optimizer step :2039-2053, fp32->bit16 copy :2174-2176) and stage3.py:2112-2174.
+MI355X-first: the whole step is asynchronous on the device -- the gradient norm, the
+non-finite check and the clip coefficient stay in device scalars that the fused HIP optimizer
+kernel reads (``scale_t``/``skip_t``), so bf16 training never synchronises the host in ``step()``
+(the reference calls ``.item()`` on the overflow flag every step, stage_1_and_2.py:2073,2342).
+"""
+import torch
+
+from ... import comm as dist
+from ...ops import optim as fused
+from ...utils.logging import log_dist
+
+
+def _kind(opt):
+    from torch.optim import Adam, AdamW, Adagrad
+    if isinstance(opt, fused.FusedAdam):
+        return "adam", opt.adam_w_mode
+    if isinstance(opt, AdamW):
+        return "adam", True
+    if isinstance(opt, Adam):
+        return "adam", False
+    if isinstance(opt, fused.FusedLion):
+        return "lion", None
+    if isinstance(opt, (fused.FusedAdagrad, Adagrad)):
+        return "adagrad", None
+    return "generic", None
+
+
+class ZeroOptimizerBase:
+    """Holds, per parameter group ``g``: ``units[g]`` (FlatUnit list), ``master[g]`` (fp32 chunk
+    concatenation), ``grads[g]`` (fp32 chunk gradient accumulator)."""
+
+    def __init__(self, init_optimizer, loss_scaler, clip_grad, partition_group, overflow_group=None,
+                 mp_group=None, device=None):
+        self.optimizer = init_optimizer
+        self.loss_scaler = loss_scaler
+        self.clip_grad = float(clip_grad or 0.0)
+        self.partition_group = partition_group
+        self.overflow_group = overflow_group
+        self.mp_group = mp_group
+        self.device = device
+        self.kind, self.adamw = _kind(init_optimizer)
+        self.units = []
+        self.master = []
+        self.grads = []
+        self.overflow = False
+        self._last_norm = None
+        self._skip_t = None
+        self.global_step = 0
+
+    # --------------------------------------------------------------------------------------------
+    def _init_master(self):
+        """Create fp32 masters/grad accumulators and re-point the wrapped optimizer at them."""
+        for g, units in enumerate(self.units):
+            total = sum(u.chunk for u in units)
+            m = torch.empty(total, dtype=torch.float32, device=self.device)
+            gr = torch.zeros(total, dtype=torch.float32, device=self.device)
+            off = 0
+            for u in units:
+                u.master = m[off:off + u.chunk]
+                u.grad = gr[off:off + u.chunk]
+                u.master.copy_(u.shard.float())
+                off += u.chunk
+            m = torch.nn.Parameter(m, requires_grad=False)
+            self.master.append(m)
+            self.grads.append(gr)
+            self.optimizer.param_groups[g]["params"] = [m]
+        self.optimizer.state.clear()
+        self._init_state()
+
+    def _init_state(self):
+        for g, m in enumerate(self.master):
+            st = self.optimizer.state[m]
+            if self.kind == "adam":
+                st["step"] = 0
+                st["exp_avg"] = torch.zeros_like(m.data)
+                st["exp_avg_sq"] = torch.zeros_like(m.data)
+            elif self.kind == "lion":
+                st["exp_avg"] = torch.zeros_like(m.data)
+            elif self.kind == "adagrad":
+                st["sum"] = torch.zeros_like(m.data)
+                st["step"] = 0
+
+    # --------------------------------------------------------------------------------------------
+    def _grad_norm_and_flags(self):
+        """Device-side: global grad norm over the partition group (unscaled), the clip/unscale
+        coefficient and the skip (non-finite) flag. No host synchronisation."""
+        sq = None
+        for gr in self.grads:
+            s = fused.sumsq(gr)
+            sq = s if sq is None else sq + s
+        sq = sq.reshape(1).float()
+        dist.all_reduce(sq, group=self.partition_group)
+        if self.mp_group is not None:
+            dist.all_reduce(sq, group=self.mp_group)
+        ls = float(self.loss_scaler.loss_scale)
+        norm = sq.sqrt() / ls
+        skip = (~torch.isfinite(norm)).float()
+        if self.overflow_group is not None:
+            # the fork's world-wide overflow agreement (reference stage_1_and_2.py:2071-2073)
+            dist.all_reduce(skip, op=dist.ReduceOp.MAX, group=self.overflow_group)
+        coef = torch.full((1,), 1.0 / ls, dtype=torch.float32, device=norm.device)
+        if self.clip_grad > 0:
+            clip = torch.clamp(self.clip_grad / (torch.nan_to_num(norm, nan=0.0, posinf=0.0) + 1e-6), max=1.0)
+            coef = coef * clip
+        self._last_norm = norm
+        self._skip_t = skip
+        return coef, skip
+
+    def _fused_update(self, coef, skip):
+        """One optimizer step over every unit chunk; writes the bit16 chunks in the same pass."""
+        for g, units in enumerate(self.units):
+            pg = self.optimizer.param_groups[g]
+            m = self.master[g]
+            st = self.optimizer.state[m]
+            if self.kind == "adam":
+                st["step"] = int(st.get("step", 0)) + 1
+                b1, b2 = pg["betas"]
+                if m.is_cuda:
+                    offs = self._unit_offsets(g)
+                    torch.ops.sxe.multi_tensor_adam_(
+                        [u.master for u in units], [u.grad for u in units],
+                        [st["exp_avg"][o:o + u.chunk] for u, o in zip(units, offs)],
+                        [st["exp_avg_sq"][o:o + u.chunk] for u, o in zip(units, offs)],
+                        [u.shard for u in units], coef, skip, float(pg["lr"]), float(b1), float(b2), float(pg["eps"]),
+                        float(pg["weight_decay"]), int(st["step"]), bool(self.adamw),
+                        bool(pg.get("bias_correction", True)), 1.0)
+                else:
+                    offs = self._unit_offsets(g)
+                    for u, o in zip(units, offs):
+                        fused.adam_flat_(u.master, u.grad, st["exp_avg"][o:o + u.chunk],
+                                         st["exp_avg_sq"][o:o + u.chunk], u.shard, lr=pg["lr"], beta1=b1, beta2=b2,
+                                         eps=pg["eps"], weight_decay=pg["weight_decay"], step=st["step"],
+                                         adamw=self.adamw, bias_correction=pg.get("bias_correction", True),
+                                         scale_t=coef, skip_t=skip)
+            elif self.kind == "lion":
+                b1, b2 = pg["betas"]
+                for u, o in zip(units, self._unit_offsets(g)):
+                    fused.lion_flat_(u.master, u.grad, st["exp_avg"][o:o + u.chunk], u.shard, lr=pg["lr"], beta1=b1,
+                                     beta2=b2, weight_decay=pg["weight_decay"], scale_t=coef, skip_t=skip)
+            elif self.kind == "adagrad":
+                st["step"] = int(st.get("step", 0)) + 1
+                for u, o in zip(units, self._unit_offsets(g)):
+                    fused.adagrad_flat_(u.master, u.grad, st["sum"][o:o + u.chunk], u.shard, lr=pg["lr"],
+                                        eps=pg.get("eps", 1e-10), weight_decay=pg.get("weight_decay", 0.0),
+                                        scale_t=coef, skip_t=skip)
+        if self.kind == "generic":
+            # any torch.optim optimizer: fp32 grads -> .grad of the master, step, copy back.
+            # (host-synchronising on skip; the fused kinds above never do)
+            if float(skip.reshape(-1)[0]) != 0.0:
+                return
+            for g, m in enumerate(self.master):
+                m.grad = self.grads[g] * coef
+            self.optimizer.step()
+            for g, units in enumerate(self.units):
+                self.master[g].grad = None
+                for u in units:
+                    u.shard.copy_(u.master)
+
+    def _unit_offsets(self, g):
+        offs, o = [], 0
+        for u in self.units[g]:
+            offs.append(o)
+            o += u.chunk
+        return offs
+
+    def zero_grad_buffers(self):
+        for gr in self.grads:
+            gr.zero_()
+
+    # --------------------------------------------------------------------------------------------
+    @property
+    def param_groups(self):
+        return self.optimizer.param_groups
+
+    @property
+    def state(self):
+        return self.optimizer.state
+
+    @property
+    def loss_scale(self):
+        return self.loss_scaler.loss_scale
+
+    @property
+    def cur_scale(self):
+        return self.loss_scaler.loss_scale
+
+    def get_global_grad_norm(self):
+        return None if self._last_norm is None else float(self._last_norm.reshape(-1)[0])
+
+    def _handle_overflow_host(self):
+        """fp16 with dynamic loss scaling needs the overflow on the host (one sync per step)."""
+        if getattr(self.loss_scaler, "dynamic", False):
+            self.overflow = bool(self._skip_t.reshape(-1)[0].item() != 0.0)
+            self.loss_scaler.update_scale(self.overflow)
+            if self.overflow:
+                log_dist(f"overflow: skipping step, loss scale -> {self.loss_scaler.cur_scale}", ranks=[0])
+        else:
+            self.overflow = False
+        return self.overflow

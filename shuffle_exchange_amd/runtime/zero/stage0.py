@@ -1,0 +1,131 @@
+"""Plain data parallelism (ZeRO stage 0) with bucketed, overlapped gradient all-reduce.
+
+Parity: reference runtime/engine.py:2170-2184 ``allreduce_gradients`` / :2616-2751
+``allreduce_bucket`` / ``buffered_allreduce_fallback`` and runtime/bf16_optimizer.py:35.
+Parameters are grouped into flat units of ``bucket_size`` elements (replicated, S = 1); the fp32
+gradient accumulator of a unit is all-reduced (``ReduceOp.AVG`` on RCCL) on a side HIP stream as
+soon as its last gradient arrives on the accumulation-boundary micro-step, then the fused optimizer
+updates fp32 masters and writes the bit16 weights in one pass.
+"""
+import torch
+
+from ... import comm as dist
+from ...accelerator import get_accelerator
+from ...utils.logging import log_dist
+from .base import ZeroOptimizerBase
+from .flat import FlatUnit, split_into_units
+
+
+class DataParallelOptimizer(ZeroOptimizerBase):
+    def __init__(self, init_optimizer, *, loss_scaler, clip_grad=0.0, dp_ranks=None, dp_group=None,
+                 bucket_size=500_000_000, mp_group=None, shuffle_exchange_cfg=None):
+        acc = get_accelerator()
+        device = torch.device(acc.current_device_name())
+        super().__init__(init_optimizer, loss_scaler, clip_grad, None, overflow_group=None, mp_group=mp_group,
+                         device=device)
+        self.dp_group = dp_group
+        self.dp_size = len(dp_ranks) if dp_ranks is not None else dist.get_world_size()
+        self.comm_stream = acc.named_stream("dp_reduce") if acc.gpu else None
+        self.boundary = True
+        self.param_unit = {}
+        self._hooks = []
+        for g, pg in enumerate(init_optimizer.param_groups):
+            params = [p for p in pg["params"] if p.requires_grad]
+            units = []
+            if params:
+                for i, plist in enumerate(split_into_units(params, max(1, int(bucket_size)))):
+                    u = FlatUnit(plist, 1, 0, params[0].dtype, device, name=f"g{g}u{i}", index=i)
+                    units.append(u)
+                    for p in plist:
+                        self.param_unit[p] = u
+            self.units.append(units)
+        self._init_master()
+        for p, u in self.param_unit.items():
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(u)))
+        log_dist(f"DP (ZeRO-0): {sum(len(u) for u in self.units)} buckets over {self.dp_size} ranks", ranks=[0])
+
+    def _make_hook(self, u):
+        def hook(p):
+            if p.grad is None or not self.boundary:
+                return
+            i = u.param_index[id(p)]
+            o, n = u.offsets[i], u.numels[i]
+            u.grad[o:o + n].add_(p.grad.reshape(-1))
+            p.grad = None
+            if not u.filled[i]:
+                u.filled[i] = True
+                u.pending -= 1
+                if u.pending == 0:
+                    self._allreduce_unit(u)
+        return hook
+
+    def _allreduce_unit(self, u):
+        if self.dp_size == 1 or u.reduced:
+            u.reduced = True
+            return
+        u.reduced = True
+        st = self.comm_stream
+        if st is not None:
+            st.wait_stream(torch.cuda.current_stream())
+        with get_accelerator().stream(st):
+            if dist.get_backend() == "nccl":
+                dist.all_reduce(u.grad, op=dist.ReduceOp.AVG, group=self.dp_group)
+            else:
+                dist.all_reduce(u.grad, group=self.dp_group)
+                u.grad.div_(self.dp_size)
+
+    def set_gradient_accumulation_boundary(self, flag):
+        self.boundary = bool(flag)
+
+    def backward_prologue(self):
+        for units in self.units:
+            for u in units:
+                u.begin_backward()
+                u.reduced = False
+
+    def reduce_gradients(self, pipeline_parallel=False):
+        if not self.boundary:
+            return
+        for units in self.units:
+            for u in units:
+                for i, p in enumerate(u.params):
+                    if p.grad is not None:
+                        o, n = u.offsets[i], u.numels[i]
+                        u.grad[o:o + n].add_(p.grad.reshape(-1))
+                        p.grad = None
+                self._allreduce_unit(u)
+
+    def step(self, closure=None):
+        if self.comm_stream is not None:
+            torch.cuda.current_stream().wait_stream(self.comm_stream)
+        coef, skip = self._grad_norm_and_flags()
+        if getattr(self.loss_scaler, "dynamic", False) and self._handle_overflow_host():
+            self.zero_grad_buffers()
+            return
+        self._fused_update(coef, skip)
+        self.zero_grad_buffers()
+        self.global_step += 1
+
+    def zero_grad(self, set_to_none=True):
+        for p in self.param_unit:
+            p.grad = None
+
+    def unit_layout(self, name_of):
+        return [[{"params": [name_of.get(p, "") for p in u.params], "shapes": u.shapes, "offsets": u.offsets,
+                  "numel": u.numel, "padded": u.padded, "chunk": u.chunk} for u in units] for units in self.units]
+
+    def state_dict(self):
+        return {"loss_scaler": self.loss_scaler.state_dict(), "clip_grad": self.clip_grad,
+                "base_optimizer_state": self.optimizer.state_dict(),
+                "single_partition_of_fp32_groups": [m.data for m in self.master], "zero_stage": 0,
+                "ds_version": "sxe-0.1"}
+
+    def load_state_dict(self, sd, load_optimizer_states=True, load_from_fp32_weights=True):
+        self.loss_scaler.load_state_dict(sd["loss_scaler"])
+        if load_optimizer_states:
+            self.optimizer.load_state_dict(sd["base_optimizer_state"])
+        for m, s in zip(self.master, sd["single_partition_of_fp32_groups"]):
+            m.data.copy_(s.to(m.device))
+        for units in self.units:
+            for u in units:
+                u.shard.copy_(u.master)

@@ -1,0 +1,245 @@
+"""ZeRO stage 1/2 optimizer with Shuffle-exchange hierarchical slices.
+
+Parity: reference runtime/zero/stage_1_and_2.py:119 ``DeepSpeedZeroOptimizer`` (init :131-690,
+grad hooks :1090-1102, bucketing :1114-1154, average_tensor :1242-1345, step :2058-2268,
+state_dict :2472) including the fork's slice groups, inter-slice groups and the RR / shuffle / H-RR /
+Gossip parameter synchronisation plus ``shuffle_exchange()``, ``synchronization()``,
+``reset_rings()`` (stage_1_and_2.py:692-734).
+
+Data flow per step on MI355X (slice of S ranks; with ``slice_count`` == DP world this is plain
+ZeRO-1/2):
+  backward: post-accumulate-grad hook copies each grad into its unit's staging buffer; when a unit
+            is complete ONE reduce-scatter (slice group) lands the averaged chunk in the owner's
+            fp32 accumulator -- on a dedicated HIP comm stream, overlapping the rest of backward.
+            Stage 1 only reduces on the gradient-accumulation boundary micro-step; stage 2 every
+            micro-step (and frees the full grads immediately).
+  step:     device-side norm/clip/overflow -> one multi-tensor fused Adam launch that also writes the
+            bit16 chunk -> inter-slice sync of the chunk (Shuffle-exchange) -> one in-place
+            all-gather per unit inside the slice.
+"""
+import torch
+
+from ... import comm as dist
+from ...accelerator import get_accelerator
+from ...utils.logging import log_dist
+from .base import ZeroOptimizerBase
+from .flat import FlatUnit, split_into_units
+from .shuffle_exchange import ShuffleExchange, SliceTopology
+
+
+class ZeroStage12Optimizer(ZeroOptimizerBase):
+    def __init__(self, init_optimizer, *, stage=2, loss_scaler, clip_grad=0.0, dp_ranks=None, dp_group=None,
+                 reduce_bucket_size=500_000_000, communication_data_type=None, overlap_comm=True,
+                 shuffle_exchange_cfg=None, method=None, slice_count=None, rings=None, shuffle_step=None,
+                 mp_group=None, timers=None, average_master=False):
+        acc = get_accelerator()
+        device = torch.device(acc.current_device_name())
+        self.stage = stage
+        dp_ranks = list(dp_ranks) if dp_ranks is not None else list(range(dist.get_world_size()))
+        # ---- Shuffle-exchange topology ------------------------------------------------------------
+        se = shuffle_exchange_cfg
+        enabled = bool(se is not None and se.enabled) or any(v is not None for v in (method, slice_count))
+        self.method = method or (se.method if se is not None else "RR")
+        S = slice_count or (se.slice_count if (se is not None and se.enabled) else len(dp_ranks))
+        if not enabled:
+            S = len(dp_ranks)
+        self.slice_count = S
+        self.topo = SliceTopology(dp_ranks, S)
+        self.shuffle_exchange_enabled = enabled and self.topo.num_slices > 1
+        self.se = ShuffleExchange(self.topo, method=self.method,
+                                  rings=rings or (se.rings if se is not None else 8),
+                                  shuffle_step=shuffle_step or (se.shuffle_step if se is not None else 50),
+                                  seed=se.seed if se is not None else 1234,
+                                  gossip_p=se.gossip_p if se is not None else 1.0,
+                                  average_master=average_master) if self.shuffle_exchange_enabled else None
+        slice_group = self.topo.slice_group if self.topo.S > 1 else None
+        world_group = dp_group if self.shuffle_exchange_enabled else None
+        super().__init__(init_optimizer, loss_scaler, clip_grad, slice_group, overflow_group=world_group,
+                         mp_group=mp_group, device=device)
+        self.comm_dtype = communication_data_type
+        self.overlap_comm = overlap_comm
+        self.comm_stream = acc.named_stream("zero_reduce") if (overlap_comm and acc.gpu) else None
+        self.timers = timers
+        self.micro_step_boundary = True
+        self._hooks = []
+        self.param_unit = {}
+        # ---- flatten every param group into units -------------------------------------------------
+        dtype = None
+        for g, pg in enumerate(init_optimizer.param_groups):
+            params = [p for p in pg["params"] if p.requires_grad]
+            if not params:
+                self.units.append([])
+                continue
+            dtype = params[0].dtype
+            units = []
+            for i, plist in enumerate(split_into_units(params, max(1, int(reduce_bucket_size)))):
+                u = FlatUnit(plist, S, self.topo.offset, dtype, device, name=f"g{g}u{i}", index=i)
+                units.append(u)
+                for p in plist:
+                    self.param_unit[p] = u
+            self.units.append(units)
+        self.bit16_dtype = dtype
+        self._init_master()
+        self._register_hooks()
+        log_dist(f"ZeRO-{stage}: {sum(len(u) for u in self.units)} units, slice_count={S}, "
+                 f"slices={self.topo.num_slices}, shuffle_exchange="
+                 f"{self.method if self.shuffle_exchange_enabled else 'off'}", ranks=[0])
+
+    # ------------------------------------------------------------------------------------- backward
+    def _register_hooks(self):
+        for p, u in self.param_unit.items():
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(u)))
+
+    def _make_hook(self, unit):
+        def hook(p):
+            if not self.micro_step_boundary and self.stage == 1:
+                return  # ZeRO-1 keeps accumulating full grads until the boundary
+            if p.grad is None:
+                return
+            if self.topo.S == 1:
+                i = unit.param_index[id(p)]
+                o, n = unit.offsets[i], unit.numels[i]
+                unit.grad[o:o + n].add_(p.grad.reshape(-1))
+                unit.filled[i] = True
+                p.grad = None
+                return
+            done = unit.stage_grad(p, p.grad)
+            p.grad = None
+            if done:
+                self._reduce_unit(unit)
+        return hook
+
+    def set_gradient_accumulation_boundary(self, flag):
+        self.micro_step_boundary = bool(flag)
+
+    def backward_prologue(self):
+        for units in self.units:
+            for u in units:
+                u.begin_backward()
+
+    def _reduce_unit(self, u):
+        st = u.staging
+        u.staging = None
+        cur = torch.cuda.current_stream() if st.is_cuda else None
+        stream = self.comm_stream
+        if stream is not None:
+            stream.wait_stream(cur)
+        with get_accelerator().stream(stream):
+            send = st if (self.comm_dtype is None or st.dtype == self.comm_dtype) else st.to(self.comm_dtype)
+            out = torch.empty(u.chunk, dtype=send.dtype, device=send.device)
+            dist.reduce_scatter_tensor(out, send, group=self.topo.slice_group)
+            u.grad.add_(out, alpha=1.0 / self.topo.S)
+            if stream is not None:
+                st.record_stream(stream)
+                send.record_stream(stream)
+                out.record_stream(stream)
+
+    def reduce_gradients(self, pipeline_parallel=False):
+        """Backward epilogue: reduce units whose params did not all produce grads (unused params)
+        and, for ZeRO-1 at the boundary, everything still pending."""
+        if self.stage == 1 and not self.micro_step_boundary:
+            return
+        for units in self.units:
+            for u in units:
+                if self.topo.S == 1:
+                    continue
+                if u.pending > 0:
+                    # params whose grads exist but whose hook did not fire (e.g. stage 1 grads
+                    # accumulated before a boundary without a new backward contribution)
+                    for i, p in enumerate(u.params):
+                        if not u.filled[i] and p.grad is not None:
+                            u.stage_grad(p, p.grad)
+                            p.grad = None
+                    if u.pending > 0:
+                        u.fill_missing()
+                    self._reduce_unit(u)
+
+    def _wait_comm(self):
+        if self.comm_stream is not None:
+            torch.cuda.current_stream().wait_stream(self.comm_stream)
+
+    # ----------------------------------------------------------------------------------------- step
+    def step(self, closure=None, lr_kwargs=None):
+        self._wait_comm()
+        if self.se is not None and self.method == "Gossip":
+            self.se.pre_step([u.shard for units in self.units for u in units])
+        coef, skip = self._grad_norm_and_flags()
+        if getattr(self.loss_scaler, "dynamic", False):
+            if self._handle_overflow_host():
+                self.zero_grad_buffers()
+                return
+        self._fused_update(coef, skip)
+        self.zero_grad_buffers()
+        if self.se is not None:
+            shards = [u.shard for units in self.units for u in units]
+            masters = [u.master for units in self.units for u in units]
+            self.se.sync(shards, masters)
+        self._allgather_params()
+        self.global_step += 1
+
+    def _allgather_params(self):
+        if self.topo.S == 1:
+            return
+        for units in self.units:
+            for u in units:
+                dist.all_gather_into_tensor(u.flat, u.shard, group=self.topo.slice_group)
+
+    def zero_grad(self, set_to_none=True):
+        for p in self.param_unit:
+            p.grad = None
+
+    # ---------------------------------------------------------------------- Shuffle-exchange hooks
+    def shuffle_exchange(self):
+        if self.se is not None:
+            self.se.shuffle_exchange()
+
+    def synchronization(self):
+        if self.se is not None and self.se.synchronization([u.shard for units in self.units for u in units]):
+            self._allgather_params()
+
+    def reset_rings(self, rings):
+        if self.se is not None:
+            self.se.reset_rings(rings)
+
+    # ------------------------------------------------------------------------------- checkpointing
+    def unit_layout(self, name_of):
+        return [[{"params": [name_of.get(p, "") for p in u.params], "shapes": u.shapes, "offsets": u.offsets,
+                  "numel": u.numel, "padded": u.padded, "chunk": u.chunk} for u in units] for units in self.units]
+
+    def state_dict(self):
+        return {
+            "loss_scaler": self.loss_scaler.state_dict(),
+            "dynamic_loss_scale": bool(getattr(self.loss_scaler, "dynamic", False)),
+            "overflow": self.overflow,
+            "clip_grad": self.clip_grad,
+            "base_optimizer_state": self.optimizer.state_dict(),
+            "single_partition_of_fp32_groups": [m.data for m in self.master],
+            "zero_stage": self.stage,
+            "group_paddings": [sum(u.padded - u.numel for u in units) for units in self.units],
+            "partition_count": [self.topo.S for _ in self.units],
+            "shuffle_exchange": self.se.state_dict() if self.se is not None else None,
+            "slice_count": self.topo.S,
+            "ds_version": "sxe-0.1",
+        }
+
+    def load_state_dict(self, sd, load_optimizer_states=True, load_from_fp32_weights=True):
+        self.loss_scaler.load_state_dict(sd["loss_scaler"])
+        self.clip_grad = sd.get("clip_grad", self.clip_grad)
+        if load_optimizer_states:
+            saved = sd["base_optimizer_state"]
+            self.optimizer.load_state_dict(saved)
+            # load_state_dict re-binds state to our master params; make sure tensors are on device
+            for m in self.master:
+                st = self.optimizer.state[m]
+                for k, v in list(st.items()):
+                    if isinstance(v, torch.Tensor) and v.numel() > 1:
+                        st[k] = v.to(m.device)
+        if load_from_fp32_weights:
+            for m, saved in zip(self.master, sd["single_partition_of_fp32_groups"]):
+                m.data.copy_(saved.to(m.device))
+            for units in self.units:
+                for u in units:
+                    u.shard.copy_(u.master)
+            self._allgather_params()
+        if self.se is not None and sd.get("shuffle_exchange"):
+            self.se.load_state_dict(sd["shuffle_exchange"])

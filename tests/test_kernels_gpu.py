@@ -1,0 +1,207 @@
+"""Numerics of every HIP kernel vs a plain PyTorch fp32 reference of the same op (MI355X only)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    from shuffle_exchange_amd.ops import native
+    native.require_hip()
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("adamw", [True, False])
+def test_adam_flat(gdt, adamw):
+    from shuffle_exchange_amd.ops.optim import adam_flat_
+    n = 1_000_003
+    p = torch.randn(n, device="cuda")
+    g = torch.randn(n, device="cuda").to(gdt)
+    m = torch.randn(n, device="cuda").abs() * 0.1
+    v = torch.rand(n, device="cuda") * 0.01
+    lp = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    ref = [t.clone().float() for t in (p, g, m, v)]
+    scale = torch.tensor([0.5], device="cuda")
+    adam_flat_(p, g, m, v, lp, lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1, step=3, adamw=adamw,
+               scale_t=scale)
+    rp, rg, rm, rv = ref
+    rg = rg * 0.5
+    if not adamw:
+        rg = rg + 0.1 * rp
+    rm = 0.9 * rm + 0.1 * rg
+    rv = 0.95 * rv + 0.05 * rg * rg
+    denom = rv.sqrt() / math.sqrt(1 - 0.95 ** 3) + 1e-8
+    if adamw:
+        rp = rp * (1 - 1e-3 * 0.1)
+    rp = rp - (1e-3 / (1 - 0.9 ** 3)) * rm / denom
+    assert _rel(p, rp) < 1e-6
+    assert _rel(m, rm) < 1e-6 and _rel(v, rv) < 1e-6
+    assert torch.equal(lp, p.to(torch.bfloat16))
+
+
+def test_adam_skip_flag():
+    from shuffle_exchange_amd.ops.optim import adam_flat_
+    p = torch.randn(4096, device="cuda")
+    p0 = p.clone()
+    g, m, v = torch.randn_like(p), torch.zeros_like(p), torch.zeros_like(p)
+    adam_flat_(p, g, m, v, lr=1.0, skip_t=torch.ones(1, device="cuda"))
+    assert torch.equal(p, p0)
+
+
+def test_multi_tensor_adam_matches_flat():
+    from shuffle_exchange_amd.ops.optim import FusedAdam
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(s, device="cuda")) for s in (17, 4096, 70001, 3)]
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    for p, r in zip(ps, ref):
+        p.grad = torch.randn_like(p)
+        r.grad = p.grad.clone()
+    opt = FusedAdam(ps, lr=1e-2, weight_decay=0.01)
+    ropt = torch.optim.AdamW(ref, lr=1e-2, weight_decay=0.01)
+    for _ in range(3):
+        opt.step()
+        ropt.step()
+    for p, r in zip(ps, ref):
+        assert _rel(p, r) < 1e-5
+
+
+@pytest.mark.parametrize("H", [128, 1000, 4096, 8192])
+@pytest.mark.parametrize("residual", [False, True])
+def test_rmsnorm(H, residual):
+    from shuffle_exchange_amd.ops.norm import rms_norm
+    H = H - H % 8
+    x = torch.randn(37, 5, H, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn_like(x, requires_grad=True) if residual else None
+    w = (torch.rand(H, device="cuda") + 0.5).to(torch.bfloat16).requires_grad_()
+    out = rms_norm(x, w, 1e-5, residual=r)
+    y, h = (out if residual else (out, None))
+    xf = x.float() + (r.float() if residual else 0)
+    yr = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn_like(y)
+    loss = (y.float() * dy.float()).sum() + ((h.float() * 0.5).sum() if residual else 0)
+    loss.backward()
+    x2 = x.detach().float().requires_grad_()
+    r2 = r.detach().float().requires_grad_() if residual else None
+    w2 = w.detach().float().requires_grad_()
+    xf2 = x2 + (r2 if residual else 0)
+    y2 = xf2 * torch.rsqrt(xf2.pow(2).mean(-1, keepdim=True) + 1e-5) * w2
+    l2 = (y2 * dy.float()).sum() + ((xf2 * 0.5).sum() if residual else 0)
+    l2.backward()
+    assert _rel(x.grad, x2.grad) < 2e-2
+    assert _rel(w.grad, w2.grad) < 2e-2
+    if residual:
+        assert _rel(r.grad, r2.grad) < 2e-2
+
+
+@pytest.mark.parametrize("H", [768, 1024])
+def test_layernorm(H):
+    from shuffle_exchange_amd.ops.norm import layer_norm
+    x = torch.randn(64, H, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.rand(H, device="cuda") + 0.5).to(torch.bfloat16).requires_grad_()
+    b = torch.randn(H, device="cuda").to(torch.bfloat16).requires_grad_()
+    y = layer_norm(x, w, b, 1e-5)
+    x2, w2, b2 = (t.detach().float().requires_grad_() for t in (x, w, b))
+    y2 = F.layer_norm(x2, (H,), w2, b2, 1e-5)
+    assert _rel(y, y2) < 1e-2
+    dy = torch.randn_like(y2)
+    (y.float() * dy).sum().backward()
+    (y2 * dy).sum().backward()
+    for a, c in ((x, x2), (w, w2), (b, b2)):
+        assert _rel(a.grad, c.grad) < 2e-2
+
+
+def test_rope_qkv_roundtrip():
+    from shuffle_exchange_amd.ops.rope import RopeCache, _ref_rope, apply_rope_qkv_
+    B, S, Hq, Hk, D = 2, 64, 8, 2, 128
+    cache = RopeCache(D, 256, 500000.0, device="cuda")
+    qkv = torch.randn(B, S, Hq + 2 * Hk, D, device="cuda", dtype=torch.bfloat16)
+    ref = qkv.clone().float()
+    pos = torch.arange(S, device="cuda").repeat(B)
+    rot = _ref_rope(ref[:, :, :Hq + Hk].reshape(B * S, Hq + Hk, D), cache.cos, cache.sin, pos).view(B, S, Hq + Hk, D)
+    x = qkv.clone().requires_grad_()
+    out = apply_rope_qkv_(x.clone(), cache, Hq + Hk)
+    assert _rel(out[:, :, :Hq + Hk], rot) < 1e-2
+    assert torch.equal(out[:, :, Hq + Hk:], qkv[:, :, Hq + Hk:])
+    g = torch.randn_like(out)
+    out.backward(g)
+    # backward of an orthogonal rotation = inverse rotation of the gradient
+    gi = _ref_rope(g[:, :, :Hq + Hk].float().reshape(B * S, Hq + Hk, D), cache.cos, -cache.sin, pos)
+    assert _rel(x.grad[:, :, :Hq + Hk].reshape(B * S, Hq + Hk, D), gi) < 1e-2
+
+
+def test_swiglu():
+    from shuffle_exchange_amd.ops.activation import swiglu
+    gu = torch.randn(33, 2 * 1024, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    y = swiglu(gu)
+    gu2 = gu.detach().float().requires_grad_()
+    g, u = gu2.chunk(2, -1)
+    y2 = F.silu(g) * u
+    assert _rel(y, y2) < 1e-2
+    d = torch.randn_like(y2)
+    (y.float() * d).sum().backward()
+    (y2 * d).sum().backward()
+    assert _rel(gu.grad, gu2.grad) < 2e-2
+
+
+def test_bias_gelu():
+    from shuffle_exchange_amd.ops.activation import bias_gelu
+    x = torch.randn(65, 3072, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    b = torch.randn(3072, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    y = bias_gelu(x, b)
+    x2, b2 = x.detach().float().requires_grad_(), b.detach().float().requires_grad_()
+    y2 = F.gelu(x2 + b2, approximate="tanh")
+    assert _rel(y, y2) < 1e-2
+    d = torch.randn_like(y2)
+    (y.float() * d).sum().backward()
+    (y2 * d).sum().backward()
+    assert _rel(x.grad, x2.grad) < 2e-2 and _rel(b.grad, b2.grad) < 2e-2
+
+
+@pytest.mark.parametrize("V", [50257, 128256])
+def test_cross_entropy(V):
+    from shuffle_exchange_amd.ops.cross_entropy import cross_entropy
+    logits = (torch.randn(67, V, device="cuda") * 3).to(torch.bfloat16).requires_grad_()
+    tgt = torch.randint(0, V, (67,), device="cuda")
+    tgt[5] = -100
+    loss = cross_entropy(logits, tgt)
+    l2 = logits.detach().float().requires_grad_()
+    ref = F.cross_entropy(l2, tgt, ignore_index=-100)
+    assert abs(loss.item() - ref.item()) < 1e-2 * abs(ref.item())
+    loss.backward()
+    ref.backward()
+    assert _rel(logits.grad, l2.grad) < 2e-2
+
+
+def test_fused_linear_cross_entropy():
+    from shuffle_exchange_amd.ops.cross_entropy import fused_linear_cross_entropy
+    T, H, V = 300, 256, 4096
+    h = (torch.randn(T, H, device="cuda") * 0.5).to(torch.bfloat16).requires_grad_()
+    W = (torch.randn(V, H, device="cuda") * 0.05).to(torch.bfloat16).requires_grad_()
+    tgt = torch.randint(0, V, (T,), device="cuda")
+    tgt[:7] = -100
+    for chunk in (None, 128):
+        h.grad, W.grad = None, None
+        loss = fused_linear_cross_entropy(h, W, tgt, chunk_tokens=chunk)
+        (loss * 2.0).backward()
+        h2, W2 = h.detach().float().requires_grad_(), W.detach().float().requires_grad_()
+        ref = F.cross_entropy(h2 @ W2.t(), tgt, ignore_index=-100)
+        (ref * 2.0).backward()
+        assert abs(loss.item() - ref.item()) < 1e-2 * abs(ref.item())
+        assert _rel(h.grad, h2.grad) < 3e-2 and _rel(W.grad, W2.grad) < 3e-2
+
+
+def test_sumsq():
+    from shuffle_exchange_amd.ops.optim import sumsq
+    x = torch.randn(3_000_001, device="cuda")
+    assert abs(sumsq(x).item() - x.double().pow(2).sum().item()) < 1e-3 * x.double().pow(2).sum().item()
+    x[7] = float("inf")
+    assert not math.isfinite(sumsq(x).item())
