@@ -65,12 +65,14 @@ def main():
     }
     engine, _, _, _ = sxe.initialize(model=model, config=ds_config)
     n_params = sum(p.numel() for p in model.parameters())
-    g = torch.Generator(device="cpu").manual_seed(rank)
-    batches = [torch.randint(0, cfg.vocab_size, (args.mbs, args.seq), generator=g).to(dev) for _ in range(args.gas)]
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1000 + rank)
 
     def train_step():
         for i in range(args.gas):
-            loss = engine(batches[i], labels=batches[i])
+            # a fresh synthetic batch every micro-step (generated on the device: no H2D in the loop)
+            batch = torch.randint(0, cfg.vocab_size, (args.mbs, args.seq), generator=gen, device=dev)
+            loss = engine(batch, labels=batch)
             engine.backward(loss)
             engine.step()
         return loss

@@ -30,6 +30,7 @@ MI355X-first differences, each a fix or a cost the reference pays per step:
   zero world size (stage_1_and_2.py:179-180).
 """
 import torch
+import torch.distributed as tdist
 
 from ... import comm as dist
 from ...utils.logging import log_dist
@@ -227,16 +228,16 @@ class ShuffleExchange:
                 self.alpha /= 2
                 a = self.alpha.reshape(1).to(dev)
                 peer = self.topo.real(dest)
-                ops.append(dist.P2POp(dist.isend, a, peer))
+                ops.append(dist.P2POp(tdist.isend, a, peer))
                 for t in shards:
-                    ops.append(dist.P2POp(dist.isend, t.contiguous(), peer))
+                    ops.append(dist.P2POp(tdist.isend, t.contiguous(), peer))
             if dest == me:
                 a = torch.empty(1, dtype=torch.float32, device=dev)
                 bufs = [torch.empty_like(t) for t in shards]
                 peer = self.topo.real(sid)
-                ops.append(dist.P2POp(dist.irecv, a, peer))
+                ops.append(dist.P2POp(tdist.irecv, a, peer))
                 for b in bufs:
-                    ops.append(dist.P2POp(dist.irecv, b, peer))
+                    ops.append(dist.P2POp(tdist.irecv, b, peer))
                 recv.append((a, bufs))
         if ops:
             for w in dist.batch_isend_irecv(ops):

@@ -1,0 +1,156 @@
+"""Rank bodies for the multi-process CPU (gloo) tests. Module-level so `spawn` can pickle them."""
+import os
+
+import torch
+
+
+def tiny_llama(seed=0, **kw):
+    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+    torch.manual_seed(seed)
+    cfg = llama_config("llama-tiny", **kw)
+    return LlamaForCausalLM(cfg), cfg
+
+
+def global_batches(cfg, world, mbs, seq, steps, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randint(0, cfg.vocab_size, (world * mbs, seq), generator=g) for _ in range(steps)]
+
+
+def full_params(engine):
+    """Full (gathered) parameters by name, on CPU, fp32."""
+    if engine.zero_optimization_stage() == 3:
+        sd = engine._zero3_consolidated_16bit_state_dict()
+        return {k: v.float() for k, v in sd.items() if k in dict(engine.module.named_parameters())}
+    return {n: p.detach().float().clone() for n, p in engine.module.named_parameters()}
+
+
+def case_train(rank, world, ds_config, steps, mbs, seq, se_kwargs=None, seed=0):
+    import shuffle_exchange_amd as sxe
+    model, cfg = tiny_llama(seed)
+    eng, _, _, _ = sxe.initialize(model=model, config=ds_config, **(se_kwargs or {}))
+    batches = global_batches(cfg, world, mbs, seq, steps)
+    losses = []
+    for b in batches:
+        local = b[rank * mbs:(rank + 1) * mbs]
+        loss = eng(local, labels=local)
+        eng.backward(loss)
+        eng.step()
+        losses.append(float(loss.detach()))
+    return {"params": full_params(eng), "losses": losses}
+
+
+def reference_train(ds_opt, steps, world, mbs, seq, seed=0, clip=0.0):
+    """Single-process reference on the global batch with torch.optim."""
+    model, cfg = tiny_llama(seed)
+    p = ds_opt["params"]
+    if ds_opt["type"].lower() in ("adamw", "adam"):
+        opt = torch.optim.AdamW(model.parameters(), lr=p["lr"], weight_decay=p.get("weight_decay", 0.0),
+                                betas=tuple(p.get("betas", (0.9, 0.999))), eps=p.get("eps", 1e-8))
+    else:
+        opt = torch.optim.SGD(model.parameters(), lr=p["lr"])
+    for b in global_batches(cfg, world, mbs, seq, steps):
+        loss = model(b, labels=b)
+        opt.zero_grad()
+        loss.backward()
+        if clip:
+            torch.nn.utils.clip_grad_norm_(model.parameters(), clip)
+        opt.step()
+    return {n: q.detach().float().clone() for n, q in model.named_parameters()}
+
+
+def case_shuffle_groups(rank, world, slice_count, rings, shuffle_step, calls):
+    import shuffle_exchange_amd as sxe
+    model, cfg = tiny_llama(0)
+    ds = {"train_micro_batch_size_per_gpu": 1, "zero_optimization": {"stage": 2},
+          "optimizer": {"type": "SGD", "params": {"lr": 0.1}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds, method="shuffle", slice_count=slice_count, rings=rings,
+                                  shuffle_step=shuffle_step)
+    hist = [list(eng.optimizer.se.current_groups())]
+    for _ in range(calls):
+        eng.shuffle_exchange()
+        hist.append(list(eng.optimizer.se.current_groups()))
+    return hist
+
+
+def case_gossip(rank, world, steps):
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd import comm
+    model, cfg = tiny_llama(0)
+    ds = {"train_micro_batch_size_per_gpu": 1, "zero_optimization": {"stage": 1},
+          "optimizer": {"type": "SGD", "params": {"lr": 0.05}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds, method="Gossip", slice_count=1)
+    batches = global_batches(cfg, world, 1, 16, steps)
+    for b in batches:
+        local = b[rank:rank + 1]
+        loss = eng(local, labels=local)
+        eng.backward(loss)
+        eng.step()
+    se = eng.optimizer.se
+    # pending (queued) mass counts as well: alpha is conserved over alpha + queued messages
+    mass = float(se.alpha) + sum(float(a) for a, _ in se.queue)
+    t = torch.tensor([mass])
+    comm.all_reduce(t)
+    eng.synchronization()
+    return {"mass": float(t), "params": full_params(eng)}
+
+
+def case_ckpt(rank, world, stage, tmpdir, steps_a, steps_b):
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd import comm
+    ds = {"train_micro_batch_size_per_gpu": 2, "zero_optimization": {"stage": stage},
+          "optimizer": {"type": "AdamW", "params": {"lr": 5e-3}},
+          "scheduler": {"type": "WarmupLR", "params": {"warmup_num_steps": 3, "warmup_max_lr": 5e-3}}}
+    model, cfg = tiny_llama(0)
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    batches = global_batches(cfg, world, 2, 16, steps_a + steps_b)
+
+    def run(e, bs):
+        out = []
+        for b in bs:
+            local = b[rank * 2:(rank + 1) * 2]
+            loss = e(local, labels=local)
+            e.backward(loss)
+            e.step()
+            out.append(float(loss.detach()))
+        return out
+
+    run(eng, batches[:steps_a])
+    eng.save_checkpoint(tmpdir, client_state={"marker": 7})
+    cont = run(eng, batches[steps_a:])
+    model2, _ = tiny_llama(123)  # different init: everything must come from the checkpoint
+    eng2, _, _, _ = sxe.initialize(model=model2, config=ds)
+    path, client = eng2.load_checkpoint(tmpdir)
+    resumed = run(eng2, batches[steps_a:])
+    files = sorted(os.listdir(os.path.join(tmpdir, f"global_step{steps_a}")))
+    return {"cont": cont, "resumed": resumed, "client": client.get("marker"), "files": files,
+            "lr": eng2.get_lr()[0], "lr_ref": eng.get_lr()[0]}
+
+
+def case_collectives(rank, world):
+    from shuffle_exchange_amd import comm
+    comm.enable_fingerprint(True)
+    comm.reset_fingerprint()
+    x = torch.full((8,), float(rank + 1))
+    comm.all_reduce(x)
+    out = torch.empty(world * 4)
+    comm.all_gather_into_tensor(out, torch.full((4,), float(rank)))
+    rs = torch.empty(2)
+    comm.reduce_scatter_tensor(rs, torch.arange(world * 2, dtype=torch.float32))
+    a2a = torch.empty(world)
+    comm.all_to_all_single(a2a, torch.full((world,), float(rank)))
+    ok = comm.verify_fingerprints()
+    return {"ar": x.tolist(), "ag": out.tolist(), "rs": rs.tolist(), "a2a": a2a.tolist(), "fp_ok": ok}
+
+
+def case_fingerprint_mismatch(rank, world):
+    from shuffle_exchange_amd import comm
+    comm.enable_fingerprint(True)
+    comm.reset_fingerprint()
+    x = torch.ones(4 if rank == 0 else 8)
+    from shuffle_exchange_amd.comm import comm as comm_impl
+    comm_impl._fp("all_reduce", None, x)  # record a divergent collective without running it
+    try:
+        comm.verify_fingerprints()
+        return "no-error"
+    except RuntimeError:
+        return "mismatch-detected"
