@@ -1,0 +1,617 @@
+// Flash attention forward + backward for gfx950 (MI355X), bf16 in / fp32 accumulate, head dim 128,
+// causal or full, GQA, arbitrary [B, S, H, D] strides (so the fused QKV projection output is read in
+// place and dq/dk/dv are written straight into one dqkv buffer).
+//
+// Reference users: FPDT's chunked attention with LSE merging (deepspeed/sequence/fpdt_layer.py:134-460),
+// Ulysses local attention (sequence/layer.py:434), the Triton flash kernels of the inference path
+// (ops/transformer/inference/triton/attention.py:263, triton_ops.py:16) and the external
+// flash-attn the FastGen blocked_flash op calls (inference/v2/kernels/ragged_ops/blocked_flash/).
+//
+// CDNA4 design (see /opt/skills/guides/cdna_hip_programming.md §3, §5.5 T2/T10/T12-T14, App. B):
+//  * v_mfma_f32_32x32x16_bf16 everywhere; 64-wide waves; one wave owns 32 query rows (fwd, dQ)
+//    or 32 key rows (dK/dV);
+//  * "swapped" products: the forward computes S^T = K Q^T so one lane holds one query's scores
+//    (softmax max/sum are lane-local + one lane^32 exchange, the rescale is a per-lane scalar),
+//    and S^T is consumed directly as the B operand of O^T += V^T P^T (the accumulator-as-operand
+//    identity of guide §3, with its permuted k order), so P never touches LDS;
+//  * V^T / K^T / Q^T / dO^T operands come from row-major LDS tiles through ds_read_b64_tr_b16
+//    (hardware transpose), with the XOR-swizzled 256-byte-row image that is conflict-free for
+//    both the row reads (ds_read_b128) and the transposed reads (guide T10, image (b));
+//  * K/V (or Q/dO) tiles are register-staged one tile ahead (T14 issue-early/write-late) into a
+//    double-buffered LDS ring: one barrier per tile;
+//  * backward = delta pre-pass + dK/dV kernel (keys on lanes, dK^T/dV^T accumulated in registers
+//    across all GQA query heads: no atomics) + dQ kernel (forward-shaped): deterministic.
+//  * heavy-first block order for the causal triangle.
+#include "sxe_common.h"
+#include <torch/library.h>
+
+namespace sxe {
+namespace fa {
+
+constexpr int D = 128;          // head dim
+constexpr int NW = 4;           // waves per workgroup
+constexpr int QW = 32;          // rows per wave
+constexpr int QB = NW * QW;     // 128 rows per workgroup
+constexpr int KT = 64;          // keys per K/V tile (forward / dQ)
+constexpr int ROWB = D * 2;     // 256 bytes per LDS row
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// Byte offset of 16-byte chunk `ch` (0..15) of row `row` in a swizzled [rows][128 bf16] tile.
+__device__ __forceinline__ int soff(int row, int ch) {
+  return row * ROWB + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__device__ __forceinline__ bf16x8 lds_row16(const char* base, int row, int ch) {
+  return *reinterpret_cast<const bf16x8*>(base + soff(row, ch));
+}
+
+// Transposed read: 4 consecutive rows x one column per lane (ds_read_b64_tr_b16).
+__device__ __forceinline__ i16x4 lds_tr(const char* base, int byte_off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) i16x4*)(const_cast<char*>(base) + byte_off));
+}
+
+// A operand of a 32x32x16 MFMA taken from a row-major [rows][d] LDS tile, transposed:
+// A[m = d][k] with d = 32*dt + (lane&31), k permuted to match an accumulator used as B operand:
+// element j of lane half h <- tile row (row0 + 8*(j>>2) + 4h + (j&3)), column d.
+__device__ __forceinline__ bf16x8 lds_trA(const char* base, int row0, int dt, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, h = g >> 1;
+  const int ch = 4 * dt + 2 * (g & 1) + (p >> 1);
+  const int row = row0 + 4 * h + q;
+  i16x4 lo = lds_tr(base, soff(row, ch) + 8 * (p & 1));
+  i16x4 hi = lds_tr(base, soff(row + 8, ch) + 8 * (p & 1));
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    r[e] = __builtin_bit_cast(__bf16, lo[e]);
+    r[4 + e] = __builtin_bit_cast(__bf16, hi[e]);
+  }
+  return r;
+}
+
+// Accumulator registers 8s..8s+7 -> bf16 B operand (k-step s of the accumulator-as-operand trick).
+__device__ __forceinline__ bf16x8 acc_to_b(const f32x16& a, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = (__bf16)a[8 * s + e];
+  return r;
+}
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// accumulator register i <-> row offset within a 32x32 tile for lane half h
+__device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+struct Strides {
+  int64_t b, s, h;  // element strides; d is unit stride
+};
+
+// Stage a [rows=ROWS][D] tile of 16-byte chunks from global into registers (each of the 256
+// threads owns ROWS*16/256 chunks), then into swizzled LDS.
+template <int ROWS>
+struct Stager {
+  static constexpr int N = ROWS * (D / 8) / (NW * 64);
+  u32x4 r[N];
+  __device__ __forceinline__ void load(const unsigned short* base, int64_t row_stride, int row0, int nrows_valid) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int c = threadIdx.x + i * NW * 64;
+      const int row = c >> 4, ch = c & 15;
+      if (row0 + row < nrows_valid)
+        r[i] = *reinterpret_cast<const u32x4*>(base + (int64_t)(row0 + row) * row_stride + ch * 8);
+      else
+        r[i] = u32x4{0, 0, 0, 0};
+    }
+  }
+  __device__ __forceinline__ void store(char* lds) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int c = threadIdx.x + i * NW * 64;
+      *reinterpret_cast<u32x4*>(lds + soff(c >> 4, c & 15)) = r[i];
+    }
+  }
+};
+
+// Heavy-first mapping of the flat block index onto (b, head, row-block) for the causal triangle.
+__device__ __forceinline__ void map_block(int nblk, int BH, bool heavy_last_index, int& bh, int& blk) {
+  const int idx = blockIdx.x;
+  const int rank = idx / BH;
+  bh = idx - rank * BH;
+  blk = heavy_last_index ? (nblk - 1 - rank) : rank;
+}
+
+// =============================================================================================
+// Forward. Grid: nqb * B * H blocks of 256 threads. q/k/v/o: [B, S, *, D] strided; lse [B, H, S].
+// =============================================================================================
+__global__ void __launch_bounds__(256, 2) fwd_kernel(const unsigned short* __restrict__ q, Strides qs,
+                                                     const unsigned short* __restrict__ k, Strides ks,
+                                                     const unsigned short* __restrict__ v, Strides vs,
+                                                     unsigned short* __restrict__ o, Strides os,
+                                                     float* __restrict__ lse, int B, int H, int Hk, int S,
+                                                     float scale, int causal) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BUF = 2 * KT * ROWB;  // one ring slot = K tile + V tile
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int nqb = S / QB;
+  int bh, qb;
+  map_block(nqb, B * H, causal != 0, bh, qb);
+  const int b = bh / H, head = bh - b * H;
+  const int kh = head / (H / Hk);
+  const int q0 = qb * QB + w * QW;  // this wave's first query
+  const unsigned short* qp = q + b * qs.b + head * qs.h;
+  const unsigned short* kp = k + b * ks.b + kh * ks.h;
+  const unsigned short* vp = v + b * vs.b + kh * vs.h;
+  const float c = scale * LOG2E;
+
+  bf16x8 qf[D / 16];
+#pragma unroll
+  for (int t = 0; t < D / 16; ++t)
+    qf[t] = *reinterpret_cast<const bf16x8*>(qp + (int64_t)(q0 + r) * qs.s + 16 * t + 8 * h);
+
+  f32x16 oacc[D / 32];
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) oacc[t] = zero16();
+  float m = -INFINITY, l = 0.f;
+
+  const int kend = causal ? (qb + 1) * QB : S;  // keys needed by the workgroup
+  const int ntiles = kend / KT;
+  Stager<KT> sk, sv;
+  sk.load(kp, ks.s, 0, S);
+  sv.load(vp, vs.s, 0, S);
+  sk.store(smem);
+  sv.store(smem + KT * ROWB);
+  __syncthreads();
+  int cur = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    const bool more = (t + 1) < ntiles;
+    if (more) {
+      sk.load(kp, ks.s, (t + 1) * KT, S);
+      sv.load(vp, vs.s, (t + 1) * KT, S);
+    }
+    const int kbase = t * KT;
+    // a wave whose queries all precede this tile has nothing to add (causal)
+    const bool active = !causal || kbase <= q0 + QW - 1;
+    if (active) {
+      const char* kt = smem + cur * BUF;
+      f32x16 s[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        s[j] = zero16();
+#pragma unroll
+        for (int t2 = 0; t2 < D / 16; ++t2) s[j] = mfma(lds_row16(kt, 32 * j + r, 2 * t2 + h), qf[t2], s[j]);
+      }
+      const bool diag = causal && (kbase + KT - 1 > q0);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float x = s[j][i] * c;
+          if (diag && (kbase + 32 * j + acc_row(i, h) > q0 + r)) x = -INFINITY;
+          s[j][i] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m, mx);
+      const float mref = (mnew == -INFINITY) ? 0.f : mnew;
+      const float alpha = exp2f(m - mref);
+      float ps = 0.f;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = exp2f(s[j][i] - mref);
+          s[j][i] = p;
+          ps += p;
+        }
+      l = l * alpha + ps;
+      m = mnew;
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+      const char* vt = smem + cur * BUF + KT * ROWB;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 pb = acc_to_b(s[j], s2);
+#pragma unroll
+          for (int dt = 0; dt < D / 32; ++dt) oacc[dt] = mfma(lds_trA(vt, 32 * j + 16 * s2, dt, lane), pb, oacc[dt]);
+        }
+    }
+    if (more) {
+      sk.store(smem + (cur ^ 1) * BUF);
+      sv.store(smem + (cur ^ 1) * BUF + KT * ROWB);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = 1.f / lt;
+  unsigned short* op = o + b * os.b + head * os.h + (int64_t)(q0 + r) * os.s;
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+      u16x4 pk;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pk[e] = f32_to_bf16(oacc[dt][4 * rg + e] * inv);
+      *reinterpret_cast<u16x4*>(op + 32 * dt + 8 * rg + 4 * h) = pk;
+    }
+  if (h == 0) lse[((int64_t)b * H + head) * S + q0 + r] = (m + log2f(lt)) * LN2;
+}
+
+// =============================================================================================
+// Backward pre-pass: delta[b, h, s] = sum_d dO * O  (fp32)
+// =============================================================================================
+__global__ void __launch_bounds__(256) delta_kernel(const unsigned short* __restrict__ dout, Strides ds,
+                                                    const unsigned short* __restrict__ o, Strides os,
+                                                    float* __restrict__ delta, int B, int H, int S) {
+  const int64_t row = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int part = threadIdx.x & 15;
+  if (row >= (int64_t)B * H * S) return;
+  const int s = (int)(row % S);
+  const int64_t bh = row / S;
+  const int hh = (int)(bh % H), b = (int)(bh / H);
+  float x[8], y[8];
+  load8<DT::BF16>(dout + b * ds.b + hh * ds.h + (int64_t)s * ds.s + part * 8, x);
+  load8<DT::BF16>(o + b * os.b + hh * os.h + (int64_t)s * os.s + part * 8, y);
+  float acc = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc += x[e] * y[e];
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
+  if (part == 0) delta[row] = acc;
+}
+
+// =============================================================================================
+// Direct-to-LDS tile loads (global_load_lds_dwordx4): no staging registers. A wave-instruction
+// writes 1 KiB = 4 rows linearly, so the XOR swizzle goes on the per-lane SOURCE chunk (the
+// swizzle is an involution: position c' of row `row` holds logical chunk c' ^ f(row)).
+// =============================================================================================
+__device__ __forceinline__ void glds16(const void* gsrc, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* gsrc, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 4, 0, 0);
+}
+template <int ROWS>
+__device__ __forceinline__ void tile_glds(const unsigned short* base, int64_t row_stride, int row0, char* lds) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < ROWS / 4 / NW; ++i) {
+    const int n = i * NW + w;
+    const int row = 4 * n + (lane >> 4);
+    const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+    glds16(base + (int64_t)(row0 + row) * row_stride + ch * 8, lds + n * 1024);
+  }
+}
+__device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// =============================================================================================
+// dQ: forward-shaped. Per wave 32 queries; per K/V tile recompute S^T, P^T, dP^T = V dO^T,
+// dS^T = P^T (dP^T - delta), dQ^T += K^T dS^T.
+// =============================================================================================
+__global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __restrict__ q, Strides qs,
+                                                    const unsigned short* __restrict__ k, Strides ks,
+                                                    const unsigned short* __restrict__ v, Strides vs,
+                                                    const unsigned short* __restrict__ dout, Strides dos,
+                                                    const float* __restrict__ lse, const float* __restrict__ delta,
+                                                    unsigned short* __restrict__ dq, Strides dqs, int B, int H,
+                                                    int Hk, int S, float scale, int causal) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BUF = 2 * KT * ROWB;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int nqb = S / QB;
+  int bh, qb;
+  map_block(nqb, B * H, causal != 0, bh, qb);
+  const int b = bh / H, head = bh - b * H;
+  const int kh = head / (H / Hk);
+  const int q0 = qb * QB + w * QW;
+  const unsigned short* qp = q + b * qs.b + head * qs.h;
+  const unsigned short* dop = dout + b * dos.b + head * dos.h;
+  const unsigned short* kp = k + b * ks.b + kh * ks.h;
+  const unsigned short* vp = v + b * vs.b + kh * vs.h;
+  const float c = scale * LOG2E;
+  const int64_t lrow = ((int64_t)b * H + head) * S + q0 + r;
+  const int kend = causal ? (qb + 1) * QB : S;
+  const int ntiles = kend / KT;
+  tile_glds<KT>(kp, ks.s, 0, smem);
+  tile_glds<KT>(vp, vs.s, 0, smem + KT * ROWB);
+
+  const float lse2 = lse[lrow] * LOG2E;
+  const float dlt = delta[lrow];
+  bf16x8 qf[D / 16], df[D / 16];
+#pragma unroll
+  for (int t = 0; t < D / 16; ++t) {
+    qf[t] = *reinterpret_cast<const bf16x8*>(qp + (int64_t)(q0 + r) * qs.s + 16 * t + 8 * h);
+    df[t] = *reinterpret_cast<const bf16x8*>(dop + (int64_t)(q0 + r) * dos.s + 16 * t + 8 * h);
+  }
+  f32x16 dqacc[D / 32];
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) dqacc[t] = zero16();
+  vm_wait_all();
+  __syncthreads();
+  int cur = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) {
+      tile_glds<KT>(kp, ks.s, (t + 1) * KT, smem + (cur ^ 1) * BUF);
+      tile_glds<KT>(vp, vs.s, (t + 1) * KT, smem + (cur ^ 1) * BUF + KT * ROWB);
+    }
+    const int kbase = t * KT;
+    const bool active = !causal || kbase <= q0 + QW - 1;
+    if (active) {
+      const char* kt = smem + cur * BUF;
+      const char* vt = smem + cur * BUF + KT * ROWB;
+      const bool diag = causal && (kbase + KT - 1 > q0);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+        for (int t2 = 0; t2 < D / 16; ++t2) {
+          s = mfma(lds_row16(kt, 32 * j + r, 2 * t2 + h), qf[t2], s);
+          dp = mfma(lds_row16(vt, 32 * j + r, 2 * t2 + h), df[t2], dp);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float p = exp2f(s[i] * c - lse2);
+          if (diag && (kbase + 32 * j + acc_row(i, h) > q0 + r)) p = 0.f;
+          s[i] = p * (dp[i] - dlt);  // dS^T
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 db = acc_to_b(s, s2);
+#pragma unroll
+          for (int dt = 0; dt < D / 32; ++dt) dqacc[dt] = mfma(lds_trA(kt, 32 * j + 16 * s2, dt, lane), db, dqacc[dt]);
+        }
+      }
+    }
+    vm_wait_all();
+    __syncthreads();
+    cur ^= 1;
+  }
+  unsigned short* op = dq + b * dqs.b + head * dqs.h + (int64_t)(q0 + r) * dqs.s;
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+      u16x4 pk;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pk[e] = f32_to_bf16(dqacc[dt][4 * rg + e] * scale);
+      *reinterpret_cast<u16x4*>(op + 32 * dt + 8 * rg + 4 * h) = pk;
+    }
+}
+
+// =============================================================================================
+// dK, dV: per wave 32 keys held on the lanes; sweep every query head of the GQA group and every
+// 32-query tile at or after the keys (causal). Q/dO tiles + LSE/delta arrive by LDS-DMA into a
+// 2-slot ring; the workgroup's V block (128 keys) sits in LDS for the whole kernel; K fragments,
+// dK^T and dV^T live in registers.
+// =============================================================================================
+constexpr int QT = 32;  // queries per tile in the dK/dV sweep
+constexpr int KV_TILE = QT * ROWB;                 // 8 KiB
+constexpr int KV_SLOT = 2 * KV_TILE + 2 * QT * 4;  // Q, dO, lse[32], delta[32]
+constexpr int KV_VBLK = QB * ROWB;                 // 32 KiB
+
+__global__ void __launch_bounds__(256, 2) dkdv_kernel(const unsigned short* __restrict__ q, Strides qs,
+                                                      const unsigned short* __restrict__ k, Strides ks,
+                                                      const unsigned short* __restrict__ v, Strides vs,
+                                                      const unsigned short* __restrict__ dout, Strides dos,
+                                                      const float* __restrict__ lse, const float* __restrict__ delta,
+                                                      unsigned short* __restrict__ dk, Strides dks,
+                                                      unsigned short* __restrict__ dv, Strides dvs, int B, int H,
+                                                      int Hk, int S, float scale, int causal) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* vblk = smem;
+  char* ring = smem + KV_VBLK;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int nkb = S / QB;
+  int bh, kb;
+  map_block(nkb, B * Hk, false, bh, kb);  // key block 0 is the heaviest under causality
+  const int b = bh / Hk, kh = bh - b * Hk;
+  const int G = H / Hk;
+  const int k0 = kb * QB + w * QW;  // this wave's first key
+  const unsigned short* kp = k + b * ks.b + kh * ks.h;
+  const unsigned short* vp = v + b * vs.b + kh * vs.h;
+  const float c = scale * LOG2E;
+  const int qstart = causal ? kb * QB : 0;
+  const int ntq = (S - qstart) / QT;
+  const int total = ntq * G;
+
+  auto issue = [&](int it, char* slot) {
+    const int hq = kh * G + it / ntq;
+    const int qt0 = qstart + (it % ntq) * QT;
+    tile_glds<QT>(q + b * qs.b + hq * qs.h, qs.s, qt0, slot);
+    tile_glds<QT>(dout + b * dos.b + hq * dos.h, dos.s, qt0, slot + KV_TILE);
+    if (w == 0) {  // 64 lanes x 4 B: lse[32] then delta[32]
+      const int64_t lr = ((int64_t)b * H + hq) * S + qt0 + (lane & 31);
+      glds4(lane < 32 ? (const void*)(lse + lr) : (const void*)(delta + lr), slot + 2 * KV_TILE);
+    }
+  };
+  tile_glds<QB>(vp, vs.s, kb * QB, vblk);
+  issue(0, ring);
+  bf16x8 kf[D / 16];
+#pragma unroll
+  for (int t = 0; t < D / 16; ++t)
+    kf[t] = *reinterpret_cast<const bf16x8*>(kp + (int64_t)(k0 + r) * ks.s + 16 * t + 8 * h);
+  f32x16 dka[D / 32], dva[D / 32];
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t) {
+    dka[t] = zero16();
+    dva[t] = zero16();
+  }
+  vm_wait_all();
+  __syncthreads();
+  int cur = 0;
+  for (int it = 0; it < total; ++it) {
+    if (it + 1 < total) issue(it + 1, ring + (cur ^ 1) * KV_SLOT);
+    const int qt0 = qstart + (it % ntq) * QT;
+    const bool active = !causal || (qt0 + QT - 1 >= k0);
+    if (active) {
+      const char* slot = ring + cur * KV_SLOT;
+      const char* qt = slot;
+      const char* dt_ = slot + KV_TILE;
+      const float* l2 = reinterpret_cast<const float*>(slot + 2 * KV_TILE);
+      const float* dl = l2 + QT;
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int t2 = 0; t2 < D / 16; ++t2) {
+        s = mfma(lds_row16(qt, r, 2 * t2 + h), kf[t2], s);                         // S  [query][key]
+        dp = mfma(lds_row16(dt_, r, 2 * t2 + h), lds_row16(vblk, w * QW + r, 2 * t2 + h), dp);  // dP
+      }
+      const bool diag = causal && (qt0 < k0 + QW);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qi = acc_row(i, h);
+        float p = exp2f(s[i] * c - l2[qi] * LOG2E);
+        if (diag && (k0 + r > qt0 + qi)) p = 0.f;
+        s[i] = p;                      // P
+        dp[i] = p * (dp[i] - dl[qi]);  // dS
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pb = acc_to_b(s, s2);
+        const bf16x8 db = acc_to_b(dp, s2);
+#pragma unroll
+        for (int t = 0; t < D / 32; ++t) {
+          dva[t] = mfma(lds_trA(dt_, 16 * s2, t, lane), pb, dva[t]);  // dV^T += dO^T P
+          dka[t] = mfma(lds_trA(qt, 16 * s2, t, lane), db, dka[t]);   // dK^T += Q^T dS
+        }
+      }
+    }
+    vm_wait_all();
+    __syncthreads();
+    cur ^= 1;
+  }
+  unsigned short* kop = dk + b * dks.b + kh * dks.h + (int64_t)(k0 + r) * dks.s;
+  unsigned short* vop = dv + b * dvs.b + kh * dvs.h + (int64_t)(k0 + r) * dvs.s;
+#pragma unroll
+  for (int t = 0; t < D / 32; ++t)
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+      u16x4 pk, pv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        pk[e] = f32_to_bf16(dka[t][4 * rg + e] * scale);
+        pv[e] = f32_to_bf16(dva[t][4 * rg + e]);
+      }
+      *reinterpret_cast<u16x4*>(kop + 32 * t + 8 * rg + 4 * h) = pk;
+      *reinterpret_cast<u16x4*>(vop + 32 * t + 8 * rg + 4 * h) = pv;
+    }
+}
+
+
+}  // namespace fa
+
+// ---------------------------------------------------------------------------------------------
+static fa::Strides strides_of(const at::Tensor& t) {
+  return fa::Strides{t.stride(0), t.stride(1), t.stride(2)};
+}
+
+static void check_qkv(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
+  SXE_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "flash_attn: tensors must be [B, S, H, D]");
+  SXE_CHECK(q.scalar_type() == at::kBFloat16 && k.scalar_type() == at::kBFloat16 && v.scalar_type() == at::kBFloat16,
+            "flash_attn: bf16 only");
+  SXE_CHECK(q.size(3) == fa::D && k.size(3) == fa::D && v.size(3) == fa::D, "flash_attn: head dim must be 128");
+  SXE_CHECK(q.stride(3) == 1 && k.stride(3) == 1 && v.stride(3) == 1, "flash_attn: unit stride on D");
+  SXE_CHECK(k.sizes() == v.sizes() && q.size(0) == k.size(0) && q.size(1) == k.size(1), "flash_attn: q/k/v shapes");
+  SXE_CHECK(q.size(2) % k.size(2) == 0, "flash_attn: Hq must be a multiple of Hkv");
+  SXE_CHECK(q.size(1) % fa::QB == 0, "flash_attn: seq_len must be a multiple of 128");
+  for (const at::Tensor* t : {&q, &k, &v})
+    SXE_CHECK((t->stride(1) % 8) == 0 && (t->stride(2) % 8) == 0 && (t->stride(0) % 8) == 0 &&
+                  (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "flash_attn: 16-byte aligned rows required");
+}
+
+std::vector<at::Tensor> flash_attn_fwd(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, double scale) {
+  check_qkv(q, k, v);
+  const int B = q.size(0), S = q.size(1), H = q.size(2), Hk = k.size(2);
+  c10::DeviceGuard guard(q.device());
+  auto o = at::empty({B, S, H, fa::D}, q.options());
+  auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  const int grid = (S / fa::QB) * B * H;
+  const size_t lds = 4 * fa::KT * fa::ROWB;
+  hipLaunchKernelGGL(fa::fwd_kernel, dim3(grid), dim3(256), lds, cur_stream(),
+                     reinterpret_cast<const unsigned short*>(q.data_ptr()), strides_of(q),
+                     reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
+                     reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),
+                     reinterpret_cast<unsigned short*>(o.data_ptr()), strides_of(o), lse.data_ptr<float>(), B, H, Hk,
+                     S, (float)scale, causal ? 1 : 0);
+  SXE_LAUNCH_CHECK();
+  return {o, lse};
+}
+
+// dq/dk/dv are caller-provided (possibly strided views of one dqkv buffer).
+void flash_attn_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
+                    at::Tensor dq, at::Tensor dk, at::Tensor dv, bool causal, double scale) {
+  check_qkv(q, k, v);
+  check_qkv(dq, dk, dv);
+  SXE_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && dout.stride(3) == 1 && o.stride(3) == 1,
+            "flash_attn_bwd: dout/o shapes");
+  SXE_CHECK(dq.sizes() == q.sizes() && dk.sizes() == k.sizes() && dv.sizes() == v.sizes(), "flash_attn_bwd: grad shapes");
+  const int B = q.size(0), S = q.size(1), H = q.size(2), Hk = k.size(2);
+  c10::DeviceGuard guard(q.device());
+  auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  const int64_t rows = (int64_t)B * H * S;
+  hipLaunchKernelGGL(fa::delta_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(),
+                     reinterpret_cast<const unsigned short*>(dout.data_ptr()), strides_of(dout),
+                     reinterpret_cast<const unsigned short*>(o.data_ptr()), strides_of(o), delta.data_ptr<float>(), B,
+                     H, S);
+  SXE_LAUNCH_CHECK();
+  const size_t lds_dq = 4 * fa::KT * fa::ROWB;
+  hipLaunchKernelGGL(fa::dq_kernel, dim3((S / fa::QB) * B * H), dim3(256), lds_dq, cur_stream(),
+                     reinterpret_cast<const unsigned short*>(q.data_ptr()), strides_of(q),
+                     reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
+                     reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),
+                     reinterpret_cast<const unsigned short*>(dout.data_ptr()), strides_of(dout),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(),
+                     reinterpret_cast<unsigned short*>(dq.data_ptr()), strides_of(dq), B, H, Hk, S, (float)scale,
+                     causal ? 1 : 0);
+  SXE_LAUNCH_CHECK();
+  const size_t lds_kv = fa::KV_VBLK + 2 * fa::KV_SLOT;
+  static bool attr_set = false;
+  if (!attr_set) {  // > 64 KiB of dynamic LDS must be opted into (gfx950 has 160 KiB per CU)
+    SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::dkdv_kernel),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(fa::dkdv_kernel, dim3((S / fa::QB) * B * Hk), dim3(256), lds_kv, cur_stream(),
+                     reinterpret_cast<const unsigned short*>(q.data_ptr()), strides_of(q),
+                     reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
+                     reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),
+                     reinterpret_cast<const unsigned short*>(dout.data_ptr()), strides_of(dout),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(),
+                     reinterpret_cast<unsigned short*>(dk.data_ptr()), strides_of(dk),
+                     reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv), B, H, Hk, S, (float)scale,
+                     causal ? 1 : 0);
+  SXE_LAUNCH_CHECK();
+}
+
+}  // namespace sxe
+
+TORCH_LIBRARY_FRAGMENT(sxe, m) {
+  m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> Tensor[]");
+  m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, "
+        "Tensor(c!) dv, bool causal, float scale) -> ()");
+}
+TORCH_LIBRARY_IMPL(sxe, CUDA, m) {
+  m.impl("flash_attn_fwd", &sxe::flash_attn_fwd);
+  m.impl("flash_attn_bwd", &sxe::flash_attn_bwd);
+}

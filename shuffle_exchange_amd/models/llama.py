@@ -23,10 +23,10 @@ import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
 from ..ops.activation import swiglu
-from ..ops.attention import attention
+from ..ops.attention import attention_qkv_rope
 from ..ops.cross_entropy import fused_linear_cross_entropy
 from ..ops.norm import RMSNorm
-from ..ops.rope import RopeCache, apply_rope_qkv_
+from ..ops.rope import RopeCache
 
 
 @dataclass
@@ -96,11 +96,7 @@ class LlamaAttention(nn.Module):
     def forward(self, x, rope: RopeCache, position_ids=None):
         B, S, _ = x.shape
         qkv = F.linear(x, self.qkv_proj.weight).view(B, S, self.nq + 2 * self.nkv, self.d)
-        qkv = apply_rope_qkv_(qkv, rope, self.nq + self.nkv, position_ids)
-        q = qkv[:, :, :self.nq]
-        k = qkv[:, :, self.nq:self.nq + self.nkv]
-        v = qkv[:, :, self.nq + self.nkv:]
-        o = attention(q, k, v, causal=True)
+        o = attention_qkv_rope(qkv, self.nq, self.nkv, rope, position_ids, causal=True)
         return F.linear(o.reshape(B, S, self.nq * self.d), self.o_proj.weight)
 
 

@@ -3,10 +3,16 @@ QKV / output projections).
 
 Backends:
 * ``hip``  -- this repo's gfx950 flash-attention kernels (csrc/kernels/flash_attn.hip): MFMA bf16,
-  online softmax, LSE output for backward / FPDT chunk merging;
-* ``sdpa`` -- ``torch.nn.functional.scaled_dot_product_attention`` (the stopgap SURVEY §7.2 step 4
-  allows until the HIP kernel covers a shape; always used on CPU).
-Selection: ``SXE_ATTN_BACKEND`` env (hip|sdpa), else hip when the kernel supports the shape.
+  online softmax, LSE output; deterministic backward (dK/dV kernel + dQ kernel, no atomics);
+* ``sdpa`` -- ``torch.nn.functional.scaled_dot_product_attention``: used on CPU (plumbing tests) and
+  for shapes the HIP kernel does not cover (head dim != 128, seq % 128 != 0); on GPU this is
+  logged once so a silent fallback cannot hide in a benchmark.
+``SXE_ATTN_BACKEND=sdpa`` forces the stopgap for A/B comparisons.
+
+``attention_qkv_rope`` is the training entry point of the Llama family: it takes the fused QKV
+projection output [B, S, Hq + 2*Hkv, D], applies RoPE in place, runs attention reading q/k/v as
+strided views, and in backward writes dq/dk/dv straight into ONE dqkv buffer (then rotates the
+dq/dk slices back in place) -- no per-view gradient scatter, no transposes, no clones.
 """
 import math
 import os
@@ -19,7 +25,6 @@ from ..utils.logging import warning_once
 
 
 def _sdpa(q, k, v, causal, scale):
-    # [B,S,H,D] -> [B,H,S,D] views; SDPA handles GQA via enable_gqa
     qt, kt, vt = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
     gqa = qt.shape[1] != kt.shape[1]
     if gqa and not q.is_cuda:
@@ -31,10 +36,11 @@ def _sdpa(q, k, v, causal, scale):
     return o.transpose(1, 2)
 
 
-def _hip_supported(q, k, v):
-    D = q.shape[-1]
-    return (q.is_cuda and q.dtype == torch.bfloat16 and D in (64, 128) and q.shape[2] % k.shape[2] == 0
-            and hasattr(torch.ops.sxe, "flash_attn_fwd"))
+def hip_supported(q, k, v):
+    if os.environ.get("SXE_ATTN_BACKEND") == "sdpa":
+        return False
+    return (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] == 128 and q.shape[1] % 128 == 0
+            and q.shape[2] % k.shape[2] == 0 and q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1)
 
 
 class _FlashAttn(torch.autograd.Function):
@@ -48,27 +54,84 @@ class _FlashAttn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lse = ctx.saved_tensors
-        dq, dk, dv = torch.ops.sxe.flash_attn_bwd(do.contiguous(), q, k, v, o, lse, bool(ctx.causal), float(ctx.scale))
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        torch.ops.sxe.flash_attn_bwd(do.contiguous(), q, k, v, o, lse, dq, dk, dv, bool(ctx.causal),
+                                     float(ctx.scale))
         return dq, dk, dv, None, None
 
 
-def attention(q, k, v, causal=True, softmax_scale=None, backend=None):
+def attention(q, k, v, causal=True, softmax_scale=None):
     """q: [B, S, Hq, D], k/v: [B, S, Hkv, D] (strided views allowed) -> [B, S, Hq, D]."""
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1])
-    backend = backend or os.environ.get("SXE_ATTN_BACKEND")
-    if q.is_cuda and backend != "sdpa":
+    if q.is_cuda:
         native.require_hip()
-        if _hip_supported(q, k, v):
+        if hip_supported(q, k, v):
             return _FlashAttn.apply(q, k, v, causal, scale)
-        warning_once(f"sxe attention: HIP kernel does not cover dtype={q.dtype} D={q.shape[-1]}; using SDPA")
+        warning_once(f"sxe attention: HIP flash kernel does not cover dtype={q.dtype} D={q.shape[-1]} "
+                     f"S={q.shape[1]}; using SDPA")
+    return _sdpa(q, k, v, causal, scale)
+
+
+class _FlashAttnQKVRope(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, nq, nkv, causal, scale, pos):
+        B, S = qkv.shape[0], qkv.shape[1]
+        if cos is not None:
+            torch.ops.sxe.rope_(qkv[:, :, :nq + nkv], cos, sin, pos, S, 0, False)
+        q, k, v = qkv[:, :, :nq], qkv[:, :, nq:nq + nkv], qkv[:, :, nq + nkv:]
+        o, lse = torch.ops.sxe.flash_attn_fwd(q, k, v, bool(causal), float(scale))
+        ctx.mark_dirty(qkv)
+        ctx.save_for_backward(qkv, o, lse, cos, sin, pos)
+        ctx.meta = (nq, nkv, causal, scale)
+        # qkv is returned too (it was modified in place) so autograd can track the dirty tensor
+        return o, qkv
+
+    @staticmethod
+    def backward(ctx, do, _dqkv_unused):
+        qkv, o, lse, cos, sin, pos = ctx.saved_tensors
+        nq, nkv, causal, scale = ctx.meta
+        dqkv = torch.empty_like(qkv)
+        q, k, v = qkv[:, :, :nq], qkv[:, :, nq:nq + nkv], qkv[:, :, nq + nkv:]
+        dq, dk, dv = dqkv[:, :, :nq], dqkv[:, :, nq:nq + nkv], dqkv[:, :, nq + nkv:]
+        torch.ops.sxe.flash_attn_bwd(do.contiguous(), q, k, v, o, lse, dq, dk, dv, bool(causal), float(scale))
+        if cos is not None:
+            torch.ops.sxe.rope_(dqkv[:, :, :nq + nkv], cos, sin, pos, qkv.shape[1], 0, True)
+        return dqkv, None, None, None, None, None, None, None
+
+
+def attention_qkv_rope(qkv, nq, nkv, rope=None, position_ids=None, causal=True, softmax_scale=None):
+    """qkv: [B, S, nq + 2*nkv, D] fused projection output. Returns o [B, S, nq, D]."""
+    D = qkv.shape[-1]
+    scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(D)
+    q, k, v = qkv[:, :, :nq], qkv[:, :, nq:nq + nkv], qkv[:, :, nq + nkv:]
+    if qkv.is_cuda:
+        native.require_hip()
+        if hip_supported(q, k, v):
+            pos = position_ids.reshape(-1).contiguous().long() if position_ids is not None else None
+            cos = rope.cos if rope is not None else None
+            sin = rope.sin if rope is not None else None
+            o, _ = _FlashAttnQKVRope.apply(qkv, cos, sin, nq, nkv, causal, scale, pos)
+            return o
+        warning_once(f"sxe attention: HIP flash kernel does not cover dtype={qkv.dtype} D={D} S={qkv.shape[1]}; "
+                     f"using RoPE kernel + SDPA")
+    if rope is not None:
+        from .rope import apply_rope_qkv_
+        qkv = apply_rope_qkv_(qkv, rope, nq + nkv, position_ids)
+    q, k, v = qkv[:, :, :nq], qkv[:, :, nq:nq + nkv], qkv[:, :, nq + nkv:]
     return _sdpa(q, k, v, causal, scale)
 
 
 def attention_with_lse(q, k, v, causal=True, softmax_scale=None):
-    """Forward-only attention returning (out, lse[B, H, S]) for chunk merging (FPDT)."""
+    """Forward-only attention returning (out [B,S,H,D], lse [B,H,S]) for chunk merging (FPDT)."""
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1])
-    if q.is_cuda and _hip_supported(q, k, v):
+    if q.is_cuda and hip_supported(q, k, v) and q.shape[1] == k.shape[1]:
         return torch.ops.sxe.flash_attn_fwd(q, k, v, bool(causal), float(scale))
+    return reference_attention(q, k, v, causal, scale, return_lse=True)
+
+
+def reference_attention(q, k, v, causal=True, scale=None, return_lse=False):
+    """fp32 eager oracle used by the tests (and the CPU path of attention_with_lse)."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
     qt, kt, vt = q.transpose(1, 2).float(), k.transpose(1, 2).float(), v.transpose(1, 2).float()
     if kt.shape[1] != qt.shape[1]:
         rep = qt.shape[1] // kt.shape[1]
@@ -79,5 +142,5 @@ def attention_with_lse(q, k, v, causal=True, softmax_scale=None):
         mask = torch.ones(S, T, dtype=torch.bool, device=s.device).tril(T - S)
         s = s.masked_fill(~mask, float("-inf"))
     lse = torch.logsumexp(s, dim=-1)
-    o = torch.matmul(torch.softmax(s, dim=-1), vt)
-    return o.transpose(1, 2).to(q.dtype), lse
+    o = torch.matmul(torch.softmax(s, dim=-1), vt).transpose(1, 2).to(q.dtype)
+    return (o, lse) if return_lse else o

@@ -1,0 +1,100 @@
+"""gfx950 flash attention (fwd + bwd) vs an fp32 PyTorch reference: causal / full, MHA / GQA,
+packed-QKV strided inputs with fused RoPE."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    from shuffle_exchange_amd.ops import native
+    native.require_hip()
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("B,S,H,Hk", [(2, 256, 4, 4), (1, 384, 8, 2), (2, 128, 4, 1)])
+def test_flash_fwd_bwd(causal, B, S, H, Hk):
+    from shuffle_exchange_amd.ops.attention import attention, reference_attention
+    torch.manual_seed(0)
+    D = 128
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    o = attention(q, k, v, causal=causal)
+    q2, k2, v2 = (t.detach().float().requires_grad_() for t in (q, k, v))
+    o2 = reference_attention(q2, k2, v2, causal=causal)
+    assert _rel(o, o2) < 1e-2
+    do = torch.randn_like(o2)
+    (o.float() * do).sum().backward()
+    (o2 * do).sum().backward()
+    assert _rel(q.grad, q2.grad) < 2e-2
+    assert _rel(k.grad, k2.grad) < 2e-2
+    assert _rel(v.grad, v2.grad) < 2e-2
+
+
+def test_flash_lse():
+    from shuffle_exchange_amd.ops.attention import attention_with_lse, reference_attention
+    q = torch.randn(1, 256, 2, 128, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(1, 256, 2, 128, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(1, 256, 2, 128, device="cuda", dtype=torch.bfloat16)
+    o, lse = attention_with_lse(q, k, v, causal=True)
+    o2, lse2 = reference_attention(q.float(), k.float(), v.float(), causal=True, return_lse=True)
+    assert _rel(o, o2) < 1e-2
+    assert (lse - lse2).abs().max().item() < 1e-2
+
+
+def test_packed_qkv_rope():
+    from shuffle_exchange_amd.ops.attention import attention_qkv_rope, reference_attention
+    from shuffle_exchange_amd.ops.rope import RopeCache, _ref_rope
+    torch.manual_seed(1)
+    B, S, nq, nkv, D = 2, 256, 8, 2, 128
+    cache = RopeCache(D, 512, 500000.0, device="cuda")
+    base = torch.randn(B, S, (nq + 2 * nkv) * D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    qkv = base.view(B, S, nq + 2 * nkv, D) * 1.0
+    o = attention_qkv_rope(qkv, nq, nkv, cache)
+    ref_in = base.detach().float().view(B, S, nq + 2 * nkv, D).requires_grad_()
+    pos = torch.arange(S, device="cuda").repeat(B)
+    rot = _ref_rope(ref_in[:, :, :nq + nkv].reshape(B * S, nq + nkv, D), cache.cos, cache.sin, pos).view(B, S, nq + nkv, D)
+    q2, k2, v2 = rot[:, :, :nq], rot[:, :, nq:], ref_in[:, :, nq + nkv:]
+    o2 = reference_attention(q2, k2, v2, causal=True)
+    assert _rel(o, o2) < 1e-2
+    do = torch.randn_like(o2)
+    (o.float() * do).sum().backward()
+    (o2 * do).sum().backward()
+    assert _rel(base.grad.view_as(ref_in), ref_in.grad) < 2e-2
+
+
+@pytest.mark.slow
+def test_flash_perf_report():
+    """Not a pass/fail perf gate: prints TFLOP/s of fwd and fwd+bwd at the Llama-3-8B shape."""
+    from shuffle_exchange_amd.ops.attention import attention
+    B, S, H, Hk, D = 4, 2048, 32, 8, 128
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    flops = 4 * B * H * S * S * D / 2
+    for _ in range(3):
+        o = attention(q, k, v)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        o = attention(q, k, v)
+    e1.record()
+    torch.cuda.synchronize()
+    tf = flops / (e0.elapsed_time(e1) / 10 / 1e3) / 1e12
+    g = torch.randn_like(o)
+    e0.record()
+    for _ in range(10):
+        torch.autograd.grad(attention(q, k, v), (q, k, v), g)
+    e1.record()
+    torch.cuda.synchronize()
+    tfb = 3.5 * flops / (e0.elapsed_time(e1) / 10 / 1e3) / 1e12
+    print(f"\n[flash] fwd {tf:.0f} TFLOP/s, fwd+bwd {tfb:.0f} TFLOP/s (model FLOPs, 3.5x fwd)")
