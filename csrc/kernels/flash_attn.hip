@@ -39,6 +39,7 @@ constexpr float LN2 = 0.6931471805599453f;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
@@ -66,13 +67,9 @@ __device__ __forceinline__ bf16x8 lds_trA(const char* base, int row0, int dt, in
   const int row = row0 + 4 * h + q;
   i16x4 lo = lds_tr(base, soff(row, ch) + 8 * (p & 1));
   i16x4 hi = lds_tr(base, soff(row + 8, ch) + 8 * (p & 1));
-  bf16x8 r;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    r[e] = __builtin_bit_cast(__bf16, lo[e]);
-    r[4 + e] = __builtin_bit_cast(__bf16, hi[e]);
-  }
-  return r;
+  // whole-vector bitcast: element-wise bf16 inserts from the tr-read result miscompile (hipcc 7.2)
+  const i16x8 c = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, c);
 }
 
 // Accumulator registers 8s..8s+7 -> bf16 B operand (k-step s of the accumulator-as-operand trick).
