@@ -80,14 +80,15 @@ class _FlashAttnQKVRope(torch.autograd.Function):
             torch.ops.sxe.rope_(qkv[:, :, :nq + nkv], cos, sin, pos, S, 0, False)
         q, k, v = qkv[:, :, :nq], qkv[:, :, nq:nq + nkv], qkv[:, :, nq + nkv:]
         o, lse = torch.ops.sxe.flash_attn_fwd(q, k, v, bool(causal), float(scale))
-        ctx.mark_dirty(qkv)
+        # qkv (the fresh QKV-projection output, consumed only here) was rotated in place; it is
+        # saved AFTER the rotation, and no other autograd node holds it, so it is not marked dirty
+        # (a dirty view input would forbid returning it).
         ctx.save_for_backward(qkv, o, lse, cos, sin, pos)
         ctx.meta = (nq, nkv, causal, scale)
-        # qkv is returned too (it was modified in place) so autograd can track the dirty tensor
-        return o, qkv
+        return o
 
     @staticmethod
-    def backward(ctx, do, _dqkv_unused):
+    def backward(ctx, do):
         qkv, o, lse, cos, sin, pos = ctx.saved_tensors
         nq, nkv, causal, scale = ctx.meta
         dqkv = torch.empty_like(qkv)
@@ -110,8 +111,7 @@ def attention_qkv_rope(qkv, nq, nkv, rope=None, position_ids=None, causal=True, 
             pos = position_ids.reshape(-1).contiguous().long() if position_ids is not None else None
             cos = rope.cos if rope is not None else None
             sin = rope.sin if rope is not None else None
-            o, _ = _FlashAttnQKVRope.apply(qkv, cos, sin, nq, nkv, causal, scale, pos)
-            return o
+            return _FlashAttnQKVRope.apply(qkv, cos, sin, nq, nkv, causal, scale, pos)
         warning_once(f"sxe attention: HIP flash kernel does not cover dtype={qkv.dtype} D={D} S={qkv.shape[1]}; "
                      f"using RoPE kernel + SDPA")
     if rope is not None:
