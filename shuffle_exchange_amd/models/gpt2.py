@@ -13,6 +13,7 @@ import torch.nn.functional as F
 from ..ops.activation import bias_gelu
 from ..ops.attention import attention
 from ..ops.cross_entropy import cross_entropy
+from ..ops.linear import linear
 from ..ops.norm import LayerNorm
 
 
@@ -61,11 +62,11 @@ class GPT2Block(nn.Module):
     def forward(self, x):
         B, S, H = x.shape
         d = H // self.n_head
-        qkv = F.linear(self.ln_1(x), self.c_attn.weight, self.c_attn.bias).view(B, S, 3, self.n_head, d)
+        qkv = linear(self.ln_1(x), self.c_attn.weight, self.c_attn.bias).view(B, S, 3, self.n_head, d)
         o = attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=True)
-        x = x + F.linear(o.reshape(B, S, H), self.c_proj.weight, self.c_proj.bias)
-        m = bias_gelu(F.linear(self.ln_2(x), self.c_fc.weight), self.c_fc.bias)
-        return x + F.linear(m, self.mlp_proj.weight, self.mlp_proj.bias)
+        x = x + linear(o.reshape(B, S, H), self.c_proj.weight, self.c_proj.bias)
+        m = bias_gelu(linear(self.ln_2(x), self.c_fc.weight), self.c_fc.bias)
+        return x + linear(m, self.mlp_proj.weight, self.mlp_proj.bias)
 
 
 class GPT2LMHeadModel(nn.Module):

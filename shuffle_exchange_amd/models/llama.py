@@ -25,6 +25,7 @@ from torch.utils.checkpoint import checkpoint
 from ..ops.activation import swiglu
 from ..ops.attention import attention_qkv_rope
 from ..ops.cross_entropy import fused_linear_cross_entropy
+from ..ops.linear import linear
 from ..ops.norm import RMSNorm
 from ..ops.rope import RopeCache
 
@@ -95,9 +96,9 @@ class LlamaAttention(nn.Module):
 
     def forward(self, x, rope: RopeCache, position_ids=None):
         B, S, _ = x.shape
-        qkv = F.linear(x, self.qkv_proj.weight).view(B, S, self.nq + 2 * self.nkv, self.d)
+        qkv = linear(x, self.qkv_proj.weight).view(B, S, self.nq + 2 * self.nkv, self.d)
         o = attention_qkv_rope(qkv, self.nq, self.nkv, rope, position_ids, causal=True)
-        return F.linear(o.reshape(B, S, self.nq * self.d), self.o_proj.weight)
+        return linear(o.reshape(B, S, self.nq * self.d), self.o_proj.weight)
 
 
 class LlamaMLP(nn.Module):
@@ -107,7 +108,7 @@ class LlamaMLP(nn.Module):
         self.down_proj = nn.Linear(cfg.intermediate_size, cfg.hidden_size, bias=False)
 
     def forward(self, x):
-        return F.linear(swiglu(F.linear(x, self.gate_up_proj.weight)), self.down_proj.weight)
+        return linear(swiglu(linear(x, self.gate_up_proj.weight)), self.down_proj.weight)
 
 
 class LlamaDecoderLayer(nn.Module):

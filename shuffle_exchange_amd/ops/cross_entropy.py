@@ -57,6 +57,16 @@ class _FusedLinearXEnt(torch.autograd.Function):
         inv_n = (1.0 / n_valid).reshape(1)
         need_grad = torch.is_grad_enabled() or h.requires_grad or weight.requires_grad
         chunk = T if not chunk_tokens else min(int(chunk_tokens), T)
+        if chunk == T:
+            # unchunked: keep d(loss)/d(logits) (written over the logits) and do both GEMMs in
+            # backward, where the weight-grad GEMM can land directly in the optimizer's buffer
+            logits = torch.matmul(h2, weight.t())
+            loss, _ = torch.ops.sxe.xent_fwd(logits, tgt, int(ignore_index), need_grad, inv_n, 1.0)
+            ctx.save_for_backward(logits if need_grad else None, h2, weight)
+            ctx.mode = "dlogits"
+            ctx.hshape = h.shape
+            return loss.sum() / n_valid
+        ctx.mode = "chunked"
         loss_sum = torch.zeros((), device=h.device, dtype=torch.float32)
         dh = torch.empty_like(h2) if need_grad else None
         dW = None
@@ -80,6 +90,16 @@ class _FusedLinearXEnt(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
+        if ctx.mode == "dlogits":
+            dl, h2, weight = ctx.saved_tensors
+            dl.mul_(gout.to(dl.dtype))  # upstream scalar (1/GAS, loss scale, ...), in place
+            dh = torch.matmul(dl, weight).view(ctx.hshape)
+            dW = None
+            if ctx.needs_input_grad[1]:
+                from .linear import write_weight_grad
+                if not write_weight_grad(weight, dl, h2):
+                    dW = dl.t() @ h2
+            return dh, dW, None, None, None
         dh, dW = ctx.saved_tensors
         g = gout.to(torch.float32)
         dh = (dh * g.to(dh.dtype)).view(ctx.hshape)

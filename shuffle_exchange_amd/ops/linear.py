@@ -1,0 +1,61 @@
+"""Linear layer whose weight gradient is written straight into the ZeRO gradient buffer.
+
+If a weight carries ``_sxe_grad_target`` (installed by the ZeRO optimizers), the backward weight-grad
+GEMM writes its result directly where the optimizer wants it:
+  * fp32 accumulator (single-rank / persistent units): ONE hipBLASLt GEMM with fp32 output and
+    beta = 1 (``aten::addmm.dtype_out``) -- no bf16 ``p.grad`` tensor, no separate fp32 add pass,
+    and micro-batch accumulation happens at fp32 precision inside the GEMM epilogue;
+  * bf16 reduce-scatter staging slot (multi-rank units): the GEMM output IS the send buffer.
+then calls ``_sxe_grad_done`` so the optimizer can launch the unit's reduce-scatter. Without a
+target it behaves exactly like ``torch.nn.functional.linear``. (The reference's analogue is
+Megatron-style ``gradient_accumulation_fusion``; DeepSpeed's ZeRO copies each ``p.grad`` into an
+IPG bucket instead, stage_1_and_2.py:1137-1139.)
+"""
+import torch
+import torch.nn.functional as F
+
+
+def write_weight_grad(w, gy2, x2):
+    """dW = gy2^T @ x2 into the optimizer-provided target of `w`; returns True if handled."""
+    tgt = getattr(w, "_sxe_grad_target", None)
+    if tgt is None:
+        return False
+    buf, accumulate = tgt(w)
+    if buf.dtype == torch.float32 and gy2.dtype != torch.float32:
+        torch.ops.aten.addmm.dtype_out(buf, gy2.t(), x2, torch.float32, beta=1 if accumulate else 0, alpha=1,
+                                       out=buf)
+    elif accumulate:
+        buf.addmm_(gy2.t(), x2)
+    else:
+        torch.mm(gy2.t(), x2, out=buf)
+    w._sxe_grad_done(w)
+    return True
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy2 = gy.reshape(-1, gy.shape[-1])
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.matmul(gy, w)
+        if ctx.needs_input_grad[1]:
+            x2 = x.reshape(-1, x.shape[-1])
+            if not write_weight_grad(w, gy2, x2):
+                dw = gy2.t() @ x2
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = gy2.sum(0)
+        return dx, dw, db
+
+
+def linear(x, weight, bias=None):
+    if weight.requires_grad and torch.is_grad_enabled() and hasattr(weight, "_sxe_grad_target"):
+        return _Linear.apply(x, weight, bias)
+    return F.linear(x, weight, bias)

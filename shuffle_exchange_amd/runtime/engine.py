@@ -69,6 +69,8 @@ class SXEEngine(nn.Module):
         self.local_rank = dist.get_local_rank()
         if acc.gpu:
             acc.set_device(self.local_rank)
+            from .gemm_tuning import load_tuned_gemms
+            load_tuned_gemms()
         self.device = torch.device(acc.current_device_name())
         if config is None and args is not None:
             config = getattr(args, "deepspeed_config", None) or getattr(args, "sxe_config", None)

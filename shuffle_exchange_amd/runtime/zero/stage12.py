@@ -87,8 +87,35 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
 
     # ------------------------------------------------------------------------------------- backward
     def _register_hooks(self):
+        fused_targets = self.stage == 2 or self.topo.S == 1
         for p, u in self.param_unit.items():
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(u)))
+            if fused_targets:
+                # weight-grad GEMMs (ops/linear.py) write into the fp32 accumulator (S == 1) or the
+                # bf16 reduce-scatter staging slot (S > 1) directly
+                p._sxe_grad_target = self._grad_target
+                p._sxe_grad_done = self._grad_done
+
+    def _grad_target(self, p):
+        u = self.param_unit[p]
+        i = u.param_index[id(p)]
+        o, n = u.offsets[i], u.numels[i]
+        if self.topo.S == 1:
+            return u.grad[o:o + n].view(p.shape), True
+        if u.staging is None:
+            u.staging = torch.empty(u.padded, dtype=u.dtype, device=u.device)
+            if u.padded > u.numel:
+                u.staging[u.numel:].zero_()
+        return u.staging[o:o + n].view(p.shape), u.filled[i]
+
+    def _grad_done(self, p):
+        u = self.param_unit[p]
+        i = u.param_index[id(p)]
+        if not u.filled[i]:
+            u.filled[i] = True
+            u.pending -= 1
+        if self.topo.S > 1 and u.pending == 0:
+            self._reduce_unit(u)
 
     def _make_hook(self, unit):
         def hook(p):

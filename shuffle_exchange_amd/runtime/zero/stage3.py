@@ -215,6 +215,35 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             self._hooks.append(fg.module.register_forward_hook(self._make_post(fg)))
         for p, u in self.param_unit.items():
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_grad_hook(u)))
+            # fused weight-grad GEMMs (ops/linear.py) write straight into the unit's buffers
+            p._sxe_grad_target = self._grad_target
+            p._sxe_grad_done = self._grad_done
+
+    def _grad_target(self, p):
+        u = self.param_unit[p]
+        i = u.param_index[id(p)]
+        o, n = u.offsets[i], u.numels[i]
+        if u.persistent and self.S == 1:
+            return u.grad[o:o + n].view(p.shape), True
+        if u.staging is None:
+            u.staging = torch.empty(u.padded, dtype=u.dtype, device=u.device)
+            if u.padded > u.numel:
+                u.staging[u.numel:].zero_()
+        return u.staging[o:o + n].view(p.shape), u.filled[i]
+
+    def _grad_done(self, p):
+        u = self.param_unit[p]
+        i = u.param_index[id(p)]
+        if u.persistent and self.S == 1:
+            u.filled[i] = True
+            return
+        if not u.filled[i]:
+            u.filled[i] = True
+            u.pending -= 1
+        if u.pending == 0:
+            self._reduce_unit(u)
+            if not u.persistent and self._in_bwd:
+                self._release_unit(u)
 
     def _make_pre(self, fg):
         def pre(mod, args):
@@ -269,7 +298,9 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 i = unit.param_index[id(p)]
                 o, n = unit.offsets[i], unit.numels[i]
                 unit.grad[o:o + n].add_(p.grad.reshape(-1))
-                unit.filled[i] = True
+                if not unit.filled[i]:
+                    unit.filled[i] = True
+                    unit.pending -= 1
                 p.grad = None
                 return
             done = unit.stage_grad(p, p.grad)
