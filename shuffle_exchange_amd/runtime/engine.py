@@ -191,7 +191,23 @@ class SXEEngine(nn.Module):
         if len(ranks) == 1:
             return
         src = ranks[0]
-        tensors = [p.data for p in self.module.parameters()] + [b for b in self.module.buffers()]
+        from ..moe.utils import is_moe_param
+        expert = [p for p in self.module.parameters() if is_moe_param(p)]
+        if expert:
+            # expert weights differ across the expert-parallel group: sync them only over their
+            # expert-data-parallel group (reference engine.py:1256-1261)
+            by_name = {}
+            for p in expert:
+                by_name.setdefault(p.group_name, []).append(p)
+            for name, ps in by_name.items():
+                ep = int(name.rsplit("_", 1)[-1])
+                groups.create_expert_and_data_parallel(ep, name)
+                edp_ranks = groups._Registry.expert[name][3]
+                if len(edp_ranks) > 1:
+                    for p in ps:
+                        dist.broadcast(p.data, src=edp_ranks[0], group=groups.get_expert_data_parallel_group(name))
+        tensors = [p.data for p in self.module.parameters() if not is_moe_param(p)] + \
+            [b for b in self.module.buffers()]
         by_dtype = {}
         for t in tensors:
             by_dtype.setdefault(t.dtype, []).append(t)
@@ -231,6 +247,9 @@ class SXEEngine(nn.Module):
 
     def _configure_optimizer(self, client_optimizer, model_parameters):
         cfg = self._config
+        from ..moe.utils import has_moe_layers, split_params_into_different_moe_groups_for_optimizer
+        if has_moe_layers(self.module)[0] and not isinstance(client_optimizer, torch.optim.Optimizer):
+            model_parameters = split_params_into_different_moe_groups_for_optimizer(list(model_parameters))
         if client_optimizer is not None and not callable(client_optimizer) or isinstance(client_optimizer,
                                                                                         torch.optim.Optimizer):
             basic = client_optimizer

@@ -32,9 +32,17 @@ class DataParallelOptimizer(ZeroOptimizerBase):
         for g, pg in enumerate(init_optimizer.param_groups):
             params = [p for p in pg["params"] if p.requires_grad]
             units = []
+            rgroup, rsize = self.dp_group, self.dp_size
+            if pg.get("moe", False):  # expert grads: expert-data-parallel group only
+                from ...parallel import groups
+                name = pg["name"]
+                groups.create_expert_and_data_parallel(int(name.rsplit("_", 1)[-1]), name)
+                rgroup = groups.get_expert_data_parallel_group(name)
+                rsize = groups.get_expert_data_parallel_world_size(name)
             if params:
                 for i, plist in enumerate(split_into_units(params, max(1, int(bucket_size)))):
                     u = FlatUnit(plist, 1, 0, params[0].dtype, device, name=f"g{g}u{i}", index=i)
+                    u.rgroup, u.rsize = rgroup, rsize
                     units.append(u)
                     for p in plist:
                         self.param_unit[p] = u
@@ -60,7 +68,7 @@ class DataParallelOptimizer(ZeroOptimizerBase):
         return hook
 
     def _allreduce_unit(self, u):
-        if self.dp_size == 1 or u.reduced:
+        if u.rsize == 1 or u.reduced:
             u.reduced = True
             return
         u.reduced = True
@@ -69,10 +77,10 @@ class DataParallelOptimizer(ZeroOptimizerBase):
             st.wait_stream(torch.cuda.current_stream())
         with get_accelerator().stream(st):
             if dist.get_backend() == "nccl":
-                dist.all_reduce(u.grad, op=dist.ReduceOp.AVG, group=self.dp_group)
+                dist.all_reduce(u.grad, op=dist.ReduceOp.AVG, group=u.rgroup)
             else:
-                dist.all_reduce(u.grad, group=self.dp_group)
-                u.grad.div_(self.dp_size)
+                dist.all_reduce(u.grad, group=u.rgroup)
+                u.grad.div_(u.rsize)
 
     def set_gradient_accumulation_boundary(self, flag):
         self.boundary = bool(flag)

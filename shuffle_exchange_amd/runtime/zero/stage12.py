@@ -63,6 +63,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         self.micro_step_boundary = True
         self._hooks = []
         self.param_unit = {}
+        self._moe_topos = {}
         # ---- flatten every param group into units -------------------------------------------------
         dtype = None
         for g, pg in enumerate(init_optimizer.param_groups):
@@ -73,24 +74,42 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
             dtype = params[0].dtype
             units = []
             for i, plist in enumerate(split_into_units(params, max(1, int(reduce_bucket_size)))):
-                u = FlatUnit(plist, S, self.topo.offset, dtype, device, name=f"g{g}u{i}", index=i)
+                gt = self._group_topo(pg)
+                u = FlatUnit(plist, gt.S, gt.offset, dtype, device, name=f"g{g}u{i}", index=i)
+                u.topo = gt
                 units.append(u)
                 for p in plist:
                     self.param_unit[p] = u
             self.units.append(units)
         self.bit16_dtype = dtype
+        if self._moe_topos:
+            if self.shuffle_exchange_enabled:
+                raise NotImplementedError("Shuffle-exchange slices with MoE expert groups are not supported")
+            # expert and dense partitions are disjoint across the whole DP group: one norm reduce
+            self.partition_group = dp_group
         self._init_master()
         self._register_hooks()
         log_dist(f"ZeRO-{stage}: {sum(len(u) for u in self.units)} units, slice_count={S}, "
                  f"slices={self.topo.num_slices}, shuffle_exchange="
                  f"{self.method if self.shuffle_exchange_enabled else 'off'}", ranks=[0])
 
+    def _group_topo(self, pg):
+        if not pg.get("moe", False):
+            return self.topo
+        name = pg["name"]
+        if name not in self._moe_topos:
+            from ...parallel import groups
+            ep = int(name.rsplit("_", 1)[-1]) if name.startswith("ep_size_") else None
+            groups.create_expert_and_data_parallel(ep, name)
+            edp = groups._Registry.expert[name][3]
+            self._moe_topos[name] = SliceTopology(edp, len(edp))
+        return self._moe_topos[name]
+
     # ------------------------------------------------------------------------------------- backward
     def _register_hooks(self):
-        fused_targets = self.stage == 2 or self.topo.S == 1
         for p, u in self.param_unit.items():
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(u)))
-            if fused_targets:
+            if self.stage == 2 or u.topo.S == 1:
                 # weight-grad GEMMs (ops/linear.py) write into the fp32 accumulator (S == 1) or the
                 # bf16 reduce-scatter staging slot (S > 1) directly
                 p._sxe_grad_target = self._grad_target
@@ -100,7 +119,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         u = self.param_unit[p]
         i = u.param_index[id(p)]
         o, n = u.offsets[i], u.numels[i]
-        if self.topo.S == 1:
+        if u.topo.S == 1:
             return u.grad[o:o + n].view(p.shape), True
         if u.staging is None:
             u.staging = torch.empty(u.padded, dtype=u.dtype, device=u.device)
@@ -114,7 +133,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         if not u.filled[i]:
             u.filled[i] = True
             u.pending -= 1
-        if self.topo.S > 1 and u.pending == 0:
+        if u.topo.S > 1 and u.pending == 0:
             self._reduce_unit(u)
 
     def _make_hook(self, unit):
@@ -123,7 +142,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                 return  # ZeRO-1 keeps accumulating full grads until the boundary
             if p.grad is None:
                 return
-            if self.topo.S == 1:
+            if unit.topo.S == 1:
                 i = unit.param_index[id(p)]
                 o, n = unit.offsets[i], unit.numels[i]
                 unit.grad[o:o + n].add_(p.grad.reshape(-1))
@@ -154,8 +173,8 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         with get_accelerator().stream(stream):
             send = st if (self.comm_dtype is None or st.dtype == self.comm_dtype) else st.to(self.comm_dtype)
             out = torch.empty(u.chunk, dtype=send.dtype, device=send.device)
-            dist.reduce_scatter_tensor(out, send, group=self.topo.slice_group)
-            u.grad.add_(out, alpha=1.0 / self.topo.S)
+            dist.reduce_scatter_tensor(out, send, group=u.topo.slice_group)
+            u.grad.add_(out, alpha=1.0 / u.topo.S)
             if stream is not None:
                 st.record_stream(stream)
                 send.record_stream(stream)
@@ -168,7 +187,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
             return
         for units in self.units:
             for u in units:
-                if self.topo.S == 1:
+                if u.topo.S == 1:
                     continue
                 if u.pending > 0:
                     # params whose grads exist but whose hook did not fire (e.g. stage 1 grads
@@ -205,11 +224,10 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         self.global_step += 1
 
     def _allgather_params(self):
-        if self.topo.S == 1:
-            return
         for units in self.units:
             for u in units:
-                dist.all_gather_into_tensor(u.flat, u.shard, group=self.topo.slice_group)
+                if u.topo.S > 1:
+                    dist.all_gather_into_tensor(u.flat, u.shard, group=u.topo.slice_group)
 
     def zero_grad(self, set_to_none=True):
         for p in self.param_unit:

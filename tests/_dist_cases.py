@@ -154,3 +154,72 @@ def case_fingerprint_mismatch(rank, world):
         return "no-error"
     except RuntimeError:
         return "mismatch-detected"
+
+
+# ------------------------------------------------------------------------------------------- MoE
+def _moe_global(seed=0):
+    from shuffle_exchange_amd.moe import MoE
+    torch.manual_seed(seed)
+    m = MoE(32, None, num_experts=4, ep_size=1, k=2, capacity_factor=4.0, min_capacity=64, use_rts=False,
+            top2_2nd_expert_sampling=False, intermediate_size=48)
+    return m
+
+
+def moe_single_reference():
+    from shuffle_exchange_amd.parallel import groups
+    groups.reset()
+    m = _moe_global()
+    m._groups_ready = True
+    torch.manual_seed(3)
+    x = torch.randn(2, 2, 8, 32)  # [rank, batch, seq, H]: both ranks' tokens
+    outs = []
+    for r in range(2):
+        o, l, c = m(x[r])
+        outs.append(o)
+        o.square().sum().backward()
+    ex = m.deepspeed_moe.experts
+    return {"out": torch.stack(outs), "g_up": ex.w_gate_up.grad.clone(), "g_down": ex.w_down.grad.clone()}
+
+
+def case_moe_ep(rank, world):
+    from shuffle_exchange_amd.moe import MoE
+    g = _moe_global()
+    torch.manual_seed(0)
+    m = MoE(32, None, num_experts=4, ep_size=2, k=2, capacity_factor=4.0, min_capacity=64, use_rts=False,
+            top2_2nd_expert_sampling=False, intermediate_size=48)
+    with torch.no_grad():
+        m.deepspeed_moe.gate.wg.weight.copy_(g.deepspeed_moe.gate.wg.weight)
+        ex, gex = m.deepspeed_moe.experts, g.deepspeed_moe.experts
+        ex.w_gate_up.copy_(gex.w_gate_up[rank * 2:rank * 2 + 2])
+        ex.w_down.copy_(gex.w_down[rank * 2:rank * 2 + 2])
+    torch.manual_seed(3)
+    x = torch.randn(2, 2, 8, 32)
+    outs = []
+    o, l, c = m(x[rank])
+    o.square().sum().backward()
+    # gather every rank's output so each test rank can compare the full picture
+    from shuffle_exchange_amd import comm
+    full = [torch.empty_like(o) for _ in range(world)]
+    comm.all_gather(full, o.detach().contiguous())
+    ex = m.deepspeed_moe.experts
+    return {"out": torch.stack(full), "g_up": ex.w_gate_up.grad.clone(), "g_down": ex.w_down.grad.clone()}
+
+
+def case_mixtral_train(rank, world, stage):
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd.models.mixtral import MixtralForCausalLM, mixtral_config
+    torch.manual_seed(0)
+    cfg = mixtral_config("mixtral-tiny", ep_size=2)
+    model = MixtralForCausalLM(cfg)
+    ds = {"train_micro_batch_size_per_gpu": 2, "zero_optimization": {"stage": stage},
+          "optimizer": {"type": "AdamW", "params": {"lr": 3e-3}}, "gradient_clipping": 1.0}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    g = torch.Generator().manual_seed(7 + rank)
+    ids = torch.randint(0, cfg.vocab_size, (2, 32), generator=g)
+    losses = []
+    for _ in range(6):
+        loss = eng(ids, labels=ids)
+        eng.backward(loss)
+        eng.step()
+        losses.append(float(loss.detach()))
+    return {"losses": losses}
