@@ -28,6 +28,12 @@ from ..ops.cross_entropy import fused_linear_cross_entropy
 from ..ops.linear import linear
 from ..ops.norm import RMSNorm
 from ..ops.rope import RopeCache
+from ..sequence.layer import ulysses_qkv_attention
+
+
+def _sp_group():
+    from ..parallel import groups
+    return groups.get_sequence_parallel_group() if groups.get_sequence_parallel_world_size() > 1 else None
 
 
 @dataclass
@@ -46,6 +52,7 @@ class LlamaConfig:
     initializer_range: float = 0.02
     activation_checkpointing: bool = False
     loss_chunk_tokens: Optional[int] = None
+    sequence_parallel: bool = False  # Ulysses: inputs are [B, S/sp] chunks of the SP group
     extra: dict = field(default_factory=dict)
 
     def __post_init__(self):
@@ -97,7 +104,11 @@ class LlamaAttention(nn.Module):
     def forward(self, x, rope: RopeCache, position_ids=None):
         B, S, _ = x.shape
         qkv = linear(x, self.qkv_proj.weight).view(B, S, self.nq + 2 * self.nkv, self.d)
-        o = attention_qkv_rope(qkv, self.nq, self.nkv, rope, position_ids, causal=True)
+        spg = _sp_group() if self.cfg.sequence_parallel else None
+        if spg is not None:
+            o = ulysses_qkv_attention(qkv, self.nq, self.nkv, rope, spg, position_ids, causal=True)
+        else:
+            o = attention_qkv_rope(qkv, self.nq, self.nkv, rope, position_ids, causal=True)
         return linear(o.reshape(B, S, self.nq * self.d), self.o_proj.weight)
 
 
@@ -142,11 +153,24 @@ class LMHeadLoss(nn.Module):
         else:
             self.weight = weight
 
-    def forward(self, h, labels=None, ignore_index=-100):
+    def forward(self, h, labels=None, ignore_index=-100, shift_labels=True):
         if labels is None:
             return F.linear(h, self.weight)
-        tgt = torch.cat([labels[:, 1:], torch.full_like(labels[:, :1], ignore_index)], dim=1)
-        return fused_linear_cross_entropy(h, self.weight, tgt, ignore_index, self.cfg.loss_chunk_tokens)
+        if shift_labels:
+            tgt = torch.cat([labels[:, 1:], torch.full_like(labels[:, :1], ignore_index)], dim=1)
+        else:
+            tgt = labels  # already shifted over the full sequence (sequence-parallel data adapter)
+        spg = _sp_group() if self.cfg.sequence_parallel else None
+        if spg is None:
+            return fused_linear_cross_entropy(h, self.weight, tgt, ignore_index, self.cfg.loss_chunk_tokens)
+        # SP: this rank's token-sum / number of valid tokens over the whole sequence (reference
+        # sequence/cross_entropy.py); summed over the SP group it is the full-sequence mean
+        from .. import comm as dist
+        n = (tgt != ignore_index).sum().float().reshape(1)
+        dist.all_reduce(n, group=spg)
+        s = fused_linear_cross_entropy(h, self.weight, tgt, ignore_index, self.cfg.loss_chunk_tokens,
+                                       reduction="sum")
+        return s / n.clamp_min(1.0).squeeze(0)
 
 
 class LlamaForCausalLM(nn.Module):
@@ -174,7 +198,7 @@ class LlamaForCausalLM(nn.Module):
             self._rope = RopeCache(self.cfg.head_dim, self.cfg.max_position_embeddings, self.cfg.rope_theta, device)
         return self._rope
 
-    def forward(self, input_ids, labels=None, position_ids=None):
+    def forward(self, input_ids, labels=None, position_ids=None, shift_labels=True):
         x = self.embed_tokens(input_ids)
         rope = self.rope(x.device)
         res = None
@@ -184,4 +208,4 @@ class LlamaForCausalLM(nn.Module):
             else:
                 x, res = layer(x, res, rope, position_ids)
         h = self.norm(x, res)[0] if res is not None else self.norm(x)
-        return self.lm_head(h, labels)
+        return self.lm_head(h, labels, shift_labels=shift_labels)

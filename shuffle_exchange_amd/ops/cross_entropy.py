@@ -48,12 +48,15 @@ def cross_entropy(logits, target, ignore_index=-100, reduction="mean"):
 
 class _FusedLinearXEnt(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, weight, target, ignore_index, chunk_tokens):
+    def forward(ctx, h, weight, target, ignore_index, chunk_tokens, reduction="mean"):
         H = h.shape[-1]
         h2 = h.reshape(-1, H)
         tgt = target.reshape(-1).contiguous()
         T = h2.shape[0]
-        n_valid = (tgt != ignore_index).sum().clamp_min(1).float()
+        if reduction == "sum":
+            n_valid = torch.ones((), device=h.device, dtype=torch.float32)
+        else:
+            n_valid = (tgt != ignore_index).sum().clamp_min(1).float()
         inv_n = (1.0 / n_valid).reshape(1)
         need_grad = torch.is_grad_enabled() or h.requires_grad or weight.requires_grad
         chunk = T if not chunk_tokens else min(int(chunk_tokens), T)
@@ -99,17 +102,18 @@ class _FusedLinearXEnt(torch.autograd.Function):
                 from .linear import write_weight_grad
                 if not write_weight_grad(weight, dl, h2):
                     dW = dl.t() @ h2
-            return dh, dW, None, None, None
+            return dh, dW, None, None, None, None
         dh, dW = ctx.saved_tensors
         g = gout.to(torch.float32)
         dh = (dh * g.to(dh.dtype)).view(ctx.hshape)
         dW = (dW * g.to(dW.dtype)).to(ctx.wdtype)
-        return dh, dW, None, None, None
+        return dh, dW, None, None, None, None
 
 
-def fused_linear_cross_entropy(h, weight, target, ignore_index=-100, chunk_tokens=None):
-    """mean-reduced CE of ``h @ weight.T`` against ``target`` (ignore_index excluded)."""
+def fused_linear_cross_entropy(h, weight, target, ignore_index=-100, chunk_tokens=None, reduction="mean"):
+    """CE of ``h @ weight.T`` against ``target`` (ignore_index excluded); mean or sum."""
     if native.use_hip(h):
-        return _FusedLinearXEnt.apply(h, weight, target, ignore_index, chunk_tokens)
+        return _FusedLinearXEnt.apply(h, weight, target, ignore_index, chunk_tokens, reduction)
     logits = torch.matmul(h, weight.t()).float()
-    return F.cross_entropy(logits.reshape(-1, logits.shape[-1]), target.reshape(-1), ignore_index=ignore_index)
+    return F.cross_entropy(logits.reshape(-1, logits.shape[-1]), target.reshape(-1), ignore_index=ignore_index,
+                           reduction=reduction)

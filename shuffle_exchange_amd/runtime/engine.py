@@ -291,6 +291,8 @@ class SXEEngine(nn.Module):
                 basic, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks, dp_group=dp_group,
                 bucket_size=zc.reduce_bucket_size, mp_group=mp_group, shuffle_exchange_cfg=se)
 
+        self.optimizer.sp_scale = float(cfg.sequence_parallel_size)
+
     def _configure_lr_scheduler(self, client_lr_scheduler):
         if client_lr_scheduler is not None:
             if callable(client_lr_scheduler) and not hasattr(client_lr_scheduler, "step"):

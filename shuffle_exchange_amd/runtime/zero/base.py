@@ -51,6 +51,10 @@ class ZeroOptimizerBase:
         self._last_norm = None
         self._skip_t = None
         self.global_step = 0
+        # Ulysses SP: ranks of one SP group hold different tokens of the same sequences, so their
+        # gradients are summed while data-parallel replicas are averaged: reduce-scatter results are
+        # scaled by sp / |DP x SP| (reference divides by dp/sp, stage_1_and_2.py:1314)
+        self.sp_scale = 1.0
 
     # --------------------------------------------------------------------------------------------
     def _init_master(self):

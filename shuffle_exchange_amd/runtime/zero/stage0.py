@@ -76,11 +76,11 @@ class DataParallelOptimizer(ZeroOptimizerBase):
         if st is not None:
             st.wait_stream(torch.cuda.current_stream())
         with get_accelerator().stream(st):
-            if dist.get_backend() == "nccl":
+            if dist.get_backend() == "nccl" and self.sp_scale == 1.0:
                 dist.all_reduce(u.grad, op=dist.ReduceOp.AVG, group=u.rgroup)
             else:
                 dist.all_reduce(u.grad, group=u.rgroup)
-                u.grad.div_(u.rsize)
+                u.grad.mul_(self.sp_scale / u.rsize)
 
     def set_gradient_accumulation_boundary(self, flag):
         self.boundary = bool(flag)

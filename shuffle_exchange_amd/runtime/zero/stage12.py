@@ -174,7 +174,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
             send = st if (self.comm_dtype is None or st.dtype == self.comm_dtype) else st.to(self.comm_dtype)
             out = torch.empty(u.chunk, dtype=send.dtype, device=send.device)
             dist.reduce_scatter_tensor(out, send, group=u.topo.slice_group)
-            u.grad.add_(out, alpha=1.0 / u.topo.S)
+            u.grad.add_(out, alpha=self.sp_scale / u.topo.S)
             if stream is not None:
                 st.record_stream(stream)
                 send.record_stream(stream)

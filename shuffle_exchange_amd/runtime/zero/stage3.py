@@ -382,9 +382,9 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 dist.reduce_scatter_tensor(out, send, group=self.topo.slice_group)
                 if self.mics:
                     dist.all_reduce(out, group=self._mics_replica)
-                    u.grad.add_(out, alpha=1.0 / (self.S * self.topo.num_slices))
+                    u.grad.add_(out, alpha=self.sp_scale / (self.S * self.topo.num_slices))
                 else:
-                    u.grad.add_(out, alpha=1.0 / self.S)
+                    u.grad.add_(out, alpha=self.sp_scale / self.S)
                 if rs is not None:
                     out.record_stream(rs)
             if rs is not None:
