@@ -267,24 +267,26 @@ class SXEEngine(nn.Module):
         mp_group = groups.get_tensor_model_parallel_group() if groups.get_tensor_model_parallel_world_size() > 1 else None
         se = self.shuffle_exchange_config
         off = zc.offload_optimizer
+        host_step = None
         if off is not None and off.device in ("cpu", "nvme"):
-            from .zero.offload import OffloadOptimizer
-            self.optimizer = OffloadOptimizer(basic, stage=stage, module=self.module, loss_scaler=scaler,
-                                              clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks, dp_group=dp_group,
-                                              offload_config=off, zero_config=zc, aio_config=cfg.model.aio)
-        elif stage == 3:
+            assert stage > 0, "optimizer offload needs ZeRO stage 1, 2 or 3"
+            from .zero.offload import HostOptimizerStep
+            host_step = HostOptimizerStep(off, aio_config=cfg.model.aio, rank=dist.get_rank())
+        offload_param = bool(zc.offload_param is not None and zc.offload_param.device in ("cpu", "nvme"))
+        if stage == 3:
             self.optimizer = ZeroStage3Optimizer(
                 self.module, basic, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks,
                 dp_group=dp_group, prefetch_depth=zc.prefetch_depth,
                 param_persistence_threshold=zc.param_persistence_threshold,
                 communication_data_type=self.communication_data_type, unit_classes=zc.fetch_units,
-                shuffle_exchange_cfg=se, mp_group=mp_group, timers=self.timers, mics_shard_size=zc.mics_shard_size)
+                shuffle_exchange_cfg=se, mp_group=mp_group, timers=self.timers, mics_shard_size=zc.mics_shard_size,
+                host_step=host_step, offload_param=offload_param)
         elif stage in (1, 2):
             self.optimizer = ZeroStage12Optimizer(
                 basic, stage=stage, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks,
                 dp_group=dp_group, reduce_bucket_size=zc.reduce_bucket_size,
                 communication_data_type=self.communication_data_type, overlap_comm=True, shuffle_exchange_cfg=se,
-                mp_group=mp_group, timers=self.timers)
+                mp_group=mp_group, timers=self.timers, host_step=host_step)
         else:
             from .zero.stage0 import DataParallelOptimizer
             self.optimizer = DataParallelOptimizer(

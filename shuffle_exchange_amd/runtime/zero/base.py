@@ -55,10 +55,15 @@ class ZeroOptimizerBase:
         # gradients are summed while data-parallel replicas are averaged: reduce-scatter results are
         # scaled by sp / |DP x SP| (reference divides by dp/sp, stage_1_and_2.py:1314)
         self.sp_scale = 1.0
+        # ZeRO-Offload / ZeRO-Infinity (runtime/zero/offload.py): masters + optimizer state on the
+        # host or NVMe, update by the C++ CPU kernels; None = everything on the GPU
+        self.host_step = None
 
     # --------------------------------------------------------------------------------------------
     def _init_master(self):
         """Create fp32 masters/grad accumulators and re-point the wrapped optimizer at them."""
+        if self.host_step is not None:
+            return self.host_step.init_master(self)
         for g, units in enumerate(self.units):
             total = sum(u.chunk for u in units)
             m = torch.empty(total, dtype=torch.float32, device=self.device)
@@ -117,6 +122,8 @@ class ZeroOptimizerBase:
 
     def _fused_update(self, coef, skip):
         """One optimizer step over every unit chunk; writes the bit16 chunks in the same pass."""
+        if self.host_step is not None:
+            return self.host_step.update(self, coef, skip)
         for g, units in enumerate(self.units):
             pg = self.optimizer.param_groups[g]
             m = self.master[g]
@@ -171,6 +178,20 @@ class ZeroOptimizerBase:
             offs.append(o)
             o += u.chunk
         return offs
+
+    def _device_masters(self):
+        """Masters for collective averaging (shuffle-exchange average_master); None if offloaded."""
+        if self.host_step is not None:
+            return None
+        return [u.master for units in self.units for u in units]
+
+    def _host_materialize(self):
+        if self.host_step is not None:
+            self.host_step.materialize(self)
+
+    def _host_flush(self):
+        if self.host_step is not None and self.host_step.device == "nvme":
+            self.host_step.flush(self)
 
     def zero_grad_buffers(self):
         for gr in self.grads:

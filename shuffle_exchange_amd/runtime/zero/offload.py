@@ -1,0 +1,354 @@
+"""ZeRO-Offload / ZeRO-Infinity: optimizer state and fp32 masters on the host (cpu) or NVMe.
+
+Parity: reference runtime/zero/stage_1_and_2.py cpu_offload paths (:1084-1180, :2094-2110),
+stage3.py offload_optimizer / sub-group swapping (:2027-2110), runtime/swap_tensor/
+partitioned_optimizer_swapper.py, ops/adam/cpu_adam.py.
+
+MI355X-first choices:
+  * gradients are reduced AND accumulated on the GPU in fp32 (one MI355X holds 288 GB; even a 70B
+    model's fp32 gradient chunk is 35 GB at dp=8), and cross PCIe ONCE per optimizer step, unit by
+    unit on a D2H stream, while the CPU updates the previous unit -- the reference streams partial
+    gradients to the host every micro-step;
+  * the CPU update is the AVX-512 C++ kernel (csrc/cpu/cpu_adam.cpp) that also writes the bf16
+    copy into a pinned buffer, which goes straight back on an H2D stream (for ZeRO-3 with
+    offload_param the pinned buffer IS the parameter shard, so nothing is copied back at all);
+  * NVMe: per-unit [master | exp_avg | exp_avg_sq] records swapped by the C++ thread-pool AIO
+    engine (csrc/cpu/aio.cpp) through a ring of pinned slots: read unit i+1 and write unit i-1
+    while unit i updates.
+The clip coefficient / overflow flag are computed on the GPU and read once per step (the only host
+sync of an offloaded step).
+"""
+import os
+
+import torch
+
+from ...accelerator import get_accelerator
+from ...ops import native
+from ...utils.logging import log_dist
+
+
+def _pinned(n, dtype):
+    return torch.empty(int(n), dtype=dtype, pin_memory=torch.cuda.is_available())
+
+
+class _NVMeSwapper:
+    """Per parameter group, one file holding every unit's [master | m | v] record (4 KiB aligned)."""
+
+    KINDS = ("master", "exp_avg", "exp_avg_sq")
+
+    def __init__(self, root, rank, units, nkinds, aio_cfg=None, buffer_count=3):
+        from ...ops.aio import AsyncIOHandle
+        self.dir = os.path.join(root, f"sxe_swap_rank{rank}")
+        os.makedirs(self.dir, exist_ok=True)
+        a = aio_cfg
+        kw = dict(block_size=getattr(a, "block_size", 1 << 20), queue_depth=getattr(a, "queue_depth", 8),
+                  intra_op_parallelism=max(2, getattr(a, "intra_op_parallelism", 1) or 1))
+        self.rd = AsyncIOHandle(**kw)
+        self.wr = AsyncIOHandle(**kw)
+        self.nkinds = nkinds
+        self.files, self.offsets = [], []
+        max_chunk = 1
+        for g, us in enumerate(units):
+            offs, o = [], 0
+            for u in us:
+                offs.append(o)
+                o += self._rec_bytes(u.chunk)
+                max_chunk = max(max_chunk, u.chunk)
+            self.files.append(os.path.join(self.dir, f"group{g}.swp"))
+            self.offsets.append(offs)
+        self.slot_elems = (self._rec_bytes(max_chunk) // 4)
+        self.slots = [_pinned(self.slot_elems, torch.float32) for _ in range(max(2, buffer_count))]
+        self.slot_write = [None] * len(self.slots)
+
+    def _rec_bytes(self, chunk):
+        b = chunk * 4 * self.nkinds
+        return (b + 4095) // 4096 * 4096
+
+    def views(self, slot, chunk):
+        buf = self.slots[slot]
+        return [buf[k * chunk:(k + 1) * chunk] for k in range(self.nkinds)]
+
+    def _rec(self, slot, chunk):
+        return self.slots[slot][:self._rec_bytes(chunk) // 4]
+
+    def read(self, slot, g, i, chunk):
+        if self.slot_write[slot] is not None:
+            self.wr.wait_request(self.slot_write[slot])
+            self.slot_write[slot] = None
+        return self.rd.async_pread(self._rec(slot, chunk), self.files[g], self.offsets[g][i])
+
+    def write(self, slot, g, i, chunk):
+        self.slot_write[slot] = self.wr.async_pwrite(self._rec(slot, chunk), self.files[g], self.offsets[g][i])
+
+    def drain(self):
+        self.rd.wait()
+        self.wr.wait()
+        self.slot_write = [None] * len(self.slots)
+
+
+class HostOptimizerStep:
+    """Plugged into a ZeRO optimizer (``ZeroOptimizerBase.host_step``): owns where the masters and
+    the optimizer state live and runs the update there."""
+
+    def __init__(self, offload_config, aio_config=None, rank=0):
+        native.require_cpu()
+        self.device = offload_config.device
+        self.pin = bool(offload_config.pin_memory) or self.device == "nvme"
+        self.nvme_path = offload_config.nvme_path
+        self.buffer_count = max(3, int(offload_config.buffer_count))
+        self.ratio = float(offload_config.ratio)
+        if self.ratio < 1.0:
+            log_dist("offload_optimizer.ratio < 1 is not supported yet: offloading the whole optimizer", ranks=[0])
+        self.aio_config = aio_config
+        self.rank = rank
+        self.swapper = None
+        self.materialized = False
+        if self.device == "nvme":
+            assert self.nvme_path, "offload_optimizer.device=nvme needs nvme_path"
+        acc = get_accelerator()
+        self.d2h = acc.named_stream("offload_d2h") if acc.gpu else None
+        self.h2d = acc.named_stream("offload_h2d") if acc.gpu else None
+        self._h2d_done = None
+
+    # ------------------------------------------------------------------------------------ layout
+    def _kinds(self, opt):
+        return {"adam": 3, "lion": 2, "adagrad": 2}.get(opt.kind, 1)
+
+    def init_master(self, opt):
+        if opt.kind == "generic" and self.device == "nvme":
+            raise ValueError("NVMe optimizer offload supports Adam/AdamW/Lion/Adagrad")
+        opt.grad_host, opt.lp_host = [], []
+        for g, units in enumerate(opt.units):
+            total = sum(u.chunk for u in units)
+            gr = torch.zeros(total, dtype=torch.float32, device=opt.device)  # GPU accumulator
+            opt.grad_host.append(_pinned(total, torch.float32))
+            needs_lp = any(u.shard.is_cuda for u in units)
+            opt.lp_host.append(_pinned(total, units[0].dtype) if needs_lp else None)
+            if self.device == "cpu":
+                m = _pinned(total, torch.float32) if self.pin else torch.empty(total, dtype=torch.float32)
+            else:
+                m = torch.empty(0, dtype=torch.float32)
+            off = 0
+            for u in units:
+                u.grad = gr[off:off + u.chunk]
+                if self.device == "cpu":
+                    u.master = m[off:off + u.chunk]
+                    u.master.copy_(u.shard.float().cpu() if u.shard.is_cuda else u.shard.float())
+                else:
+                    u.master = None
+                off += u.chunk
+            m = torch.nn.Parameter(m, requires_grad=False)
+            opt.master.append(m)
+            opt.grads.append(gr)
+            opt.optimizer.param_groups[g]["params"] = [m]
+        opt.optimizer.state.clear()
+        if self.device == "cpu":
+            opt._init_state()
+            return
+        self.swapper = _NVMeSwapper(self.nvme_path, self.rank, opt.units, self._kinds(opt), self.aio_config,
+                                    self.buffer_count)
+        for g, units in enumerate(opt.units):
+            st = opt.optimizer.state[opt.master[g]]
+            st["step"] = 0
+            for i, u in enumerate(units):
+                views = self.swapper.views(0, u.chunk)
+                views[0].copy_(u.shard.float().cpu() if u.shard.is_cuda else u.shard.float())
+                for v in views[1:]:
+                    v.zero_()
+                self.swapper.write(0, g, i, u.chunk)
+                self.swapper.drain()
+        log_dist(f"ZeRO-Infinity: optimizer state on NVMe under {self.swapper.dir}", ranks=[0])
+
+    # ------------------------------------------------------------------------------------ update
+    def _host_kernel(self, opt, pg, st, master, grad, states, lp, coef):
+        ops = torch.ops.sxe_cpu
+        if opt.kind == "adam":
+            b1, b2 = pg["betas"]
+            fused_lp = lp if (lp is not None and lp.dtype in (torch.bfloat16, torch.float16)) else None
+            ops.adam_step_(master, grad, states[0], states[1], fused_lp, float(pg["lr"]), float(b1), float(b2),
+                           float(pg["eps"]), float(pg["weight_decay"]), int(st["step"]), bool(opt.adamw),
+                           bool(pg.get("bias_correction", True)), coef)
+            if lp is not None and fused_lp is None:
+                lp.copy_(master)
+        elif opt.kind == "lion":
+            b1, b2 = pg["betas"]
+            grad.mul_(coef)
+            ops.lion_step_(master, grad, states[0], float(pg["lr"]), float(b1), float(b2), float(pg["weight_decay"]))
+            if lp is not None:
+                lp.copy_(master)
+        elif opt.kind == "adagrad":
+            grad.mul_(coef)
+            ops.adagrad_step_(master, grad, states[0], float(pg["lr"]), float(pg.get("eps", 1e-10)),
+                              float(pg.get("weight_decay", 0.0)))
+            if lp is not None:
+                lp.copy_(master)
+
+    def _state_views(self, opt, g, o, n):
+        st = opt.optimizer.state[opt.master[g]]
+        if opt.kind == "adam":
+            return [st["exp_avg"][o:o + n], st["exp_avg_sq"][o:o + n]]
+        if opt.kind == "lion":
+            return [st["exp_avg"][o:o + n]]
+        if opt.kind == "adagrad":
+            return [st["sum"][o:o + n]]
+        return []
+
+    def update(self, opt, coef_t, skip_t):
+        flags = torch.cat([coef_t.reshape(1).float(), skip_t.reshape(1).float()]).cpu()  # the one sync
+        coef, skip = float(flags[0]), float(flags[1])
+        if skip != 0.0:
+            return
+        if self.materialized and self.device == "nvme":
+            self.flush(opt)
+        cur = torch.cuda.current_stream() if opt.device is not None and opt.device.type == "cuda" else None
+        if self._h2d_done is not None:
+            self._h2d_done.synchronize()  # lp_host of the previous step fully consumed
+        # 1. all D2H grad copies in unit order, one event each
+        events = []
+        if cur is not None:
+            self.d2h.wait_stream(cur)
+        with get_accelerator().stream(self.d2h):
+            for g, units in enumerate(opt.units):
+                off = 0
+                for u in units:
+                    opt.grad_host[g][off:off + u.chunk].copy_(u.grad, non_blocking=True)
+                    off += u.chunk
+                    if cur is not None:
+                        ev = torch.cuda.Event()
+                        ev.record(self.d2h)
+                        events.append(ev)
+        if cur is not None:
+            cur.wait_stream(self.d2h)  # zero_grad_buffers() must not overtake the copies
+        # 2. CPU update unit by unit as grads land; bf16 results go back on the H2D stream
+        k = 0
+        nvme = self.device == "nvme"
+        for g, units in enumerate(opt.units):
+            pg = opt.optimizer.param_groups[g]
+            st = opt.optimizer.state[opt.master[g]]
+            if opt.kind in ("adam", "adagrad"):
+                st["step"] = int(st.get("step", 0)) + 1
+            if opt.kind == "generic":
+                self._generic(opt, g, events, k, coef)
+                k += len(units)
+                continue
+            off = 0
+            nslot = len(self.swapper.slots) if nvme else 0
+            pend = {}
+            if nvme and units:
+                pend[0] = self.swapper.read(0, g, 0, units[0].chunk)
+            for i, u in enumerate(units):
+                if nvme and i + 1 < len(units):
+                    pend[i + 1] = self.swapper.read((i + 1) % nslot, g, i + 1, units[i + 1].chunk)
+                if events:
+                    events[k].synchronize()
+                grad = opt.grad_host[g][off:off + u.chunk]
+                if nvme:
+                    self.swapper.rd.wait_request(pend.pop(i))
+                    views = self.swapper.views(i % nslot, u.chunk)
+                    master, states = views[0], views[1:]
+                else:
+                    master, states = u.master, self._state_views(opt, g, off, u.chunk)
+                lp = u.shard if not u.shard.is_cuda else opt.lp_host[g][off:off + u.chunk]
+                self._host_kernel(opt, pg, st, master, grad, states, lp, coef)
+                if nvme:
+                    self.swapper.write(i % nslot, g, i, u.chunk)
+                if u.shard.is_cuda:
+                    with get_accelerator().stream(self.h2d):
+                        u.shard.copy_(lp, non_blocking=True)
+                off += u.chunk
+                k += 1
+        if nvme:
+            self.swapper.drain()
+        if cur is not None:
+            self._h2d_done = torch.cuda.Event()
+            self._h2d_done.record(self.h2d)
+            cur.wait_stream(self.h2d)
+
+    def _generic(self, opt, g, events, k, coef):
+        units = opt.units[g]
+        for j in range(len(units)):
+            if events:
+                events[k + j].synchronize()
+        m = opt.master[g]
+        m.grad = opt.grad_host[g] * coef
+        # step only this group's params
+        saved = [pg["params"] for pg in opt.optimizer.param_groups]
+        for j, pg in enumerate(opt.optimizer.param_groups):
+            pg["params"] = saved[j] if j == g else []
+        opt.optimizer.step()
+        for j, pg in enumerate(opt.optimizer.param_groups):
+            pg["params"] = saved[j]
+        m.grad = None
+        off = 0
+        for u in units:
+            if u.shard.is_cuda:
+                lp = opt.lp_host[g][off:off + u.chunk]
+                lp.copy_(u.master)
+                with get_accelerator().stream(self.h2d):
+                    u.shard.copy_(lp, non_blocking=True)
+            else:
+                u.shard.copy_(u.master)
+            off += u.chunk
+
+    # ------------------------------------------------------------------------- checkpoint support
+    def materialize(self, opt):
+        """NVMe: read every record into full host tensors (master + optimizer state) so the usual
+        state_dict() sees them. No-op for cpu offload."""
+        if self.device != "nvme" or self.materialized:
+            return
+        sw = self.swapper
+        for g, units in enumerate(opt.units):
+            total = sum(u.chunk for u in units)
+            full = [torch.empty(total, dtype=torch.float32) for _ in range(sw.nkinds)]
+            off = 0
+            for i, u in enumerate(units):
+                sw.rd.wait_request(sw.read(0, g, i, u.chunk))
+                for dst, src in zip(full, sw.views(0, u.chunk)):
+                    dst[off:off + u.chunk].copy_(src)
+                u.master = full[0][off:off + u.chunk]
+                off += u.chunk
+            opt.master[g].data = full[0]
+            st = opt.optimizer.state[opt.master[g]]
+            names = {"adam": ["exp_avg", "exp_avg_sq"], "lion": ["exp_avg"], "adagrad": ["sum"]}[opt.kind]
+            for name, t in zip(names, full[1:]):
+                st[name] = t
+        self.materialized = True
+
+    def flush(self, opt):
+        """NVMe: write materialized host tensors back to the swap files and drop them."""
+        if self.device != "nvme":
+            return
+        sw = self.swapper
+        names = {"adam": ["exp_avg", "exp_avg_sq"], "lion": ["exp_avg"], "adagrad": ["sum"]}[opt.kind]
+        for g, units in enumerate(opt.units):
+            st = opt.optimizer.state[opt.master[g]]
+            full = [opt.master[g].data] + [st[n] for n in names]
+            off = 0
+            for i, u in enumerate(units):
+                for dst, src in zip(sw.views(0, u.chunk), full):
+                    dst.copy_(src[off:off + u.chunk])
+                sw.write(0, g, i, u.chunk)
+                sw.drain()
+                u.master = None
+                off += u.chunk
+            opt.master[g].data = torch.empty(0, dtype=torch.float32)
+            for n in names:
+                st.pop(n, None)
+        self.materialized = False
+
+    def write_master(self, opt, u):
+        """After an external edit of a unit's bit16 shard: refresh its fp32 master."""
+        if self.device == "cpu":
+            u.master.copy_(u.shard.float().cpu() if u.shard.is_cuda else u.shard.float())
+            return
+        g = next(i for i, us in enumerate(opt.units) if any(x is u for x in us))
+        i = next(j for j, x in enumerate(opt.units[g]) if x is u)
+        sw = self.swapper
+        sw.rd.wait_request(sw.read(0, g, i, u.chunk))
+        sw.views(0, u.chunk)[0].copy_(u.shard.float().cpu() if u.shard.is_cuda else u.shard.float())
+        sw.write(0, g, i, u.chunk)
+        sw.drain()
+
+
+def OffloadOptimizer(*a, **kw):  # pragma: no cover - kept for the reference's class name
+    raise TypeError("use HostOptimizerStep via the engine's zero_optimization.offload_optimizer config")

@@ -31,7 +31,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
     def __init__(self, init_optimizer, *, stage=2, loss_scaler, clip_grad=0.0, dp_ranks=None, dp_group=None,
                  reduce_bucket_size=500_000_000, communication_data_type=None, overlap_comm=True,
                  shuffle_exchange_cfg=None, method=None, slice_count=None, rings=None, shuffle_step=None,
-                 mp_group=None, timers=None, average_master=False):
+                 mp_group=None, timers=None, average_master=False, host_step=None):
         acc = get_accelerator()
         device = torch.device(acc.current_device_name())
         self.stage = stage
@@ -56,6 +56,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         world_group = dp_group if self.shuffle_exchange_enabled else None
         super().__init__(init_optimizer, loss_scaler, clip_grad, slice_group, overflow_group=world_group,
                          mp_group=mp_group, device=device)
+        self.host_step = host_step
         self.comm_dtype = communication_data_type
         self.overlap_comm = overlap_comm
         self.comm_stream = acc.named_stream("zero_reduce") if (overlap_comm and acc.gpu) else None
@@ -218,8 +219,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         self.zero_grad_buffers()
         if self.se is not None:
             shards = [u.shard for units in self.units for u in units]
-            masters = [u.master for units in self.units for u in units]
-            self.se.sync(shards, masters)
+            self.se.sync(shards, self._device_masters())
         self._allgather_params()
         self.global_step += 1
 
@@ -252,6 +252,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                   "numel": u.numel, "padded": u.padded, "chunk": u.chunk} for u in units] for units in self.units]
 
     def state_dict(self):
+        self._host_materialize()
         return {
             "loss_scaler": self.loss_scaler.state_dict(),
             "dynamic_loss_scale": bool(getattr(self.loss_scaler, "dynamic", False)),
@@ -270,6 +271,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
     def load_state_dict(self, sd, load_optimizer_states=True, load_from_fp32_weights=True):
         self.loss_scaler.load_state_dict(sd["loss_scaler"])
         self.clip_grad = sd.get("clip_grad", self.clip_grad)
+        self._host_materialize()
         if load_optimizer_states:
             saved = sd["base_optimizer_state"]
             self.optimizer.load_state_dict(saved)
@@ -286,5 +288,6 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                 for u in units:
                     u.shard.copy_(u.master)
             self._allgather_params()
+        self._host_flush()
         if self.se is not None and sd.get("shuffle_exchange"):
             self.se.load_state_dict(sd["shuffle_exchange"])

@@ -100,7 +100,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
     def __init__(self, module, init_optimizer, *, loss_scaler, clip_grad=0.0, dp_ranks=None, dp_group=None,
                  prefetch_depth=2, param_persistence_threshold=100_000, communication_data_type=None,
                  unit_classes=None, shuffle_exchange_cfg=None, mp_group=None, timers=None, mics_shard_size=-1,
-                 average_master=False):
+                 average_master=False, host_step=None, offload_param=False):
         acc = get_accelerator()
         device = torch.device(acc.current_device_name())
         self.module = module
@@ -123,6 +123,12 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         super().__init__(init_optimizer, loss_scaler, clip_grad, part_group,
                          overflow_group=dp_group if self.se is not None else None, mp_group=mp_group,
                          device=device)
+        self.host_step = host_step
+        # ZeRO-Infinity parameter offload: partitioned bit16 shards live in pinned host memory and
+        # are DMA'd in on the all-gather stream at fetch time
+        self.offload_param = bool(offload_param)
+        if self.offload_param and self.se is not None:
+            raise NotImplementedError("offload_param with shuffle-exchange slices is not supported")
         self.S = self.topo.S
         self.prefetch_depth = max(0, int(prefetch_depth))
         self.persist_thr = int(param_persistence_threshold)
@@ -186,7 +192,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         u = FlatUnit(params, self.S, self.topo.offset, dtype, self.device, name=name, materialize_full=False)
         u.fg = fg
         u.owner = self
-        u.persistent = (self.S == 1) or (u.numel < self.persist_thr)
+        u.persistent = (self.S == 1 and not self.offload_param) or (u.numel < self.persist_thr)
         flat = torch.zeros(u.padded, dtype=dtype, device=self.device)
         with torch.no_grad():
             for p, o, n in zip(u.params, u.offsets, u.numels):
@@ -198,7 +204,11 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             u.shard = flat[u.lo:u.hi]
             u.state = AVAILABLE
         else:
-            u.shard = flat[u.lo:u.hi].clone()
+            if self.offload_param:
+                u.shard = torch.empty(u.chunk, dtype=dtype, pin_memory=flat.is_cuda)
+                u.shard.copy_(flat[u.lo:u.hi])
+            else:
+                u.shard = flat[u.lo:u.hi].clone()
             u.flat.untyped_storage().resize_(0)
             u.state = RELEASED
         u.event = None
@@ -319,7 +329,15 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             st.wait_stream(cur)
         with get_accelerator().stream(st):
             u.flat.untyped_storage().resize_(u.padded * u.flat.element_size())
-            dist.all_gather_into_tensor(u.flat, u.shard, group=self.topo.slice_group)
+            src = u.shard
+            if src.device != u.flat.device:
+                src = src.to(u.flat.device, non_blocking=True)
+                if st is not None:
+                    src.record_stream(st)
+            if self.S == 1:
+                u.flat.copy_(src)
+            else:
+                dist.all_gather_into_tensor(u.flat, src, group=self.topo.slice_group)
             if st is not None:
                 u.event = torch.cuda.Event()
                 u.event.record(st)
@@ -351,7 +369,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             self._release_unit(u)
 
     def _prefetch_after(self, fg, backward):
-        if self.prefetch_depth == 0 or self.S == 1:
+        if self.prefetch_depth == 0 or (self.S == 1 and not self.offload_param):
             return
         order = list(reversed(self.trace)) if backward else self.trace
         if fg.idx not in order:
@@ -441,8 +459,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         self._fused_update(coef, skip)
         self.zero_grad_buffers()
         if self.se is not None:
-            self.se.sync([u.shard for units in self.units for u in units],
-                         [u.master for units in self.units for u in units])
+            self.se.sync([u.shard for units in self.units for u in units], self._device_masters())
         self._refresh_persistent()
         self.global_step += 1
         # start gathering the first units of the next forward now
@@ -489,7 +506,10 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 dist.broadcast(u.flat, src=src_rank, group=group)
             if not u.persistent:
                 u.shard.copy_(u.flat[u.lo:u.hi])
-            u.master.copy_(u.shard.float())
+            if self.host_step is not None:
+                self.host_step.write_master(self, u)
+            else:
+                u.master.copy_(u.shard.float())
 
     # ----------------------------------------------------------------------------- checkpointing
     def shuffle_exchange(self):
@@ -509,6 +529,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                   "numel": u.numel, "padded": u.padded, "chunk": u.chunk} for u in units] for units in self.units]
 
     def state_dict(self):
+        self._host_materialize()
         return {
             "loss_scaler": self.loss_scaler.state_dict(),
             "dynamic_loss_scale": bool(getattr(self.loss_scaler, "dynamic", False)),
@@ -525,6 +546,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
 
     def load_state_dict(self, sd, load_optimizer_states=True, load_from_fp32_weights=True):
         self.loss_scaler.load_state_dict(sd["loss_scaler"])
+        self._host_materialize()
         if load_optimizer_states:
             self.optimizer.load_state_dict(sd["optimizer_state_dict"])
             for m in self.master:
@@ -537,6 +559,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         for units in self.units:
             for u in units:
                 u.shard.copy_(u.master)
+        self._host_flush()
         self._refresh_persistent()
         if self.se is not None and sd.get("shuffle_exchange"):
             self.se.load_state_dict(sd["shuffle_exchange"])

@@ -1,38 +1,99 @@
-"""Tune every GEMM shape of the Llama-3-8B training step with PyTorch TunableOp (hipBLASLt + rocBLAS
-solution search) on the MI355X and write the winners to a CSV that bench.py / the engine load.
+"""Tune the distinct GEMM shapes of the Llama-3-8B training step with PyTorch TunableOp (hipBLASLt
+solution search only, bounded per solution) and report tuned-vs-default TFLOP/s per shape.
 
-Runs a 2-layer model (identical GEMM shapes to the 32-layer one) for one fwd+bwd micro-step with
-tuning enabled. Prints a heartbeat so the box's silence watchdog sees progress.
+Standalone (no model): every shape is issued exactly like ops/linear.py issues it -- forward
+``x @ W.T``, input grad ``gy @ W``, weight grad ``gy.T @ x`` (bf16 out, and the fp32-accumulating
+``addmm.dtype_out`` the ZeRO buffers use). Writes the TunableOp CSV that
+runtime/gemm_tuning.py loads (SXE_TUNABLEOP_FILE or the packaged tuning/ file).
+
+usage: python tools/tune_gemms.py OUT.csv [tokens] [--max-ms 8] [--iters 10]
 """
-import os, sys, threading, time
-out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/tunableop_llama3_8b.csv"
-mbs = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-seq = int(sys.argv[3]) if len(sys.argv) > 3 else 2048
-import torch
-torch.cuda.tunable.enable(True)
-torch.cuda.tunable.tuning_enable(True)
-torch.cuda.tunable.set_filename(out)
-torch.cuda.tunable.set_max_tuning_duration(40)
-torch.cuda.tunable.set_max_tuning_iterations(30)
-sys.path.insert(0, ".")
-import shuffle_exchange_amd as sxe
-from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+import argparse
+import os
+import sys
+import threading
+import time
+
+ap = argparse.ArgumentParser()
+ap.add_argument("out")
+ap.add_argument("tokens", nargs="?", type=int, default=8192)
+ap.add_argument("--max-ms", type=int, default=8)
+ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--hidden", type=int, default=4096)
+ap.add_argument("--inter", type=int, default=14336)
+ap.add_argument("--qkv", type=int, default=6144)
+ap.add_argument("--vocab", type=int, default=128256)
+a = ap.parse_args()
+os.environ.setdefault("PYTORCH_TUNABLEOP_ROCBLAS_ENABLED", "0")
+import torch  # noqa: E402
+
 done = False
+
+
 def beat():
     t0 = time.time()
     while not done:
-        time.sleep(20); print(f"[tune] alive {time.time()-t0:.0f}s", flush=True)
+        time.sleep(20)
+        print(f"[tune] alive {time.time() - t0:.0f}s", flush=True)
+
+
 threading.Thread(target=beat, daemon=True).start()
-cfg = llama_config("llama3-8b", num_hidden_layers=2)
-with sxe.zero.Init(dtype=torch.bfloat16):
-    model = LlamaForCausalLM(cfg)
-ds = {"train_micro_batch_size_per_gpu": mbs, "bf16": {"enabled": True}, "zero_optimization": {"stage": 3},
-      "optimizer": {"type": "AdamW", "params": {"lr": 1e-4}}}
-eng, _, _, _ = sxe.initialize(model=model, config=ds)
-ids = torch.randint(0, cfg.vocab_size, (mbs, seq), device="cuda")
-for i in range(2):
-    loss = eng(ids, labels=ids); eng.backward(loss); eng.step()
-    torch.cuda.synchronize(); print(f"[tune] step {i} done", flush=True)
-torch.cuda.tunable.write_file()
+T, H = a.tokens, a.hidden
+layers = {"qkv": (a.qkv, H), "o": (H, H), "gate_up": (2 * a.inter, H), "down": (H, a.inter), "lm_head": (a.vocab, H)}
+dev = "cuda"
+
+
+def timeit(fn, n=10):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n
+
+
+cases = []
+for name, (N, K) in layers.items():
+    x = torch.randn(T, K, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
+    gy = torch.randn(T, N, device=dev, dtype=torch.bfloat16)
+    acc = torch.zeros(N, K, device=dev, dtype=torch.float32)
+    fl = 2.0 * T * N * K
+    cases.append((f"{name} fwd", fl, lambda x=x, w=w: x @ w.t()))
+    cases.append((f"{name} dgrad", fl, lambda gy=gy, w=w: gy @ w))
+    cases.append((f"{name} wgrad-bf16", fl, lambda gy=gy, x=x: gy.t() @ x))
+    cases.append((f"{name} wgrad-fp32acc", fl,
+                  lambda gy=gy, x=x, acc=acc: torch.ops.aten.addmm.dtype_out(acc, gy.t(), x, torch.float32, beta=1,
+                                                                              alpha=1, out=acc)))
+
+base = {}
+for nm, fl, fn in cases:
+    base[nm] = timeit(fn)
+    print(f"[default] {nm:24s} {base[nm] * 1e3:8.3f} ms {fl / base[nm] / 1e12:7.0f} TF/s", flush=True)
+
+tun = torch.cuda.tunable
+tun.enable(True)
+tun.tuning_enable(True)
+tun.set_filename(a.out)
+tun.set_max_tuning_duration(a.max_ms)
+tun.set_max_tuning_iterations(a.iters)
+for nm, fl, fn in cases:
+    t0 = time.time()
+    fn()
+    torch.cuda.synchronize()
+    print(f"[tuning] {nm} took {time.time() - t0:.1f}s", flush=True)
+tun.write_file()
+tun.tuning_enable(False)
+tot_b = tot_t = 0.0
+for nm, fl, fn in cases:
+    t = timeit(fn)
+    tot_b += base[nm]
+    tot_t += t
+    print(f"[tuned]   {nm:24s} {t * 1e3:8.3f} ms {fl / t / 1e12:7.0f} TF/s  (default {fl / base[nm] / 1e12:5.0f})",
+          flush=True)
+print(f"[tune] sum of shapes: default {tot_b * 1e3:.2f} ms -> tuned {tot_t * 1e3:.2f} ms", flush=True)
 done = True
-print("[tune] wrote", out, flush=True)
+print("[tune] wrote", a.out, flush=True)
+sys.exit(0)
