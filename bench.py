@@ -33,7 +33,14 @@ def main():
     ap.add_argument("--ac", action="store_true", help="activation checkpointing")
     ap.add_argument("--layers", type=int, default=None, help="override layer count (debug only; invalid for the metric)")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu = plumbing dry-run over gloo (tests only; invalid for the metric)")
     args = ap.parse_args()
+    on_gpu = args.device == "cuda"
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
 
     import shuffle_exchange_amd as sxe
     from shuffle_exchange_amd import comm as dist
@@ -49,7 +56,7 @@ def main():
     if args.layers:
         over["num_hidden_layers"] = args.layers
     cfg = llama_config(args.model, **over)
-    dev = torch.device("cuda", torch.cuda.current_device())
+    dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
     with sxe.zero.Init(dtype=torch.bfloat16):
         model = LlamaForCausalLM(cfg)
     ds_config = {
@@ -79,15 +86,15 @@ def main():
 
     for _ in range(args.warmup):
         loss = train_step()
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = train_step()
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -96,7 +103,7 @@ def main():
     tps = tokens / elapsed
     flops_tok = cfg.flops_per_token(args.seq)
     mfu_tflops = tps * flops_tok / args.gpus / 1e12
-    valid = args.layers is None and args.model == "llama3-8b" and args.stage == 3
+    valid = args.layers is None and args.model == "llama3-8b" and args.stage == 3 and on_gpu
     if rank == 0:
         out = {
             "metric": "tokens/sec Llama-3-8B ZeRO-3 bf16 (training, whole job)",
@@ -116,7 +123,7 @@ def main():
                        "parallelism": f"zero{args.stage}-dp{args.gpus}", "params": n_params,
                        "activation_checkpointing": args.ac, "optimizer": "AdamW(fp32 master, fused HIP)"},
             "tflops_per_gpu": round(mfu_tflops, 1),
-            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if on_gpu else None,
             "final_loss": round(float(loss.detach()), 4),
             "valid_for_metric": valid,
         }

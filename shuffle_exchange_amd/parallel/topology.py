@@ -91,7 +91,7 @@ class PipelineParallelGrid:
         self.data_parallel_size = max(topology.get_dim("data"), 1)
         self.pipe_parallel_size = max(topology.get_dim("pipe"), 1)
         self.model_parallel_size = max(topology.get_dim("model"), 1)
-        self.slice_parallel_size = self.model_parallel_size
+        self.slice_parallel_size = self.model_parallel_size * self.pipe_parallel_size
         assert topology.world_size() == self.world_size, "topology size must equal world size"
         coord = topology.get_coord(self.global_rank)
         self.stage_id = coord.pipe if "pipe" in topology.axes else 0
@@ -109,6 +109,14 @@ class PipelineParallelGrid:
         self.dp_group, self.dp_ranks = mk("data")
         self.pp_group, self.pp_ranks = mk("pipe")
         self.mp_group, self.mp_ranks = mk("model")
+        # "slice" = every rank holding a different piece of the same model replica (pipe x model),
+        # i.e. the ranks sharing this data-parallel coordinate (reference topology.py slice_proc_group)
+        self.slice_group, self.slice_ranks = None, [self.global_rank]
+        for d in range(self.data_parallel_size):
+            lst = sorted(topology.filter_match(data=d)) if "data" in topology.axes else list(range(self.world_size))
+            g = dist.new_group(lst)
+            if self.global_rank in lst:
+                self.slice_group, self.slice_ranks = g, lst
         self.ds_model_proc_group = self.mp_group
         # pipe-neighbour p2p groups are not needed: isend/irecv ride the world communicator.
         self.p2p_groups = None
@@ -154,13 +162,13 @@ class PipelineParallelGrid:
     get_tensor_model_parallel_group = get_model_parallel_group
 
     def get_slice_parallel_rank(self):
-        return self.model_parallel_id
+        return self.slice_ranks.index(self.global_rank)
 
     def get_slice_parallel_world_size(self):
         return self.slice_parallel_size
 
     def get_slice_parallel_group(self):
-        return self.mp_group
+        return self.slice_group
 
     def stage_to_global(self, stage_id, **kwargs):
         me = self._topo.get_coord(self.global_rank)._asdict()

@@ -264,7 +264,7 @@ class SXEEngine(nn.Module):
         zc = cfg.zero_config
         dp_ranks = groups.group_ranks("seq_data")
         dp_group = groups.get_sequence_data_parallel_group()
-        mp_group = groups.get_tensor_model_parallel_group() if groups.get_tensor_model_parallel_world_size() > 1 else None
+        mp_group = self._norm_group()
         se = self.shuffle_exchange_config
         off = zc.offload_optimizer
         host_step = None
@@ -294,6 +294,11 @@ class SXEEngine(nn.Module):
                 bucket_size=zc.reduce_bucket_size, mp_group=mp_group, shuffle_exchange_cfg=se)
 
         self.optimizer.sp_scale = float(cfg.sequence_parallel_size)
+
+    def _norm_group(self):
+        """Group over which the squared gradient norm is summed besides the ZeRO partition group
+        (ranks holding different pieces of one model replica)."""
+        return groups.get_tensor_model_parallel_group() if groups.get_tensor_model_parallel_world_size() > 1 else None
 
     def _configure_lr_scheduler(self, client_lr_scheduler):
         if client_lr_scheduler is not None:

@@ -189,6 +189,13 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         for units in self.units:
             for u in units:
                 if u.topo.S == 1:
+                    # grads still held in .grad (accumulated before the boundary, e.g. pipeline
+                    # micro-batches) go straight into the fp32 accumulator
+                    for i, p in enumerate(u.params):
+                        if p.grad is not None:
+                            o, n = u.offsets[i], u.numels[i]
+                            u.grad[o:o + n].add_(p.grad.reshape(-1))
+                            p.grad = None
                     continue
                 if u.pending > 0:
                     # params whose grads exist but whose hook did not fire (e.g. stage 1 grads
