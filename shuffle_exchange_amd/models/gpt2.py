@@ -13,7 +13,7 @@ import torch.nn.functional as F
 from ..ops.activation import bias_gelu
 from ..ops.attention import attention
 from ..ops.cross_entropy import cross_entropy
-from ..ops.linear import linear
+from ..ops.linear import Linear
 from ..ops.norm import LayerNorm
 
 
@@ -52,21 +52,29 @@ class GPT2Block(nn.Module):
         super().__init__()
         h = cfg.n_embd
         self.n_head = cfg.n_head
+        self.head_dim = h // cfg.n_head
         self.ln_1 = LayerNorm(h, cfg.layer_norm_epsilon)
-        self.c_attn = nn.Linear(h, 3 * h)
-        self.c_proj = nn.Linear(h, h)
+        self.c_attn = Linear(h, 3 * h)
+        self.c_proj = Linear(h, h)
         self.ln_2 = LayerNorm(h, cfg.layer_norm_epsilon)
-        self.c_fc = nn.Linear(h, 4 * h)
-        self.mlp_proj = nn.Linear(4 * h, h)
+        self.c_fc = Linear(h, 4 * h)
+        self.mlp_proj = Linear(4 * h, h)
+        self.c_attn._tp_layout = ("chunks", 3)
+        self.c_proj._tp_row_parallel = True
+        self.mlp_proj._tp_row_parallel = True
+
+    def tp_shard_(self, tp):
+        assert self.n_head % tp == 0
+        self.n_head //= tp
 
     def forward(self, x):
         B, S, H = x.shape
-        d = H // self.n_head
-        qkv = linear(self.ln_1(x), self.c_attn.weight, self.c_attn.bias).view(B, S, 3, self.n_head, d)
+        d = self.head_dim
+        qkv = self.c_attn(self.ln_1(x)).view(B, S, 3, self.n_head, d)
         o = attention(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], causal=True)
-        x = x + linear(o.reshape(B, S, H), self.c_proj.weight, self.c_proj.bias)
-        m = bias_gelu(linear(self.ln_2(x), self.c_fc.weight), self.c_fc.bias)
-        return x + linear(m, self.mlp_proj.weight, self.mlp_proj.bias)
+        x = x + self.c_proj(o.reshape(B, S, self.n_head * d))
+        m = bias_gelu(self.c_fc(self.ln_2(x), skip_bias=True), self.c_fc.bias)
+        return x + self.mlp_proj(m)
 
 
 class GPT2LMHeadModel(nn.Module):

@@ -25,7 +25,7 @@ from torch.utils.checkpoint import checkpoint
 from ..ops.activation import swiglu
 from ..ops.attention import attention_qkv_rope
 from ..ops.cross_entropy import fused_linear_cross_entropy
-from ..ops.linear import linear
+from ..ops.linear import Linear, linear
 from ..ops.norm import RMSNorm
 from ..ops.rope import RopeCache
 from ..sequence.layer import ulysses_qkv_attention
@@ -98,28 +98,38 @@ class LlamaAttention(nn.Module):
         super().__init__()
         self.cfg = cfg
         self.nq, self.nkv, self.d = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
-        self.qkv_proj = nn.Linear(cfg.hidden_size, (self.nq + 2 * self.nkv) * self.d, bias=False)
-        self.o_proj = nn.Linear(self.nq * self.d, cfg.hidden_size, bias=False)
+        self.qkv_proj = Linear(cfg.hidden_size, (self.nq + 2 * self.nkv) * self.d, bias=False)
+        self.o_proj = Linear(self.nq * self.d, cfg.hidden_size, bias=False)
+        # AutoTP: split q|k|v by heads (GQA-aware); nq/nkv become per-rank counts
+        self.qkv_proj._tp_layout = ("heads", [self.nq, self.nkv, self.nkv], self.d)
+        self.o_proj._tp_row_parallel = True
 
     def forward(self, x, rope: RopeCache, position_ids=None):
         B, S, _ = x.shape
-        qkv = linear(x, self.qkv_proj.weight).view(B, S, self.nq + 2 * self.nkv, self.d)
+        qkv = self.qkv_proj(x).view(B, S, self.nq + 2 * self.nkv, self.d)
         spg = _sp_group() if self.cfg.sequence_parallel else None
         if spg is not None:
             o = ulysses_qkv_attention(qkv, self.nq, self.nkv, rope, spg, position_ids, causal=True)
         else:
             o = attention_qkv_rope(qkv, self.nq, self.nkv, rope, position_ids, causal=True)
-        return linear(o.reshape(B, S, self.nq * self.d), self.o_proj.weight)
+        return self.o_proj(o.reshape(B, S, self.nq * self.d))
+
+    def tp_shard_(self, tp):
+        assert self.nq % tp == 0 and self.nkv % tp == 0, "heads must divide the TP degree"
+        self.nq //= tp
+        self.nkv //= tp
 
 
 class LlamaMLP(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
-        self.gate_up_proj = nn.Linear(cfg.hidden_size, 2 * cfg.intermediate_size, bias=False)
-        self.down_proj = nn.Linear(cfg.intermediate_size, cfg.hidden_size, bias=False)
+        self.gate_up_proj = Linear(cfg.hidden_size, 2 * cfg.intermediate_size, bias=False)
+        self.down_proj = Linear(cfg.intermediate_size, cfg.hidden_size, bias=False)
+        self.gate_up_proj._tp_layout = ("chunks", 2)
+        self.down_proj._tp_row_parallel = True
 
     def forward(self, x):
-        return linear(swiglu(linear(x, self.gate_up_proj.weight)), self.down_proj.weight)
+        return self.down_proj(swiglu(self.gate_up_proj(x)))
 
 
 class LlamaDecoderLayer(nn.Module):

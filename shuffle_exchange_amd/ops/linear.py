@@ -59,3 +59,11 @@ def linear(x, weight, bias=None):
     if weight.requires_grad and torch.is_grad_enabled() and hasattr(weight, "_sxe_grad_target"):
         return _Linear.apply(x, weight, bias)
     return F.linear(x, weight, bias)
+
+
+class Linear(torch.nn.Linear):
+    """``nn.Linear`` whose GEMMs go through ``linear`` (fused weight-grad into ZeRO buffers).
+    AutoTP swaps it for a column/row-parallel layer with the same call signature."""
+
+    def forward(self, x, skip_bias=False):
+        return linear(x, self.weight, None if skip_bias else self.bias)

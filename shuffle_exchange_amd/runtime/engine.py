@@ -46,6 +46,25 @@ _DTYPE = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16, 
           "float16": torch.float16, "bfloat16": torch.bfloat16}
 
 
+def _split_tp_replicated(model_parameters, tp):
+    """Separate TP-sharded from TP-replicated parameters so the global gradient norm counts the
+    replicated ones once (their grads are identical on every TP rank)."""
+    plist = list(model_parameters)
+    if plist and isinstance(plist[0], dict):
+        pgs = plist
+    else:
+        pgs = [{"params": plist}]
+    out = []
+    for pg in pgs:
+        sharded = [p for p in pg["params"] if getattr(p, "tensor_model_parallel", False)]
+        repl = [p for p in pg["params"] if not getattr(p, "tensor_model_parallel", False)]
+        if sharded:
+            out.append({**pg, "params": sharded})
+        if repl:
+            out.append({**pg, "params": repl, "norm_weight": 1.0 / tp})
+    return out
+
+
 class SXEEngine(nn.Module):
     def __init__(self, args=None, model=None, optimizer=None, model_parameters=None, training_data=None,
                  lr_scheduler=None, mpu=None, dist_init_required=None, collate_fn=None, config=None,
@@ -173,6 +192,11 @@ class SXEEngine(nn.Module):
     # ----------------------------------------------------------------------------------- model
     def _configure_distributed_model(self, model, dont_change_device):
         dtype = self.model_dtype()
+        tp = groups.get_tensor_model_parallel_world_size()
+        if tp > 1 and groups._Registry.mpu is None and not getattr(model, "_sxe_tp_size", 0):
+            # AutoTP training (reference engine.py:450-516 _configure_tensor_parallel)
+            from ..module_inject.auto_tp import tp_model_init
+            tp_model_init(model, tp, tp_group=groups.get_tensor_model_parallel_group())
         zero_init = any(hasattr(p, "ds_tensor") for p in model.parameters())
         if not zero_init:
             if dtype != torch.float32:
@@ -250,6 +274,9 @@ class SXEEngine(nn.Module):
         from ..moe.utils import has_moe_layers, split_params_into_different_moe_groups_for_optimizer
         if has_moe_layers(self.module)[0] and not isinstance(client_optimizer, torch.optim.Optimizer):
             model_parameters = split_params_into_different_moe_groups_for_optimizer(list(model_parameters))
+        tp = groups.get_tensor_model_parallel_world_size()
+        if tp > 1 and not isinstance(client_optimizer, torch.optim.Optimizer):
+            model_parameters = _split_tp_replicated(model_parameters, tp)
         if client_optimizer is not None and not callable(client_optimizer) or isinstance(client_optimizer,
                                                                                         torch.optim.Optimizer):
             basic = client_optimizer

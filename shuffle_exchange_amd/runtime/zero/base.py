@@ -99,11 +99,15 @@ class ZeroOptimizerBase:
         """Device-side: global grad norm over the partition group (unscaled), the clip/unscale
         coefficient and the skip (non-finite) flag. No host synchronisation."""
         sq = None
-        for gr in self.grads:
+        for g, gr in enumerate(self.grads):
             s = fused.sumsq(gr)
+            w = self.optimizer.param_groups[g].get("norm_weight", 1.0) if g < len(self.optimizer.param_groups) else 1.0
+            if w != 1.0:
+                s = s * w
             sq = s if sq is None else sq + s
         sq = sq.reshape(1).float()
-        dist.all_reduce(sq, group=self.partition_group)
+        if self.partition_group is not None:  # None = unpartitioned (replicated) optimizer state
+            dist.all_reduce(sq, group=self.partition_group)
         if self.mp_group is not None:
             dist.all_reduce(sq, group=self.mp_group)
         ls = float(self.loss_scaler.loss_scale)
