@@ -15,6 +15,7 @@ from .comm import init_distributed  # noqa: F401
 from .runtime.config import SXEConfig, DeepSpeedConfig  # noqa: F401
 from .runtime.engine import SXEEngine  # noqa: F401
 from .runtime import lr_schedules  # noqa: F401
+from .runtime.activation_checkpointing import checkpointing  # noqa: F401
 from .utils.logging import logger, log_dist  # noqa: F401
 
 __version__ = "0.1.0"

@@ -20,9 +20,9 @@ from typing import Optional
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
-from torch.utils.checkpoint import checkpoint
 
 from ..ops.activation import swiglu
+from ..runtime.activation_checkpointing.checkpointing import checkpoint
 from ..ops.attention import attention_qkv_rope
 from ..ops.cross_entropy import fused_linear_cross_entropy
 from ..ops.linear import Linear, linear
@@ -214,7 +214,7 @@ class LlamaForCausalLM(nn.Module):
         res = None
         for layer in self.layers:
             if self.cfg.activation_checkpointing and self.training and torch.is_grad_enabled():
-                x, res = checkpoint(layer, x, res, rope, position_ids, use_reentrant=False)
+                x, res = checkpoint(layer, x, res, rope, position_ids)
             else:
                 x, res = layer(x, res, rope, position_ids)
         h = self.norm(x, res)[0] if res is not None else self.norm(x)

@@ -9,9 +9,9 @@ from dataclasses import dataclass
 
 import torch
 import torch.nn as nn
-from torch.utils.checkpoint import checkpoint
 
 from ..moe.layer import MoE
+from ..runtime.activation_checkpointing.checkpointing import checkpoint
 from ..ops.norm import RMSNorm
 from .llama import LlamaAttention, LlamaConfig, LlamaForCausalLM, LMHeadLoss
 
@@ -94,7 +94,7 @@ class MixtralForCausalLM(LlamaForCausalLM):
         aux = []
         for layer in self.layers:
             if self.cfg.activation_checkpointing and self.training and torch.is_grad_enabled():
-                x, res, l_aux = checkpoint(layer, x, res, rope, position_ids, use_reentrant=False)
+                x, res, l_aux = checkpoint(layer, x, res, rope, position_ids)
             else:
                 x, res, l_aux = layer(x, res, rope, position_ids)
             aux.append(l_aux)

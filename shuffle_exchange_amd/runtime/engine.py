@@ -108,6 +108,8 @@ class SXEEngine(nn.Module):
                                        if v is not None})
         self.shuffle_exchange_config = se
         self.timers = SynchronizedWallClockTimer() if cfg.wall_clock_breakdown else NoopTimer()
+        from .activation_checkpointing import checkpointing as _ac
+        _ac.configure(mpu, deepspeed_config=cfg)
         self.module = model
         self._configure_distributed_model(model, dont_change_device)
         self.tput_timer = ThroughputTimer(batch_size=cfg.train_batch_size, steps_per_output=cfg.steps_per_print,

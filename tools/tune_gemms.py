@@ -84,8 +84,7 @@ for nm, fl, fn in cases:
     fn()
     torch.cuda.synchronize()
     print(f"[tuning] {nm} took {time.time() - t0:.1f}s", flush=True)
-tun.write_file()
-tun.tuning_enable(False)
+tun.tuning_enable(False)  # results are flushed to the file at exit
 tot_b = tot_t = 0.0
 for nm, fl, fn in cases:
     t = timeit(fn)
