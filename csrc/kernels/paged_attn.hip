@@ -1,0 +1,365 @@
+// Ragged / paged-KV attention for the FastGen-style inference engine (gfx950).
+//
+// Parity: reference inference/v2/kernels/ragged_ops/linear_blocked_kv_rotary (KV append into the
+// blocked cache) and ragged_ops/blocked_flash (attention over blocked KV; the reference links an
+// external flash-attn build for sm80+). Designed for MI355X instead:
+//
+//  * cache layout per layer: [num_blocks, 2 (k|v), n_kv_heads, block_size, D] bf16 -- the keys of
+//    one (block, head) are one contiguous run, so a wave reading 64 consecutive keys streams
+//    64 x 256 B = 16 KB with no stride;
+//  * one workgroup (4 waves, 256 threads) per (sequence, kv head, KV split): all G = nq/nkv query
+//    heads of the GQA group (x the sequence's new tokens) share every K/V byte loaded, so decode is
+//    pure HBM streaming at the GQA-reduced byte count;
+//  * key phase: lane = key (K row in 16 B vector registers, q rows broadcast from LDS); value phase:
+//    lane = 2 output dims, V rows read coalesced; probabilities hop through LDS;
+//  * flash-decoding split over the KV length when (sequences x kv heads) is too small to fill the
+//    256 CUs, merged by a second kernel (fp32 partials);
+//  * causal masking by absolute position (chunked prefill / speculative tokens just work).
+#include "sxe_common.h"
+#include <torch/library.h>
+
+namespace sxe {
+namespace pa {
+
+constexpr int kRows = 16;     // query rows (token x head-in-group) per pass
+constexpr int kWaves = 4;
+constexpr float kLog2e = 1.4426950408889634f;
+
+template <int D>
+__global__ __launch_bounds__(256) void kv_append_kernel(const unsigned short* __restrict qkv, int64_t tok_stride,
+                                                        int nq, int nkv, const int64_t* __restrict slots,
+                                                        unsigned short* __restrict cache, int bs) {
+  const int t = blockIdx.x;
+  const int64_t slot = slots[t];
+  if (slot < 0) return;
+  const int64_t blk = slot / bs, off = slot % bs;
+  constexpr int V = D / 8;
+  const int total = 2 * nkv * V;
+  for (int i = threadIdx.x; i < total; i += blockDim.x) {
+    const int kv = i / (nkv * V);
+    const int rem = i - kv * nkv * V;
+    const int h = rem / V, v = rem - h * V;
+    const unsigned short* src = qkv + (int64_t)t * tok_stride + (int64_t)(nq + kv * nkv + h) * D + v * 8;
+    unsigned short* dst = cache + (((blk * 2 + kv) * nkv + h) * bs + off) * D + v * 8;
+    *reinterpret_cast<u16x8*>(dst) = *reinterpret_cast<const u16x8*>(src);
+  }
+}
+
+struct Args {
+  const unsigned short* q;
+  int64_t q_tok_stride;  // elements between consecutive tokens (heads are D apart)
+  const unsigned short* cache;
+  const int* block_table;
+  int max_blocks;
+  const int* q_start;
+  const int* q_len;
+  const int* kv_len;
+  int nq, nkv, bs;
+  float scale_log2;
+  int splits, keys_per_split;
+  unsigned short* out;
+  int64_t out_tok_stride;
+  float* part_o;   // [splits, T, nq, D]
+  float* part_ml;  // [splits, T, nq, 2]
+  int T;
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void paged_attn_kernel(Args a) {
+  constexpr int DPL = D / 64;  // output dims per lane in the value phase
+  constexpr int KV16 = D / 8;  // 16-byte vectors per K row
+  __shared__ float q_lds[kRows][D];
+  __shared__ float p_lds[kWaves][kRows][64];
+  __shared__ float mrg_o[kWaves][kRows][D];
+  __shared__ float mrg_ml[kWaves][kRows][2];
+
+  const int seq = blockIdx.x / a.nkv, kvh = blockIdx.x - (blockIdx.x / a.nkv) * a.nkv;
+  const int split = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int G = a.nq / a.nkv;
+  const int qs = a.q_start[seq], ql = a.q_len[seq], kl = a.kv_len[seq];
+  const int k_begin = split * a.keys_per_split;
+  const int k_end = min(kl, k_begin + a.keys_per_split);
+  const int nrows_total = ql * G;
+  const int* bt = a.block_table + (int64_t)seq * a.max_blocks;
+  const int64_t head_stride = (int64_t)a.bs * D;          // between kv heads inside a block half
+  const int64_t half_stride = (int64_t)a.nkv * head_stride;  // k half -> v half
+  const int64_t block_stride = 2 * half_stride;
+
+  for (int row0 = 0; row0 < nrows_total; row0 += kRows) {
+    const int nrows = min(kRows, nrows_total - row0);
+    // ---- q rows -> LDS (fp32, pre-scaled by softmax scale * log2 e) -------------------------
+    for (int i = threadIdx.x; i < kRows * D; i += 256) {
+      const int r = i / D, d = i - r * D;
+      float v = 0.f;
+      if (r < nrows) {
+        const int row = row0 + r, tok = row / G, g = row - tok * G;
+        v = bf16_to_f32(a.q[(int64_t)(qs + tok) * a.q_tok_stride + (int64_t)(kvh * G + g) * D + d]) * a.scale_log2;
+      }
+      q_lds[r][d] = v;
+    }
+    __syncthreads();
+    const int max_pos = kl - ql + (row0 + nrows - 1) / G;  // causal horizon of this tile
+    const int k_hi = min(k_end, max_pos + 1);
+    float m[kRows], l[kRows], o[kRows][DPL];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      m[r] = -INFINITY;
+      l[r] = 0.f;
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) o[r][j] = 0.f;
+    }
+    for (int kb = k_begin + wave * 64; kb < k_hi; kb += kWaves * 64) {
+      // ---- key phase: lane = key ------------------------------------------------------------
+      const int key = kb + lane;
+      const bool valid = key < k_hi;
+      u16x8 kr[KV16];
+      if (valid) {
+        const int blk = bt[key / a.bs], off = key - (key / a.bs) * a.bs;
+        const unsigned short* kp = a.cache + (int64_t)blk * block_stride + kvh * head_stride + (int64_t)off * D;
+#pragma unroll
+        for (int v = 0; v < KV16; ++v) kr[v] = *reinterpret_cast<const u16x8*>(kp + v * 8);
+      } else {
+#pragma unroll
+        for (int v = 0; v < KV16; ++v) kr[v] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+      float s[kRows];
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) s[r] = 0.f;
+#pragma unroll
+      for (int v = 0; v < KV16; ++v) {
+        float kf[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) kf[e] = bf16_to_f32(kr[v][e]);
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+          if (r < nrows) {
+            const f32x4 q0 = *reinterpret_cast<const f32x4*>(&q_lds[r][v * 8]);
+            const f32x4 q1 = *reinterpret_cast<const f32x4*>(&q_lds[r][v * 8 + 4]);
+            s[r] += q0[0] * kf[0] + q0[1] * kf[1] + q0[2] * kf[2] + q0[3] * kf[3] + q1[0] * kf[4] + q1[1] * kf[5] +
+                    q1[2] * kf[6] + q1[3] * kf[7];
+          }
+        }
+      }
+      // ---- online softmax per row -----------------------------------------------------------
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) {
+        if (r < nrows) {
+          const int pos = kl - ql + (row0 + r) / G;
+          const float sv = (valid && key <= pos) ? s[r] : -INFINITY;
+          const float mx = wave_max(sv);
+          const float mn = fmaxf(m[r], mx);
+          float p = 0.f, alpha = 1.f;
+          if (mn != -INFINITY) {
+            p = (sv == -INFINITY) ? 0.f : exp2f(sv - mn);
+            alpha = (m[r] == -INFINITY) ? 0.f : exp2f(m[r] - mn);
+          }
+          l[r] = l[r] * alpha + wave_sum(p);
+#pragma unroll
+          for (int j = 0; j < DPL; ++j) o[r][j] *= alpha;
+          m[r] = mn;
+          p_lds[wave][r][lane] = p;
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): p_lds visible within the wave
+      __builtin_amdgcn_wave_barrier();
+      // ---- value phase: lane = DPL output dims ------------------------------------------------
+      const int nk = min(64, k_hi - kb);
+      for (int j = 0; j < nk; ++j) {
+        const int kj = kb + j;
+        const int blk = bt[kj / a.bs], off = kj - (kj / a.bs) * a.bs;
+        const unsigned short* vp =
+            a.cache + (int64_t)blk * block_stride + half_stride + kvh * head_stride + (int64_t)off * D + lane * DPL;
+        float vv[DPL];
+        if constexpr (DPL == 2) {
+          const unsigned int w = *reinterpret_cast<const unsigned int*>(vp);
+          vv[0] = bf16_to_f32(w & 0xffff);
+          vv[1] = bf16_to_f32(w >> 16);
+        } else {
+#pragma unroll
+          for (int e = 0; e < DPL; ++e) vv[e] = bf16_to_f32(vp[e]);
+        }
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+          if (r < nrows) {
+            const float p = p_lds[wave][r][j];
+#pragma unroll
+            for (int e = 0; e < DPL; ++e) o[r][e] += p * vv[e];
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    // ---- merge the 4 waves ------------------------------------------------------------------
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      if (r < nrows) {
+#pragma unroll
+        for (int e = 0; e < DPL; ++e) mrg_o[wave][r][lane * DPL + e] = o[r][e];
+        if (lane == 0) {
+          mrg_ml[wave][r][0] = m[r];
+          mrg_ml[wave][r][1] = l[r];
+        }
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nrows * D; i += 256) {
+      const int r = i / D, d = i - r * D;
+      float M = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) M = fmaxf(M, mrg_ml[w][r][0]);
+      float acc = 0.f, L = 0.f;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) {
+        const float mw = mrg_ml[w][r][0];
+        const float f = (mw == -INFINITY) ? 0.f : exp2f(mw - M);
+        acc += f * mrg_o[w][r][d];
+        L += f * mrg_ml[w][r][1];
+      }
+      const int row = row0 + r, tok = row / G, g = row - tok * G;
+      const int t = qs + tok, h = kvh * G + g;
+      if (a.splits == 1) {
+        a.out[(int64_t)t * a.out_tok_stride + (int64_t)h * D + d] = f32_to_bf16(L > 0.f ? acc / L : 0.f);
+      } else {
+        const int64_t idx = ((int64_t)split * a.T + t) * a.nq + h;
+        a.part_o[idx * D + d] = acc;
+        if (d == 0) {
+          a.part_ml[idx * 2 + 0] = M;
+          a.part_ml[idx * 2 + 1] = L;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(D) void merge_kernel(const float* __restrict part_o, const float* __restrict part_ml,
+                                                  int splits, int T, int nq, unsigned short* __restrict out,
+                                                  int64_t out_tok_stride) {
+  const int th = blockIdx.x;  // t * nq + h
+  const int t = th / nq, h = th - t * nq;
+  const int d = threadIdx.x;
+  float M = -INFINITY;
+  for (int s = 0; s < splits; ++s) M = fmaxf(M, part_ml[((int64_t)s * T * nq + th) * 2]);
+  float acc = 0.f, L = 0.f;
+  for (int s = 0; s < splits; ++s) {
+    const int64_t idx = (int64_t)s * T * nq + th;
+    const float ms = part_ml[idx * 2];
+    if (ms == -INFINITY) continue;
+    const float f = exp2f(ms - M);
+    acc += f * part_o[idx * D + d];
+    L += f * part_ml[idx * 2 + 1];
+  }
+  out[(int64_t)t * out_tok_stride + (int64_t)h * D + d] = f32_to_bf16(L > 0.f ? acc / L : 0.f);
+}
+
+}  // namespace pa
+
+// qkv: [T, nq + 2 nkv, D] bf16 (token stride may exceed the row); slots: [T] int64 (-1 = skip)
+void kv_cache_append(const at::Tensor& qkv, at::Tensor cache, const at::Tensor& slots, int64_t nq, int64_t nkv) {
+  SXE_CHECK_CUDA(qkv);
+  SXE_CHECK(qkv.scalar_type() == at::kBFloat16 && cache.scalar_type() == at::kBFloat16, "bf16 only");
+  SXE_CHECK(qkv.dim() == 3 && qkv.stride(2) == 1 && qkv.stride(1) == qkv.size(2), "qkv must be [T, H, D] row-major");
+  SXE_CHECK(cache.dim() == 5 && cache.is_contiguous(), "cache must be [blocks, 2, nkv, bs, D]");
+  SXE_CHECK(slots.scalar_type() == at::kLong && slots.numel() == qkv.size(0), "slots: int64 [T]");
+  const int D = qkv.size(2);
+  const int T = qkv.size(0);
+  if (T == 0) return;
+  c10::DeviceGuard g(qkv.device());
+  auto* q = reinterpret_cast<const unsigned short*>(qkv.data_ptr());
+  auto* c = reinterpret_cast<unsigned short*>(cache.data_ptr());
+  const int bs = cache.size(3);
+  if (D == 128)
+    hipLaunchKernelGGL(pa::kv_append_kernel<128>, dim3(T), dim3(256), 0, cur_stream(), q, qkv.stride(0), (int)nq,
+                       (int)nkv, slots.data_ptr<int64_t>(), c, bs);
+  else if (D == 64)
+    hipLaunchKernelGGL(pa::kv_append_kernel<64>, dim3(T), dim3(256), 0, cur_stream(), q, qkv.stride(0), (int)nq,
+                       (int)nkv, slots.data_ptr<int64_t>(), c, bs);
+  else
+    SXE_CHECK(false, "kv_cache_append: head_dim must be 64 or 128");
+  SXE_LAUNCH_CHECK();
+}
+
+// q: [T, nq, D] (token stride free); returns out [T, nq, D] bf16
+at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const at::Tensor& block_table,
+                           const at::Tensor& q_start, const at::Tensor& q_len, const at::Tensor& kv_len, double scale,
+                           int64_t max_kv_len, int64_t splits) {
+  SXE_CHECK_CUDA(q);
+  SXE_CHECK(q.scalar_type() == at::kBFloat16 && cache.scalar_type() == at::kBFloat16, "bf16 only");
+  SXE_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == q.size(2), "q must be [T, nq, D] with head stride D");
+  SXE_CHECK(cache.dim() == 5 && cache.is_contiguous(), "cache must be [blocks, 2, nkv, bs, D]");
+  SXE_CHECK(block_table.scalar_type() == at::kInt && block_table.is_contiguous() && block_table.dim() == 2,
+            "block_table int32 [S, max_blocks]");
+  for (auto* t : {&q_start, &q_len, &kv_len})
+    SXE_CHECK(t->scalar_type() == at::kInt && t->is_contiguous() && t->numel() == block_table.size(0),
+              "q_start/q_len/kv_len: int32 [S]");
+  const int T = q.size(0), nq = q.size(1), D = q.size(2);
+  const int nkv = cache.size(2), bs = cache.size(3);
+  SXE_CHECK(cache.size(4) == D && nq % nkv == 0, "head layout mismatch");
+  const int S = block_table.size(0);
+  auto out = at::empty({T, nq, D}, q.options());
+  if (T == 0 || S == 0) return out;
+  c10::DeviceGuard g(q.device());
+  splits = std::max<int64_t>(1, splits);
+  int64_t kps = (std::max<int64_t>(max_kv_len, 1) + splits - 1) / splits;
+  kps = (kps + 63) / 64 * 64;
+  splits = (std::max<int64_t>(max_kv_len, 1) + kps - 1) / kps;
+  at::Tensor part_o, part_ml;
+  pa::Args a;
+  a.q = reinterpret_cast<const unsigned short*>(q.data_ptr());
+  a.q_tok_stride = q.stride(0);
+  a.cache = reinterpret_cast<const unsigned short*>(cache.data_ptr());
+  a.block_table = block_table.data_ptr<int>();
+  a.max_blocks = block_table.size(1);
+  a.q_start = q_start.data_ptr<int>();
+  a.q_len = q_len.data_ptr<int>();
+  a.kv_len = kv_len.data_ptr<int>();
+  a.nq = nq;
+  a.nkv = nkv;
+  a.bs = bs;
+  a.scale_log2 = (float)scale * pa::kLog2e;
+  a.splits = (int)splits;
+  a.keys_per_split = (int)kps;
+  a.out = reinterpret_cast<unsigned short*>(out.data_ptr());
+  a.out_tok_stride = out.stride(0);
+  a.T = T;
+  a.part_o = nullptr;
+  a.part_ml = nullptr;
+  if (splits > 1) {
+    part_o = at::empty({splits, T, nq, D}, q.options().dtype(at::kFloat));
+    part_ml = at::empty({splits, T, nq, 2}, q.options().dtype(at::kFloat));
+    a.part_o = part_o.data_ptr<float>();
+    a.part_ml = part_ml.data_ptr<float>();
+  }
+  dim3 grid(S * nkv, splits);
+  if (D == 128)
+    hipLaunchKernelGGL(pa::paged_attn_kernel<128>, grid, dim3(256), 0, cur_stream(), a);
+  else if (D == 64)
+    hipLaunchKernelGGL(pa::paged_attn_kernel<64>, grid, dim3(256), 0, cur_stream(), a);
+  else
+    SXE_CHECK(false, "paged_attention: head_dim must be 64 or 128");
+  SXE_LAUNCH_CHECK();
+  if (splits > 1) {
+    if (D == 128)
+      hipLaunchKernelGGL(pa::merge_kernel<128>, dim3(T * nq), dim3(128), 0, cur_stream(), a.part_o, a.part_ml,
+                         (int)splits, T, nq, a.out, a.out_tok_stride);
+    else
+      hipLaunchKernelGGL(pa::merge_kernel<64>, dim3(T * nq), dim3(64), 0, cur_stream(), a.part_o, a.part_ml,
+                         (int)splits, T, nq, a.out, a.out_tok_stride);
+    SXE_LAUNCH_CHECK();
+  }
+  return out;
+}
+
+}  // namespace sxe
+
+TORCH_LIBRARY_FRAGMENT(sxe, m) {
+  m.def("kv_cache_append(Tensor qkv, Tensor(a!) cache, Tensor slots, int nq, int nkv) -> ()");
+  m.def("paged_attention(Tensor q, Tensor cache, Tensor block_table, Tensor q_start, Tensor q_len, Tensor kv_len, "
+        "float scale, int max_kv_len, int splits) -> Tensor");
+}
+TORCH_LIBRARY_IMPL(sxe, CUDA, m) {
+  m.impl("kv_cache_append", &sxe::kv_cache_append);
+  m.impl("paged_attention", &sxe::paged_attention);
+}

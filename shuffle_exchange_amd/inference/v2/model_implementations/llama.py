@@ -1,0 +1,139 @@
+"""Ragged (continuous-batching) forward for the Llama / Mixtral families over a paged KV cache.
+
+Parity: reference inference/v2/model_implementations/llama_v2/model.py and mixtral/model.py
+(``_forward_embed`` / ``_forward_transformer_layer`` / ``_forward_unembed``), with the module
+choices the reference makes through its registry (blocked KV rotary, blocked flash, pre-RMS norm,
+BLAS linear, cutlass MoE GEMM) replaced by this framework's gfx950 kernels:
+
+  * RMSNorm with fused residual add (norm.hip), projections through hipBLASLt,
+  * RoPE in place on the packed QKV (rope.hip), KV scatter into the blocked cache and paged
+    attention (paged_attn.hip); sequences in pure prefill (no history, >= 128 new tokens) run the
+    training flash-attention kernel instead (MFMA, causal; their padding rows are discarded),
+  * SwiGLU (act.hip); Mixtral experts via the grouped MoE path of moe/,
+  * only the last token of every sequence goes through the final norm + LM head.
+The weights are the training modules' own parameters (no copy): a trained LlamaForCausalLM /
+MixtralForCausalLM serves directly.
+"""
+import torch
+import torch.nn.functional as F
+
+from ....ops import native
+from ....ops.activation import swiglu
+from ....ops.paged_attention import kv_cache_append, paged_attention
+from ....ops.rope import apply_rope_tokens_
+
+FLASH_PREFILL_MIN = 128
+
+
+class RaggedLlama:
+    def __init__(self, model):
+        self.model = model
+        self.cfg = model.cfg
+        self.is_moe = hasattr(model.layers[0], "block_sparse_moe") or hasattr(model.layers[0], "moe")
+        a0 = model.layers[0].self_attn
+        self.nq, self.nkv, self.head_dim = a0.nq, a0.nkv, a0.d
+        self.num_layers = len(model.layers)
+        self.vocab_size = self.cfg.vocab_size
+
+    @property
+    def device(self):
+        return next(self.model.parameters()).device
+
+    @property
+    def dtype(self):
+        return next(self.model.parameters()).dtype
+
+    def _attention(self, qkv, kv_layer, batch):
+        nq, D = self.nq, self.head_dim
+        scale = D ** -0.5
+        q = qkv[:, :nq]
+        use_flash = native.use_hip(qkv) and D == 128 and qkv.dtype == torch.bfloat16
+        flash_ids = [i for i in range(batch.num_seqs)
+                     if use_flash and batch.host_seen[i] == 0 and batch.host_q_len[i] >= FLASH_PREFILL_MIN] \
+            if use_flash else []
+        if not flash_ids:
+            return paged_attention(q, kv_layer, batch.block_table, batch.q_start, batch.q_len, batch.kv_len, scale,
+                                   batch.max_kv_len)
+        out = torch.empty(qkv.shape[0], nq, D, dtype=qkv.dtype, device=qkv.device)
+        fset = set(flash_ids)
+        rest = [i for i in range(batch.num_seqs) if i not in fset]
+        for i in flash_ids:
+            s, n = batch.host_q_start[i], batch.host_q_len[i]
+            pad = (-n) % 128
+            x = qkv[s:s + n]
+            if pad:
+                x = torch.cat([x, x.new_zeros(pad, *x.shape[1:])])
+            x = x.unsqueeze(0)
+            o, _ = torch.ops.sxe.flash_attn_fwd(x[:, :, :nq], x[:, :, nq:nq + self.nkv], x[:, :, nq + self.nkv:],
+                                                True, float(scale))
+            out[s:s + n] = o[0, :n]
+        if rest:
+            idx = torch.tensor(rest, device=qkv.device)
+            o = paged_attention(q, kv_layer, batch.block_table.index_select(0, idx).contiguous(),
+                                batch.q_start.index_select(0, idx).contiguous(),
+                                batch.q_len.index_select(0, idx).contiguous(),
+                                batch.kv_len.index_select(0, idx).contiguous(), scale,
+                                max(batch.host_kv_len[i] for i in rest))
+            for i in rest:
+                s, n = batch.host_q_start[i], batch.host_q_len[i]
+                out[s:s + n] = o[s:s + n]
+        return out
+
+    def _mlp(self, layer, m):
+        if hasattr(layer, "mlp"):
+            mlp = layer.mlp
+            return mlp.down_proj(swiglu(mlp.gate_up_proj(m)))
+        moe = layer.block_sparse_moe if hasattr(layer, "block_sparse_moe") else layer.moe
+        return self._moe_dropless(moe.deepspeed_moe, m)
+
+    def _moe_dropless(self, moe, m):
+        """Exact top-k routing for inference (no capacity, no dropped tokens): tokens are grouped
+        by expert (one argsort), each expert runs its two GEMMs on its rows, results are scattered
+        back weighted by the renormalised top-k gate probabilities (reference
+        ragged_ops/top_k_gating + moe_scatter + moe_gather)."""
+        gate, ex = moe.gate, moe.experts
+        assert moe.ep_size == 1, "ragged inference runs experts locally (ep_size == 1)"
+        k = gate.k
+        probs = torch.softmax(F.linear(m.float(), gate.wg.weight.float()), dim=-1)
+        topw, topi = probs.topk(k, dim=-1)
+        topw = topw / topw.sum(-1, keepdim=True)
+        flat = topi.reshape(-1)
+        order = torch.argsort(flat, stable=True)
+        tok = order // k
+        counts = torch.bincount(flat, minlength=ex.num_local_experts).tolist()
+        xs = m.index_select(0, tok)
+        ws = topw.reshape(-1).index_select(0, order).to(m.dtype).unsqueeze(1)
+        out = torch.zeros_like(m)
+        o = 0
+        for e, c in enumerate(counts):
+            if c == 0:
+                continue
+            y = torch.matmul(swiglu(torch.matmul(xs[o:o + c], ex.w_gate_up[e])), ex.w_down[e])
+            out.index_add_(0, tok[o:o + c], y * ws[o:o + c])
+            o += c
+        return out
+
+    @torch.no_grad()
+    def forward(self, batch, kv_cache):
+        model = self.model
+        rope = model.rope(self.device)
+        T = batch.num_tokens
+        x = model.embed_tokens(batch.input_ids)
+        res = None
+        for li, layer in enumerate(model.layers):
+            if res is None:
+                a, h = layer.input_layernorm(x), x
+            else:
+                a, h = layer.input_layernorm(x, res)
+            attn = layer.self_attn
+            qkv = attn.qkv_proj(a).view(T, self.nq + 2 * self.nkv, self.head_dim)
+            apply_rope_tokens_(qkv, rope, self.nq + self.nkv, batch.positions)
+            kv_layer = kv_cache.layer(li)
+            kv_cache_append(qkv, kv_layer, batch.slots, self.nq, self.nkv)
+            o = self._attention(qkv, kv_layer, batch)
+            o = attn.o_proj(o.reshape(T, self.nq * self.head_dim))
+            m, h2 = layer.post_attention_layernorm(o, h)
+            x, res = self._mlp(layer, m), h2
+        last = batch.last_idx
+        h = model.norm(x.index_select(0, last), res.index_select(0, last))[0]
+        return F.linear(h, model.lm_head.weight).float()

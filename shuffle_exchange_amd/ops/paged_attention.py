@@ -1,0 +1,79 @@
+"""Paged-KV attention ops for the ragged inference engine (HIP kernels in csrc/kernels/paged_attn.hip).
+
+Cache layout per layer: ``[num_blocks, 2, n_kv_heads, block_size, head_dim]`` (bf16 on GPU).
+``kv_cache_append`` scatters the k/v rows of the new tokens into their slots
+(``slot = block_id * block_size + offset``); ``paged_attention`` runs causal attention of the new
+tokens of each sequence over all of its cached keys. Both have PyTorch reference implementations
+(CPU processes / numerics oracles).
+"""
+import math
+
+import torch
+
+from . import native
+
+
+def kv_cache_append(qkv, cache, slots, nq, nkv):
+    """qkv: [T, nq + 2 nkv, D]; cache: [blocks, 2, nkv, bs, D]; slots: int64 [T] (-1 = skip)."""
+    if native.use_hip(qkv):
+        torch.ops.sxe.kv_cache_append(qkv, cache, slots, int(nq), int(nkv))
+        return
+    bs = cache.shape[3]
+    ok = slots >= 0
+    if not bool(ok.any()):
+        return
+    s = slots[ok]
+    blk, off = s // bs, s % bs
+    k = qkv[ok, nq:nq + nkv]
+    v = qkv[ok, nq + nkv:nq + 2 * nkv]
+    cache[blk, 0, :, off] = k.to(cache.dtype)
+    cache[blk, 1, :, off] = v.to(cache.dtype)
+
+
+def _gather_kv(cache, block_row, kv_len):
+    bs = cache.shape[3]
+    nb = (kv_len + bs - 1) // bs
+    blocks = block_row[:nb].long()
+    kv = cache[blocks]  # [nb, 2, nkv, bs, D]
+    k = kv[:, 0].permute(1, 0, 2, 3).reshape(kv.shape[2], nb * bs, -1)[:, :kv_len]
+    v = kv[:, 1].permute(1, 0, 2, 3).reshape(kv.shape[2], nb * bs, -1)[:, :kv_len]
+    return k, v  # [nkv, kv_len, D]
+
+
+def paged_attention_reference(q, cache, block_table, q_start, q_len, kv_len, scale):
+    T, nq, D = q.shape
+    nkv = cache.shape[2]
+    G = nq // nkv
+    out = torch.zeros(T, nq, D, dtype=q.dtype, device=q.device)
+    for s in range(block_table.shape[0]):
+        qs, ql, kl = int(q_start[s]), int(q_len[s]), int(kv_len[s])
+        if ql == 0:
+            continue
+        k, v = _gather_kv(cache, block_table[s], kl)
+        k = k.float().repeat_interleave(G, dim=0)
+        v = v.float().repeat_interleave(G, dim=0)
+        qq = q[qs:qs + ql].float().transpose(0, 1)  # [nq, ql, D]
+        sc = torch.matmul(qq, k.transpose(1, 2)) * scale  # [nq, ql, kl]
+        pos = torch.arange(kl - ql, kl, device=q.device)[:, None]
+        keys = torch.arange(kl, device=q.device)[None, :]
+        sc = sc.masked_fill(keys > pos, float("-inf"))
+        o = torch.matmul(torch.softmax(sc, dim=-1), v)  # [nq, ql, D]
+        out[qs:qs + ql] = o.transpose(0, 1).to(q.dtype)
+    return out
+
+
+def choose_splits(num_seqs, nkv, max_kv_len, target_wgs=512):
+    """KV splits so (seqs x kv heads x splits) fills the 256 CUs, never below 256 keys per split."""
+    base = max(1, num_seqs * nkv)
+    want = max(1, math.ceil(target_wgs / base))
+    return max(1, min(want, math.ceil(max(max_kv_len, 1) / 256)))
+
+
+def paged_attention(q, cache, block_table, q_start, q_len, kv_len, scale, max_kv_len, splits=None):
+    """q: [T, nq, D] (head stride D); metadata int32 [S]; returns [T, nq, D]."""
+    if native.use_hip(q):
+        if splits is None:
+            splits = choose_splits(block_table.shape[0], cache.shape[2], max_kv_len)
+        return torch.ops.sxe.paged_attention(q, cache, block_table, q_start, q_len, kv_len, float(scale),
+                                             int(max_kv_len), int(splits))
+    return paged_attention_reference(q, cache, block_table, q_start, q_len, kv_len, scale)

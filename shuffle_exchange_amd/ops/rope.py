@@ -85,3 +85,18 @@ def apply_rope(x, cache, position_ids=None, pos_offset=0):
                               position_ids.reshape(-1).contiguous().long() if position_ids is not None else None,
                               pos_offset)
     return apply_rope_qkv_(x, cache, H, position_ids, pos_offset)
+
+
+def apply_rope_tokens_(qkv, cache, n_rot, positions):
+    """In-place RoPE on the first ``n_rot`` heads of a ragged token batch ``qkv`` [T, H, D] with
+    absolute ``positions`` [T] (inference engine; no autograd)."""
+    T = qkv.shape[0]
+    if T == 0:
+        return qkv
+    pos = positions.reshape(-1).contiguous().long()
+    if native.use_hip(qkv):
+        torch.ops.sxe.rope_(qkv.unsqueeze(0)[:, :, :n_rot, :], cache.cos, cache.sin, pos, T, 0, False)
+        return qkv
+    x = qkv[:, :n_rot, :].float()
+    qkv[:, :n_rot, :] = _ref_rope(x, cache.cos.to(qkv.device), cache.sin.to(qkv.device), pos).to(qkv.dtype)
+    return qkv

@@ -1,0 +1,59 @@
+"""Paged-KV attention HIP kernels vs the fp32 PyTorch reference: decode, multi-token (speculative /
+chunked prefill) rows, GQA groups, block sizes, KV splits, and the KV append scatter."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    from shuffle_exchange_amd.ops import native
+    native.require_hip()
+
+
+def _setup(seqs, nq, nkv, D, bs, seed=0):
+    """seqs: list of (cached_tokens_before, new_tokens). Builds cache with random history."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    total_blocks = sum((c + n + bs - 1) // bs for c, n in seqs) + 3
+    cache = torch.randn(total_blocks, 2, nkv, bs, D, device="cuda", generator=g).to(torch.bfloat16)
+    perm = torch.randperm(total_blocks, device="cpu").tolist()
+    maxb = max((c + n + bs - 1) // bs for c, n in seqs)
+    bt = torch.zeros(len(seqs), maxb, dtype=torch.int32)
+    q_start, q_len, kv_len, slots = [], [], [], []
+    t = 0
+    for i, (c, n) in enumerate(seqs):
+        nb = (c + n + bs - 1) // bs
+        blocks = [perm.pop() for _ in range(nb)]
+        bt[i, :nb] = torch.tensor(blocks, dtype=torch.int32)
+        q_start.append(t)
+        q_len.append(n)
+        kv_len.append(c + n)
+        for p in range(c, c + n):
+            slots.append(blocks[p // bs] * bs + p % bs)
+        t += n
+    T = t
+    qkv = torch.randn(T, nq + 2 * nkv, D, device="cuda", generator=g).to(torch.bfloat16)
+    i32 = lambda x: torch.tensor(x, dtype=torch.int32, device="cuda")
+    return (qkv, cache, bt.cuda(), i32(q_start), i32(q_len), i32(kv_len),
+            torch.tensor(slots, dtype=torch.int64, device="cuda"), max(kv_len))
+
+
+@pytest.mark.parametrize("seqs", [[(0, 1)], [(37, 1), (500, 1), (0, 5)], [(130, 3), (1, 20), (2000, 1)],
+                                  [(0, 70)], [(4100, 1)] * 2])
+@pytest.mark.parametrize("nq,nkv,D,bs", [(8, 2, 128, 64), (4, 4, 64, 16), (32, 8, 128, 32)])
+@pytest.mark.parametrize("splits", [None, 1, 3])
+def test_paged_attention(seqs, nq, nkv, D, bs, splits):
+    from shuffle_exchange_amd.ops.paged_attention import (kv_cache_append, paged_attention,
+                                                          paged_attention_reference)
+    qkv, cache, bt, qs, ql, kl, slots, maxkv = _setup(seqs, nq, nkv, D, bs)
+    ref_cache = cache.clone()
+    kv_cache_append(qkv, cache, slots, nq, nkv)
+    kv_cache_append(qkv.cpu().float(), ref_cache_cpu := ref_cache.cpu().float(), slots.cpu(), nq, nkv)
+    assert torch.equal(cache.cpu().float(), ref_cache_cpu)
+    q = qkv[:, :nq]
+    scale = D ** -0.5
+    out = paged_attention(q, cache, bt, qs, ql, kl, scale, maxkv, splits)
+    ref = paged_attention_reference(q.float(), cache.float(), bt, qs, ql, kl, scale)
+    err = ((out.float() - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
