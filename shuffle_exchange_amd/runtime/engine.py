@@ -267,8 +267,9 @@ class SXEEngine(nn.Module):
         if name == "sgd":
             return torch.optim.SGD(model_parameters, **p)
         if name in ("onebitadam", "zerooneadam", "onebitlamb"):
-            from .fp16.onebit import OnebitAdam
-            return OnebitAdam(model_parameters, **p)
+            assert self.zero_optimization_stage() == 0, "1-bit optimizers run with ZeRO stage 0 (as in the reference)"
+            from .fp16.onebit import build_onebit
+            return build_onebit(name, model_parameters, groups.get_sequence_data_parallel_group(), deepspeed=self, **p)
         raise ValueError(f"unsupported optimizer type {name}")
 
     def _configure_optimizer(self, client_optimizer, model_parameters):

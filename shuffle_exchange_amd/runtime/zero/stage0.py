@@ -48,6 +48,13 @@ class DataParallelOptimizer(ZeroOptimizerBase):
                         self.param_unit[p] = u
             self.units.append(units)
         self._init_master()
+        if hasattr(self.optimizer, "set_segments"):  # layer-wise optimizers (LAMB) on flat masters
+            for g, units in enumerate(self.units):
+                segs, base = [], 0
+                for u in units:
+                    segs += [(base + o, n) for o, n in zip(u.offsets, u.numels)]
+                    base += u.chunk
+                self.optimizer.set_segments(self.master[g], segs)
         for p, u in self.param_unit.items():
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(u)))
         log_dist(f"DP (ZeRO-0): {sum(len(u) for u in self.units)} buckets over {self.dp_size} ranks", ranks=[0])
@@ -68,7 +75,8 @@ class DataParallelOptimizer(ZeroOptimizerBase):
         return hook
 
     def _allreduce_unit(self, u):
-        if u.rsize == 1 or u.reduced:
+        # 1-bit optimizers past their warm-up synchronise compressed momentum themselves
+        if u.rsize == 1 or u.reduced or getattr(self.optimizer, "comm_active", False):
             u.reduced = True
             return
         u.reduced = True

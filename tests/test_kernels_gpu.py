@@ -205,3 +205,24 @@ def test_sumsq():
     assert abs(sumsq(x).item() - x.double().pow(2).sum().item()) < 1e-3 * x.double().pow(2).sum().item()
     x[7] = float("inf")
     assert not math.isfinite(sumsq(x).item())
+
+
+def test_onebit_pack_unpack():
+    n = 8 * 100003
+    x = torch.randn(n, device="cuda")
+    err = torch.empty_like(x)
+    scale = (x.norm() / n ** 0.5).reshape(1)
+    packed = torch.empty(n // 8, dtype=torch.uint8, device="cuda")
+    torch.ops.sxe.sign_pack_ef_(x, err, scale, packed)
+    bits = ((packed.cpu().to(torch.int32).unsqueeze(-1) >> torch.arange(8)) & 1).view(-1)
+    assert torch.equal(bits.bool(), (x >= 0).cpu())
+    dec = torch.where(x >= 0, scale, -scale)
+    assert torch.allclose(err, x - dec, atol=1e-6)
+    W = 3
+    pk = torch.stack([packed, packed ^ 0xFF, packed])
+    sc = torch.tensor([1.0, 2.0, 0.5], device="cuda")
+    out = torch.empty(n, device="cuda")
+    torch.ops.sxe.unpack_avg(pk, sc, out)
+    s = (x >= 0).float() * 2 - 1
+    ref = (s * 1.0 - s * 2.0 + s * 0.5) / W
+    assert torch.allclose(out, ref, atol=1e-6)
