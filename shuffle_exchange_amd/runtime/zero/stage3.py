@@ -17,6 +17,12 @@ MI355X-first design (not a port of the per-parameter coordinator):
   single rank every unit is persistent, so ZeRO-3 on one GPU has zero gather/release overhead.
 * Optional Shuffle-exchange slices (the fork's feature extended to stage 3): partitioning inside
   a slice, bit16 chunk averaging across slices after each step.
+* ZeRO++ (reference partition_parameters.py:824-863, coalesced_collectives.py:31-155,
+  groups.py:692-749): qwZ all-gathers int8 shards + per-group scales (quantized once per step,
+  dequantized by a HIP kernel into the unit buffer); qgZ replaces the reduce-scatter by an int8/int4
+  all-to-all whose receive side dequantizes and reduces the W chunks in one kernel; hpZ keeps a
+  secondary shard per intra-node group (captured from the forward gather) so backward re-gathers
+  only inside that group.
 """
 import torch
 import torch.nn as nn
@@ -100,7 +106,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
     def __init__(self, module, init_optimizer, *, loss_scaler, clip_grad=0.0, dp_ranks=None, dp_group=None,
                  prefetch_depth=2, param_persistence_threshold=100_000, communication_data_type=None,
                  unit_classes=None, shuffle_exchange_cfg=None, mp_group=None, timers=None, mics_shard_size=-1,
-                 average_master=False, host_step=None, offload_param=False):
+                 average_master=False, host_step=None, offload_param=False, quantized_weights=False,
+                 quantized_gradients=False, hpz_partition_size=1, quant_group_size=128, grad_quant_bits=8):
         acc = get_accelerator()
         device = torch.device(acc.current_device_name())
         self.module = module
@@ -130,6 +137,24 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         if self.offload_param and self.se is not None:
             raise NotImplementedError("offload_param with shuffle-exchange slices is not supported")
         self.S = self.topo.S
+        # ZeRO++ knobs
+        self.qwz = bool(quantized_weights) and self.S > 1
+        self.qgz = bool(quantized_gradients) and self.S > 1
+        self.qgroup = int(quant_group_size)
+        self.gbits = int(grad_quant_bits)
+        self.hpz = int(hpz_partition_size or 1)
+        self.hpz_group = None
+        if self.hpz > 1 and self.S > self.hpz:
+            assert self.S % self.hpz == 0, "zero_hpz_partition_size must divide the partition size"
+            ranks = self.topo.dp_ranks  # every rank creates every block's group (collective)
+            me = dist.get_rank()
+            for i in range(0, len(ranks), self.hpz):
+                blk = ranks[i:i + self.hpz]
+                g = dist.new_group(blk)
+                if me in blk:
+                    self.hpz_group, self.hpz_rank = g, blk.index(me)
+        else:
+            self.hpz = 1
         self.prefetch_depth = max(0, int(prefetch_depth))
         self.persist_thr = int(param_persistence_threshold)
         self.comm_dtype = communication_data_type
@@ -212,6 +237,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             u.flat.untyped_storage().resize_(0)
             u.state = RELEASED
         u.event = None
+        u.qshard = None
+        u.sec_shard, u.sec_valid = None, False
         for p in params:
             p.ds_unit = u
         return u
@@ -336,12 +363,40 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                     src.record_stream(st)
             if self.S == 1:
                 u.flat.copy_(src)
+            elif self.hpz > 1 and self._in_bwd and u.sec_valid:
+                # hpZ: backward re-gather inside the intra-node group from the secondary shards
+                dist.all_gather_into_tensor(u.flat, u.sec_shard, group=self.hpz_group)
+            elif self.qwz:
+                self._quantized_gather(u, st)
             else:
                 dist.all_gather_into_tensor(u.flat, src, group=self.topo.slice_group)
             if st is not None:
                 u.event = torch.cuda.Event()
                 u.event.record(st)
         u.state = INFLIGHT
+
+    def _qgroup(self, u):
+        return self.qgroup if u.chunk % self.qgroup == 0 else 64
+
+    def _quantize_shard(self, u):
+        from ...ops.quantizer import quantize
+        q, sc = quantize(u.shard, self._qgroup(u), 8)
+        u.qshard = (q, sc)
+
+    def _quantized_gather(self, u, st):
+        """qwZ: all-gather int8 shards + fp32 group scales, dequantize into the unit buffer."""
+        from ...ops.quantizer import dequantize
+        if u.qshard is None:
+            self._quantize_shard(u)
+        q, sc = u.qshard
+        qa = torch.empty(q.numel() * self.S, dtype=q.dtype, device=q.device)
+        sa = torch.empty(sc.numel() * self.S, dtype=sc.dtype, device=sc.device)
+        dist.all_gather_into_tensor(qa, q, group=self.topo.slice_group)
+        dist.all_gather_into_tensor(sa, sc, group=self.topo.slice_group)
+        dequantize(qa, sa, self._qgroup(u), 8, out=u.flat)
+        if st is not None:
+            qa.record_stream(st)
+            sa.record_stream(st)
 
     def _fetch(self, fg, wait=True):
         for u in fg.units:
@@ -361,6 +416,12 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             return
         if u.state == INFLIGHT and u.event is not None:
             torch.cuda.current_stream().wait_event(u.event)
+        if self.hpz > 1 and not self._in_bwd and not u.sec_valid:
+            n = u.padded // self.hpz
+            if u.sec_shard is None:
+                u.sec_shard = torch.empty(n, dtype=u.flat.dtype, device=u.flat.device)
+            u.sec_shard.copy_(u.flat[self.hpz_rank * n:(self.hpz_rank + 1) * n])
+            u.sec_valid = True
         u.flat.untyped_storage().resize_(0)
         u.state = RELEASED
 
@@ -395,6 +456,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             send = st if (self.comm_dtype is None or st.dtype == self.comm_dtype) else st.to(self.comm_dtype)
             if self.S == 1:
                 u.grad.add_(send)
+            elif self.qgz and not self.mics:
+                self._quantized_reduce_scatter(u, st)
             else:
                 out = torch.empty(u.chunk, dtype=send.dtype, device=send.device)
                 dist.reduce_scatter_tensor(out, send, group=self.topo.slice_group)
@@ -408,6 +471,20 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             if rs is not None:
                 st.record_stream(rs)
                 send.record_stream(rs)
+
+    def _quantized_reduce_scatter(self, u, staging):
+        """qgZ: quantize the full gradient unit per destination chunk, all-to-all the packed
+        chunks, dequantize + reduce the W received chunks straight into this rank's accumulator."""
+        from ...ops.quantizer import dequant_reduce, quantize
+        qg = self._qgroup(u)
+        q, sc = quantize(staging, qg, self.gbits)
+        rq, rs = torch.empty_like(q), torch.empty_like(sc)
+        dist.all_to_all_single(rq, q, group=self.topo.slice_group)
+        dist.all_to_all_single(rs, sc, group=self.topo.slice_group)
+        dequant_reduce(rq, rs, self.S, qg, self.gbits, u.grad, alpha=self.sp_scale / self.S, accumulate=True)
+        if self.rs_stream is not None:
+            for t in (q, sc, rq, rs):
+                t.record_stream(self.rs_stream)
 
     def forward_prologue(self):
         self._in_bwd = False
@@ -461,6 +538,11 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         if self.se is not None:
             self.se.sync([u.shard for units in self.units for u in units], self._device_masters())
         self._refresh_persistent()
+        for units in self.units:
+            for u in units:
+                u.sec_valid = False
+                if self.qwz and not u.persistent:
+                    self._quantize_shard(u)
         self.global_step += 1
         # start gathering the first units of the next forward now
         for j in self.trace[:self.prefetch_depth]:

@@ -226,3 +226,43 @@ def test_onebit_pack_unpack():
     s = (x >= 0).float() * 2 - 1
     ref = (s * 1.0 - s * 2.0 + s * 0.5) / W
     assert torch.allclose(out, ref, atol=1e-6)
+
+
+@pytest.mark.parametrize("bits", [8, 4])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_quantize_sym(bits, dt):
+    from shuffle_exchange_amd.ops import quantizer as Q
+    x = torch.randn(128 * 1001, device="cuda").to(dt)
+    q, s = Q.quantize(x, 128, bits)
+    rq, rs = Q._ref_quant(x.cpu(), 128, bits)
+    assert torch.allclose(s.cpu(), rs, rtol=1e-6)
+    if bits == 8:  # rounding ties may differ by one step
+        assert (q.cpu().view(torch.int8).to(torch.int32) - rq.view(torch.int8).to(torch.int32)).abs().max() <= 1
+    out = Q.dequantize(q, s, 128, bits, out=torch.empty_like(x))
+    ref = Q._ref_dequant(q.cpu(), s.cpu(), 128, bits, x.numel(), torch.float32)
+    assert torch.allclose(out.float().cpu(), ref, atol=1e-2 if dt == torch.bfloat16 else 1e-6)
+    err = (out.float() - x.float()).abs().max() / x.float().abs().max()
+    assert err < (0.01 if bits == 8 else 0.15)
+
+
+def test_dequant_reduce():
+    from shuffle_exchange_amd.ops import quantizer as Q
+    W, m = 4, 128 * 50
+    xs = [torch.randn(m, device="cuda") for _ in range(W)]
+    qs, ss = zip(*[Q.quantize(x, 128, 8) for x in xs])
+    out = torch.zeros(m, device="cuda")
+    Q.dequant_reduce(torch.cat(qs), torch.cat(ss), W, 128, 8, out, alpha=0.25)
+    ref = sum(Q.dequantize(q, s, 128, 8, out=torch.empty(m, device="cuda")) for q, s in zip(qs, ss)) * 0.25
+    assert torch.allclose(out, ref, atol=1e-5)
+
+
+def test_fp8_quantize():
+    from shuffle_exchange_amd.ops import quantizer as Q
+    x = torch.randn(512 * 300, device="cuda", dtype=torch.bfloat16) * 3
+    q, s = Q.quantize_fp8(x, 512)
+    rq, rs = Q.quantize_fp8(x.cpu(), 512)
+    assert torch.allclose(s.cpu(), rs, rtol=1e-5)
+    out = Q.dequantize_fp8(q, s, 512)
+    ref = Q.dequantize_fp8(rq, rs, 512)
+    assert ((out.float().cpu() - ref.float()).abs() > 1e-2 * ref.float().abs().clamp_min(1e-3)).float().mean() < 0.01
+    assert ((out.float() - x.float()).norm() / x.float().norm()) < 0.05

@@ -111,3 +111,22 @@ def test_collectives_and_fingerprint():
         assert out["fp_ok"]
     res = run_dist(C.case_fingerprint_mismatch, world)
     assert res == ["mismatch-detected"] * world
+
+
+@pytest.mark.parametrize("knobs,tol", [({"zero_quantized_weights": True}, 5e-2),
+                                       ({"zero_quantized_gradients": True}, 5e-2),
+                                       ({"zero_hpz_partition_size": 2}, 1e-5)])
+def test_zeropp_matches_zero3(knobs, tol):
+    """ZeRO++ qwZ / qgZ (int8) track plain ZeRO-3 closely; hpZ (secondary intra-group shards) is exact."""
+    world, mbs, seq, steps = 4, 1, 16, 3
+    base = {"stage": 3, "stage3_param_persistence_threshold": 0}
+    SGD = {"type": "SGD", "params": {"lr": 0.05}}
+    ds = {"train_micro_batch_size_per_gpu": mbs, "zero_optimization": dict(base, **knobs), "optimizer": SGD}
+    ref_ds = {"train_micro_batch_size_per_gpu": mbs, "zero_optimization": base, "optimizer": SGD}
+    res = run_dist(C.case_train, world, ds, steps, mbs, seq)
+    ref = run_dist(C.case_train, world, ref_ds, steps, mbs, seq)
+    for a, b in zip(res[0]["losses"], ref[0]["losses"]):
+        assert abs(a - b) <= tol * abs(b)
+    for k, v in ref[0]["params"].items():
+        d = (res[0]["params"][k] - v).norm() / (v.norm() + 1e-12)
+        assert d < tol, (k, float(d))
