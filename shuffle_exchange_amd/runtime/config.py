@@ -375,6 +375,14 @@ class SXEConfig:
         m = self.model
         tb, mb, gas = m.train_batch_size, m.train_micro_batch_size_per_gpu, m.gradient_accumulation_steps
         dp = self.dp_world_size
+        if m.elasticity.enabled:
+            # elastic batch: pick the batch valid for the most GPU counts (reference config.py:870-936)
+            from ..elasticity import compute_elastic_config
+            el = m.elasticity.model_dump() if hasattr(m.elasticity, "model_dump") else dict(m.elasticity)
+            tb, _, mb = compute_elastic_config({"elasticity": el}, world_size=self.world_size, return_microbatch=True)
+            if not el.get("ignore_non_elastic_batch_info", False) and m.train_batch_size not in (None, tb):
+                logger.warning(f"elasticity overrides train_batch_size {m.train_batch_size} -> {tb}")
+            gas = None
         if tb is not None and mb is not None and gas is not None:
             pass
         elif tb is not None and mb is not None:

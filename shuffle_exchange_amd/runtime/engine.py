@@ -361,11 +361,24 @@ class SXEEngine(nn.Module):
         self.timers(FORWARD_MICRO_TIMER).start()
         if self.optimizer is not None and hasattr(self.optimizer, "forward_prologue"):
             self.optimizer.forward_prologue()
+        fp = self._config.model.flops_profiler
+        prof = None
+        if fp.enabled and self.global_steps + 1 == fp.profile_step and self.micro_steps % max(
+                1, self.gradient_accumulation_steps()) == 0:
+            from ..profiling.flops_profiler import FlopsProfiler
+            prof = FlopsProfiler(self.module, ds_engine=self, recompute_fwd_factor=fp.recompute_fwd_factor)
+            prof.start_profile()
         if self.fp16_enabled() and self._config.model.fp16.auto_cast:
             with torch.autocast(device_type=self.device.type, dtype=torch.float16):
                 out = self.module(*inputs, **kwargs)
         else:
             out = self.module(*inputs, **kwargs)
+        if prof is not None:
+            prof.stop_profile()
+            if self.global_rank == 0:
+                prof.print_model_profile(profile_step=fp.profile_step, module_depth=fp.module_depth,
+                                         top_modules=fp.top_modules, detailed=fp.detailed, output_file=fp.output_file)
+            self.flops_profiler = prof
         self.timers(FORWARD_MICRO_TIMER).stop()
         return out
 
