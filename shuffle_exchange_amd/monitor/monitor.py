@@ -51,9 +51,56 @@ class TensorBoardMonitor(Monitor):
             self.writer.flush()
 
 
+class WandbMonitor(Monitor):
+    """Weights & Biases (reference monitor/wandb.py:12); active only if ``wandb`` imports."""
+
+    def __init__(self, cfg):
+        self.enabled = False
+        if not getattr(cfg, "enabled", False):
+            return
+        try:
+            import wandb
+            wandb.init(project=getattr(cfg, "project", None) or "sxe", group=getattr(cfg, "group", None),
+                       entity=getattr(cfg, "team", None))
+            self._wandb = wandb
+            self.enabled = True
+        except Exception:
+            self.enabled = False
+
+    def write_events(self, events):
+        if self.enabled:
+            for name, value, step in events:
+                self._wandb.log({name: value}, step=step)
+
+
+class CometMonitor(Monitor):
+    """Comet ML (reference monitor/comet.py:23); active only if ``comet_ml`` imports."""
+
+    def __init__(self, cfg):
+        self.enabled = False
+        if not getattr(cfg, "enabled", False):
+            return
+        try:
+            import comet_ml
+            self._exp = comet_ml.Experiment(project_name=getattr(cfg, "project", None),
+                                            workspace=getattr(cfg, "workspace", None))
+            name = getattr(cfg, "experiment_name", None)
+            if name:
+                self._exp.set_name(name)
+            self.enabled = True
+        except Exception:
+            self.enabled = False
+
+    def write_events(self, events):
+        if self.enabled:
+            for name, value, step in events:
+                self._exp.log_metric(name, value, step=step)
+
+
 class MonitorMaster(Monitor):
     def __init__(self, model_cfg):
-        self.monitors = [CSVMonitor(model_cfg.csv_monitor), TensorBoardMonitor(model_cfg.tensorboard)]
+        self.monitors = [CSVMonitor(model_cfg.csv_monitor), TensorBoardMonitor(model_cfg.tensorboard),
+                         WandbMonitor(model_cfg.wandb), CometMonitor(model_cfg.comet)]
         self.enabled = any(m.enabled for m in self.monitors)
 
     def write_events(self, events):

@@ -132,6 +132,39 @@ class SXEEngine(nn.Module):
         except Exception as e:  # monitors are optional
             logger.debug(f"monitor disabled: {e}")
         self._auto_se_steps = 0
+        self._configure_training_aux()
+
+    def _configure_training_aux(self):
+        """Progressive layer drop, legacy curriculum learning and MoQ from the raw config
+        (reference engine.py _configure_progressive_layer_drop / curriculum / quantizer)."""
+        raw = self._config._param_dict
+        pld = raw.get("progressive_layer_drop", {})
+        self.progressive_layer_drop = None
+        if pld.get("enabled"):
+            from .progressive_layer_drop import ProgressiveLayerDrop
+            self.progressive_layer_drop = ProgressiveLayerDrop(pld.get("theta", 0.5), pld.get("gamma", 0.001))
+        cl = raw.get("curriculum_learning", {})
+        self.curriculum_scheduler_legacy = None
+        if cl.get("enabled") and cl.get("curriculum_type", "seqlen") == "seqlen":
+            from .data_pipeline import CurriculumScheduler
+            self.curriculum_scheduler_legacy = CurriculumScheduler(cl)
+        qt = raw.get("quantize_training", {})
+        self.quantizer = None
+        if qt.get("enabled"):
+            from .quantize import Quantizer
+            bits = qt.get("quantize_bits", {})
+            sch = qt.get("quantize_schedule", {})
+            self.quantizer = Quantizer(q_groups=qt.get("quantize_groups", 1), q_type=int(qt.get("quantize_type",
+                                       "symmetric") != "symmetric"), q_rounding=int(qt.get("rounding", "nearest") ==
+                                       "stochastic"), q_start_bits=bits.get("start_bits", 16),
+                                       q_target_bits=bits.get("target_bits", 8),
+                                       q_period=sch.get("quantize_period", 100))
+
+    def curriculum_enabled_legacy(self):
+        return self.curriculum_scheduler_legacy is not None
+
+    def get_sequence_parallel_group(self):
+        return groups.get_sequence_parallel_group()
 
     # ------------------------------------------------------------------------------------ config
     @property
@@ -361,6 +394,10 @@ class SXEEngine(nn.Module):
         self.timers(FORWARD_MICRO_TIMER).start()
         if self.optimizer is not None and hasattr(self.optimizer, "forward_prologue"):
             self.optimizer.forward_prologue()
+        if self.progressive_layer_drop is not None:
+            kwargs.update(self.progressive_layer_drop.get_state())
+        if self.curriculum_scheduler_legacy is not None:
+            kwargs["curriculum_seqlen"] = self.curriculum_scheduler_legacy.update_difficulty(self.global_steps + 1)
         fp = self._config.model.flops_profiler
         prof = None
         if fp.enabled and self.global_steps + 1 == fp.profile_step and self.micro_steps % max(
@@ -427,6 +464,10 @@ class SXEEngine(nn.Module):
     def _take_model_step(self, lr_kwargs=None):
         self.optimizer.step()
         overflow = bool(getattr(self.optimizer, "overflow", False))
+        if self.progressive_layer_drop is not None:
+            self.progressive_layer_drop.update_state(self.global_steps + 1)
+        if self.quantizer is not None and self.zero_optimization_stage() < 3:
+            self.quantizer.quantize([[p for p in self.module.parameters() if p.requires_grad]], overflow)
         self.optimizer.zero_grad()
         if overflow:
             self.skipped_steps += 1
