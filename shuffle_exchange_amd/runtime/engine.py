@@ -494,6 +494,15 @@ class SXEEngine(nn.Module):
     def zero_grad(self):
         self.optimizer.zero_grad()
 
+    def offload_states(self, include=None, device="cpu", pin_memory=True, non_blocking=False):
+        """Free HBM held by optimizer-side state (reference engine.py:4042-4089)."""
+        assert self.zero_optimization_stage() >= 0 and hasattr(self.optimizer, "offload_states")
+        self.optimizer.offload_states(include=include, device=device, pin_memory=pin_memory,
+                                      non_blocking=non_blocking)
+
+    def reload_states(self, non_blocking=False):
+        self.optimizer.reload_states(non_blocking=non_blocking)
+
     def get_lr(self):
         return [g["lr"] for g in self.optimizer.param_groups] if self.optimizer is not None else []
 

@@ -197,6 +197,78 @@ class ZeroOptimizerBase:
         if self.host_step is not None and self.host_step.device == "nvme":
             self.host_step.flush(self)
 
+    # ----------------------------------------------------------------------- offload_states API
+    def _rebind_views(self):
+        for g, units in enumerate(self.units):
+            off = 0
+            for u in units:
+                if self.master[g].numel():
+                    u.master = self.master[g].data[off:off + u.chunk]
+                u.grad = self.grads[g][off:off + u.chunk]
+                off += u.chunk
+
+    def offload_states(self, include=None, device="cpu", pin_memory=True, non_blocking=False):
+        """Move optimizer states / fp32 masters / grad accumulators (and ZeRO-3 bit16 shards) to the
+        host to free HBM between phases (reference runtime/zero/offload_states.py:17-71)."""
+        inc = set(include or ["optim_states", "hp_params", "lp_grads", "lp_params"])
+        pin = pin_memory and torch.cuda.is_available()
+
+        def mv(t):
+            if t is None or not torch.is_tensor(t) or t.device.type == "cpu":
+                return t
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=pin)
+            h.copy_(t, non_blocking=non_blocking)
+            return h
+
+        self._offloaded = getattr(self, "_offloaded", {})
+        if "hp_params" in inc:
+            for m in self.master:
+                self._offloaded.setdefault("dev", m.device)
+                m.data = mv(m.data)
+        if "lp_grads" in inc:
+            self.grads = [mv(g) for g in self.grads]
+        if "optim_states" in inc:
+            for m in self.master:
+                st = self.optimizer.state[m]
+                for k, v in list(st.items()):
+                    if torch.is_tensor(v) and v.numel() > 1:
+                        st[k] = mv(v)
+        if "lp_params" in inc and getattr(self, "fgroups", None) is not None:
+            for units in self.units:
+                for u in units:
+                    if not u.persistent:
+                        u.shard = mv(u.shard)
+        self._rebind_views()
+        self._offloaded["include"] = inc
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    def reload_states(self, non_blocking=False):
+        dev = self.device
+        inc = getattr(self, "_offloaded", {}).get("include", set())
+
+        def back(t):
+            return t.to(dev, non_blocking=non_blocking) if torch.is_tensor(t) and t.device != dev else t
+
+        if "hp_params" in inc and self.host_step is None:
+            for m in self.master:
+                m.data = back(m.data)
+        if "lp_grads" in inc:
+            self.grads = [back(g) for g in self.grads]
+        if "optim_states" in inc and self.host_step is None:
+            for m in self.master:
+                st = self.optimizer.state[m]
+                for k, v in list(st.items()):
+                    if torch.is_tensor(v) and v.numel() > 1:
+                        st[k] = back(v)
+        if "lp_params" in inc and getattr(self, "fgroups", None) is not None:
+            for units in self.units:
+                for u in units:
+                    if not u.persistent and not getattr(self, "offload_param", False):
+                        u.shard = back(u.shard)
+        self._rebind_views()
+        self._offloaded = {}
+
     def zero_grad_buffers(self):
         for gr in self.grads:
             gr.zero_()

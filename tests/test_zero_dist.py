@@ -130,3 +130,34 @@ def test_zeropp_matches_zero3(knobs, tol):
     for k, v in ref[0]["params"].items():
         d = (res[0]["params"][k] - v).norm() / (v.norm() + 1e-12)
         assert d < tol, (k, float(d))
+
+
+def _case_offload_states(rank, world, stage):
+    import shuffle_exchange_amd as sxe
+    model, cfg = C.tiny_llama(0)
+    ds = {"train_micro_batch_size_per_gpu": 1, "zero_optimization": {"stage": stage,
+                                                                     "stage3_param_persistence_threshold": 0},
+          "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    batches = C.global_batches(cfg, world, 1, 16, 4)
+
+    def run(bs):
+        for b in bs:
+            local = b[rank:rank + 1]
+            loss = eng(local, labels=local)
+            eng.backward(loss)
+            eng.step()
+    run(batches[:2])
+    eng.offload_states()
+    eng.reload_states()
+    run(batches[2:])
+    return C.full_params(eng)
+
+
+@pytest.mark.parametrize("stage", [1, 3])
+def test_offload_reload_states_roundtrip(stage):
+    a = run_dist(_case_offload_states, 2, stage)
+    b = run_dist(C.case_train, 2, {"train_micro_batch_size_per_gpu": 1,
+                                   "zero_optimization": {"stage": stage, "stage3_param_persistence_threshold": 0},
+                                   "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}}}, 4, 1, 16)
+    _close(a[0], b[0]["params"], tol=1e-6)
