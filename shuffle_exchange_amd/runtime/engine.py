@@ -636,6 +636,9 @@ class SXEEngine(nn.Module):
                 return None, None
             with open(latest) as f:
                 tag = f.read().strip()
+        if self._config.model.checkpoint.load_universal:
+            return self.load_universal_checkpoint(os.path.join(load_dir, str(tag)), load_optimizer_states,
+                                                  load_lr_scheduler_states)
         d, model_path, optim_path = self._ckpt_names(load_dir, tag)
         ce = self.checkpoint_engine
         state = ce.load(model_path, map_location="cpu")
@@ -661,6 +664,21 @@ class SXEEngine(nn.Module):
                 "mp_world_size", "ds_config", "ds_version"}
         client = {k: v for k, v in state.items() if k not in skip}
         return os.path.join(load_dir, str(tag)), client
+
+    def load_universal_checkpoint(self, universal_dir, load_optimizer_states=True, load_lr_scheduler_states=True):
+        """Resume from a universal checkpoint under any data-parallel / slice layout."""
+        from ..checkpoint.universal import load_universal_into_optimizer
+        meta = load_universal_into_optimizer(self.optimizer, universal_dir, self._param_names())
+        state = {}
+        files = sorted(f for f in os.listdir(universal_dir) if f.endswith("model_states.pt"))
+        if files:
+            state = torch.load(os.path.join(universal_dir, files[0]), map_location="cpu", weights_only=False)
+        if load_lr_scheduler_states and self.lr_scheduler is not None and state.get("lr_scheduler"):
+            self.lr_scheduler.load_state_dict(state["lr_scheduler"])
+        self.global_steps = state.get("global_steps", meta.get("step", 0))
+        self.global_samples = state.get("global_samples", 0)
+        dist.barrier()
+        return universal_dir, {}
 
     def _zero3_load_16bit(self, sd, strict=True):
         opt = self.optimizer
