@@ -46,7 +46,15 @@ def initialize(args=None, model=None, optimizer=None, model_parameters=None, tra
                                 training_data=training_data, lr_scheduler=lr_scheduler, mpu=model.mpu(),
                                 dist_init_required=dist_init_required, collate_fn=collate_fn, config=config)
     else:
-        engine = SXEEngine(args=args, model=model, optimizer=optimizer, model_parameters=model_parameters,
+        cls = SXEEngine
+        try:
+            from .runtime.config import _load_raw
+            if _load_raw(config).get("hybrid_engine", {}).get("enabled", False):
+                from .runtime.hybrid_engine import SXEHybridEngine
+                cls = SXEHybridEngine
+        except Exception:
+            pass
+        engine = cls(args=args, model=model, optimizer=optimizer, model_parameters=model_parameters,
                            training_data=training_data, lr_scheduler=lr_scheduler, mpu=mpu,
                            dist_init_required=dist_init_required, collate_fn=collate_fn, config=config,
                            rings=rings, shuffle_step=shuffle_step, method=method, slice_count=slice_count)

@@ -235,6 +235,16 @@ class PipelineConfig(ConfigModel):
     grad_partitioned: bool = True
 
 
+class HybridEngineConfig(ConfigModel):
+    enabled: bool = False
+    max_out_tokens: int = 512
+    inference_tp_size: int = 1
+    release_inference_cache: bool = False
+    pin_parameters: bool = True
+    tp_gather_partition_size: int = 8
+    kv_cache_fraction: float = 0.3
+
+
 class TensorParallelConfig(ConfigModel):
     autotp_size: int = 1
     tp_size: int = 1
@@ -302,6 +312,7 @@ class SXEConfigModel(ConfigModel):
     aio: AIOConfig = Field(default_factory=AIOConfig)
     pipeline: PipelineConfig = Field(default_factory=PipelineConfig)
     tensor_parallel: TensorParallelConfig = Field(default_factory=TensorParallelConfig)
+    hybrid_engine: HybridEngineConfig = Field(default_factory=HybridEngineConfig)
     elasticity: ElasticityConfig = Field(default_factory=ElasticityConfig)
     moe: MoEConfig = Field(default_factory=MoEConfig)
     amp: Dict[str, Any] = Field(default_factory=dict)

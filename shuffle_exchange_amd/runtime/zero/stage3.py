@@ -412,7 +412,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 u.state = AVAILABLE
 
     def _release_unit(self, u):
-        if u.persistent or u.state == RELEASED:
+        if u.persistent or u.state == RELEASED or getattr(self, "_hold", False):
             return
         if u.state == INFLIGHT and u.event is not None:
             torch.cuda.current_stream().wait_event(u.event)
@@ -561,11 +561,15 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             p.grad = None
 
     # ---------------------------------------------------------------------- gathered-param access
-    def gather_all(self):
+    def gather_all(self, hold=True):
+        """Gather every unit; with ``hold`` the module hooks do not release them until
+        ``release_all`` (generation / evaluation phases of the hybrid engine)."""
         for fg in self.fgroups:
             self._fetch(fg, wait=True)
+        self._hold = bool(hold)
 
     def release_all(self):
+        self._hold = False
         for fg in self.fgroups:
             self._release(fg)
 
