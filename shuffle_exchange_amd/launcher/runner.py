@@ -45,6 +45,8 @@ def parse_args(args=None):
     p.add_argument("--bind_core_list", default=None)
     p.add_argument("--elastic_training", action="store_true")
     p.add_argument("--dry_run", action="store_true", help="print the per-node commands and exit")
+    p.add_argument("--autotuning", default="", choices=["", "tune", "run"],
+                   help="tune: search ZeRO stage x micro batch with short runs; run: tune then launch the best")
     p.add_argument("user_script")
     p.add_argument("user_args", nargs=argparse.REMAINDER)
     return p.parse_args(args)
@@ -198,8 +200,48 @@ def multinode_commands(args, active, master_addr):
     return cmds
 
 
+def _autotune(args):
+    import json
+    from ..autotuning import Autotuner, subprocess_runner
+    ua = list(args.user_args)
+    cfg_path = None
+    for i, a in enumerate(ua):
+        if a in ("--deepspeed_config", "--sxe_config") and i + 1 < len(ua):
+            cfg_path = ua[i + 1]
+            rest = ua[:i] + ua[i + 2:]
+            break
+    else:
+        raise SystemExit("--autotuning needs --deepspeed_config <json> in the user arguments")
+    with open(cfg_path) as f:
+        base = json.load(f)
+    at_cfg = base.get("autotuning", {})
+    nproc = args.num_gpus if args.num_gpus > 0 else _local_gpu_count()
+    tuner = Autotuner(base, world_size=nproc, tuner_type=at_cfg.get("tuner_type", "gridsearch"),
+                      tuner_num_trials=at_cfg.get("tuner_num_trials", 50),
+                      tuner_early_stopping=at_cfg.get("tuner_early_stopping", 5),
+                      results_dir=at_cfg.get("results_dir", "autotuning_results"))
+    best = tuner.tune(subprocess_runner(args.user_script, rest, nproc=nproc))
+    best_cfg = tuner.best_config()
+    print(f"autotuning best: {best}")
+    if args.autotuning == "run" and best_cfg is not None:
+        best_cfg.pop("autotuning", None)
+        out = os.path.join(tuner.results_dir, "best_config.json")
+        with open(out, "w") as f:
+            json.dump(best_cfg, f, indent=2)
+        args.user_args = rest + ["--deepspeed_config", out]
+        args.autotuning = ""
+        return main_with(args)
+    return 0
+
+
 def main(args=None):
     args = parse_args(args)
+    if args.autotuning:
+        return _autotune(args)
+    return main_with(args)
+
+
+def main_with(args):
     pool = fetch_hostfile(args.hostfile)
     if pool is None:
         n = args.num_gpus if args.num_gpus > 0 else _local_gpu_count()

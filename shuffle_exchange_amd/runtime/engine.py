@@ -461,6 +461,29 @@ class SXEEngine(nn.Module):
         if boundary and self.wall_clock_breakdown() and self.global_steps % self.steps_per_print() == 0:
             self.timers.log([FORWARD_MICRO_TIMER, BACKWARD_MICRO_TIMER, STEP_MICRO_TIMER])
 
+    def _autotuning_probe(self):
+        """Autotuning experiments: time steps (start, end] and write the metric file, then exit
+        (reference engine autotuning hooks)."""
+        at = self._config._param_dict.get("autotuning", {})
+        if not at.get("enabled") or not at.get("metric_path"):
+            return
+        s0, s1 = at.get("start_profile_step", 3), at.get("end_profile_step", 5)
+        if self.global_steps == s0:
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            self._at_t0 = time.perf_counter()
+        elif self.global_steps == s1 and hasattr(self, "_at_t0"):
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            dt = (time.perf_counter() - self._at_t0) / max(1, s1 - s0)
+            if self.global_rank == 0:
+                import json
+                with open(at["metric_path"], "w") as f:
+                    json.dump({"throughput": self.train_batch_size() / dt, "latency": dt}, f)
+            if at.get("exit_after_profile", True):
+                dist.barrier()
+                raise SystemExit(0)
+
     def _take_model_step(self, lr_kwargs=None):
         self.optimizer.step()
         overflow = bool(getattr(self.optimizer, "overflow", False))
@@ -475,6 +498,7 @@ class SXEEngine(nn.Module):
             self.lr_scheduler.step(**(lr_kwargs or {}))
         self.global_steps += 1
         self.global_samples += self.train_batch_size()
+        self._autotuning_probe()
         se = self.shuffle_exchange_config
         if se.enabled and se.auto_shuffle:
             self.shuffle_exchange()
