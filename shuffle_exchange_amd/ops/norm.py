@@ -49,7 +49,16 @@ class _NormFn(torch.autograd.Function):
         dres = dh.contiguous().view(-1, H) if (ctx.has_res and dh is not None) else None
         dx, dw, db = torch.ops.sxe.norm_bwd(dy2, hin, rstd, mean, weight, dres, bool(ctx.layernorm))
         dx = dx.view(ctx.shape)
-        dw = dw.to(weight.dtype)
+        tgt_fn = getattr(weight, "_sxe_grad_target", None)
+        if tgt_fn is not None and ctx.needs_input_grad[2]:
+            # the fp32 dgamma goes straight into the optimizer's buffer (no bf16 round trip, no
+            # mixed-dtype accumulate in a hook)
+            tgt, acc = tgt_fn(weight)
+            (tgt.view(-1).add_ if acc else tgt.view(-1).copy_)(dw.view(-1))
+            weight._sxe_grad_done(weight)
+            dw = None
+        else:
+            dw = dw.to(weight.dtype)
         db = db.to(weight.dtype) if ctx.has_bias else None
         return dx, (dx if ctx.has_res else None), dw, db, None, None
 
