@@ -23,7 +23,7 @@ constexpr int NWAVE = 8, NTHR = NWAVE * 64;
 constexpr int ROWB = 256;                   // bytes per LDS row (128 bf16)
 constexpr int HALF = BK * ROWB;             // one [BK][128] half tile
 constexpr int STAGE = 4 * HALF;             // A (2 halves) + B (2 halves) = 32 KiB
-constexpr int NSTAGE = 2;
+constexpr int NSTAGE = 4;               // 128 KiB ring: slabs issued 3 ahead
 constexpr int GROUP_M = 8;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -52,9 +52,14 @@ __device__ __forceinline__ bf16x8 frag(const char* base, int row0, int dt, int l
   return __builtin_bit_cast(bf16x8, c);
 }
 
+// LDS-DMA issued from inline asm: hipcc's waitcnt pass cannot see it, so it does not put a
+// conservative `s_waitcnt vmcnt(0)` in front of every ds_read of the ring (it did with the
+// builtin: the whole prefetch drained each K-step). Completion is tracked by the explicit counted
+// vmcnt + barrier in the main loop.
 __device__ __forceinline__ void glds16(const void* gsrc, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+  const unsigned lds = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(gsrc) : "memory", "m0");
 }
 
 // One K-slab: rows k0..k0+BK of A[:, m0:m0+256] and B[:, n0:n0+256] into stage `st`.
@@ -108,12 +113,25 @@ __global__ void __launch_bounds__(NTHR, 1) wgrad_kernel(const unsigned short* __
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   const int nk = K / BK;
-  load_stage(A, lda, B, ldb, 0, m0, n0, smem);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // prologue: slabs 0..NSTAGE-2 in flight
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s)
+    if (s < nk) load_stage(A, lda, B, ldb, s * BK, m0, n0, smem + s * STAGE);
   for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * STAGE;
-    if (kt + 1 < nk) load_stage(A, lda, B, ldb, (kt + 1) * BK, m0, n0, smem + ((kt + 1) & 1) * STAGE);
+    // slab kt must have landed; slabs issued after it (up to NSTAGE-2 of them, 4 loads each) may
+    // still be in flight -- counted wait, never vmcnt(0) in steady state
+    const int after = min(nk - 1 - kt, NSTAGE - 2);
+    if (after >= 2)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (after == 1)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // WAR-safe: stage (kt-1)%NSTAGE was last read in iteration kt-1, which every wave has left
+    if (kt + NSTAGE - 1 < nk)
+      load_stage(A, lda, B, ldb, (kt + NSTAGE - 1) * BK, m0, n0, smem + ((kt + NSTAGE - 1) % NSTAGE) * STAGE);
+    const char* cur = smem + (kt % NSTAGE) * STAGE;
     const char* Ah = cur + wr * HALF;                         // A columns wr*128 .. +128
     const char* Bh = cur + (2 + (wc >> 1)) * HALF;            // B columns (wc>>1)*128 .. +128
 #pragma unroll
@@ -123,28 +141,38 @@ __global__ void __launch_bounds__(NTHR, 1) wgrad_kernel(const unsigned short* __
       for (int i = 0; i < 4; ++i) a[i] = frag(Ah, ks * 16, i, lane);
 #pragma unroll
       for (int j = 0; j < 2; ++j) b[j] = frag(Bh, ks * 16, (wc & 1) * 2 + j, lane);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
-  // ---- epilogue: C (+)= alpha * acc ---------------------------------------------------------
+  // ---- epilogue: C (+)= alpha * acc, two accumulator tiles (32 values / lane) per batch so the
+  // C reads are in flight together instead of one dependent round trip per value
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int h = lane >> 5, col = lane & 31;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i) {
+    float* rowp[2];
+    float old[2][16];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      rowp[j] = C + (int64_t)(m0 + wr * 128 + i * 32) * ldc + n0 + wc * 64 + j * 32 + col;
+      if (ACCUM) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) old[j][e] = __builtin_nontemporal_load(rowp[j] + (int64_t)acc_row(e, h) * ldc);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int m = m0 + wr * 128 + i * 32 + acc_row(e, h);
-        const int n = n0 + wc * 64 + j * 32 + col;
-        float* p = C + (int64_t)m * ldc + n;
         const float v = alpha * acc[i][j][e];
-        *p = ACCUM ? *p + v : v;
+        rowp[j][(int64_t)acc_row(e, h) * ldc] = ACCUM ? old[j][e] + v : v;
       }
+  }
 }
 
 }  // namespace wg
