@@ -13,6 +13,7 @@ stream (the result is needed immediately), so TP degree should stay within a nod
 """
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .. import comm as dist
 from ..ops.linear import linear
@@ -65,6 +66,65 @@ class _GatherFromTP(torch.autograd.Function):
         return g.chunk(ws, dim=-1)[ctx.rank].contiguous(), None
 
 
+class _ColumnParallelLinear(torch.autograd.Function):
+    """Column-parallel GEMM whose backward overlaps the input-gradient all-reduce with the
+    weight-gradient GEMM: dX = dY W is computed first and its all-reduce is launched
+    asynchronously (RCCL runs on its own stream over xGMI) before dW = dY^T X is issued on the
+    compute stream. Without ``handles`` the wait is at the end of this backward; with a
+    ``handles`` list (Domino) the Work is parked there and waited by ``wait_grad_handles``
+    further down the graph, so it also overlaps the other micro-batch's backward.
+    (Reference: runtime/domino/async_linear.py:14-36 ``DominoAsyncColumnParallelLinearImpl``.)"""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, group, handles):
+        ctx.save_for_backward(x, weight)
+        ctx.group, ctx.handles, ctx.has_bias = group, handles, bias is not None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        from ..ops.linear import write_weight_grad
+        x, w = ctx.saved_tensors
+        dx = dw = db = None
+        work = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.matmul(gy, w).contiguous()
+            work = dist.all_reduce(dx, group=ctx.group, async_op=True)
+        gy2 = gy.reshape(-1, gy.shape[-1])
+        if ctx.needs_input_grad[1]:
+            x2 = x.reshape(-1, x.shape[-1])
+            if not write_weight_grad(w, gy2, x2):
+                dw = gy2.t() @ x2
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = gy2.sum(0)
+        if work is not None:
+            if ctx.handles is not None:
+                ctx.handles.append(work)
+            else:
+                work.wait()
+        return dx, dw, db, None, None
+
+
+class _WaitGradHandles(torch.autograd.Function):
+    """Identity; its backward waits for the input-grad all-reduces parked by the column-parallel
+    layers that consume this tensor (reference runtime/domino/transformer.py:50-70 ``NoOper``)."""
+
+    @staticmethod
+    def forward(ctx, x, handles):
+        ctx.handles = handles
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        while ctx.handles:
+            ctx.handles.pop().wait()
+        return g, None
+
+
+def wait_grad_handles(x, handles):
+    return _WaitGradHandles.apply(x, handles)
+
+
 def copy_to_tp(x, group):
     return _CopyToTP.apply(x, group)
 
@@ -111,10 +171,13 @@ class LinearLayer(TensorParallelLinearBase):
             self.bias.tensor_model_parallel = True
         self.gather_output = gather_output
 
-    def forward(self, x, skip_bias=False):
-        if self.tp_group is not None and self.tp_world_size > 1:
-            x = copy_to_tp(x, self.tp_group)
-        y = linear(x, self.weight, None if skip_bias else self.bias)
+    def forward(self, x, skip_bias=False, grad_handles=None):
+        b = None if skip_bias else self.bias
+        if self.tp_group is not None and self.tp_world_size > 1 and torch.is_grad_enabled() and (
+                x.requires_grad or self.weight.requires_grad):
+            y = _ColumnParallelLinear.apply(x, self.weight, b, self.tp_group, grad_handles)
+        else:
+            y = linear(x, self.weight, b)
         if self.gather_output and self.tp_world_size > 1:
             y = gather_from_tp(y, self.tp_group)
         return y
@@ -133,6 +196,10 @@ class LinearAllreduce(TensorParallelLinearBase):
         if self.bias is not None and not skip_bias:
             y = y + self.bias
         return y
+
+    def forward_partial(self, x):
+        """x_local W_local^T without the reduction (Domino launches it asynchronously)."""
+        return linear(x, self.weight)
 
 
 class LmHeadLinearAllreduce(LinearAllreduce):
