@@ -65,7 +65,11 @@ def main():
         "bf16": {"enabled": True},
         "gradient_clipping": 1.0,
         "zero_optimization": {"stage": args.stage, "overlap_comm": True, "reduce_bucket_size": 500_000_000,
-                              "stage3_param_persistence_threshold": 100_000, "prefetch_depth": 2},
+                              "stage3_param_persistence_threshold": 100_000, "prefetch_depth": 2,
+                              # 288 GB HBM: the whole bf16 model (16 GB for 8B) may stay gathered from
+                              # its forward use to its backward re-use -> no backward all-gather
+                              "stage3_max_reuse_distance": 2 * cfg.num_params(),
+                              "stage3_max_live_parameters": cfg.num_params()},
         "optimizer": {"type": "AdamW", "params": {"lr": 3e-4, "betas": [0.9, 0.95], "eps": 1e-8,
                                                    "weight_decay": 0.1}},
         "steps_per_print": 1000000,

@@ -107,7 +107,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                  prefetch_depth=2, param_persistence_threshold=100_000, communication_data_type=None,
                  unit_classes=None, shuffle_exchange_cfg=None, mp_group=None, timers=None, mics_shard_size=-1,
                  average_master=False, host_step=None, offload_param=False, quantized_weights=False,
-                 quantized_gradients=False, hpz_partition_size=1, quant_group_size=128, grad_quant_bits=8):
+                 quantized_gradients=False, hpz_partition_size=1, quant_group_size=128, grad_quant_bits=8,
+                 max_reuse_distance=1_000_000_000, max_live_parameters=1_000_000_000):
         acc = get_accelerator()
         device = torch.device(acc.current_device_name())
         self.module = module
@@ -157,6 +158,9 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             self.hpz = 1
         self.prefetch_depth = max(0, int(prefetch_depth))
         self.persist_thr = int(param_persistence_threshold)
+        self.max_reuse_distance = int(max_reuse_distance)
+        self.max_live_parameters = int(max_live_parameters)
+        self._kept_numel = 0
         self.comm_dtype = communication_data_type
         self.timers = timers
         self.ag_stream = acc.named_stream("zero3_allgather") if acc.gpu else None
@@ -294,7 +298,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         def post(mod, args, out):
             if torch.is_grad_enabled() and any(u.params[0].requires_grad for u in fg.units):
                 out = self._wrap_outputs(fg, out)
-            if not self._in_bwd and not (torch.is_grad_enabled() and self._is_last_forward(fg)):
+            if not self._in_bwd and not (torch.is_grad_enabled() and self._keep_for_backward(fg)):
                 self._release(fg)
             return out
         return post
@@ -326,6 +330,36 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
 
     def _is_last_forward(self, fg):
         return bool(self.trace) and self.trace[-1] == fg.idx
+
+    def _reuse_distances(self):
+        """Per fetch group: gathered numel traversed between its forward use and its backward
+        re-use (the later forward groups, then the same groups again in reverse), i.e. the
+        reference's reuse distance (partitioned_param_coordinator.py:529-559) on our unit trace."""
+        key = tuple(self.trace)
+        if getattr(self, "_reuse_key", None) != key:
+            size = {fg.idx: sum(u.padded for u in fg.units if not u.persistent) for fg in self.fgroups}
+            dist_, acc = {}, 0
+            for i in reversed(self.trace):
+                dist_[i] = 2 * acc
+                acc += size.get(i, 0)
+            self._reuse, self._reuse_key, self._fg_numel = dist_, key, size
+        return self._reuse
+
+    def _keep_for_backward(self, fg):
+        """Keep a forward-gathered group resident for its backward re-use when its reuse distance is
+        below ``max_reuse_distance`` and the resident budget ``max_live_parameters`` allows it. With
+        288 GB of HBM per GPU a whole 8B model fits (16 GB bf16), which removes the backward
+        all-gather (one third of ZeRO-3's per-micro-step traffic)."""
+        if self._is_last_forward(fg):
+            return True
+        if self.max_reuse_distance <= 0 or self.S == 1:
+            return False
+        d = self._reuse_distances().get(fg.idx)
+        n = self._fg_numel.get(fg.idx, 0)
+        if d is None or d >= self.max_reuse_distance or self._kept_numel + n > self.max_live_parameters:
+            return False
+        self._kept_numel += n
+        return True
 
     def _make_grad_hook(self, unit):
         def hook(p):
@@ -489,6 +523,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
     def forward_prologue(self):
         self._in_bwd = False
         self._observed = []
+        self._kept_numel = 0
 
     def backward_prologue(self):
         for units in self.units:

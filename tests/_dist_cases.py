@@ -223,3 +223,29 @@ def case_mixtral_train(rank, world, stage):
         eng.step()
         losses.append(float(loss.detach()))
     return {"losses": losses}
+
+
+def case_zero3_reuse(rank, world, max_reuse, steps, mbs, seq):
+    """ZeRO-3 with a reuse-distance budget: count the unit all-gathers issued by the optimizer."""
+    import shuffle_exchange_amd as sxe
+    model, cfg = tiny_llama(0)
+    ds = {"train_micro_batch_size_per_gpu": mbs,
+          "zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 0,
+                                "stage3_max_reuse_distance": max_reuse, "stage3_max_live_parameters": 10**12},
+          "optimizer": {"type": "AdamW", "params": {"lr": 1e-2, "weight_decay": 0.01}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    opt = eng.optimizer
+    n_gathers = [0]
+    orig = opt._launch_gather
+
+    def counting(u):
+        n_gathers[0] += 1
+        return orig(u)
+    opt._launch_gather = counting
+    for b in global_batches(cfg, world, mbs, seq, steps):
+        local = b[rank * mbs:(rank + 1) * mbs]
+        loss = eng(local, labels=local)
+        eng.backward(loss)
+        eng.step()
+    opt._launch_gather = orig
+    return {"params": full_params(eng), "gathers": n_gathers[0]}

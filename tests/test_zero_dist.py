@@ -161,3 +161,16 @@ def test_offload_reload_states_roundtrip(stage):
                                    "zero_optimization": {"stage": stage, "stage3_param_persistence_threshold": 0},
                                    "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}}}, 4, 1, 16)
     _close(a[0], b[0]["params"], tol=1e-6)
+
+
+def test_zero3_reuse_distance_skips_backward_gathers():
+    """stage3_max_reuse_distance (reference partitioned_param_coordinator.py:529-559): units whose
+    forward->backward reuse distance fits the budget stay gathered, so the backward all-gathers
+    disappear; the numerics are unchanged (== single-process AdamW)."""
+    world, mbs, seq, steps = 2, 2, 16, 3
+    keep = run_dist(C.case_zero3_reuse, world, 10**12, steps, mbs, seq)
+    drop = run_dist(C.case_zero3_reuse, world, 0, steps, mbs, seq)
+    ref = C.reference_train(ADAMW, steps, world, mbs, seq)
+    for r in keep + drop:
+        _close(r["params"], ref)
+    assert keep[0]["gathers"] < drop[0]["gathers"], (keep[0]["gathers"], drop[0]["gathers"])
