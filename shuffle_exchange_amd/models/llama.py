@@ -53,6 +53,9 @@ class LlamaConfig:
     activation_checkpointing: bool = False
     loss_chunk_tokens: Optional[int] = None
     sequence_parallel: bool = False  # Ulysses: inputs are [B, S/sp] chunks of the SP group
+    fpdt_chunk_size: int = 0         # >0: FPDT chunked attention (global chunk length); inputs laid
+                                     # out by sequence.fpdt_layer.FPDT_InputConstruct
+    fpdt_offload: bool = False       # FPDT: keep the saved q/k/v/o chunks in pinned host memory
     extra: dict = field(default_factory=dict)
 
     def __post_init__(self):
@@ -108,7 +111,13 @@ class LlamaAttention(nn.Module):
         B, S, _ = x.shape
         qkv = self.qkv_proj(x).view(B, S, self.nq + 2 * self.nkv, self.d)
         spg = _sp_group() if self.cfg.sequence_parallel else None
-        if spg is not None:
+        if self.cfg.fpdt_chunk_size:
+            from ..sequence.fpdt_layer import fpdt_attention
+            from .. import comm as dist
+            p = dist.get_world_size(spg) if spg is not None else 1
+            n = max(1, S * p // self.cfg.fpdt_chunk_size)
+            o = fpdt_attention(qkv, self.nq, self.nkv, rope, spg, n, offload=self.cfg.fpdt_offload)
+        elif spg is not None:
             o = ulysses_qkv_attention(qkv, self.nq, self.nkv, rope, spg, position_ids, causal=True)
         else:
             o = attention_qkv_rope(qkv, self.nq, self.nkv, rope, position_ids, causal=True)
