@@ -1,5 +1,5 @@
 // Activation kernels for gfx950: SwiGLU/GeGLU (gated, concatenated [gate | up] layout) and
-// bias + activation (GELU-tanh / ReLU / SiLU / identity), forward and backward.
+// bias + activation (GELU-tanh / exact GELU / ReLU / SiLU / identity), forward and backward.
 //
 // Reference semantics: core_ops/bias_activations/bias_activation_cuda.cu:17-51 (in-place
 // act(x + b)) and core_ops/gated_activations/gated_activation_kernels_cuda.cu:45 (gated act).
@@ -12,7 +12,7 @@
 
 namespace sxe {
 
-enum Act : int { ACT_IDENTITY = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_SILU = 3 };
+enum Act : int { ACT_IDENTITY = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_SILU = 3, ACT_GELU_ERF = 4 };
 
 __device__ __forceinline__ float act_f(float x, int act) {
   switch (act) {
@@ -23,6 +23,7 @@ __device__ __forceinline__ float act_f(float x, int act) {
       return 0.5f * x * (1.f + t);
     }
     case ACT_SILU: return x / (1.f + __expf(-x));
+    case ACT_GELU_ERF: return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
     default: return x;
   }
 }
@@ -39,6 +40,10 @@ __device__ __forceinline__ float act_df(float x, int act) {
     case ACT_SILU: {
       float s = 1.f / (1.f + __expf(-x));
       return s * (1.f + x * (1.f - s));
+    }
+    case ACT_GELU_ERF: {
+      const float cdf = 0.5f * (1.f + erff(x * 0.7071067811865476f));
+      return cdf + x * 0.3989422804014327f * __expf(-0.5f * x * x);
     }
     default: return 1.f;
   }

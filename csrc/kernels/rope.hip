@@ -15,11 +15,13 @@
 
 namespace sxe {
 
-// x: base pointer of token 0, head 0; token t, head h, dim d at x[t*tok_stride + h*D + d].
+// x: base pointer of token 0, head 0; token t, head h, dim d at x[t*tok_stride + h*head_stride + d]
+// (head_stride > D: partial rotary -- only the first D dims of each head rotate, Phi/GPT-NeoX style).
 // Each thread rotates 8 consecutive pairs (16-byte vectors from both halves of one head).
 template <DT T>
 __global__ void __launch_bounds__(256) rope_kernel(typename dt_traits<T>::storage* __restrict__ x, int64_t tokens,
-                                                   int64_t tok_stride, int nheads, int D, const float* __restrict__ cos_t,
+                                                   int64_t tok_stride, int64_t head_stride, int nheads, int D,
+                                                   const float* __restrict__ cos_t,
                                                    const float* __restrict__ sin_t, const int64_t* __restrict__ pos,
                                                    int64_t seq_len, int64_t pos_offset, float sign) {
   const int half = D / 2;
@@ -33,7 +35,7 @@ __global__ void __launch_bounds__(256) rope_kernel(typename dt_traits<T>::storag
     const int h = rem / vec_per_head;
     const int c = (rem - h * vec_per_head) * 8;
     const int64_t p = pos ? pos[t] : (t % seq_len) + pos_offset;
-    typename dt_traits<T>::storage* base = x + t * tok_stride + (int64_t)h * D;
+    typename dt_traits<T>::storage* base = x + t * tok_stride + (int64_t)h * head_stride;
     float a[8], b[8], cs[8], sn[8];
     load8<T>(base + c, a);
     load8<T>(base + half + c, b);
@@ -51,14 +53,17 @@ __global__ void __launch_bounds__(256) rope_kernel(typename dt_traits<T>::storag
   }
 }
 
-// x: [..., tokens, heads, D] view with unit stride on D and a uniform token stride.
+// x: [..., tokens, heads, D] view with unit stride on D, head stride >= D (a partial-rotary view
+// x[..., :rot] of the full heads is allowed) and a uniform token stride.
 void rope_(at::Tensor x, at::Tensor cos_t, at::Tensor sin_t, c10::optional<at::Tensor> pos, int64_t seq_len,
            int64_t pos_offset, bool inverse) {
   SXE_CHECK(x.dim() >= 3, "rope_: x must be [..., tokens, heads, D]");
   const int D = (int)x.size(-1);
   const int nheads = (int)x.size(-2);
   SXE_CHECK(D % 16 == 0, "rope_: head dim must be a multiple of 16");
-  SXE_CHECK(x.stride(-1) == 1 && x.stride(-2) == D, "rope_: heads must be packed with unit stride on D");
+  SXE_CHECK(x.stride(-1) == 1 && x.stride(-2) >= D && x.stride(-2) % 8 == 0,
+            "rope_: unit stride on D, 16-byte aligned head stride >= D");
+  const int64_t head_stride = x.stride(-2);
   const int64_t tok_stride = x.stride(-3);
   const int64_t tokens = x.numel() / ((int64_t)nheads * D);
   // tokens must be uniformly strided across the leading dims ([B, S] flattened).
@@ -78,7 +83,8 @@ void rope_(at::Tensor x, at::Tensor cos_t, at::Tensor sin_t, c10::optional<at::T
   SXE_DISPATCH_DT(d, TT, {
     using S = typename dt_traits<TT>::storage;
     hipLaunchKernelGGL((rope_kernel<TT>), dim3(stream_grid(work, 256)), dim3(256), 0, cur_stream(),
-                       reinterpret_cast<S*>(x.data_ptr()), tokens, tok_stride, nheads, D, cos_t.data_ptr<float>(),
+                       reinterpret_cast<S*>(x.data_ptr()), tokens, tok_stride, head_stride, nheads, D,
+                       cos_t.data_ptr<float>(),
                        sin_t.data_ptr<float>(), hp ? pos->data_ptr<int64_t>() : nullptr, seq_len > 0 ? seq_len : 1,
                        pos_offset, inverse ? -1.f : 1.f);
   });

@@ -1,0 +1,20 @@
+"""Build a ragged inference engine from a Hugging Face model or checkpoint directory.
+
+Parity: reference inference/v2/engine_factory.py:69-133 ``build_hf_engine(path, engine_config,
+debug_level)`` -- reads the checkpoint's ``config.json``, picks the model implementation by
+``model_type`` (llama / mistral / mixtral / opt / falcon / phi / phi3 / qwen2 / qwen2_moe) and
+returns an ``InferenceEngineV2``. No hub access here: ``path`` is a local directory (or an
+already-instantiated transformers model); weights are read with safetensors / ``weights_only``.
+"""
+import torch
+
+from .engine_v2 import InferenceEngineV2, RaggedInferenceEngineConfig
+from .model_implementations.hf_decoder import load_hf_decoder
+
+
+def build_hf_engine(path_or_model, engine_config: RaggedInferenceEngineConfig = None, dtype=torch.bfloat16,
+                    device=None, debug_level=None):
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+    model = load_hf_decoder(path_or_model, dtype=dtype, device=device)
+    return InferenceEngineV2(model, engine_config)

@@ -1,9 +1,24 @@
-"""Ragged model implementations (reference inference/v2/model_implementations/)."""
+"""Ragged model implementations (reference inference/v2/model_implementations/).
+
+* ``RaggedLlama``: serves this framework's own LlamaForCausalLM / MixtralForCausalLM training
+  modules in place (no weight copy);
+* ``RaggedDecoder`` (hf_decoder.py): Hugging Face checkpoints of the FastGen families -- Llama-2/3,
+  Mistral, Mixtral, Qwen2, Qwen2-MoE, Phi, Phi-3, Falcon, OPT -- converted once into the packed
+  layout of the gfx950 kernels.
+"""
+from .hf_decoder import RaggedDecoder, load_hf_decoder, spec_from_hf_config  # noqa: F401
 from .llama import RaggedLlama  # noqa: F401
 
 
 def ragged_model_for(model):
-    """Pick the ragged implementation for a framework model (Llama-family incl. Mixtral)."""
+    """Pick the ragged implementation for a model object."""
+    if isinstance(model, (RaggedDecoder, RaggedLlama)):
+        return model
+    if hasattr(model, "config") and hasattr(model.config, "model_type") and hasattr(model.config, "to_dict"):
+        p = next(model.parameters())
+        dtype = p.dtype if p.dtype in (__import__("torch").bfloat16, __import__("torch").float16,
+                                       __import__("torch").float32) else None
+        return load_hf_decoder(model, dtype=dtype, device=p.device)
     if hasattr(model, "layers") and hasattr(model.layers[0], "self_attn") and hasattr(model, "embed_tokens"):
         return RaggedLlama(model)
     raise NotImplementedError(f"no ragged inference implementation for {type(model).__name__}")

@@ -8,7 +8,9 @@ import torch.nn.functional as F
 
 from . import native
 
-ACT = {"identity": 0, "relu": 1, "gelu": 2, "silu": 3}
+ACT = {"identity": 0, "relu": 1, "gelu": 2, "silu": 3, "gelu_exact": 4,
+       # HF activation names
+       "gelu_new": 2, "gelu_pytorch_tanh": 2, "gelu_fast": 2, "swish": 3}
 
 
 def _act_ref(x, act):
@@ -18,6 +20,8 @@ def _act_ref(x, act):
         return F.gelu(x, approximate="tanh")
     if act == 3:
         return F.silu(x)
+    if act == 4:
+        return F.gelu(x)
     return x
 
 

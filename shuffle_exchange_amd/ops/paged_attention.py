@@ -15,7 +15,7 @@ from . import native
 
 def kv_cache_append(qkv, cache, slots, nq, nkv):
     """qkv: [T, nq + 2 nkv, D]; cache: [blocks, 2, nkv, bs, D]; slots: int64 [T] (-1 = skip)."""
-    if native.use_hip(qkv):
+    if native.use_hip(qkv) and qkv.shape[-1] in (64, 128) and qkv.is_contiguous():
         torch.ops.sxe.kv_cache_append(qkv, cache, slots, int(nq), int(nkv))
         return
     bs = cache.shape[3]
@@ -40,7 +40,7 @@ def _gather_kv(cache, block_row, kv_len):
     return k, v  # [nkv, kv_len, D]
 
 
-def paged_attention_reference(q, cache, block_table, q_start, q_len, kv_len, scale):
+def paged_attention_reference(q, cache, block_table, q_start, q_len, kv_len, scale, window=None):
     T, nq, D = q.shape
     nkv = cache.shape[2]
     G = nq // nkv
@@ -56,7 +56,10 @@ def paged_attention_reference(q, cache, block_table, q_start, q_len, kv_len, sca
         sc = torch.matmul(qq, k.transpose(1, 2)) * scale  # [nq, ql, kl]
         pos = torch.arange(kl - ql, kl, device=q.device)[:, None]
         keys = torch.arange(kl, device=q.device)[None, :]
-        sc = sc.masked_fill(keys > pos, float("-inf"))
+        mask = keys > pos
+        if window:  # sliding-window attention (Mistral / Qwen2): only the last `window` keys
+            mask = mask | (keys <= pos - window)
+        sc = sc.masked_fill(mask, float("-inf"))
         o = torch.matmul(torch.softmax(sc, dim=-1), v)  # [nq, ql, D]
         out[qs:qs + ql] = o.transpose(0, 1).to(q.dtype)
     return out
@@ -69,11 +72,19 @@ def choose_splits(num_seqs, nkv, max_kv_len, target_wgs=512):
     return max(1, min(want, math.ceil(max(max_kv_len, 1) / 256)))
 
 
-def paged_attention(q, cache, block_table, q_start, q_len, kv_len, scale, max_kv_len, splits=None):
-    """q: [T, nq, D] (head stride D); metadata int32 [S]; returns [T, nq, D]."""
-    if native.use_hip(q):
+def paged_attention(q, cache, block_table, q_start, q_len, kv_len, scale, max_kv_len, splits=None, window=None):
+    """q: [T, nq, D] (head stride D); metadata int32 [S]; returns [T, nq, D]. ``window``: sliding
+    window length (keys older than ``window`` positions are masked); the HIP kernel covers head dims
+    64/128 with the window wider than every context."""
+    if window is not None and max_kv_len <= window:
+        window = None
+    if native.use_hip(q) and window is None and q.shape[-1] in (64, 128):
         if splits is None:
             splits = choose_splits(block_table.shape[0], cache.shape[2], max_kv_len)
         return torch.ops.sxe.paged_attention(q, cache, block_table, q_start, q_len, kv_len, float(scale),
                                              int(max_kv_len), int(splits))
-    return paged_attention_reference(q, cache, block_table, q_start, q_len, kv_len, scale)
+    if q.is_cuda:
+        from ..utils.logging import warning_once
+        warning_once(f"paged_attention: head_dim={q.shape[-1]} window={window} not covered by the HIP kernel; "
+                     f"using the PyTorch reference")
+    return paged_attention_reference(q, cache, block_table, q_start, q_len, kv_len, scale, window)

@@ -87,16 +87,18 @@ def apply_rope(x, cache, position_ids=None, pos_offset=0):
     return apply_rope_qkv_(x, cache, H, position_ids, pos_offset)
 
 
-def apply_rope_tokens_(qkv, cache, n_rot, positions):
+def apply_rope_tokens_(qkv, cache, n_rot, positions, rot_dim=None):
     """In-place RoPE on the first ``n_rot`` heads of a ragged token batch ``qkv`` [T, H, D] with
-    absolute ``positions`` [T] (inference engine; no autograd)."""
+    absolute ``positions`` [T] (inference engine; no autograd). ``rot_dim`` < D rotates only the
+    first ``rot_dim`` dims of each head (partial rotary: Phi, GPT-NeoX); ``cache`` is built for it."""
     T = qkv.shape[0]
     if T == 0:
         return qkv
+    rd = rot_dim or qkv.shape[-1]
     pos = positions.reshape(-1).contiguous().long()
-    if native.use_hip(qkv):
-        torch.ops.sxe.rope_(qkv.unsqueeze(0)[:, :, :n_rot, :], cache.cos, cache.sin, pos, T, 0, False)
+    if native.use_hip(qkv) and rd % 16 == 0:
+        torch.ops.sxe.rope_(qkv.unsqueeze(0)[:, :, :n_rot, :rd], cache.cos, cache.sin, pos, T, 0, False)
         return qkv
-    x = qkv[:, :n_rot, :].float()
-    qkv[:, :n_rot, :] = _ref_rope(x, cache.cos.to(qkv.device), cache.sin.to(qkv.device), pos).to(qkv.dtype)
+    x = qkv[:, :n_rot, :rd].float()
+    qkv[:, :n_rot, :rd] = _ref_rope(x, cache.cos.to(qkv.device), cache.sin.to(qkv.device), pos).to(qkv.dtype)
     return qkv
