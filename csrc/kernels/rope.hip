@@ -67,7 +67,8 @@ void rope_(at::Tensor x, at::Tensor cos_t, at::Tensor sin_t, c10::optional<at::T
   const int64_t tok_stride = x.stride(-3);
   const int64_t tokens = x.numel() / ((int64_t)nheads * D);
   // tokens must be uniformly strided across the leading dims ([B, S] flattened).
-  if (x.dim() > 3) SXE_CHECK(x.stride(-4) == tok_stride * x.size(-3), "rope_: leading dims must flatten uniformly");
+  if (x.dim() > 3 && x.size(-4) > 1)
+    SXE_CHECK(x.stride(-4) == tok_stride * x.size(-3), "rope_: leading dims must flatten uniformly");
   SXE_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat && cos_t.is_contiguous() &&
                 sin_t.is_contiguous() && cos_t.size(-1) == D / 2, "rope_: cos/sin tables must be fp32 [max_pos, D/2]");
   const bool hp = pos.has_value() && pos->defined();

@@ -212,7 +212,7 @@ class _FPDTAttention(torch.autograd.Function):
         qs, ks, vs, os_, lses = [], [], [], [], []
         outs = []
         for c in range(num_chunks):
-            x = qkv[:, c * L:(c + 1) * L].clone()
+            x = qkv[:, c * L:(c + 1) * L].clone(memory_format=torch.contiguous_format)
             # local chunk c of rank r is global chunk c*p + r (FPDT_InputConstruct layout)
             pos = (torch.arange(L, device=x.device) + (c * p + r) * L).repeat(B)
             _rope_(x, rope, nq + nkv, pos)
