@@ -62,6 +62,10 @@ class ZeroOptimizerBase:
     # --------------------------------------------------------------------------------------------
     def _init_master(self):
         """Create fp32 masters/grad accumulators and re-point the wrapped optimizer at them."""
+        for g, units in enumerate(self.units):  # lp -> hp linkage for utils/tensor_fragment.py
+            for u in units:
+                for i, p in enumerate(u.params):
+                    p._sxe_zero = (self, g, u, i)
         if self.host_step is not None:
             return self.host_step.init_master(self)
         for g, units in enumerate(self.units):
