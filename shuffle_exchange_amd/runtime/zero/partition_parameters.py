@@ -132,3 +132,21 @@ def gather_all(engine_or_optimizer):
         yield
     finally:
         opt.release_all()
+
+
+def register_external_parameter(module, parameter):
+    """Declare that ``module``'s forward uses ``parameter`` although another module owns it
+    (reference partition_parameters.py ``register_external_parameter``): under ZeRO-3 the module's
+    fetch then gathers the owning unit as well. Call before ``initialize()``. Parameters of a
+    module that are owned by another unit (tied weights) are detected automatically."""
+    lst = getattr(module, "_sxe_external_params", None)
+    if lst is None:
+        lst = []
+        module._sxe_external_params = lst
+    if all(p is not parameter for p in lst):
+        lst.append(parameter)
+
+
+def unregister_external_parameter(module, parameter):
+    lst = getattr(module, "_sxe_external_params", [])
+    module._sxe_external_params = [p for p in lst if p is not parameter]

@@ -204,6 +204,32 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 for p in plist:
                     self.param_unit[p] = u
             self.fgroups.append(fg)
+        # external parameters: a module that uses a parameter owned by another unit (tied
+        # embeddings / LM head, or register_external_parameter) fetches that unit too (reference
+        # partition_parameters.py register_external_parameter, parameter_offload.py external params)
+        fg_of = {id(fg.module): fg for fg in self.fgroups}
+
+        def scan(mod, name, cover):
+            fg = fg_of.get(id(mod))
+            here = fg if fg is not None else cover  # the fetch group whose hook runs around mod
+            ext = list(getattr(mod, "_sxe_external_params", []))
+            ext += [p for p in mod.parameters(recurse=False)
+                    if p in self.param_unit and self.param_unit[p].fg is not here]
+            ext_units = []
+            for p in ext:
+                u = self.param_unit.get(p)
+                if u is not None and u not in ext_units and (here is None or u not in here.units):
+                    ext_units.append(u)
+            if ext_units:
+                if fg is None:
+                    fg = _FetchGroup(len(self.fgroups), (name or "#root") + "#external", mod, True)
+                    self.fgroups.append(fg)
+                    fg_of[id(mod)] = fg
+                fg.units.extend(ext_units)
+            nxt = cover if (fg is not None and fg.own_only) else (fg if fg is not None else cover)
+            for cname, child in mod.named_children():
+                scan(child, f"{name}.{cname}" if name else cname, nxt)
+        scan(self.module, "", None)
         # any trainable param not under a discovered module (should not happen) -> root unit
         rest = [p for pg in self.optimizer.param_groups for p in pg["params"] if p.requires_grad and p not in self.param_unit]
         if rest:

@@ -249,3 +249,20 @@ def case_zero3_reuse(rank, world, max_reuse, steps, mbs, seq):
         eng.step()
     opt._launch_gather = orig
     return {"params": full_params(eng), "gathers": n_gathers[0]}
+
+
+def case_tied_zero3(rank, world, steps):
+    """ZeRO-3 with tied embedding / LM head and no reuse budget: the LM head must fetch the
+    embedding's unit itself (external parameter)."""
+    import shuffle_exchange_amd as sxe
+    model, cfg = tiny_llama(0, tie_word_embeddings=True)
+    ds = {"train_micro_batch_size_per_gpu": 1,
+          "zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 0, "stage3_max_reuse_distance": 0},
+          "optimizer": {"type": "SGD", "params": {"lr": 0.1}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    for b in global_batches(cfg, world, 1, 16, steps):
+        local = b[rank:rank + 1]
+        loss = eng(local, labels=local)
+        eng.backward(loss)
+        eng.step()
+    return {"params": full_params(eng), "fgs": [fg.name for fg in eng.optimizer.fgroups]}

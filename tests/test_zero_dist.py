@@ -174,3 +174,18 @@ def test_zero3_reuse_distance_skips_backward_gathers():
     for r in keep + drop:
         _close(r["params"], ref)
     assert keep[0]["gathers"] < drop[0]["gathers"], (keep[0]["gathers"], drop[0]["gathers"])
+
+
+def test_zero3_tied_embeddings_external_parameter():
+    res = run_dist(C.case_tied_zero3, 2, 2)
+    model, cfg = C.tiny_llama(0, tie_word_embeddings=True)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    for b in C.global_batches(cfg, 2, 1, 16, 2):
+        loss = model(b, labels=b)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    ref = {n: p.detach().clone() for n, p in model.named_parameters()}
+    for r in res:
+        assert "lm_head#external" in r["fgs"]
+        _close(r["params"], ref)
