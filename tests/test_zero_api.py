@@ -71,3 +71,36 @@ def test_runtime_utils():
     assert parts[0] == 0 and parts[-1] == 6 and len(parts) == 4
     loads = [sum([1, 1, 1, 10, 1, 1][parts[i]:parts[i + 1]]) for i in range(3)]
     assert max(loads) == 10
+
+
+def _case_fp16_wrappers(rank, world):
+    import shuffle_exchange_amd as sxe  # noqa: F401
+    from shuffle_exchange_amd.runtime.fp16.fused_optimizer import BF16_Optimizer, FP16_Optimizer
+    from shuffle_exchange_amd.parallel import groups
+    groups.initialize()
+    out = {}
+    for name, make in (("fp16", lambda o: FP16_Optimizer(o, static_loss_scale=1.0)),
+                       ("bf16", lambda o: BF16_Optimizer(o))):
+        torch.manual_seed(0)
+        m = torch.nn.Linear(8, 4)
+        opt = make(torch.optim.SGD(m.parameters(), lr=0.1))
+        x = torch.randn(4, 8, generator=torch.Generator().manual_seed(rank))
+        opt.backward_prologue()
+        m(x).pow(2).mean().backward()
+        opt.reduce_gradients()
+        opt.step()
+        out[name] = m.weight.detach().clone()
+    return out
+
+
+def test_fp16_bf16_optimizer_wrappers():
+    res = run_dist(_case_fp16_wrappers, 2)
+    torch.manual_seed(0)
+    m = torch.nn.Linear(8, 4)
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)
+    xs = [torch.randn(4, 8, generator=torch.Generator().manual_seed(r)) for r in range(2)]
+    (sum(m(x).pow(2).mean() for x in xs) / 2).backward()
+    opt.step()
+    for r in res:
+        for k in ("fp16", "bf16"):
+            assert torch.allclose(r[k], m.weight.detach(), atol=1e-6), k
