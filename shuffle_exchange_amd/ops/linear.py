@@ -11,8 +11,23 @@ target it behaves exactly like ``torch.nn.functional.linear``. (The reference's 
 Megatron-style ``gradient_accumulation_fusion``; DeepSpeed's ZeRO copies each ``p.grad`` into an
 IPG bucket instead, stage_1_and_2.py:1137-1139.)
 """
+import os
+
 import torch
 import torch.nn.functional as F
+
+# Large weight-gradient GEMMs (MLP projections, LM head) run faster as two HBM-speed transposes +
+# a forward-layout ("TN") bf16 GEMM + an fp32 accumulate than as one fp32-output GEMM in the
+# token-major "NT" layout: hipBLASLt reaches 1.47-1.61 PF in TN vs 1.06-1.19 PF in NT on MI355X
+# (tools/wgrad_layout_exp.py, tools/wgrad_tn_exp.py: -0.13 ms per 28672x4096 / 4096x14336 call,
+# -0.47 ms for the 128256x4096 LM head, at K = 8192 tokens). Smaller weights keep the fused path.
+TN_MIN_ELEMS = int(os.environ.get("SXE_WGRAD_TN_MIN_ELEMS", 32 * 2**20))
+
+
+def _tn_ok(gy2, x2):
+    return (gy2.is_cuda and gy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and TN_MIN_ELEMS > 0
+            and gy2.shape[1] * x2.shape[1] >= TN_MIN_ELEMS and gy2.shape[0] % 64 == 0 and gy2.shape[1] % 64 == 0
+            and x2.shape[1] % 64 == 0 and gy2.is_contiguous() and x2.is_contiguous())
 
 
 def write_weight_grad(w, gy2, x2):
@@ -21,7 +36,14 @@ def write_weight_grad(w, gy2, x2):
     if tgt is None:
         return False
     buf, accumulate = tgt(w)
-    if buf.dtype == torch.float32 and gy2.dtype != torch.float32:
+    if _tn_ok(gy2, x2) and buf.is_contiguous():
+        a, b = torch.ops.sxe.transpose16(gy2), torch.ops.sxe.transpose16(x2).t()
+        if buf.dtype == gy2.dtype and not accumulate:
+            torch.mm(a, b, out=buf)  # the reduce-scatter staging slot of a multi-rank unit
+        else:
+            dw = torch.mm(a, b)
+            buf.add_(dw) if accumulate else buf.copy_(dw)
+    elif buf.dtype == torch.float32 and gy2.dtype != torch.float32:
         torch.ops.aten.addmm.dtype_out(buf, gy2.t(), x2, torch.float32, beta=1 if accumulate else 0, alpha=1,
                                        out=buf)
     elif accumulate:
