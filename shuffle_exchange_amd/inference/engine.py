@@ -31,6 +31,7 @@ class InferenceConfig:
     mp_size: Optional[int] = None
     kv_block_size: int = 64
     kv_cache_fraction: float = 0.5
+    weight_quantization: Optional[dict] = None  # {"post_init_quant": {name-key: {num_bits, group_size, ...}}}
 
     def __post_init__(self):
         if isinstance(self.dtype, str):
@@ -63,6 +64,9 @@ class InferenceEngine(torch.nn.Module):
             sd = torch.load(config.checkpoint, map_location="cpu", weights_only=True)
             model.load_state_dict(sd.get("module", sd), strict=False)
         model.to(device=dev, dtype=config.dtype).eval()
+        if config.weight_quantization:
+            from .quantization import _init_group_wise_weight_quantization
+            _init_group_wise_weight_quantization(model, {"weight_quantization": config.weight_quantization})
         self.device = dev
         self._graphs = {}
         self._ragged = None

@@ -104,3 +104,18 @@ def test_build_hf_engine_from_checkpoint_dir(tmp_path):
     gen = eng.generate([ids], max_new_tokens=4)
     ref = model.generate(torch.tensor([ids]), max_new_tokens=4, do_sample=False)[0, len(ids):].tolist()
     assert gen[0] == ref
+
+
+def test_init_inference_kernel_inject_hf_model_generate():
+    """v1 API (reference inference/engine.py + module_inject): init_inference on a transformers model
+    with replace_with_kernel_inject routes generation through the ragged HF decoder."""
+    import shuffle_exchange_amd as sxe
+    torch.manual_seed(0)
+    model = _tiny("mistral").eval()
+    ref_model = _tiny("mistral").eval()
+    ref_model.load_state_dict(model.state_dict())
+    eng = sxe.init_inference(model, dtype=torch.float32, replace_with_kernel_inject=True)
+    ids = torch.tensor([[5, 9, 17, 33, 2, 71, 8]])
+    out = eng.generate(ids, max_new_tokens=5)
+    ref = ref_model.generate(ids, max_new_tokens=5, do_sample=False)
+    assert out.tolist() == ref.tolist()
