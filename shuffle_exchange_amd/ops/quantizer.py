@@ -93,22 +93,8 @@ def dequantize_fp8(q, scales, group_size=128, out=None, dtype=torch.bfloat16):
     return out
 
 
-class FP_Quantize:
-    """Reference-compatible wrapper (ops/fp_quantizer/quantize.py:17)."""
-
-    def __init__(self, group_size=512):
-        self.group_size = group_size
-        self._scales = None
-        self._shape = None
-
-    def quantize(self, x, q_bits=8, q_mantisa_bits=3, stochastic_mode=False, return_meta_tensor=False):
-        assert q_bits == 8, "FP8 (e4m3) only"
-        self._shape, self._dtype = x.shape, x.dtype
-        q, s = quantize_fp8(x, self.group_size)
-        self._scales = s
-        return (q, s) if return_meta_tensor else q
-
-    def dequantize(self, q, fp_out=None, q_bits=8, q_mantisa_bits=3, scale=None):
-        s = scale if scale is not None else self._scales
-        out = dequantize_fp8(q, s, self.group_size, out=fp_out, dtype=getattr(self, "_dtype", torch.bfloat16))
-        return out.view(self._shape) if self._shape is not None and fp_out is None else out
+def __getattr__(name):  # FP_Quantize lives in ops/fp_quantizer.py (FP8/FP6/FP4)
+    if name == "FP_Quantize":
+        from .fp_quantizer import FP_Quantize
+        return FP_Quantize
+    raise AttributeError(name)

@@ -1,0 +1,60 @@
+"""FP quantizer (reference ops/fp_quantizer): FP8 e4m3 / FP6 e3m2 / FP4 e2m1 group-scaled round trips
+(exact on representable values, bounded error otherwise), selective dequantize, and the FP8 GEMMs."""
+import pytest
+import torch
+
+
+def test_value_tables_match_formats():
+    from shuffle_exchange_amd.ops.fp_quantizer import _TABLES
+    assert _TABLES[4].tolist() == [0.0, 0.5, 1.0, 1.5, 2.0, 3.0, 4.0, 6.0]  # e2m1
+    assert float(_TABLES[6].max()) == 28.0 and len(_TABLES[6]) == 32      # e3m2
+
+
+@pytest.mark.parametrize("bits,mant,tol", [(8, 3, 0.04), (6, 2, 0.09), (4, 1, 0.2)])
+def test_fp_quantize_roundtrip(bits, mant, tol):
+    from shuffle_exchange_amd.ops.fp_quantizer import FP_Quantize
+    torch.manual_seed(0)
+    x = torch.randn(16, 256)
+    fq = FP_Quantize(group_size=128)
+    q = fq.quantize(x, q_bits=bits, q_mantisa_bits=mant)
+    assert q.dtype == torch.uint8 and q.numel() == x.numel() * (bits if bits != 6 else 8) // 8
+    y = fq.dequantize(q).float()
+    assert y.shape == x.shape
+    rel = ((y - x).norm() / x.norm()).item()
+    assert rel < tol, rel
+    # selective dequantize of rows 3 and 7
+    sel = fq.selective_dequantize(q, torch.tensor([3, 7])).float()
+    assert torch.allclose(sel, y[[3, 7]])
+
+
+def test_fp4_exact_on_representable():
+    from shuffle_exchange_amd.ops.fp_quantizer import FP_Quantize
+    vals = torch.tensor([0.0, 0.5, -1.0, 1.5, 2.0, -3.0, 4.0, 6.0] * 16)
+    fq = FP_Quantize(group_size=128)
+    q = fq.quantize(vals, q_bits=4, q_mantisa_bits=1)
+    assert torch.equal(fq.dequantize(q).float(), vals)
+
+
+def test_fp8_linear_and_matmul_fp8_cpu():
+    from shuffle_exchange_amd.ops.fp_quantizer import FP8Linear, matmul_fp8
+    from shuffle_exchange_amd.ops.quantizer import quantize_fp8
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(64, 32)
+    x = torch.randn(8, 64)
+    y = FP8Linear(lin)(x)
+    assert ((y - lin(x)).norm() / lin(x).norm()).item() < 0.06
+    w = torch.randn(64, 48)
+    q, s = quantize_fp8(w.reshape(-1), 64)
+    out = matmul_fp8(x.bfloat16(), q.view(64, 48), s, 64)
+    assert ((out.float() - x @ w).norm() / (x @ w).norm()).item() < 0.05
+
+
+@pytest.mark.gpu
+def test_fp8_linear_gpu_scaled_mm():
+    from shuffle_exchange_amd.ops.fp_quantizer import FP8Linear
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(1024, 512).cuda().bfloat16()
+    x = torch.randn(256, 1024, device="cuda", dtype=torch.bfloat16)
+    ref = lin(x).float()
+    y = FP8Linear(lin)(x).float()
+    assert ((y - ref).norm() / ref.norm()).item() < 0.06
