@@ -2,6 +2,8 @@
 decoupled_checkpoint_engine.py:68, fast_checkpoint_engine.py:16).
 
 * ``TorchCheckpointEngine``: synchronous ``torch.save``.
+* ``FastCheckpointEngine``: ``torch.save`` streamed through ``io.FastFileWriter`` (pinned double
+  buffer -> C++ AIO engine, O_DIRECT); reference fast_checkpoint_engine.py:16.
 * ``AsyncCheckpointEngine`` (the decoupled engine): tensors are snapshotted to pinned host memory on
   a side HIP stream (no GPU stall beyond the D2H copy), then a background thread serialises them;
   ``commit()`` waits. Training continues while the file is written.
@@ -100,3 +102,20 @@ class AsyncCheckpointEngine(CheckpointEngine):
     def commit(self, tag):
         self.wait()
         return True
+
+
+class FastCheckpointEngine(CheckpointEngine):
+    def __init__(self, config_params=None, buffer_size=64 << 20):
+        from ..io import FastFileWriterConfig
+        self.cfg = FastFileWriterConfig(buffer_size=buffer_size)
+
+    def save(self, state_dict, path):
+        from ..io import FastFileWriter
+        tmp = path + ".tmp"
+        w = FastFileWriter(tmp, self.cfg)
+        torch.save(state_dict, w)
+        w.close()
+        os.replace(tmp, path)
+
+
+DecoupledCheckpointEngine = AsyncCheckpointEngine

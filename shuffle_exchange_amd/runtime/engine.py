@@ -42,6 +42,8 @@ FORWARD_GLOBAL_TIMER = "fwd"
 BACKWARD_GLOBAL_TIMER = "bwd"
 STEP_GLOBAL_TIMER = "step"
 
+_FAULTS = bool(os.environ.get("SXE_FAULT"))  # utils/fault.py injection rules present
+
 _DTYPE = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16, "float32": torch.float32,
           "float16": torch.float16, "bfloat16": torch.bfloat16}
 
@@ -124,7 +126,14 @@ class SXEEngine(nn.Module):
             self._configure_optimizer(optimizer, model_parameters)
             self._configure_lr_scheduler(lr_scheduler)
         ckpt = cfg.model.checkpoint
-        self.checkpoint_engine = AsyncCheckpointEngine() if ckpt.async_save else TorchCheckpointEngine()
+        wtype = str((ckpt.writer or {}).get("type", "")).lower()
+        if wtype == "fast":  # reference checkpoint.writer {"type": "fast", "io_buffer_size": ...}
+            from .checkpoint_engine import FastCheckpointEngine
+            self.checkpoint_engine = FastCheckpointEngine(buffer_size=int(ckpt.writer.get("io_buffer_size", 64 << 20)))
+        elif wtype == "decoupled" or ckpt.async_save:
+            self.checkpoint_engine = AsyncCheckpointEngine()
+        else:
+            self.checkpoint_engine = TorchCheckpointEngine()
         self.monitor = None
         try:
             from ..monitor.monitor import MonitorMaster
@@ -499,6 +508,9 @@ class SXEEngine(nn.Module):
             self.lr_scheduler.step(**(lr_kwargs or {}))
         self.global_steps += 1
         self.global_samples += self.train_batch_size()
+        if _FAULTS:
+            from ..utils.fault import maybe_inject
+            maybe_inject(self.global_rank, self.global_steps)
         self._autotuning_probe()
         se = self.shuffle_exchange_config
         if se.enabled and se.auto_shuffle:

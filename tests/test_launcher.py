@@ -65,3 +65,50 @@ def test_env_report_runs():
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
     assert r.returncode == 0, r.stdout
     assert "torch version" in r.stdout and "cpu (Adam" in r.stdout
+
+
+TRAIN_SCRIPT = """
+import os, sys, time
+sys.path.insert(0, os.environ["SXE_ROOT"])
+import torch
+import shuffle_exchange_amd as sxe
+from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+sxe.init_distributed(dist_backend="gloo", verbose=False)
+cfg = llama_config("llama-tiny")
+model = LlamaForCausalLM(cfg)
+eng, _, _, _ = sxe.initialize(model=model, config={"train_micro_batch_size_per_gpu": 1,
+    "zero_optimization": {"stage": 1}, "optimizer": {"type": "SGD", "params": {"lr": 0.1}}})
+ids = torch.randint(0, cfg.vocab_size, (1, 16))
+for step in range(6):
+    loss = eng(ids, labels=ids)
+    eng.backward(loss)
+    eng.step()
+open(os.path.join(sys.argv[-1], f"done{eng.global_rank}"), "w").close()
+"""
+
+
+def test_fault_injection_kill_triggers_launcher_fail_fast(tmp_path):
+    """SXE_FAULT=kill@1:2: rank 1 dies at step 2; the launcher tears the job down with its status
+    instead of leaving rank 0 blocked in the next collective (reference launch.py:338-359)."""
+    script = tmp_path / "t.py"
+    script.write_text(TRAIN_SCRIPT)
+    env = dict(os.environ, PYTHONPATH=ROOT, SXE_ROOT=ROOT, SXE_FAULT="kill@1:2")
+    r = subprocess.run([sys.executable, "-m", "shuffle_exchange_amd.launcher.runner", "-H", "/nonexistent",
+                        "--num_gpus", "2", "--master_port", "29679", "--no_local_rank", str(script), str(tmp_path)],
+                       env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert r.returncode == 17, r.stdout[-3000:]
+    assert "[sxe fault] kill on rank 1 at step 2" in r.stdout
+    assert not (tmp_path / "done0").exists() and not (tmp_path / "done1").exists()
+
+
+def test_fault_rules_parse():
+    from shuffle_exchange_amd.utils import fault
+    os.environ["SXE_FAULT"] = "raise@*:4; kill@3:9"
+    try:
+        assert fault._rules() == [("raise", "*", 4), ("kill", "3", 9)]
+        import pytest
+        with pytest.raises(fault.InjectedFault):
+            fault.maybe_inject(0, 4)
+        fault.maybe_inject(0, 5)
+    finally:
+        del os.environ["SXE_FAULT"]
