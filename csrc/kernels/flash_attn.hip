@@ -124,6 +124,45 @@ struct Stager {
   }
 };
 
+
+// Block-sparse attention (reference ops/sparse_attention: Triton SDD/DSD matmuls + block softmax):
+// a uint8 layout [H, nb, nb] over blk x blk blocks (blk in {16, 32, 64, 128, ...}, a multiple of 16)
+// says which (query block, key block) pairs exist. The kernels below walk only the K (or Q) tiles
+// that intersect a non-zero block -- a compacted tile list built in LDS at kernel start -- and mask
+// scores element-wise inside them, so compute and HBM traffic scale with the layout's density.
+struct Sparse {
+  const uint8_t* layout;  // nullptr = dense
+  int blk, nb;
+};
+
+// Build the list of tiles [t_lo, t_hi) of `tile` rows along one axis whose block range intersects
+// a non-zero block of rows [r_lo, r_hi) along the other axis; `q_axis_rows` says whether the fixed
+// range is the query axis. Returns the count (also in list[-1]); all threads participate.
+__device__ __forceinline__ int build_tile_list(const Sparse sp, int head, int t_lo, int t_hi, int tile, int r_lo,
+                                               int r_hi, bool fixed_is_query, int* list) {
+  int* flags = list + 1024;  // scratch after the list (t_hi - t_lo <= 1024)
+  for (int t = t_lo + (int)threadIdx.x; t < t_hi; t += blockDim.x) {
+    const int a0 = r_lo / sp.blk, a1 = (r_hi - 1) / sp.blk;
+    const int b0 = (t * tile) / sp.blk, b1 = (t * tile + tile - 1) / sp.blk;
+    int act = 0;
+    for (int a = a0; a <= a1 && !act; ++a)
+      for (int bb = b0; bb <= b1; ++bb) {
+        const int qb_ = fixed_is_query ? a : bb, kb_ = fixed_is_query ? bb : a;
+        if (sp.layout[((int64_t)head * sp.nb + qb_) * sp.nb + kb_]) { act = 1; break; }
+      }
+    flags[t - t_lo] = act;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int n = 0;
+    for (int t = t_lo; t < t_hi; ++t)
+      if (flags[t - t_lo]) list[n++] = t;
+    list[-1] = n;
+  }
+  __syncthreads();
+  return list[-1];
+}
+
 // Heavy-first mapping of the flat block index onto (b, head, row-block) for the causal triangle.
 __device__ __forceinline__ void map_block(int nblk, int BH, bool heavy_last_index, int& bh, int& blk) {
   const int idx = blockIdx.x;
@@ -140,9 +179,10 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const unsigned short* __res
                                                      const unsigned short* __restrict__ v, Strides vs,
                                                      unsigned short* __restrict__ o, Strides os,
                                                      float* __restrict__ lse, int B, int H, int Hk, int S,
-                                                     float scale, int causal) {
+                                                     float scale, int causal, Sparse sp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BUF = 2 * KT * ROWB;  // one ring slot = K tile + V tile
+  int* tlist = reinterpret_cast<int*>(smem + 4 * KT * ROWB) + 1;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int nqb = S / QB;
   int bh, qb;
@@ -166,10 +206,14 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const unsigned short* __res
   float m = -INFINITY, l = 0.f;
 
   const int kend = causal ? (qb + 1) * QB : S;  // keys needed by the workgroup
-  const int ntiles = kend / KT;
+  const int ntiles = sp.layout ? build_tile_list(sp, head, 0, kend / KT, KT, qb * QB, qb * QB + QB, true, tlist)
+                               : kend / KT;
+  auto tile_at = [&](int i) { return sp.layout ? tlist[i] : i; };
+  const uint8_t* lrow = sp.layout ? sp.layout + ((int64_t)head * sp.nb + (q0 + r) / sp.blk) * sp.nb : nullptr;
   Stager<KT> sk, sv;
-  sk.load(kp, ks.s, 0, S);
-  sv.load(vp, vs.s, 0, S);
+  const int t0 = ntiles > 0 ? tile_at(0) : 0;
+  sk.load(kp, ks.s, t0 * KT, S);
+  sv.load(vp, vs.s, t0 * KT, S);
   sk.store(smem);
   sv.store(smem + KT * ROWB);
   __syncthreads();
@@ -177,10 +221,10 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const unsigned short* __res
   for (int t = 0; t < ntiles; ++t) {
     const bool more = (t + 1) < ntiles;
     if (more) {
-      sk.load(kp, ks.s, (t + 1) * KT, S);
-      sv.load(vp, vs.s, (t + 1) * KT, S);
+      sk.load(kp, ks.s, tile_at(t + 1) * KT, S);
+      sv.load(vp, vs.s, tile_at(t + 1) * KT, S);
     }
-    const int kbase = t * KT;
+    const int kbase = tile_at(t) * KT;
     // a wave whose queries all precede this tile has nothing to add (causal)
     const bool active = !causal || kbase <= q0 + QW - 1;
     if (active) {
@@ -195,14 +239,21 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const unsigned short* __res
       const bool diag = causal && (kbase + KT - 1 > q0);
       float mx = -INFINITY;
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j) {
+        bool b0 = true, b1 = true;  // layout bits of keys kbase+32j+[0,16) and +[16,32)
+        if (lrow) {
+          b0 = lrow[(kbase + 32 * j) / sp.blk] != 0;
+          b1 = lrow[(kbase + 32 * j + 16) / sp.blk] != 0;
+        }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           float x = s[j][i] * c;
           if (diag && (kbase + 32 * j + acc_row(i, h) > q0 + r)) x = -INFINITY;
+          if (!(acc_row(i, h) < 16 ? b0 : b1)) x = -INFINITY;
           s[j][i] = x;
           mx = fmaxf(mx, x);
         }
+      }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(m, mx);
       const float mref = (mnew == -INFINITY) ? 0.f : mnew;
@@ -240,7 +291,7 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const unsigned short* __res
     cur ^= 1;
   }
   const float lt = l + __shfl_xor(l, 32, 64);
-  const float inv = 1.f / lt;
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;  // a fully masked (sparse) row outputs zeros
   unsigned short* op = o + b * os.b + head * os.h + (int64_t)(q0 + r) * os.s;
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt)
@@ -251,7 +302,7 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const unsigned short* __res
       for (int e = 0; e < 4; ++e) pk[e] = f32_to_bf16(oacc[dt][4 * rg + e] * inv);
       *reinterpret_cast<u16x4*>(op + 32 * dt + 8 * rg + 4 * h) = pk;
     }
-  if (h == 0) lse[((int64_t)b * H + head) * S + q0 + r] = (m + log2f(lt)) * LN2;
+  if (h == 0) lse[((int64_t)b * H + head) * S + q0 + r] = lt > 0.f ? (m + log2f(lt)) * LN2 : INFINITY;
 }
 
 // =============================================================================================
@@ -313,9 +364,10 @@ __global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __rest
                                                     const unsigned short* __restrict__ dout, Strides dos,
                                                     const float* __restrict__ lse, const float* __restrict__ delta,
                                                     unsigned short* __restrict__ dq, Strides dqs, int B, int H,
-                                                    int Hk, int S, float scale, int causal) {
+                                                    int Hk, int S, float scale, int causal, Sparse sp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BUF = 2 * KT * ROWB;
+  int* tlist = reinterpret_cast<int*>(smem + 4 * KT * ROWB) + 1;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int nqb = S / QB;
   int bh, qb;
@@ -330,9 +382,14 @@ __global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __rest
   const float c = scale * LOG2E;
   const int64_t lrow = ((int64_t)b * H + head) * S + q0 + r;
   const int kend = causal ? (qb + 1) * QB : S;
-  const int ntiles = kend / KT;
-  tile_glds<KT>(kp, ks.s, 0, smem);
-  tile_glds<KT>(vp, vs.s, 0, smem + KT * ROWB);
+  const int ntiles = sp.layout ? build_tile_list(sp, head, 0, kend / KT, KT, qb * QB, qb * QB + QB, true, tlist)
+                               : kend / KT;
+  auto tile_at = [&](int i) { return sp.layout ? tlist[i] : i; };
+  const uint8_t* lay_row = sp.layout ? sp.layout + ((int64_t)head * sp.nb + (q0 + r) / sp.blk) * sp.nb : nullptr;
+  if (ntiles > 0) {
+    tile_glds<KT>(kp, ks.s, tile_at(0) * KT, smem);
+    tile_glds<KT>(vp, vs.s, tile_at(0) * KT, smem + KT * ROWB);
+  }
 
   const float lse2 = lse[lrow] * LOG2E;
   const float dlt = delta[lrow];
@@ -350,10 +407,10 @@ __global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __rest
   int cur = 0;
   for (int t = 0; t < ntiles; ++t) {
     if (t + 1 < ntiles) {
-      tile_glds<KT>(kp, ks.s, (t + 1) * KT, smem + (cur ^ 1) * BUF);
-      tile_glds<KT>(vp, vs.s, (t + 1) * KT, smem + (cur ^ 1) * BUF + KT * ROWB);
+      tile_glds<KT>(kp, ks.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF);
+      tile_glds<KT>(vp, vs.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF + KT * ROWB);
     }
-    const int kbase = t * KT;
+    const int kbase = tile_at(t) * KT;
     const bool active = !causal || kbase <= q0 + QW - 1;
     if (active) {
       const char* kt = smem + cur * BUF;
@@ -367,10 +424,16 @@ __global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __rest
           s = mfma(lds_row16(kt, 32 * j + r, 2 * t2 + h), qf[t2], s);
           dp = mfma(lds_row16(vt, 32 * j + r, 2 * t2 + h), df[t2], dp);
         }
+        bool b0 = true, b1 = true;
+        if (lay_row) {
+          b0 = lay_row[(kbase + 32 * j) / sp.blk] != 0;
+          b1 = lay_row[(kbase + 32 * j + 16) / sp.blk] != 0;
+        }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           float p = exp2f(s[i] * c - lse2);
           if (diag && (kbase + 32 * j + acc_row(i, h) > q0 + r)) p = 0.f;
+          if (!(acc_row(i, h) < 16 ? b0 : b1)) p = 0.f;
           s[i] = p * (dp[i] - dlt);  // dS^T
         }
 #pragma unroll
@@ -422,10 +485,11 @@ __global__ void __launch_bounds__(256, 2) dkdv_kernel(const unsigned short* __re
                                                       unsigned short* __restrict__ dk, Strides dks,
                                                       unsigned short* __restrict__ dv, Strides dvs,
                                                       float* __restrict__ pk, float* __restrict__ pv, int B, int H,
-                                                      int Hk, int S, float scale, int causal) {
+                                                      int Hk, int S, float scale, int causal, Sparse sp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* vblk = smem;
   char* ring = smem + KV_VBLK;
+  int* tlist = reinterpret_cast<int*>(ring + 2 * KV_SLOT) + 1;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int nkb = S / QB;
   int bh, kb;
@@ -441,11 +505,15 @@ __global__ void __launch_bounds__(256, 2) dkdv_kernel(const unsigned short* __re
   const float c = scale * LOG2E;
   const int qstart = causal ? kb * QB : 0;
   const int ntq = (S - qstart) / QT;
-  const int total = ntq * G;
+  // sparse: SPLIT mode (G == 1), list of the active 32-query tiles of this key block
+  const int total = sp.layout ? build_tile_list(sp, hq0, qstart / QT, S / QT, QT, kb * QB, kb * QB + QB, false, tlist)
+                              : ntq * G;
+  auto qtile_at = [&](int it) { return sp.layout ? tlist[it] * QT : qstart + (it % ntq) * QT; };
+  const int kbl = sp.layout ? (k0 + r) / sp.blk : 0;
 
   auto issue = [&](int it, char* slot) {
-    const int hq = hq0 + it / ntq;
-    const int qt0 = qstart + (it % ntq) * QT;
+    const int hq = sp.layout ? hq0 : hq0 + it / ntq;
+    const int qt0 = qtile_at(it);
     tile_glds<QT>(q + b * qs.b + hq * qs.h, qs.s, qt0, slot);
     tile_glds<QT>(dout + b * dos.b + hq * dos.h, dos.s, qt0, slot + KV_TILE);
     if (w == 0) {  // 64 lanes x 4 B: lse[32] then delta[32]
@@ -454,7 +522,7 @@ __global__ void __launch_bounds__(256, 2) dkdv_kernel(const unsigned short* __re
     }
   };
   tile_glds<QB>(vp, vs.s, kb * QB, vblk);
-  issue(0, ring);
+  if (total > 0) issue(0, ring);
   bf16x8 kf[D / 16];
 #pragma unroll
   for (int t = 0; t < D / 16; ++t)
@@ -470,7 +538,7 @@ __global__ void __launch_bounds__(256, 2) dkdv_kernel(const unsigned short* __re
   int cur = 0;
   for (int it = 0; it < total; ++it) {
     if (it + 1 < total) issue(it + 1, ring + (cur ^ 1) * KV_SLOT);
-    const int qt0 = qstart + (it % ntq) * QT;
+    const int qt0 = qtile_at(it);
     const bool active = !causal || (qt0 + QT - 1 >= k0);
     if (active) {
       const char* slot = ring + cur * KV_SLOT;
@@ -485,11 +553,17 @@ __global__ void __launch_bounds__(256, 2) dkdv_kernel(const unsigned short* __re
         dp = mfma(lds_row16(dt_, r, 2 * t2 + h), lds_row16(vblk, w * QW + r, 2 * t2 + h), dp);  // dP
       }
       const bool diag = causal && (qt0 < k0 + QW);
+      bool b0 = true, b1 = true;  // layout bits of query rows qt0+[0,16) and qt0+[16,32) vs this key
+      if (sp.layout) {
+        b0 = sp.layout[((int64_t)hq0 * sp.nb + qt0 / sp.blk) * sp.nb + kbl] != 0;
+        b1 = sp.layout[((int64_t)hq0 * sp.nb + (qt0 + 16) / sp.blk) * sp.nb + kbl] != 0;
+      }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int qi = acc_row(i, h);
         float p = exp2f(s[i] * c - l2[qi] * LOG2E);
         if (diag && (k0 + r > qt0 + qi)) p = 0.f;
+        if (!(qi < 16 ? b0 : b1)) p = 0.f;
         s[i] = p;                      // P
         dp[i] = p * (dp[i] - dl[qi]);  // dS
       }
@@ -508,7 +582,7 @@ __global__ void __launch_bounds__(256, 2) dkdv_kernel(const unsigned short* __re
     __syncthreads();
     cur ^= 1;
   }
-  if constexpr (SPLIT) {  // fp32 partials, layout [B, S, H, D] contiguous
+  if (SPLIT && pk != nullptr) {  // fp32 partials, layout [B, S, H, D] contiguous
     float* kp32 = pk + (((int64_t)b * S + k0 + r) * H + hq0) * D;
     float* vp32 = pv + (((int64_t)b * S + k0 + r) * H + hq0) * D;
 #pragma unroll
@@ -592,27 +666,47 @@ static void check_qkv(const at::Tensor& q, const at::Tensor& k, const at::Tensor
                   (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "flash_attn: 16-byte aligned rows required");
 }
 
-std::vector<at::Tensor> flash_attn_fwd(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, double scale) {
+static fa::Sparse sparse_of(const c10::optional<at::Tensor>& layout, int64_t block, const at::Tensor& q) {
+  if (!layout.has_value() || !layout->defined()) return fa::Sparse{nullptr, 0, 0};
+  const at::Tensor& L = *layout;
+  const int S = q.size(1), H = q.size(2);
+  SXE_CHECK(L.is_cuda() && L.scalar_type() == at::kByte && L.is_contiguous() && L.dim() == 3, "layout: uint8 [H, nb, nb]");
+  SXE_CHECK(block >= 16 && block % 16 == 0 && S % block == 0, "layout block must be a multiple of 16 dividing seq_len");
+  SXE_CHECK(L.size(0) == H && L.size(1) == S / block && L.size(2) == S / block, "layout shape must be [H, S/block, S/block]");
+  SXE_CHECK(S / fa::KT <= 1024, "sparse attention: seq_len <= 65536");
+  return fa::Sparse{L.data_ptr<uint8_t>(), (int)block, (int)(S / block)};
+}
+
+constexpr size_t kListBytes = (1 + 2048) * sizeof(int) + 16;  // tile list + scratch flags (sparse mode)
+
+static std::vector<at::Tensor> fwd_impl(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, double scale,
+                                        fa::Sparse sp) {
   check_qkv(q, k, v);
   const int B = q.size(0), S = q.size(1), H = q.size(2), Hk = k.size(2);
   c10::DeviceGuard guard(q.device());
   auto o = at::empty({B, S, H, fa::D}, q.options());
   auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
   const int grid = (S / fa::QB) * B * H;
-  const size_t lds = 4 * fa::KT * fa::ROWB;
+  const size_t lds = 4 * fa::KT * fa::ROWB + (sp.layout ? kListBytes : 0);
+  static bool attr = false;
+  if (!attr) {
+    SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::fwd_kernel),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * fa::KT * fa::ROWB + kListBytes)));
+    attr = true;
+  }
   hipLaunchKernelGGL(fa::fwd_kernel, dim3(grid), dim3(256), lds, cur_stream(),
                      reinterpret_cast<const unsigned short*>(q.data_ptr()), strides_of(q),
                      reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
                      reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),
                      reinterpret_cast<unsigned short*>(o.data_ptr()), strides_of(o), lse.data_ptr<float>(), B, H, Hk,
-                     S, (float)scale, causal ? 1 : 0);
+                     S, (float)scale, causal ? 1 : 0, sp);
   SXE_LAUNCH_CHECK();
   return {o, lse};
 }
 
 // dq/dk/dv are caller-provided (possibly strided views of one dqkv buffer).
-void flash_attn_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
-                    at::Tensor dq, at::Tensor dk, at::Tensor dv, bool causal, double scale) {
+static void bwd_impl(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
+                     at::Tensor dq, at::Tensor dk, at::Tensor dv, bool causal, double scale, fa::Sparse sp) {
   check_qkv(q, k, v);
   check_qkv(dq, dk, dv);
   SXE_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && dout.stride(3) == 1 && o.stride(3) == 1,
@@ -627,7 +721,18 @@ void flash_attn_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, a
                      reinterpret_cast<const unsigned short*>(o.data_ptr()), strides_of(o), delta.data_ptr<float>(), B,
                      H, S);
   SXE_LAUNCH_CHECK();
-  const size_t lds_dq = 4 * fa::KT * fa::ROWB;
+  const size_t lds_dq = 4 * fa::KT * fa::ROWB + (sp.layout ? kListBytes : 0);
+  const size_t lds_kv_max = fa::KV_VBLK + 2 * fa::KV_SLOT + kListBytes;
+  static bool attr_set = false;
+  if (!attr_set) {  // > 64 KiB of dynamic LDS must be opted into (gfx950 has 160 KiB per CU)
+    SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::dq_kernel),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * fa::KT * fa::ROWB + kListBytes)));
+    SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::dkdv_kernel<false>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv_max));
+    SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::dkdv_kernel<true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv_max));
+    attr_set = true;
+  }
   hipLaunchKernelGGL(fa::dq_kernel, dim3((S / fa::QB) * B * H), dim3(256), lds_dq, cur_stream(),
                      reinterpret_cast<const unsigned short*>(q.data_ptr()), strides_of(q),
                      reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
@@ -635,20 +740,15 @@ void flash_attn_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, a
                      reinterpret_cast<const unsigned short*>(dout.data_ptr()), strides_of(dout),
                      lse.data_ptr<float>(), delta.data_ptr<float>(),
                      reinterpret_cast<unsigned short*>(dq.data_ptr()), strides_of(dq), B, H, Hk, S, (float)scale,
-                     causal ? 1 : 0);
+                     causal ? 1 : 0, sp);
   SXE_LAUNCH_CHECK();
-  const size_t lds_kv = fa::KV_VBLK + 2 * fa::KV_SLOT;
-  static bool attr_set = false;
-  if (!attr_set) {  // > 64 KiB of dynamic LDS must be opted into (gfx950 has 160 KiB per CU)
-    SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::dkdv_kernel<false>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv));
-    SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::dkdv_kernel<true>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv));
-    attr_set = true;
-  }
-  const bool split = causal && H > Hk;
+  // sparse: always one workgroup per query head (per-head tile lists); with GQA the per-head fp32
+  // partials are reduced; causal GQA: split to remove the key-block-0 tail (see dkdv_kernel)
+  const bool split = sp.layout != nullptr || (causal && H > Hk);
+  const bool partials = split && H > Hk;
+  const size_t lds_kv = fa::KV_VBLK + 2 * fa::KV_SLOT + (sp.layout ? kListBytes : 0);
   at::Tensor pk, pv;
-  if (split) {
+  if (partials) {
     pk = at::empty({B, S, H, fa::D}, q.options().dtype(at::kFloat));
     pv = at::empty({B, S, H, fa::D}, q.options().dtype(at::kFloat));
   }
@@ -661,20 +761,42 @@ void flash_attn_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, a
                        lse.data_ptr<float>(), delta.data_ptr<float>(),
                        reinterpret_cast<unsigned short*>(dk.data_ptr()), strides_of(dk),
                        reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv),
-                       split ? pk.data_ptr<float>() : nullptr, split ? pv.data_ptr<float>() : nullptr, B, H, Hk, S,
-                       (float)scale, causal ? 1 : 0);
+                       partials ? pk.data_ptr<float>() : nullptr, partials ? pv.data_ptr<float>() : nullptr, B, H, Hk,
+                       S, (float)scale, causal ? 1 : 0, sp);
   };
   if (split) {
     launch(fa::dkdv_kernel<true>, H);
     SXE_LAUNCH_CHECK();
-    const int64_t n8 = (int64_t)B * S * Hk * (fa::D / 8);
-    hipLaunchKernelGGL(fa::dkdv_reduce_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, cur_stream(),
-                       pk.data_ptr<float>(), pv.data_ptr<float>(), reinterpret_cast<unsigned short*>(dk.data_ptr()),
-                       strides_of(dk), reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv), B, S, H, Hk);
+    if (partials) {
+      const int64_t n8 = (int64_t)B * S * Hk * (fa::D / 8);
+      hipLaunchKernelGGL(fa::dkdv_reduce_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, cur_stream(),
+                         pk.data_ptr<float>(), pv.data_ptr<float>(), reinterpret_cast<unsigned short*>(dk.data_ptr()),
+                         strides_of(dk), reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv), B, S, H, Hk);
+    }
   } else {
     launch(fa::dkdv_kernel<false>, Hk);
   }
   SXE_LAUNCH_CHECK();
+}
+
+std::vector<at::Tensor> flash_attn_fwd(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, double scale) {
+  return fwd_impl(q, k, v, causal, scale, fa::Sparse{nullptr, 0, 0});
+}
+
+void flash_attn_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
+                    at::Tensor dq, at::Tensor dk, at::Tensor dv, bool causal, double scale) {
+  bwd_impl(dout, q, k, v, o, lse, dq, dk, dv, causal, scale, fa::Sparse{nullptr, 0, 0});
+}
+
+std::vector<at::Tensor> flash_attn_fwd_sparse(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor layout,
+                                              int64_t block, bool causal, double scale) {
+  return fwd_impl(q, k, v, causal, scale, sparse_of(layout, block, q));
+}
+
+void flash_attn_bwd_sparse(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
+                           at::Tensor dq, at::Tensor dk, at::Tensor dv, at::Tensor layout, int64_t block, bool causal,
+                           double scale) {
+  bwd_impl(dout, q, k, v, o, lse, dq, dk, dv, causal, scale, sparse_of(layout, block, q));
 }
 
 }  // namespace sxe
@@ -683,8 +805,13 @@ TORCH_LIBRARY_FRAGMENT(sxe, m) {
   m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> Tensor[]");
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, "
         "Tensor(c!) dv, bool causal, float scale) -> ()");
+  m.def("flash_attn_fwd_sparse(Tensor q, Tensor k, Tensor v, Tensor layout, int block, bool causal, float scale) -> Tensor[]");
+  m.def("flash_attn_bwd_sparse(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, "
+        "Tensor(b!) dk, Tensor(c!) dv, Tensor layout, int block, bool causal, float scale) -> ()");
 }
 TORCH_LIBRARY_IMPL(sxe, CUDA, m) {
   m.impl("flash_attn_fwd", &sxe::flash_attn_fwd);
   m.impl("flash_attn_bwd", &sxe::flash_attn_bwd);
+  m.impl("flash_attn_fwd_sparse", &sxe::flash_attn_fwd_sparse);
+  m.impl("flash_attn_bwd_sparse", &sxe::flash_attn_bwd_sparse);
 }
