@@ -30,6 +30,7 @@ def parse_args(args=None):
     p.add_argument("--enable_each_rank_log", default="None")
     p.add_argument("--bind_cores_to_rank", action="store_true")
     p.add_argument("--bind_core_list", default=None)
+    p.add_argument("--max_restarts", type=int, default=0)
     p.add_argument("user_script")
     p.add_argument("user_args", nargs=argparse.REMAINDER)
     return p.parse_args(args)
@@ -51,7 +52,22 @@ def _core_list(rank_local, nlocal, core_list=None):
 
 
 def main(args=None):
+    """Run the local worker group; on a failure tear it down and, while restarts remain, start a
+    fresh group (the reference's DSElasticAgent restart policy, elasticity/elastic_agent.py:127-145).
+    Workers see ``SXE_RESTART_COUNT`` (= torchelastic's TORCHELASTIC_RESTART_COUNT) and resume from
+    their last checkpoint."""
     a = parse_args(args)
+    rc = 0
+    for attempt in range(a.max_restarts + 1):
+        rc = _run_group(a, attempt)
+        if rc == 0:
+            return 0
+        if attempt < a.max_restarts:
+            sys.stderr.write(f"[sxe launch] worker group failed (rc={rc}); restart {attempt + 1}/{a.max_restarts}\n")
+    return rc
+
+
+def _run_group(a, attempt):
     world = decode_world_info(a.world_info)
     hosts = list(world.keys())
     gpus_per_node = [len(world[h]) for h in hosts]
@@ -60,8 +76,9 @@ def main(args=None):
     base_rank = sum(gpus_per_node[:a.node_rank])
     procs = []
     env_base = os.environ.copy()
-    env_base.update(MASTER_ADDR=a.master_addr, MASTER_PORT=str(a.master_port), WORLD_SIZE=str(world_size),
-                    LOCAL_SIZE=str(len(local)), CROSS_SIZE=str(len(hosts)), CROSS_RANK=str(a.node_rank))
+    env_base.update(MASTER_ADDR=a.master_addr, MASTER_PORT=str(a.master_port + attempt), WORLD_SIZE=str(world_size),
+                    LOCAL_SIZE=str(len(local)), CROSS_SIZE=str(len(hosts)), CROSS_RANK=str(a.node_rank),
+                    SXE_RESTART_COUNT=str(attempt), TORCHELASTIC_RESTART_COUNT=str(attempt))
     env_base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     if "HIP_VISIBLE_DEVICES" not in env_base:
         env_base["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in local)

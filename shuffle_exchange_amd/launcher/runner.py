@@ -44,6 +44,8 @@ def parse_args(args=None):
     p.add_argument("--bind_cores_to_rank", action="store_true")
     p.add_argument("--bind_core_list", default=None)
     p.add_argument("--elastic_training", action="store_true")
+    p.add_argument("--max_restarts", type=int, default=0,
+                   help="restart the local worker group up to N times after a failure (elastic agent)")
     p.add_argument("--dry_run", action="store_true", help="print the per-node commands and exit")
     p.add_argument("--autotuning", default="", choices=["", "tune", "run"],
                    help="tune: search ZeRO stage x micro batch with short runs; run: tune then launch the best")
@@ -179,6 +181,8 @@ def build_launch_cmd(args, world_info_b64, node_rank, master_addr):
             cmd.append(f"--bind_core_list={args.bind_core_list}")
     if args.enable_each_rank_log != "None":
         cmd.append(f"--enable_each_rank_log={args.enable_each_rank_log}")
+    if getattr(args, "max_restarts", 0):
+        cmd.append(f"--max_restarts={args.max_restarts}")
     return cmd + [args.user_script] + list(args.user_args)
 
 

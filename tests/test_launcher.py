@@ -112,3 +112,38 @@ def test_fault_rules_parse():
         fault.maybe_inject(0, 5)
     finally:
         del os.environ["SXE_FAULT"]
+
+
+FLAKY_SCRIPT = """
+import os, sys
+sys.path.insert(0, os.environ["SXE_ROOT"])
+import torch, torch.distributed as dist
+dist.init_process_group("gloo")
+attempt = int(os.environ["SXE_RESTART_COUNT"])
+if attempt == 0 and dist.get_rank() == 1:
+    os._exit(3)  # first incarnation: rank 1 crashes
+t = torch.ones(1)
+dist.all_reduce(t)
+open(os.path.join(sys.argv[-1], f"ok{dist.get_rank()}_{attempt}"), "w").write(str(t.item()))
+dist.destroy_process_group()
+"""
+
+
+def test_launcher_restarts_failed_worker_group(tmp_path):
+    """--max_restarts (elastic agent policy): the failed group is torn down and restarted; the
+    second incarnation (SXE_RESTART_COUNT=1) completes."""
+    script = tmp_path / "f.py"
+    script.write_text(FLAKY_SCRIPT)
+    env = dict(os.environ, PYTHONPATH=ROOT, SXE_ROOT=ROOT)
+    r = subprocess.run([sys.executable, "-m", "shuffle_exchange_amd.launcher.runner", "-H", "/nonexistent",
+                        "--num_gpus", "2", "--master_port", "29683", "--no_local_rank", "--max_restarts", "2",
+                        str(script), str(tmp_path)],
+                       env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert (tmp_path / "ok0_1").read_text() == "2.0" and (tmp_path / "ok1_1").exists()
+    assert "restart 1/2" in r.stdout
+
+
+def test_elastic_agent_importable():
+    from shuffle_exchange_amd.elasticity.elastic_agent import SXEElasticAgent
+    assert SXEElasticAgent.__name__ == "SXEElasticAgent"
