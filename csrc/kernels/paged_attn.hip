@@ -11,7 +11,10 @@
 //    heads of the GQA group (x the sequence's new tokens) share every K/V byte loaded, so decode is
 //    pure HBM streaming at the GQA-reduced byte count;
 //  * key phase: lane = key (K row in 16 B vector registers, q rows broadcast from LDS); value phase:
-//    lane = 2 output dims, V rows read coalesced; probabilities hop through LDS;
+//    lane = 4 output dims of one of KG V rows per load instruction, the 64 rows' cache offsets
+//    precomputed in the key phase so all V loads of a chunk are in flight together (a per-key
+//    block-table lookup -> load chain made the value phase latency-bound); probabilities hop
+//    through LDS; key-group partial sums fold once per pass with lane shuffles;
 //  * flash-decoding split over the KV length when (sequences x kv heads) is too small to fill the
 //    256 CUs, merged by a second kernel (fp32 partials);
 //  * causal masking by absolute position (chunked prefill / speculative tokens just work).
@@ -21,7 +24,6 @@
 namespace sxe {
 namespace pa {
 
-constexpr int kRows = 16;     // query rows (token x head-in-group) per pass
 constexpr int kWaves = 4;
 constexpr float kLog2e = 1.4426950408889634f;
 
@@ -64,18 +66,23 @@ struct Args {
   int T;
 };
 
-template <int D>
+// R = query rows (token x head-in-group) per pass: 4 / 8 / 16 picked on the host from the GQA group
+// size so decode rows (q_len = 1) fill one pass without idle row slots.
+template <int D, int R>
 __global__ __launch_bounds__(256) void paged_attn_kernel(Args a) {
-  constexpr int DPL = D / 64;  // output dims per lane in the value phase
-  constexpr int KV16 = D / 8;  // 16-byte vectors per K row
-  __shared__ float q_lds[kRows][D];
-  __shared__ float p_lds[kWaves][kRows][64];
-  __shared__ float mrg_o[kWaves][kRows][D];
-  __shared__ float mrg_ml[kWaves][kRows][2];
+  constexpr int KV16 = D / 8;   // 16-byte vectors per K row
+  constexpr int LPR = D / 4;    // value phase: lanes per V row (4 dims = 8 bytes each)
+  constexpr int KG = 64 / LPR;  // V rows per wave load instruction
+  __shared__ float q_lds[R][D];
+  __shared__ float p_lds[kWaves][R][64];
+  __shared__ int64_t voff_lds[kWaves][64];
+  __shared__ float mrg_o[kWaves][R][D];
+  __shared__ float mrg_ml[kWaves][R][2];
 
   const int seq = blockIdx.x / a.nkv, kvh = blockIdx.x - (blockIdx.x / a.nkv) * a.nkv;
   const int split = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kg = lane / LPR, dl = lane - (lane / LPR) * LPR;
   const int G = a.nq / a.nkv;
   const int qs = a.q_start[seq], ql = a.q_len[seq], kl = a.kv_len[seq];
   const int k_begin = split * a.keys_per_split;
@@ -86,10 +93,10 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(Args a) {
   const int64_t half_stride = (int64_t)a.nkv * head_stride;  // k half -> v half
   const int64_t block_stride = 2 * half_stride;
 
-  for (int row0 = 0; row0 < nrows_total; row0 += kRows) {
-    const int nrows = min(kRows, nrows_total - row0);
+  for (int row0 = 0; row0 < nrows_total; row0 += R) {
+    const int nrows = min(R, nrows_total - row0);
     // ---- q rows -> LDS (fp32, pre-scaled by softmax scale * log2 e) -------------------------
-    for (int i = threadIdx.x; i < kRows * D; i += 256) {
+    for (int i = threadIdx.x; i < R * D; i += 256) {
       const int r = i / D, d = i - r * D;
       float v = 0.f;
       if (r < nrows) {
@@ -101,39 +108,39 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(Args a) {
     __syncthreads();
     const int max_pos = kl - ql + (row0 + nrows - 1) / G;  // causal horizon of this tile
     const int k_hi = min(k_end, max_pos + 1);
-    float m[kRows], l[kRows], o[kRows][DPL];
+    float m[R], l[R], acc[R][4];
 #pragma unroll
-    for (int r = 0; r < kRows; ++r) {
+    for (int r = 0; r < R; ++r) {
       m[r] = -INFINITY;
       l[r] = 0.f;
 #pragma unroll
-      for (int j = 0; j < DPL; ++j) o[r][j] = 0.f;
+      for (int e = 0; e < 4; ++e) acc[r][e] = 0.f;
     }
     for (int kb = k_begin + wave * 64; kb < k_hi; kb += kWaves * 64) {
-      // ---- key phase: lane = key ------------------------------------------------------------
+      // q rows are re-read from LDS every chunk: without this fence LICM hoists all R x D of them
+      // into registers (R = 4 alone would need 512 VGPRs and spill to scratch)
+      asm volatile("" ::: "memory");
+      // ---- key phase: lane = key; invalid lanes re-read key kb (in range) and get p = 0 ------
       const int key = kb + lane;
       const bool valid = key < k_hi;
+      const int kc = valid ? key : kb;
+      const int blk = bt[kc / a.bs], off = kc - (kc / a.bs) * a.bs;
+      const int64_t koff = (int64_t)blk * block_stride + kvh * head_stride + (int64_t)off * D;
+      voff_lds[wave][lane] = koff + half_stride;
       u16x8 kr[KV16];
-      if (valid) {
-        const int blk = bt[key / a.bs], off = key - (key / a.bs) * a.bs;
-        const unsigned short* kp = a.cache + (int64_t)blk * block_stride + kvh * head_stride + (int64_t)off * D;
 #pragma unroll
-        for (int v = 0; v < KV16; ++v) kr[v] = *reinterpret_cast<const u16x8*>(kp + v * 8);
-      } else {
+      for (int v = 0; v < KV16; ++v) kr[v] = *reinterpret_cast<const u16x8*>(a.cache + koff + v * 8);
+      float s[R];
 #pragma unroll
-        for (int v = 0; v < KV16; ++v) kr[v] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      }
-      float s[kRows];
-#pragma unroll
-      for (int r = 0; r < kRows; ++r) s[r] = 0.f;
+      for (int r = 0; r < R; ++r) s[r] = 0.f;
 #pragma unroll
       for (int v = 0; v < KV16; ++v) {
         float kf[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) kf[e] = bf16_to_f32(kr[v][e]);
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) {
-          if (r < nrows) {
+        for (int r = 0; r < R; ++r) {
+          if (r < nrows) {  // (uniform) guard also keeps the scheduler from hoisting all R x D q reads
             const f32x4 q0 = *reinterpret_cast<const f32x4*>(&q_lds[r][v * 8]);
             const f32x4 q1 = *reinterpret_cast<const f32x4*>(&q_lds[r][v * 8 + 4]);
             s[r] += q0[0] * kf[0] + q0[1] * kf[1] + q0[2] * kf[2] + q0[3] * kf[3] + q1[0] * kf[4] + q1[1] * kf[5] +
@@ -143,7 +150,7 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(Args a) {
       }
       // ---- online softmax per row -----------------------------------------------------------
 #pragma unroll
-      for (int r = 0; r < kRows; ++r) {
+      for (int r = 0; r < R; ++r) {
         if (r < nrows) {
           const int pos = kl - ql + (row0 + r) / G;
           const float sv = (valid && key <= pos) ? s[r] : -INFINITY;
@@ -156,46 +163,50 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(Args a) {
           }
           l[r] = l[r] * alpha + wave_sum(p);
 #pragma unroll
-          for (int j = 0; j < DPL; ++j) o[r][j] *= alpha;
+          for (int e = 0; e < 4; ++e) acc[r][e] *= alpha;
           m[r] = mn;
           p_lds[wave][r][lane] = p;
+        } else {
+          p_lds[wave][r][lane] = 0.f;
         }
       }
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): p_lds visible within the wave
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): p_lds / voff_lds visible within the wave
       __builtin_amdgcn_wave_barrier();
-      // ---- value phase: lane = DPL output dims ------------------------------------------------
-      const int nk = min(64, k_hi - kb);
-      for (int j = 0; j < nk; ++j) {
-        const int kj = kb + j;
-        const int blk = bt[kj / a.bs], off = kj - (kj / a.bs) * a.bs;
-        const unsigned short* vp =
-            a.cache + (int64_t)blk * block_stride + half_stride + kvh * head_stride + (int64_t)off * D + lane * DPL;
-        float vv[DPL];
-        if constexpr (DPL == 2) {
-          const unsigned int w = *reinterpret_cast<const unsigned int*>(vp);
-          vv[0] = bf16_to_f32(w & 0xffff);
-          vv[1] = bf16_to_f32(w >> 16);
-        } else {
+      // ---- value phase: KG V rows per load, lane = 4 dims of one row; all 64 rows issued
+      //      back to back (offsets precomputed in the key phase, so no dependent block lookups) --
+#pragma unroll 16
+      for (int j0 = 0; j0 < 64; j0 += KG) {
+        const int j = j0 + kg;
+        const uint2 w = *reinterpret_cast<const uint2*>(a.cache + voff_lds[wave][j] + dl * 4);
+        const float v0 = bf16_to_f32(w.x & 0xffff), v1 = bf16_to_f32(w.x >> 16);
+        const float v2 = bf16_to_f32(w.y & 0xffff), v3 = bf16_to_f32(w.y >> 16);
 #pragma unroll
-          for (int e = 0; e < DPL; ++e) vv[e] = bf16_to_f32(vp[e]);
-        }
-#pragma unroll
-        for (int r = 0; r < kRows; ++r) {
-          if (r < nrows) {
-            const float p = p_lds[wave][r][j];
-#pragma unroll
-            for (int e = 0; e < DPL; ++e) o[r][e] += p * vv[e];
-          }
+        for (int r = 0; r < R; ++r) {
+          const float p = p_lds[wave][r][j];
+          acc[r][0] += p * v0;
+          acc[r][1] += p * v1;
+          acc[r][2] += p * v2;
+          acc[r][3] += p * v3;
         }
       }
       __builtin_amdgcn_wave_barrier();
     }
-    // ---- merge the 4 waves ------------------------------------------------------------------
+    // ---- fold the KG key groups of each wave, then merge the 4 waves ---------------------------
 #pragma unroll
-    for (int r = 0; r < kRows; ++r) {
+    for (int r = 0; r < R; ++r) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int o = LPR; o < 64; o <<= 1) acc[r][e] += __shfl_xor(acc[r][e], o, 64);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
       if (r < nrows) {
+        if (kg == 0) {
 #pragma unroll
-        for (int e = 0; e < DPL; ++e) mrg_o[wave][r][lane * DPL + e] = o[r][e];
+          for (int e = 0; e < 4; ++e) mrg_o[wave][r][dl * 4 + e] = acc[r][e];
+        }
         if (lane == 0) {
           mrg_ml[wave][r][0] = m[r];
           mrg_ml[wave][r][1] = l[r];
@@ -208,21 +219,21 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(Args a) {
       float M = -INFINITY;
 #pragma unroll
       for (int w = 0; w < kWaves; ++w) M = fmaxf(M, mrg_ml[w][r][0]);
-      float acc = 0.f, L = 0.f;
+      float sum = 0.f, L = 0.f;
 #pragma unroll
       for (int w = 0; w < kWaves; ++w) {
         const float mw = mrg_ml[w][r][0];
         const float f = (mw == -INFINITY) ? 0.f : exp2f(mw - M);
-        acc += f * mrg_o[w][r][d];
+        sum += f * mrg_o[w][r][d];
         L += f * mrg_ml[w][r][1];
       }
       const int row = row0 + r, tok = row / G, g = row - tok * G;
       const int t = qs + tok, h = kvh * G + g;
       if (a.splits == 1) {
-        a.out[(int64_t)t * a.out_tok_stride + (int64_t)h * D + d] = f32_to_bf16(L > 0.f ? acc / L : 0.f);
+        a.out[(int64_t)t * a.out_tok_stride + (int64_t)h * D + d] = f32_to_bf16(L > 0.f ? sum / L : 0.f);
       } else {
         const int64_t idx = ((int64_t)split * a.T + t) * a.nq + h;
-        a.part_o[idx * D + d] = acc;
+        a.part_o[idx * D + d] = sum;
         if (d == 0) {
           a.part_ml[idx * 2 + 0] = M;
           a.part_ml[idx * 2 + 1] = L;
@@ -333,12 +344,19 @@ at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const a
     a.part_ml = part_ml.data_ptr<float>();
   }
   dim3 grid(S * nkv, splits);
-  if (D == 128)
-    hipLaunchKernelGGL(pa::paged_attn_kernel<128>, grid, dim3(256), 0, cur_stream(), a);
-  else if (D == 64)
-    hipLaunchKernelGGL(pa::paged_attn_kernel<64>, grid, dim3(256), 0, cur_stream(), a);
-  else
-    SXE_CHECK(false, "paged_attention: head_dim must be 64 or 128");
+  const int G = nq / nkv;
+  SXE_CHECK(D == 128 || D == 64, "paged_attention: head_dim must be 64 or 128");
+#define SXE_PA_LAUNCH(DD, RR) hipLaunchKernelGGL((pa::paged_attn_kernel<DD, RR>), grid, dim3(256), 0, cur_stream(), a)
+  if (D == 128) {
+    if (G <= 4) SXE_PA_LAUNCH(128, 4);
+    else if (G <= 8) SXE_PA_LAUNCH(128, 8);
+    else SXE_PA_LAUNCH(128, 16);
+  } else {
+    if (G <= 4) SXE_PA_LAUNCH(64, 4);
+    else if (G <= 8) SXE_PA_LAUNCH(64, 8);
+    else SXE_PA_LAUNCH(64, 16);
+  }
+#undef SXE_PA_LAUNCH
   SXE_LAUNCH_CHECK();
   if (splits > 1) {
     if (D == 128)

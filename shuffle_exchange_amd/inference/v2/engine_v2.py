@@ -60,6 +60,7 @@ class RaggedInferenceEngineConfig:
     kv_block_size: int = 64
     num_kv_blocks: Optional[int] = None
     tensor_parallel: dict = field(default_factory=lambda: {"tp_size": 1})
+    decode_graphs: bool = True  # replay pure-decode steps from captured HIP graphs (decode_graphs.py)
 
 
 class InferenceEngineV2:
@@ -75,6 +76,7 @@ class InferenceEngineV2:
                                   dtype=self._model.dtype, device=dev)
         max_blocks_seq = math.ceil(sm.max_context / bs)
         self._state = DSStateManager(self._kv, sm.max_tracked_sequences, max_blocks_seq)
+        self._decode_graphs = None
 
     def _size_cache(self, dev, bs):
         m = self._model
@@ -119,11 +121,31 @@ class InferenceEngineV2:
             self._state.allocate_blocks(s, t.numel())
             s.pre_forward(t.numel())
             seqs.append(s)
-        batch = RaggedBatch(seqs, tokens, self._kv.block_size, self._model.device)
-        logits = self._model.forward(batch, self._kv)
+        runner = self._decode_runner()
+        if runner is not None and runner.eligible(seqs, [t.numel() for t in tokens]):
+            logits = runner.run(seqs, tokens)
+        else:
+            batch = RaggedBatch(seqs, tokens, self._kv.block_size, self._model.device)
+            logits = self._model.forward(batch, self._kv)
         for s in seqs:
             s.post_forward()
         return logits
+
+    def _decode_runner(self):
+        """HIP-graph decode runner (decode_graphs.py), created on first use: GPU, dense models."""
+        if self._decode_graphs is None:
+            m = self._model
+            dense = not getattr(m, "is_moe", False) and not any(
+                "router" in L for L in getattr(m, "w", {}).get("layers", []))
+            ok = (self._config.decode_graphs and m.device.type == "cuda" and dense and self._kv.free_blocks > 1)
+            if ok:
+                from .decode_graphs import DecodeGraphRunner
+                sm = self._config.state_manager
+                self._decode_graphs = DecodeGraphRunner(m, self._kv, max_seqs=min(256, sm.max_ragged_sequence_count),
+                                                        max_context=sm.max_context)
+            else:
+                self._decode_graphs = False
+        return self._decode_graphs or None
 
     def query(self, uid, max_request_tokens, max_request_blocks):
         """(tokens, blocks) the sequence could take now, bounded by the request and free blocks."""

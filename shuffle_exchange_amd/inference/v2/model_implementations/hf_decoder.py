@@ -32,6 +32,7 @@ import torch.nn.functional as F
 
 from ....ops import native
 from ....ops.activation import ACT, bias_act, gated_act
+from ....ops.linear import linear
 from ....ops.norm import layer_norm, rms_norm
 from ....ops.paged_attention import kv_cache_append, paged_attention
 from ....ops.rope import RopeCache, apply_rope_tokens_
@@ -393,8 +394,8 @@ def dropless_moe(x, router_w, e_gu, e_down, top_k, norm_topk, act="silu"):
     for e, c in enumerate(counts):
         if c == 0:
             continue
-        h = gated_act(F.linear(xs[o:o + c], e_gu[e]), act)
-        out.index_add_(0, tok[o:o + c], F.linear(h, e_down[e]) * ws[o:o + c])
+        h = gated_act(linear(xs[o:o + c], e_gu[e]), act)
+        out.index_add_(0, tok[o:o + c], linear(h, e_down[e]) * ws[o:o + c])
         o += c
     return out
 
@@ -442,26 +443,26 @@ class RaggedDecoder:
     def _attn(self, a, L, li, batch, kv_cache):
         s, T = self.spec, a.shape[0]
         nq, nkv, D = s.nq, s.nkv, s.head_dim
-        qkv = F.linear(a, L["qkv_w"], L.get("qkv_b")).view(T, nq + 2 * nkv, D)
+        qkv = linear(a, L["qkv_w"], L.get("qkv_b")).view(T, nq + 2 * nkv, D)
         if self.rope is not None:
             apply_rope_tokens_(qkv, self.rope, nq + nkv, batch.positions, rot_dim=s.rotary_dim)
         kv_layer = kv_cache.layer(li)
         kv_cache_append(qkv, kv_layer, batch.slots, nq, nkv)
         o = ragged_attention(qkv, kv_layer, batch, nq, nkv, D, self.scale, s.sliding_window)
-        return F.linear(o.reshape(T, nq * D), L["o_w"], L.get("o_b"))
+        return linear(o.reshape(T, nq * D), L["o_w"], L.get("o_b"))
 
     def _mlp(self, m, L):
         s = self.spec
         if "router" in L:
             out = dropless_moe(m, L["router"], L["e_gu"], L["e_down"], s.top_k, s.norm_topk, s.act)
             if "sh_gu" in L:
-                sh = F.linear(gated_act(F.linear(m, L["sh_gu"]), s.act), L["sh_down"])
-                out = out + torch.sigmoid(F.linear(m, L["sh_gate"])) * sh
+                sh = linear(gated_act(linear(m, L["sh_gu"]), s.act), L["sh_down"])
+                out = out + torch.sigmoid(linear(m, L["sh_gate"])) * sh
             return out
         if "gu_w" in L:
-            return F.linear(gated_act(F.linear(m, L["gu_w"]), s.act), L["down_w"])
-        h = bias_act(F.linear(m, L["fc1_w"]), L.get("fc1_b"), ACT[s.act])
-        return F.linear(h, L["fc2_w"], L.get("fc2_b"))
+            return linear(gated_act(linear(m, L["gu_w"]), s.act), L["down_w"])
+        h = bias_act(linear(m, L["fc1_w"]), L.get("fc1_b"), ACT[s.act])
+        return linear(h, L["fc2_w"], L.get("fc2_b"))
 
     @torch.no_grad()
     def forward(self, batch, kv_cache):
@@ -485,7 +486,7 @@ class RaggedDecoder:
         last = batch.last_idx
         h = x.index_select(0, last) + res.index_select(0, last)
         h = self._norm(h, W["final_w"], W.get("final_b"))
-        return F.linear(h, W["lm_head"], W.get("lm_head_b")).float()
+        return linear(h, W["lm_head"], W.get("lm_head_b")).float()
 
 
 def load_hf_decoder(model_or_path, dtype=torch.bfloat16, device=None):

@@ -19,6 +19,7 @@ import torch.nn.functional as F
 
 from ....ops import native
 from ....ops.activation import swiglu
+from ....ops.linear import linear
 from ....ops.paged_attention import kv_cache_append, paged_attention
 from ....ops.rope import apply_rope_tokens_
 
@@ -136,4 +137,4 @@ class RaggedLlama:
             x, res = self._mlp(layer, m), h2
         last = batch.last_idx
         h = model.norm(x.index_select(0, last), res.index_select(0, last))[0]
-        return F.linear(h, model.lm_head.weight).float()
+        return linear(h, model.lm_head.weight).float()

@@ -23,6 +23,29 @@ import torch.nn.functional as F
 # -0.47 ms for the 128256x4096 LM head, at K = 8192 tokens). Smaller weights keep the fused path.
 TN_MIN_ELEMS = int(os.environ.get("SXE_WGRAD_TN_MIN_ELEMS", 32 * 2**20))
 
+# Decode-shaped products (<= 4 rows, no autograd) stream the weight through the MFMA skinny-GEMM
+# kernel (csrc/kernels/skinny_gemm.hip) instead of hipBLASLt's general tiles. Measured on MI355X
+# (tools/skinny_bench.py, profiles/skinny_bench.log), Llama-3-8B shapes, M = 1: o_proj 7.3 vs
+# 11.8 us, gate_up 42 vs 56 us, down 24.8 vs 25.7 us, LM head 169 vs 180 us, QKV 12.4 vs 10.6 us;
+# at M = 8-16 hipBLASLt is as fast or faster (the kernel supports M <= 16).
+SKINNY_MAX_M = int(os.environ.get("SXE_SKINNY_MAX_M", 4))
+
+
+def _skinny(x, weight, bias):
+    K = x.shape[-1]
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and weight.dim() == 2
+            and weight.is_contiguous() and K % 8 == 0 and weight.data_ptr() % 16 == 0):
+        return None
+    if bias is not None and not (bias.dtype == torch.bfloat16 and bias.is_contiguous()):
+        return None
+    x2 = x.reshape(-1, K)
+    if not (0 < x2.shape[0] <= SKINNY_MAX_M and x2.stride(1) == 1 and x2.stride(0) % 8 == 0
+            and x2.data_ptr() % 16 == 0):
+        return None
+    from . import native
+    native.require_hip()
+    return torch.ops.sxe.skinny_gemm(x2, weight, bias).view(*x.shape[:-1], weight.shape[0])
+
 
 def _tn_ok(gy2, x2):
     return (gy2.is_cuda and gy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and TN_MIN_ELEMS > 0
@@ -78,8 +101,13 @@ class _Linear(torch.autograd.Function):
 
 
 def linear(x, weight, bias=None):
-    if weight.requires_grad and torch.is_grad_enabled() and hasattr(weight, "_sxe_grad_target"):
+    grad = torch.is_grad_enabled() and (weight.requires_grad or x.requires_grad)
+    if grad and weight.requires_grad and hasattr(weight, "_sxe_grad_target"):
         return _Linear.apply(x, weight, bias)
+    if not grad and SKINNY_MAX_M > 0 and x.is_cuda:
+        y = _skinny(x, weight, bias)
+        if y is not None:
+            return y
     return F.linear(x, weight, bias)
 
 

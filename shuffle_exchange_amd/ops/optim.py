@@ -232,3 +232,64 @@ class FusedLamb(torch.optim.Optimizer):
                 self.lamb_coeffs.append(coeff)
                 p.copy_(pf - group["lr"] * coeff * upd)
         return loss
+
+
+# ------------------------------------------------------------------------------------------------
+# muP (maximal update parametrization) optimizers -- reference engine optimizer types MuAdam /
+# MuAdamW / MuSGD (runtime/engine.py:1473-1569, backed by the ``mup`` package's optim.py).
+def _mup_shape(p):
+    """(ninf, width_mult, fanin_fanout_ratio) of a parameter: from ``p.infshape`` when ``mup``'s
+    set_base_shapes ran, else from ``p.mup_width_mult`` (matrix-like if 2-D+, vector-like if 1-D)."""
+    inf = getattr(p, "infshape", None)
+    if inf is not None:
+        ratio = inf.fanin_fanout_mult_ratio() if inf.ninf() == 2 else inf.width_mult()
+        return inf.ninf(), inf.width_mult(), ratio
+    wm = float(getattr(p, "mup_width_mult", 1.0))
+    if wm == 1.0:
+        return 0, 1.0, 1.0
+    return (2 if p.dim() >= 2 else 1), wm, wm
+
+
+def mup_param_groups(params, kind, decoupled_wd=False, defaults=None):
+    """Split param groups by muP width multiplier. ``kind`` 'adam': matrix-like (two infinite dims)
+    lr / width_mult; 'sgd': vector-like lr * width_mult, matrix-like lr / fanin_fanout_ratio.
+    Multipliers land in ``lr_mult`` / ``wd_mult`` so LR schedules keep them (lr_schedules._set_lrs)."""
+    groups = list(params)
+    if not groups or not isinstance(groups[0], dict):
+        groups = [{"params": groups}]
+    out = []
+    for g in groups:
+        rest = dict(defaults or {})
+        rest.update({k: v for k, v in g.items() if k != "params"})
+        buckets = {}
+        for p in g["params"]:
+            ninf, wm, ratio = _mup_shape(p)
+            if ninf > 2:
+                raise NotImplementedError("muP: more than 2 infinite dimensions")
+            if kind == "adam":
+                lr_mult = 1.0 / wm if ninf == 2 else 1.0
+            else:
+                lr_mult = wm if ninf == 1 else (1.0 / ratio if ninf == 2 else 1.0)
+            buckets.setdefault(lr_mult, []).append(p)
+        for lr_mult, ps in buckets.items():
+            ng = dict(rest, params=ps, lr_mult=lr_mult)
+            if "lr" in ng:
+                ng["lr"] = ng["lr"] * lr_mult
+            if not decoupled_wd and lr_mult != 1.0 and ng.get("weight_decay"):
+                ng["weight_decay"] = ng["weight_decay"] / lr_mult
+            out.append(ng)
+    return out
+
+
+def MuAdam(params, lr=1e-3, weight_decay=0.0, decoupled_wd=False, adam_w_mode=False, **kw):
+    groups = mup_param_groups(params, "adam", decoupled_wd, {"lr": lr, "weight_decay": weight_decay})
+    return FusedAdam(groups, lr=lr, weight_decay=weight_decay, adam_w_mode=adam_w_mode, **kw)
+
+
+def MuAdamW(params, lr=1e-3, weight_decay=0.0, decoupled_wd=False, **kw):
+    return MuAdam(params, lr=lr, weight_decay=weight_decay, decoupled_wd=decoupled_wd, adam_w_mode=True, **kw)
+
+
+def MuSGD(params, lr=1e-3, weight_decay=0.0, decoupled_wd=False, **kw):
+    groups = mup_param_groups(params, "sgd", decoupled_wd, {"lr": lr, "weight_decay": weight_decay})
+    return torch.optim.SGD(groups, lr=lr, weight_decay=weight_decay, **kw)

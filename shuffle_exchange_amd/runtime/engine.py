@@ -308,6 +308,9 @@ class SXEEngine(nn.Module):
             return fused.FusedLamb(model_parameters, **p)
         if name == "sgd":
             return torch.optim.SGD(model_parameters, **p)
+        if name in ("muadam", "muadamw", "musgd"):
+            ctor = {"muadam": fused.MuAdam, "muadamw": fused.MuAdamW, "musgd": fused.MuSGD}[name]
+            return ctor(model_parameters, **p)
         if name in ("onebitadam", "zerooneadam", "onebitlamb"):
             assert self.zero_optimization_stage() == 0, "1-bit optimizers run with ZeRO stage 0 (as in the reference)"
             from .fp16.onebit import build_onebit

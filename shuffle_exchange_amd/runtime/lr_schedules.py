@@ -26,8 +26,10 @@ def _per_group(optimizer, v):
 
 
 def _set_lrs(optimizer, lrs):
+    # ``lr_mult``: per-group learning-rate multiplier that schedules must keep (muP width scaling,
+    # ops/optim.py mup_param_groups)
     for g, lr in zip(_groups(optimizer), lrs):
-        g["lr"] = lr
+        g["lr"] = lr * g.get("lr_mult", 1.0)
     return [g["lr"] for g in _groups(optimizer)]
 
 
@@ -53,7 +55,7 @@ class WarmupLR(_Sched):
                  warmup_type=WARMUP_LOG_RATE, last_batch_iteration=-1):
         self.optimizer = optimizer
         if warmup_max_lr is None:
-            warmup_max_lr = _groups(optimizer)[0]["lr"]
+            warmup_max_lr = [g["lr"] / g.get("lr_mult", 1.0) for g in _groups(optimizer)]
         self.min_lrs = _per_group(optimizer, warmup_min_lr)
         self.max_lrs = _per_group(optimizer, warmup_max_lr)
         self.warmup_num_steps = max(2, int(warmup_num_steps))
@@ -101,7 +103,7 @@ class WarmupCosineLR(_Sched):
         self.cos_min_ratio = cos_min_ratio
         self.warmup_type = warmup_type
         self.last_batch_iteration = last_batch_iteration
-        self.org_lrs = [g["lr"] for g in _groups(optimizer)]
+        self.org_lrs = [g["lr"] / g.get("lr_mult", 1.0) for g in _groups(optimizer)]
         if last_batch_iteration == -1:
             self._last_lr = _set_lrs(optimizer, self.get_lr())
 
