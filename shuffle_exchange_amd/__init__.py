@@ -19,6 +19,7 @@ from .runtime.activation_checkpointing import checkpointing  # noqa: F401
 from .utils.logging import logger, log_dist  # noqa: F401
 from .utils.init_on_device import OnDevice  # noqa: F401
 from .runtime.utils import see_memory_usage  # noqa: F401
+from .ops.transformer import DeepSpeedTransformerConfig, DeepSpeedTransformerLayer  # noqa: F401
 
 __version__ = "0.1.0"
 __git_branch__ = "main"

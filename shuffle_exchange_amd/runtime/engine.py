@@ -404,6 +404,9 @@ class SXEEngine(nn.Module):
         self._boundary_override = is_boundary
 
     def forward(self, *inputs, **kwargs):
+        if (getattr(self, "_fwd_graphs", None) is not None and not kwargs and not torch.is_grad_enabled()
+                and all(a.is_cuda for a in inputs if torch.is_tensor(a))):
+            return self._graph_forward(inputs)
         self.timers(FORWARD_MICRO_TIMER).start()
         if self.optimizer is not None and hasattr(self.optimizer, "forward_prologue"):
             self.optimizer.forward_prologue()
@@ -498,7 +501,12 @@ class SXEEngine(nn.Module):
                 raise SystemExit(0)
 
     def _take_model_step(self, lr_kwargs=None):
+        off = getattr(self, "_offload_opt_states", False)
+        if off:
+            self.optimizer.reload_states()
         self.optimizer.step()
+        if off:
+            self.optimizer.offload_states(include=["optim_states"], non_blocking=True)
         overflow = bool(getattr(self.optimizer, "overflow", False))
         if self.progressive_layer_drop is not None:
             self.progressive_layer_drop.update_state(self.global_steps + 1)
@@ -542,6 +550,69 @@ class SXEEngine(nn.Module):
 
     def reload_states(self, non_blocking=False):
         self.optimizer.reload_states(non_blocking=non_blocking)
+
+    # ------------------------------------------------------------------------------- compile
+    def compile(self, backend="hipgraph", compile_kwargs=None, schedule=None):
+        """Counterpart of the reference's ``engine.compile`` / DeepCompile (runtime/engine.py:3970,
+        compile/backend.py:217, compile/config.py). There is no tracing compiler here: the ZeRO
+        passes DeepCompile inserts into an FX graph -- all-gather / release placement from a profiled
+        trace, prefetch scheduling, selective unsharding (keep gathered weights for backward) --
+        are what ZeRO-3 (zero/stage3.py) already does eagerly from its recorded module trace and
+        reuse-distance policy. ``compile`` maps the ``"compile"`` config section onto those
+        mechanisms and adds HIP graphs where launch overhead matters:
+
+          * ``deepcompile`` + ``offload_opt_states``: optimizer states live in (reused) pinned host
+            buffers during forward/backward and come back to HBM for the optimizer step;
+          * ``double_buffer``: ZeRO-3 prefetch depth >= 2 (off: 1);
+          * backend ``"hipgraph"``: eval / no-grad forwards with static input shapes (ZeRO 0-2,
+            parameters resident) replay a captured HIP graph per input signature.
+        Training forward/backward stay eager: ZeRO collectives are launched from autograd hooks on
+        side streams, which a captured graph would freeze at capture time. ``schedule`` is accepted
+        for API parity and ignored (the prefetch schedule is the recorded trace)."""
+        if self.is_compiled:
+            return
+        cc = dict(self._config._param_dict.get("compile", {}) or {})
+        cc.update(compile_kwargs or {})
+        self._compile_cfg = cc
+        opt = self.optimizer
+        if cc.get("deepcompile") and cc.get("offload_opt_states"):
+            assert opt is not None and hasattr(opt, "offload_states"), "offload_opt_states needs a ZeRO optimizer"
+            self._offload_opt_states = True
+            opt.offload_states(include=["optim_states"], non_blocking=True)
+        if cc.get("deepcompile") and hasattr(opt, "prefetch_depth"):
+            opt.prefetch_depth = max(2, opt.prefetch_depth) if cc.get("double_buffer", True) else 1
+        if backend == "hipgraph" and self.device.type == "cuda" and self.zero_optimization_stage() < 3:
+            self._fwd_graphs = {}
+        self._is_compiled = True
+        log_dist(f"compile: backend={backend} deepcompile={bool(cc.get('deepcompile'))} "
+                 f"offload_opt_states={getattr(self, '_offload_opt_states', False)} "
+                 f"hip_graph_forward={getattr(self, '_fwd_graphs', None) is not None}", ranks=[0])
+
+    @property
+    def is_compiled(self):
+        return getattr(self, "_is_compiled", False)
+
+    def _graph_forward(self, inputs):
+        key = tuple((a.shape, a.dtype, a.device) if torch.is_tensor(a) else ("py", a) for a in inputs)
+        g = self._fwd_graphs.get(key)
+        if g is None:
+            static_in = [a.clone() if torch.is_tensor(a) else a for a in inputs]
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(2):  # lazy inits / GEMM heuristics outside the capture
+                    self.module(*static_in)
+            torch.cuda.current_stream().wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                static_out = self.module(*static_in)
+            g = self._fwd_graphs[key] = (graph, static_in, static_out)
+        graph, static_in, static_out = g
+        for dst, src in zip(static_in, inputs):
+            if torch.is_tensor(src):
+                dst.copy_(src)
+        graph.replay()
+        return static_out
 
     def get_lr(self):
         return [g["lr"] for g in self.optimizer.param_groups] if self.optimizer is not None else []

@@ -217,31 +217,39 @@ class ZeroOptimizerBase:
         inc = set(include or ["optim_states", "hp_params", "lp_grads", "lp_params"])
         pin = pin_memory and torch.cuda.is_available()
 
-        def mv(t):
+        # pinned host buffers are kept across offload/reload cycles (per-step offloading, e.g.
+        # engine.compile's offload_opt_states, must not pay a pinned allocation every step)
+        cache = self.__dict__.setdefault("_pinned_host", {})
+
+        def mv(t, *slot):
             if t is None or not torch.is_tensor(t) or t.device.type == "cpu":
                 return t
-            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=pin)
+            key = (slot, tuple(t.shape), t.dtype)
+            h = cache.get(key)
+            if h is None:
+                h = torch.empty(t.shape, dtype=t.dtype, pin_memory=pin)
+                cache[key] = h
             h.copy_(t, non_blocking=non_blocking)
             return h
 
         self._offloaded = getattr(self, "_offloaded", {})
         if "hp_params" in inc:
-            for m in self.master:
+            for gi, m in enumerate(self.master):
                 self._offloaded.setdefault("dev", m.device)
-                m.data = mv(m.data)
+                m.data = mv(m.data, "hp", gi)
         if "lp_grads" in inc:
-            self.grads = [mv(g) for g in self.grads]
+            self.grads = [mv(g, "grad", gi) for gi, g in enumerate(self.grads)]
         if "optim_states" in inc:
-            for m in self.master:
+            for gi, m in enumerate(self.master):
                 st = self.optimizer.state[m]
                 for k, v in list(st.items()):
                     if torch.is_tensor(v) and v.numel() > 1:
-                        st[k] = mv(v)
+                        st[k] = mv(v, "opt", gi, k)
         if "lp_params" in inc and getattr(self, "fgroups", None) is not None:
-            for units in self.units:
-                for u in units:
+            for gi, units in enumerate(self.units):
+                for ui, u in enumerate(units):
                     if not u.persistent:
-                        u.shard = mv(u.shard)
+                        u.shard = mv(u.shard, "lp", gi, ui)
         self._rebind_views()
         self._offloaded["include"] = inc
         if torch.cuda.is_available():

@@ -101,3 +101,16 @@ def test_zero3_linear_matches_functional():
     torch.testing.assert_close(zero3_linear_wrap(x, m.weight, m.bias), y)
     y.sum().backward()
     assert m.weight.grad is not None and x.grad is not None
+
+
+def test_nhwc_bias_add_variants():
+    from shuffle_exchange_amd.ops.spatial import nhwc_bias_add
+    x = torch.randn(2, 8, 4, 4).to(memory_format=torch.channels_last)
+    o = torch.randn(2, 8, 4, 4).to(memory_format=torch.channels_last)
+    b, ob = torch.randn(8), torch.randn(8)
+    bb = b.view(1, 8, 1, 1)
+    torch.testing.assert_close(nhwc_bias_add(x, b), x + bb)
+    torch.testing.assert_close(nhwc_bias_add(x, b, o), x + bb + o)
+    torch.testing.assert_close(nhwc_bias_add(x, b, o, ob), x + bb + o + ob.view(1, 8, 1, 1))
+    y = torch.randn(2, 4, 4, 8)  # plain NHWC tensor
+    torch.testing.assert_close(nhwc_bias_add(y, b), y + b)
