@@ -80,6 +80,10 @@ __device__ __forceinline__ bf16x8 acc_to_b(const f32x16& a, int s) {
   return r;
 }
 
+// raw v_exp_f32: exp2f() wraps it in denormal range reduction, pure VALU overhead for softmax
+// probabilities (a denormal p is 0 for every purpose here)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -255,24 +259,30 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const unsigned short* __res
         }
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx);
+      // lazy rescale: the reference max only moves when the tile max exceeds it by > 2^8, so
+      // p <= 256 (harmless in fp32 / bf16) and the 64-register O rescale is skipped whenever no
+      // lane of the wave moved (most tiles after the first few)
+      const bool grow = mx > m + 8.f;
+      const float mnew = grow ? mx : m;
       const float mref = (mnew == -INFINITY) ? 0.f : mnew;
-      const float alpha = exp2f(m - mref);
+      const float alpha = fast_exp2(m - mref);
       float ps = 0.f;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float p = exp2f(s[j][i] - mref);
+          const float p = fast_exp2(s[j][i] - mref);
           s[j][i] = p;
           ps += p;
         }
       l = l * alpha + ps;
       m = mnew;
+      if (__any(grow)) {
 #pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt)
+        for (int dt = 0; dt < D / 32; ++dt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+          for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+      }
       const char* vt = smem + cur * BUF + KT * ROWB;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
@@ -431,7 +441,7 @@ __global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __rest
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float p = exp2f(s[i] * c - lse2);
+          float p = fast_exp2(s[i] * c - lse2);
           if (diag && (kbase + 32 * j + acc_row(i, h) > q0 + r)) p = 0.f;
           if (!(acc_row(i, h) < 16 ? b0 : b1)) p = 0.f;
           s[i] = p * (dp[i] - dlt);  // dS^T
@@ -463,7 +473,8 @@ __global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __rest
 // =============================================================================================
 // dK, dV: per wave 32 keys held on the lanes; sweep every query head of the GQA group and every
 // 32-query tile at or after the keys (causal). Q/dO tiles + LSE/delta arrive by LDS-DMA into a
-// 2-slot ring; the workgroup's V block (128 keys) sits in LDS for the whole kernel; K fragments,
+// 2-slot ring; the workgroup's V block (128 keys) sits in LDS for the whole kernel (V fragments in
+// registers too would exceed the 256-VGPR budget of 2 waves/SIMD and spill); K fragments,
 // dK^T and dV^T live in registers.
 // =============================================================================================
 constexpr int QT = 32;  // queries per tile in the dK/dV sweep
@@ -561,7 +572,7 @@ __global__ void __launch_bounds__(256, 2) dkdv_kernel(const unsigned short* __re
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int qi = acc_row(i, h);
-        float p = exp2f(s[i] * c - l2[qi] * LOG2E);
+        float p = fast_exp2(s[i] * c - l2[qi] * LOG2E);
         if (diag && (k0 + r > qt0 + qi)) p = 0.f;
         if (!(qi < 16 ? b0 : b1)) p = 0.f;
         s[i] = p;                      // P

@@ -96,10 +96,10 @@ class _FusedLinearXEnt(torch.autograd.Function):
         if ctx.mode == "dlogits":
             dl, h2, weight = ctx.saved_tensors
             dl.mul_(gout.to(dl.dtype))  # upstream scalar (1/GAS, loss scale, ...), in place
-            dh = torch.matmul(dl, weight).view(ctx.hshape)
+            from .linear import data_grad, write_weight_grad
+            dh = data_grad(dl, weight).view(ctx.hshape)
             dW = None
             if ctx.needs_input_grad[1]:
-                from .linear import write_weight_grad
                 if not write_weight_grad(weight, dl, h2):
                     dW = dl.t() @ h2
             return dh, dW, None, None, None, None

@@ -53,6 +53,22 @@ def _tn_ok(gy2, x2):
             and x2.shape[1] % 64 == 0 and gy2.is_contiguous() and x2.is_contiguous())
 
 
+# Data-gradient GEMMs dX = dY W run in hipBLASLt's "NN" layout at 1.03-1.35 PF on MI355X; with W^T
+# materialised by the HBM-speed transpose they run in the forward layout at 1.25-1.56 PF
+# (tools/gemm_layout_bench.py, profiles/gemm_layout.log: net -0.03..-0.06 ms per Llama-3-8B layer
+# GEMM, -0.48 ms for the LM head, at 8192 tokens). The transpose reads/writes only the weight.
+DGRAD_WT_MIN_ELEMS = int(os.environ.get("SXE_DGRAD_WT_MIN_ELEMS", 16 * 2**20))
+
+
+def data_grad(gy, w):
+    """dX = gy @ w for w [N, K] (gy [..., N])."""
+    if (DGRAD_WT_MIN_ELEMS > 0 and gy.is_cuda and gy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and w.dim() == 2 and w.is_contiguous() and w.numel() >= DGRAD_WT_MIN_ELEMS and w.shape[0] % 64 == 0
+            and w.shape[1] % 64 == 0 and gy.numel() // gy.shape[-1] >= 2048):
+        return torch.matmul(gy, torch.ops.sxe.transpose16(w).t())
+    return torch.matmul(gy, w)
+
+
 def write_weight_grad(w, gy2, x2):
     """dW = gy2^T @ x2 into the optimizer-provided target of `w`; returns True if handled."""
     tgt = getattr(w, "_sxe_grad_target", None)
@@ -90,7 +106,7 @@ class _Linear(torch.autograd.Function):
         gy2 = gy.reshape(-1, gy.shape[-1])
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.matmul(gy, w)
+            dx = data_grad(gy, w)
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
             if not write_weight_grad(w, gy2, x2):

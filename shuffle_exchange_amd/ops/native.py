@@ -16,7 +16,7 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-HIP_LIB = os.path.join(_HERE, "_sxe_hip.so")
+HIP_LIB = os.environ.get("SXE_HIP_LIB") or os.path.join(_HERE, "_sxe_hip.so")  # override: A/B kernel experiments
 CPU_LIB = os.path.join(_HERE, "_sxe_cpu.so")
 
 _lock = threading.Lock()
