@@ -227,7 +227,11 @@ class ZeroOptimizerBase:
             key = (slot, tuple(t.shape), t.dtype)
             h = cache.get(key)
             if h is None:
-                h = torch.empty(t.shape, dtype=t.dtype, pin_memory=pin)
+                if pin:
+                    from .offload import pinned_empty
+                    h = pinned_empty(t.numel(), t.dtype).view(t.shape)
+                else:
+                    h = torch.empty(t.shape, dtype=t.dtype)
                 cache[key] = h
             h.copy_(t, non_blocking=non_blocking)
             return h

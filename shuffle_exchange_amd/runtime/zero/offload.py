@@ -28,7 +28,26 @@ from ...utils.logging import log_dist
 
 
 def _pinned(n, dtype):
-    return torch.empty(int(n), dtype=dtype, pin_memory=torch.cuda.is_available())
+    return pinned_empty(n, dtype)
+
+
+def _offsets(units):
+    off, out = 0, []
+    for u in units:
+        out.append(off)
+        off += u.chunk
+    return out
+
+
+def pinned_empty(n, dtype):
+    """Exact-size pinned host buffer (host_mem.hip) -- the caching host allocator behind
+    ``pin_memory=True`` rounds to a power of two, up to +100 % of the host tier's footprint.
+    Small buffers and GPU-less processes use the regular path."""
+    n = int(n)
+    if torch.cuda.is_available() and n * torch.tensor([], dtype=dtype).element_size() >= (64 << 20) \
+            and native.hip_available():
+        return torch.ops.sxe.pinned_empty(n, dtype)
+    return torch.empty(n, dtype=dtype, pin_memory=torch.cuda.is_available())
 
 
 class _NVMeSwapper:
@@ -106,6 +125,7 @@ class HostOptimizerStep:
         if self.device == "nvme":
             assert self.nvme_path, "offload_optimizer.device=nvme needs nvme_path"
         acc = get_accelerator()
+        self.STAGE_SLOTS = max(2, int(os.environ.get("SXE_OFFLOAD_STAGE_SLOTS", 3)))
         self.d2h = acc.named_stream("offload_d2h") if acc.gpu else None
         self.h2d = acc.named_stream("offload_h2d") if acc.gpu else None
         self._h2d_done = None
@@ -118,12 +138,24 @@ class HostOptimizerStep:
         if opt.kind == "generic" and self.device == "nvme":
             raise ValueError("NVMe optimizer offload supports Adam/AdamW/Lion/Adagrad")
         opt.grad_host, opt.lp_host = [], []
+        # Host staging of gradients (fp32, D2H) and updated bit16 params (H2D): a ring of
+        # STAGE_SLOTS unit-sized pinned slots instead of full-model mirrors (6 B/param less on the
+        # host -- the host tier is what bounds the trainable model size); generic torch optimizers
+        # step whole groups and keep the full mirrors.
+        self.streamed = opt.kind != "generic"
+        all_units = [u for units in opt.units for u in units]
+        if self.streamed and all_units:
+            maxc = max(u.chunk for u in all_units)
+            self.gslots = [_pinned(maxc, torch.float32) for _ in range(self.STAGE_SLOTS)]
+            lp_dtype = next((u.dtype for u in all_units if u.shard.is_cuda), None)
+            self.lslots = [_pinned(maxc, lp_dtype) for _ in range(self.STAGE_SLOTS)] if lp_dtype else None
+            self._lslot_ev = [None] * self.STAGE_SLOTS
         for g, units in enumerate(opt.units):
             total = sum(u.chunk for u in units)
             gr = torch.zeros(total, dtype=torch.float32, device=opt.device)  # GPU accumulator
-            opt.grad_host.append(_pinned(total, torch.float32))
             needs_lp = any(u.shard.is_cuda for u in units)
-            opt.lp_host.append(_pinned(total, units[0].dtype) if needs_lp else None)
+            opt.grad_host.append(None if self.streamed else _pinned(total, torch.float32))
+            opt.lp_host.append(_pinned(total, units[0].dtype) if needs_lp and not self.streamed else None)
             if self.device == "cpu":
                 m = _pinned(total, torch.float32) if self.pin else torch.empty(total, dtype=torch.float32)
             else:
@@ -201,9 +233,84 @@ class HostOptimizerStep:
         if self.materialized and self.device == "nvme":
             self.flush(opt)
         cur = torch.cuda.current_stream() if opt.device is not None and opt.device.type == "cuda" else None
+        if not self.streamed:
+            return self._update_mirrored(opt, cur, coef)
+        # units in step order; unit k's gradient lands in staging slot k % NS, so at most NS units'
+        # copies are in flight ahead of the CPU update
+        flat = [(g, i, u, off) for g, units in enumerate(opt.units)
+                for i, u, off in zip(range(len(units)), units, _offsets(units))]
+        NS = len(self.gslots)
+        d2h_ev = {}
+
+        def issue_d2h(k):
+            u = flat[k][2]
+            dst = self.gslots[k % NS][:u.chunk]
+            if cur is None:
+                dst.copy_(u.grad)
+                return
+            with get_accelerator().stream(self.d2h):
+                dst.copy_(u.grad, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.d2h)
+                d2h_ev[k] = ev
+
+        if cur is not None:
+            self.d2h.wait_stream(cur)
+        for k in range(min(NS, len(flat))):
+            issue_d2h(k)
+        nvme = self.device == "nvme"
+        nslot = len(self.swapper.slots) if nvme else 0
+        for g, units in enumerate(opt.units):
+            st = opt.optimizer.state[opt.master[g]]
+            if opt.kind in ("adam", "adagrad"):
+                st["step"] = int(st.get("step", 0)) + 1
+        pend = {}
+        if nvme and flat:
+            g0, i0, u0, _ = flat[0]
+            pend[0] = self.swapper.read(0, g0, i0, u0.chunk)
+        for k, (g, i, u, off) in enumerate(flat):
+            pg = opt.optimizer.param_groups[g]
+            st = opt.optimizer.state[opt.master[g]]
+            if nvme and k + 1 < len(flat):
+                gn, iN, un, _ = flat[k + 1]
+                pend[k + 1] = self.swapper.read((k + 1) % nslot, gn, iN, un.chunk)
+            if k in d2h_ev:
+                d2h_ev.pop(k).synchronize()
+            slot = k % NS
+            grad = self.gslots[slot][:u.chunk]
+            if nvme:
+                self.swapper.rd.wait_request(pend.pop(k))
+                views = self.swapper.views(k % nslot, u.chunk)
+                master, states = views[0], views[1:]
+            else:
+                master, states = u.master, self._state_views(opt, g, off, u.chunk)
+            if u.shard.is_cuda:
+                if self._lslot_ev[slot] is not None:
+                    self._lslot_ev[slot].synchronize()  # its previous H2D has drained
+                lp = self.lslots[slot][:u.chunk]
+            else:
+                lp = u.shard
+            self._host_kernel(opt, pg, st, master, grad, states, lp, coef)
+            if nvme:
+                self.swapper.write(k % nslot, g, i, u.chunk)
+            if k + NS < len(flat):
+                issue_d2h(k + NS)  # this grad slot is free again
+            if u.shard.is_cuda:
+                with get_accelerator().stream(self.h2d):
+                    u.shard.copy_(lp, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self.h2d)
+                    self._lslot_ev[slot] = ev
+        if nvme:
+            self.swapper.drain()
+        if cur is not None:
+            cur.wait_stream(self.d2h)  # zero_grad_buffers() must not overtake the copies
+            cur.wait_stream(self.h2d)
+
+    def _update_mirrored(self, opt, cur, coef):
+        """Generic (torch) optimizers: full host mirrors of grads / bit16 params."""
         if self._h2d_done is not None:
             self._h2d_done.synchronize()  # lp_host of the previous step fully consumed
-        # 1. all D2H grad copies in unit order, one event each
         events = []
         if cur is not None:
             self.d2h.wait_stream(cur)
@@ -218,47 +325,11 @@ class HostOptimizerStep:
                         ev.record(self.d2h)
                         events.append(ev)
         if cur is not None:
-            cur.wait_stream(self.d2h)  # zero_grad_buffers() must not overtake the copies
-        # 2. CPU update unit by unit as grads land; bf16 results go back on the H2D stream
+            cur.wait_stream(self.d2h)
         k = 0
-        nvme = self.device == "nvme"
         for g, units in enumerate(opt.units):
-            pg = opt.optimizer.param_groups[g]
-            st = opt.optimizer.state[opt.master[g]]
-            if opt.kind in ("adam", "adagrad"):
-                st["step"] = int(st.get("step", 0)) + 1
-            if opt.kind == "generic":
-                self._generic(opt, g, events, k, coef)
-                k += len(units)
-                continue
-            off = 0
-            nslot = len(self.swapper.slots) if nvme else 0
-            pend = {}
-            if nvme and units:
-                pend[0] = self.swapper.read(0, g, 0, units[0].chunk)
-            for i, u in enumerate(units):
-                if nvme and i + 1 < len(units):
-                    pend[i + 1] = self.swapper.read((i + 1) % nslot, g, i + 1, units[i + 1].chunk)
-                if events:
-                    events[k].synchronize()
-                grad = opt.grad_host[g][off:off + u.chunk]
-                if nvme:
-                    self.swapper.rd.wait_request(pend.pop(i))
-                    views = self.swapper.views(i % nslot, u.chunk)
-                    master, states = views[0], views[1:]
-                else:
-                    master, states = u.master, self._state_views(opt, g, off, u.chunk)
-                lp = u.shard if not u.shard.is_cuda else opt.lp_host[g][off:off + u.chunk]
-                self._host_kernel(opt, pg, st, master, grad, states, lp, coef)
-                if nvme:
-                    self.swapper.write(i % nslot, g, i, u.chunk)
-                if u.shard.is_cuda:
-                    with get_accelerator().stream(self.h2d):
-                        u.shard.copy_(lp, non_blocking=True)
-                off += u.chunk
-                k += 1
-        if nvme:
-            self.swapper.drain()
+            self._generic(opt, g, events, k, coef)
+            k += len(units)
         if cur is not None:
             self._h2d_done = torch.cuda.Event()
             self._h2d_done.record(self.h2d)

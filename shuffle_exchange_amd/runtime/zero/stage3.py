@@ -260,7 +260,11 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             u.state = AVAILABLE
         else:
             if self.offload_param:
-                u.shard = torch.empty(u.chunk, dtype=dtype, pin_memory=flat.is_cuda)
+                if flat.is_cuda:
+                    from .offload import pinned_empty  # exact-size pinned (no power-of-2 rounding)
+                    u.shard = pinned_empty(u.chunk, dtype)
+                else:
+                    u.shard = torch.empty(u.chunk, dtype=dtype)
                 u.shard.copy_(flat[u.lo:u.hi])
             else:
                 u.shard = flat[u.lo:u.hi].clone()
@@ -410,7 +414,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
 
     # ------------------------------------------------------------------------------ fetch/release
     def _launch_gather(self, u):
-        cur = torch.cuda.current_stream() if u.shard.is_cuda else None
+        cur = torch.cuda.current_stream() if u.flat.is_cuda else None  # shard may be host-resident (offload_param)
         st = self.ag_stream
         if st is not None:
             st.wait_stream(cur)
