@@ -107,7 +107,8 @@ def main():
     tps = tokens / elapsed
     flops_tok = cfg.flops_per_token(args.seq)
     mfu_tflops = tps * flops_tok / args.gpus / 1e12
-    valid = args.layers is None and args.model == "llama3-8b" and args.stage == 3 and on_gpu
+    valid = (args.layers is None and args.model == "llama3-8b" and args.stage == 3 and on_gpu and args.seq == 2048
+             and args.mbs * args.gas == 16)
     if rank == 0:
         out = {
             "metric": "tokens/sec Llama-3-8B ZeRO-3 bf16 (training, whole job)",

@@ -49,5 +49,11 @@ class GroupedSwiGLUExperts(nn.Module):
             p.group_name = expert_group_name
 
     def forward(self, x):
-        # x: [E_local, T, H] -> bmm -> [E_local, T, 2I] -> swiglu -> bmm -> [E_local, T, H]
-        return torch.bmm(swiglu(torch.bmm(x, self.w_gate_up)), self.w_down)
+        # x: [E_local, C, H] -> per expert [C, H] @ [H, 2I] -> SwiGLU (one HIP launch over all
+        # experts) -> [C, I] @ [I, H]. Plain 2-D GEMMs per expert rather than torch.bmm: at
+        # Mixtral-8x7B sizes (C = 1280 tokens, H = 4096, I = 14336) each GEMM is 30-150 GFLOP, so
+        # batching buys nothing, and the strided-batched backward of bmm under the TunableOp
+        # lookup-only GEMM path faulted on MI355X (illegal address in the autograd thread).
+        gu = torch.stack([torch.matmul(x[e], self.w_gate_up[e]) for e in range(self.num_local_experts)])
+        h = swiglu(gu)
+        return torch.stack([torch.matmul(h[e], self.w_down[e]) for e in range(self.num_local_experts)])
