@@ -49,11 +49,58 @@ class GroupedSwiGLUExperts(nn.Module):
             p.group_name = expert_group_name
 
     def forward(self, x):
-        # x: [E_local, C, H] -> per expert [C, H] @ [H, 2I] -> SwiGLU (one HIP launch over all
-        # experts) -> [C, I] @ [I, H]. Plain 2-D GEMMs per expert rather than torch.bmm: at
-        # Mixtral-8x7B sizes (C = 1280 tokens, H = 4096, I = 14336) each GEMM is 30-150 GFLOP, so
-        # batching buys nothing, and the strided-batched backward of bmm under the TunableOp
-        # lookup-only GEMM path faulted on MI355X (illegal address in the autograd thread).
-        gu = torch.stack([torch.matmul(x[e], self.w_gate_up[e]) for e in range(self.num_local_experts)])
-        h = swiglu(gu)
-        return torch.stack([torch.matmul(h[e], self.w_down[e]) for e in range(self.num_local_experts)])
+        # x: [E_local, C, H] -> [E_local, C, 2I] -> SwiGLU (one HIP launch for all experts) -> [E_local, C, H]
+        return grouped_mm(swiglu(grouped_mm(x, self.w_gate_up)), self.w_down)
+
+
+class _GroupedMM(torch.autograd.Function):
+    """y[e] = x[e] @ W[e] for x [E, C, K], W [E, K, N]: one plain 2-D hipBLASLt GEMM per expert,
+    written in place into the output (no stacking copies). Backward: dX per expert in place, and
+    dW straight into the ZeRO gradient buffer of W (fp32 accumulate with beta = 1 inside the GEMM,
+    like ops/linear.py) -- autograd's select/stack backward would instead materialise a zeroed
+    full-size [E, K, N] gradient per expert and sum them (measured: 36 % of a Mixtral step).
+    Plain GEMMs rather than torch.bmm: the strided-batched backward of bmm under the TunableOp
+    lookup-only path faulted on MI355X at Mixtral sizes (illegal address in the autograd thread)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        E, C, _ = x.shape
+        x = x.contiguous()
+        y = x.new_empty(E, C, w.shape[2])
+        for e in range(E):
+            torch.mm(x[e], w[e], out=y[e])
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        E = x.shape[0]
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            for e in range(E):
+                torch.mm(dy[e], w[e].t(), out=dx[e])
+        if ctx.needs_input_grad[1]:
+            tgt = getattr(w, "_sxe_grad_target", None)
+            if tgt is not None:
+                buf, acc = tgt(w)
+                for e in range(E):
+                    if buf.dtype == torch.float32 and dy.dtype != torch.float32:
+                        torch.ops.aten.addmm.dtype_out(buf[e], x[e].t(), dy[e], torch.float32, beta=1 if acc else 0,
+                                                       alpha=1, out=buf[e])
+                    elif acc:
+                        buf[e].addmm_(x[e].t(), dy[e])
+                    else:
+                        torch.mm(x[e].t(), dy[e], out=buf[e])
+                w._sxe_grad_done(w)
+            else:
+                dw = torch.empty_like(w)
+                for e in range(E):
+                    torch.mm(x[e].t(), dy[e], out=dw[e])
+        return dx, dw
+
+
+def grouped_mm(x, w):
+    return _GroupedMM.apply(x, w)

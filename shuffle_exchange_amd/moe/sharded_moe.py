@@ -67,12 +67,14 @@ def _positions(expert_idx, E, mask=None):
     """Cumulative position of each (token, choice) inside its expert, choice-major like the
     reference (all first choices are placed before all second choices)."""
     S, k = expert_idx.shape
-    oh = F.one_hot(expert_idx.t().reshape(-1), E)  # [k*S, E], choice-major
+    oh = F.one_hot(expert_idx.t().reshape(-1), E).to(torch.int32)  # [k*S, E], choice-major
     if mask is not None:
         oh = oh * mask.t().reshape(-1, 1).to(oh.dtype)
-    loc = torch.cumsum(oh, dim=0) - 1
+    # scan along the contiguous dimension ([E, k*S]): the outer-dim int64 scan of [k*S, E] was
+    # 1.5 ms per MoE layer on MI355X at 8K tokens
+    loc = torch.cumsum(oh.t().contiguous(), dim=1).t() - 1
     loc = (loc * oh).sum(1).view(k, S).t()
-    return loc
+    return loc.to(torch.int64)
 
 
 def _max_capacity(exp_counts, ep_group, num_tokens):
@@ -158,7 +160,7 @@ def topkgating(logits, k, capacity_factor, min_capacity, drop_tokens=True, ep_gr
     else:
         capacity = _max_capacity(exp_counts, ep_group, S)
     # positions along the token axis per expert (the reference's cumsum over tokens)
-    locs = torch.cumsum(mask.to(torch.int64), dim=0) - 1
+    locs = (torch.cumsum(mask.to(torch.int32).t().contiguous(), dim=1).t() - 1).to(torch.int64)
     loc_k = torch.gather(locs, 1, top_idx)
     keep_k = torch.gather(mask, 1, top_idx) & (loc_k < capacity)
     gates_k = torch.gather(gates, 1, top_idx) * keep_k
