@@ -69,7 +69,10 @@ def main():
                               # 288 GB HBM: the whole bf16 model (16 GB for 8B) may stay gathered from
                               # its forward use to its backward re-use -> no backward all-gather
                               "stage3_max_reuse_distance": 2 * cfg.num_params(),
-                              "stage3_max_live_parameters": cfg.num_params()},
+                              "stage3_max_live_parameters": cfg.num_params(),
+                              # and keep fp32 gradient sums local across the grad-accumulation
+                              # micro-steps: one reduce-scatter per step instead of one per micro-step
+                              "stage3_defer_reduce": True},
         "optimizer": {"type": "AdamW", "params": {"lr": 3e-4, "betas": [0.9, 0.95], "eps": 1e-8,
                                                    "weight_decay": 0.1}},
         "steps_per_print": 1000000,

@@ -89,6 +89,9 @@ class ZeroConfig(ConfigModel):
     # MI355X-specific knobs (new): units of ZeRO-3 fetch (module class names) and prefetch depth
     fetch_units: Optional[List[str]] = None
     prefetch_depth: int = 2
+    # MI355X (288 GB HBM): ZeRO-3 keeps each unit's fp32 gradient sum across the micro-steps of one
+    # optimizer step and reduce-scatters once at the accumulation boundary
+    defer_reduce: bool = Field(False, alias="stage3_defer_reduce")
 
     @model_validator(mode="after")
     def _compat(self):

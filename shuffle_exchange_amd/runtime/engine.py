@@ -357,7 +357,8 @@ class SXEEngine(nn.Module):
                 shuffle_exchange_cfg=se, mp_group=mp_group, timers=self.timers, mics_shard_size=zc.mics_shard_size,
                 host_step=host_step, offload_param=offload_param, quantized_weights=zc.zero_quantized_weights,
                 quantized_gradients=zc.zero_quantized_gradients, hpz_partition_size=zc.zero_hpz_partition_size,
-                max_reuse_distance=zc.max_reuse_distance, max_live_parameters=zc.max_live_parameters)
+                max_reuse_distance=zc.max_reuse_distance, max_live_parameters=zc.max_live_parameters,
+                defer_reduce=zc.defer_reduce)
         elif stage in (1, 2):
             self.optimizer = ZeroStage12Optimizer(
                 basic, stage=stage, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks,

@@ -54,6 +54,8 @@ class FlatUnit:
         self.master = None         # fp32 chunk (view into the group master buffer)
         self.grad = None           # fp32 chunk gradient accumulator (view into group grad buffer)
         self.staging = None        # full-size grad staging buffer during backward
+        self.staging_dtype = None  # None: the unit dtype; fp32 when gradients carry across micro-steps
+        self.carry = False         # staging already holds earlier micro-steps' gradients (deferred RS)
         self.filled = None         # per-param "grad copied to staging" flags
         self.pending = 0
         self.param_index = {id(p): i for i, p in enumerate(self.params)}
@@ -90,13 +92,15 @@ class FlatUnit:
     def stage_grad(self, p, grad):
         i = self.param_index[id(p)]
         if self.staging is None:
-            self.staging = torch.empty(self.padded, dtype=grad.dtype if grad.dtype == self.dtype else self.dtype,
-                                       device=self.device)
+            self.staging = torch.empty(self.padded, dtype=self.staging_dtype or self.dtype, device=self.device)
             if self.padded > self.numel:
                 self.staging[self.numel:].zero_()
         o, n = self.offsets[i], self.numels[i]
-        if self.filled[i]:
+        if self.filled[i] or self.carry:
             self.staging[o:o + n].add_(grad.reshape(-1))
+            if not self.filled[i]:
+                self.filled[i] = True
+                self.pending -= 1
         else:
             self.staging[o:o + n].copy_(grad.reshape(-1))
             self.filled[i] = True
@@ -106,8 +110,8 @@ class FlatUnit:
     def fill_missing(self):
         """Zero the staging slots of parameters that received no gradient this backward."""
         if self.staging is None:
-            self.staging = torch.zeros(self.padded, dtype=self.dtype, device=self.device)
-        else:
+            self.staging = torch.zeros(self.padded, dtype=self.staging_dtype or self.dtype, device=self.device)
+        elif not self.carry:  # carried slots hold earlier micro-steps' sums: nothing to zero
             for i, f in enumerate(self.filled):
                 if not f:
                     o, n = self.offsets[i], self.numels[i]

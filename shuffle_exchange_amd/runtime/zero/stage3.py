@@ -108,7 +108,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                  unit_classes=None, shuffle_exchange_cfg=None, mp_group=None, timers=None, mics_shard_size=-1,
                  average_master=False, host_step=None, offload_param=False, quantized_weights=False,
                  quantized_gradients=False, hpz_partition_size=1, quant_group_size=128, grad_quant_bits=8,
-                 max_reuse_distance=1_000_000_000, max_live_parameters=1_000_000_000):
+                 max_reuse_distance=1_000_000_000, max_live_parameters=1_000_000_000, defer_reduce=False):
         acc = get_accelerator()
         device = torch.device(acc.current_device_name())
         self.module = module
@@ -172,13 +172,22 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         self._build(unit_classes)
         self._init_master()
         self._register()
+        # deferred reduce-scatter (zero_optimization.stage3_defer_reduce): units keep an fp32
+        # gradient sum across micro-steps (4 B/param of HBM) and reduce-scatter at the boundary
+        self.defer_reduce = bool(defer_reduce) and self.S > 1 and not self.qgz
+        self._boundary = True
+        if self.defer_reduce:
+            for units in self.units:
+                for u in units:
+                    u.staging_dtype = torch.float32
         self.trace = [fg.idx for fg in self.fgroups]
         self._observed = []
         n_units = sum(len(u) for u in self.units)
         n_persist = sum(1 for units in self.units for u in units if u.persistent)
         log_dist(f"ZeRO-3: {len(self.fgroups)} fetch groups / {n_units} units ({n_persist} persistent), "
                  f"partition={self.S}, slices={self.topo.num_slices}, prefetch_depth={self.prefetch_depth}, "
-                 f"mics={self.mics}, shuffle_exchange={se.method if self.se is not None else 'off'}", ranks=[0])
+                 f"mics={self.mics}, shuffle_exchange={se.method if self.se is not None else 'off'}, "
+                 f"defer_reduce={self.defer_reduce}", ranks=[0])
 
     # ------------------------------------------------------------------------------------- layout
     def _build(self, unit_classes):
@@ -297,10 +306,10 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         if u.persistent and self.S == 1:
             return u.grad[o:o + n].view(p.shape), True
         if u.staging is None:
-            u.staging = torch.empty(u.padded, dtype=u.dtype, device=u.device)
+            u.staging = torch.empty(u.padded, dtype=u.staging_dtype or u.dtype, device=u.device)
             if u.padded > u.numel:
                 u.staging[u.numel:].zero_()
-        return u.staging[o:o + n].view(p.shape), u.filled[i]
+        return u.staging[o:o + n].view(p.shape), u.filled[i] or u.carry
 
     def _grad_done(self, p):
         u = self.param_unit[p]
@@ -510,6 +519,13 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
 
     # ------------------------------------------------------------------------------ grad reduction
     def _reduce_unit(self, u):
+        if self.defer_reduce and not self._boundary:
+            # 288 GB HBM: keep the unit's fp32 gradient sum local across the micro-steps of one
+            # optimizer step and reduce-scatter it once, at the accumulation boundary (1/GAS of
+            # the per-micro-step reduce-scatter traffic over xGMI)
+            u.carry = True
+            return
+        u.carry = False
         st = u.staging
         u.staging = None
         cur = torch.cuda.current_stream() if st.is_cuda else None
@@ -517,7 +533,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         if rs is not None:
             rs.wait_stream(cur)
         with get_accelerator().stream(rs):
-            send = st if (self.comm_dtype is None or st.dtype == self.comm_dtype) else st.to(self.comm_dtype)
+            want = self.comm_dtype or (u.dtype if self.defer_reduce else None)
+            send = st if (want is None or st.dtype == want) else st.to(want)
             if self.S == 1:
                 u.grad.add_(send)
             elif self.qgz and not self.mics:
@@ -561,7 +578,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 u.begin_backward()
 
     def set_gradient_accumulation_boundary(self, flag):
-        pass
+        self._boundary = bool(flag)
 
     def reduce_gradients(self, pipeline_parallel=False):
         for units in self.units:

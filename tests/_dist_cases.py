@@ -266,3 +266,35 @@ def case_tied_zero3(rank, world, steps):
         eng.backward(loss)
         eng.step()
     return {"params": full_params(eng), "fgs": [fg.name for fg in eng.optimizer.fgroups]}
+
+
+def case_zero3_defer(rank, world, defer, steps, mbs, gas, seq):
+    """ZeRO-3 with gradient accumulation, with/without the deferred (boundary-only) reduce-scatter;
+    counts the reduce-scatters issued."""
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd import comm as dist
+    model, cfg = tiny_llama(0)
+    ds = {"train_micro_batch_size_per_gpu": mbs, "gradient_accumulation_steps": gas,
+          "zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 0, "stage3_defer_reduce": defer},
+          "optimizer": {"type": "AdamW", "params": {"lr": 1e-2, "weight_decay": 0.01}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    n_rs = [0]
+    orig = dist.reduce_scatter_tensor
+
+    def counting(*a, **k):
+        n_rs[0] += 1
+        return orig(*a, **k)
+    dist.reduce_scatter_tensor = counting
+    import shuffle_exchange_amd.runtime.zero.stage3 as s3
+    s3_orig = s3.dist.reduce_scatter_tensor
+    s3.dist.reduce_scatter_tensor = counting
+    try:
+        for b in global_batches(cfg, world, mbs, seq, steps * gas):
+            local = b[rank * mbs:(rank + 1) * mbs]
+            loss = eng(local, labels=local)
+            eng.backward(loss)
+            eng.step()
+    finally:
+        dist.reduce_scatter_tensor = orig
+        s3.dist.reduce_scatter_tensor = s3_orig
+    return {"params": full_params(eng), "rs": n_rs[0], "defer": eng.optimizer.defer_reduce}

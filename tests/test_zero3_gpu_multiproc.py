@@ -13,7 +13,7 @@ from .dist_utils import run_dist
 pytestmark = pytest.mark.gpu
 
 
-def _case(rank, world, reuse, stage=3, se=None):
+def _case(rank, world, reuse, stage=3, se=None, defer=False):
     os.environ["LOCAL_RANK"] = "0"  # both ranks on GPU 0
     import shuffle_exchange_amd as sxe
     from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
@@ -25,7 +25,7 @@ def _case(rank, world, reuse, stage=3, se=None):
         model = LlamaForCausalLM(cfg)
     ds = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": 2, "bf16": {"enabled": True},
           "zero_optimization": {"stage": stage, "stage3_param_persistence_threshold": 0,
-                                "stage3_max_reuse_distance": reuse},
+                                "stage3_max_reuse_distance": reuse, "stage3_defer_reduce": defer},
           "optimizer": {"type": "SGD", "params": {"lr": 0.05}}}
     eng, _, _, _ = sxe.initialize(model=model, config=ds, **(se or {}))
     g = torch.Generator().manual_seed(7)
@@ -40,10 +40,10 @@ def _case(rank, world, reuse, stage=3, se=None):
     return {"params": C.full_params(eng), "S": getattr(eng.optimizer, "S", None)}
 
 
-@pytest.mark.parametrize("reuse", [0, 10**12])
-def test_zero3_two_ranks_one_gpu_matches_single_rank(reuse):
+@pytest.mark.parametrize("reuse,defer", [(0, False), (10**12, False), (10**12, True)])
+def test_zero3_two_ranks_one_gpu_matches_single_rank(reuse, defer):
     try:
-        two = run_dist(_case, 2, reuse)
+        two = run_dist(_case, 2, reuse, 3, None, defer)
     except RuntimeError as e:
         if "gloo" in str(e).lower() and "cuda" in str(e).lower():
             pytest.skip(f"gloo without GPU tensor support on this build: {str(e)[-200:]}")

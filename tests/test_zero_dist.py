@@ -189,3 +189,15 @@ def test_zero3_tied_embeddings_external_parameter():
     for r in res:
         assert "lm_head#external" in r["fgs"]
         _close(r["params"], ref)
+
+
+def test_zero3_deferred_reduce_scatter_matches_per_microstep():
+    """stage3_defer_reduce: one reduce-scatter per unit per optimizer step (not per micro-step),
+    same parameters as reducing every micro-step."""
+    world, steps, mbs, gas, seq = 2, 2, 2, 3, 16
+    d = run_dist(C.case_zero3_defer, world, True, steps, mbs, gas, seq)
+    n = run_dist(C.case_zero3_defer, world, False, steps, mbs, gas, seq)
+    assert d[0]["defer"] and not n[0]["defer"]
+    assert n[0]["rs"] == gas * d[0]["rs"], (n[0]["rs"], d[0]["rs"])
+    for k, v in n[0]["params"].items():
+        torch.testing.assert_close(d[0]["params"][k], v, atol=1e-4, rtol=1e-3)  # Adam amplifies sum order
