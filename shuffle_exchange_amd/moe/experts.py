@@ -87,9 +87,12 @@ class _GroupedMM(torch.autograd.Function):
             if tgt is not None:
                 buf, acc = tgt(w)
                 for e in range(E):
-                    if buf.dtype == torch.float32 and dy.dtype != torch.float32:
+                    if buf.dtype == torch.float32 and dy.dtype != torch.float32 and dy.is_cuda:
                         torch.ops.aten.addmm.dtype_out(buf[e], x[e].t(), dy[e], torch.float32, beta=1 if acc else 0,
                                                        alpha=1, out=buf[e])
+                    elif buf.dtype != dy.dtype:
+                        d = (x[e].t() @ dy[e]).to(buf.dtype)
+                        buf[e].add_(d) if acc else buf[e].copy_(d)
                     elif acc:
                         buf[e].addmm_(x[e].t(), dy[e])
                     else:

@@ -83,8 +83,12 @@ def write_weight_grad(w, gy2, x2):
             dw = torch.mm(a, b)
             buf.add_(dw) if accumulate else buf.copy_(dw)
     elif buf.dtype == torch.float32 and gy2.dtype != torch.float32:
-        torch.ops.aten.addmm.dtype_out(buf, gy2.t(), x2, torch.float32, beta=1 if accumulate else 0, alpha=1,
-                                       out=buf)
+        if gy2.is_cuda:
+            torch.ops.aten.addmm.dtype_out(buf, gy2.t(), x2, torch.float32, beta=1 if accumulate else 0, alpha=1,
+                                           out=buf)
+        else:  # CPU processes (gloo plumbing runs): no fp32-out GEMM for 16-bit inputs there
+            dw = (gy2.t() @ x2).float()
+            buf.add_(dw) if accumulate else buf.copy_(dw)
     elif accumulate:
         buf.addmm_(gy2.t(), x2)
     else:
