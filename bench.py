@@ -72,7 +72,9 @@ def main():
                               "stage3_max_live_parameters": cfg.num_params(),
                               # and keep fp32 gradient sums local across the grad-accumulation
                               # micro-steps: one reduce-scatter per step instead of one per micro-step
-                              "stage3_defer_reduce": True},
+                              "stage3_defer_reduce": True,
+                              # gathered weights stay valid until the optimizer step: gather once per step
+                              "stage3_retain_params_in_step": True},
         "optimizer": {"type": "AdamW", "params": {"lr": 3e-4, "betas": [0.9, 0.95], "eps": 1e-8,
                                                    "weight_decay": 0.1}},
         "steps_per_print": 1000000,

@@ -92,6 +92,8 @@ class ZeroConfig(ConfigModel):
     # MI355X (288 GB HBM): ZeRO-3 keeps each unit's fp32 gradient sum across the micro-steps of one
     # optimizer step and reduce-scatters once at the accumulation boundary
     defer_reduce: bool = Field(False, alias="stage3_defer_reduce")
+    # ... and keeps gathered parameters resident across those micro-steps (one all-gather per step)
+    retain_params: bool = Field(False, alias="stage3_retain_params_in_step")
 
     @model_validator(mode="after")
     def _compat(self):

@@ -108,7 +108,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                  unit_classes=None, shuffle_exchange_cfg=None, mp_group=None, timers=None, mics_shard_size=-1,
                  average_master=False, host_step=None, offload_param=False, quantized_weights=False,
                  quantized_gradients=False, hpz_partition_size=1, quant_group_size=128, grad_quant_bits=8,
-                 max_reuse_distance=1_000_000_000, max_live_parameters=1_000_000_000, defer_reduce=False):
+                 max_reuse_distance=1_000_000_000, max_live_parameters=1_000_000_000, defer_reduce=False,
+                 retain_params=False):
         acc = get_accelerator()
         device = torch.device(acc.current_device_name())
         self.module = module
@@ -175,6 +176,9 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         # deferred reduce-scatter (zero_optimization.stage3_defer_reduce): units keep an fp32
         # gradient sum across micro-steps (4 B/param of HBM) and reduce-scatter at the boundary
         self.defer_reduce = bool(defer_reduce) and self.S > 1 and not self.qgz
+        # retain gathered units across the micro-steps of one optimizer step (weights cannot change
+        # before the step): one all-gather per unit per step instead of one or two per micro-step
+        self.retain_params = bool(retain_params) and self.S > 1
         self._boundary = True
         if self.defer_reduce:
             for units in self.units:
@@ -187,7 +191,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         log_dist(f"ZeRO-3: {len(self.fgroups)} fetch groups / {n_units} units ({n_persist} persistent), "
                  f"partition={self.S}, slices={self.topo.num_slices}, prefetch_depth={self.prefetch_depth}, "
                  f"mics={self.mics}, shuffle_exchange={se.method if self.se is not None else 'off'}, "
-                 f"defer_reduce={self.defer_reduce}", ranks=[0])
+                 f"defer_reduce={self.defer_reduce}, retain_params={self.retain_params}", ranks=[0])
 
     # ------------------------------------------------------------------------------------- layout
     def _build(self, unit_classes):
@@ -487,6 +491,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
     def _release_unit(self, u):
         if u.persistent or u.state == RELEASED or getattr(self, "_hold", False):
             return
+        if getattr(self, "retain_params", False) and (not self._in_bwd or not self._boundary):
+            return  # still valid until the optimizer step: only the boundary backward releases
         if u.state == INFLIGHT and u.event is not None:
             torch.cuda.current_stream().wait_event(u.event)
         if self.hpz > 1 and not self._in_bwd and not u.sec_valid:

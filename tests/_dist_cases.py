@@ -268,16 +268,25 @@ def case_tied_zero3(rank, world, steps):
     return {"params": full_params(eng), "fgs": [fg.name for fg in eng.optimizer.fgroups]}
 
 
-def case_zero3_defer(rank, world, defer, steps, mbs, gas, seq):
+def case_zero3_defer(rank, world, defer, steps, mbs, gas, seq, retain=False):
     """ZeRO-3 with gradient accumulation, with/without the deferred (boundary-only) reduce-scatter;
     counts the reduce-scatters issued."""
     import shuffle_exchange_amd as sxe
     from shuffle_exchange_amd import comm as dist
     model, cfg = tiny_llama(0)
     ds = {"train_micro_batch_size_per_gpu": mbs, "gradient_accumulation_steps": gas,
-          "zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 0, "stage3_defer_reduce": defer},
+          "zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 0, "stage3_defer_reduce": defer,
+                                "stage3_retain_params_in_step": retain},
           "optimizer": {"type": "AdamW", "params": {"lr": 1e-2, "weight_decay": 0.01}}}
     eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    opt = eng.optimizer
+    n_ag = [0]
+    orig_gather = opt._launch_gather
+
+    def counting_gather(u):
+        n_ag[0] += 1
+        return orig_gather(u)
+    opt._launch_gather = counting_gather
     n_rs = [0]
     orig = dist.reduce_scatter_tensor
 
@@ -297,4 +306,6 @@ def case_zero3_defer(rank, world, defer, steps, mbs, gas, seq):
     finally:
         dist.reduce_scatter_tensor = orig
         s3.dist.reduce_scatter_tensor = s3_orig
-    return {"params": full_params(eng), "rs": n_rs[0], "defer": eng.optimizer.defer_reduce}
+    opt._launch_gather = orig_gather
+    return {"params": full_params(eng), "rs": n_rs[0], "ag": n_ag[0], "defer": eng.optimizer.defer_reduce,
+            "n_units": sum(len(us) for us in opt.units)}

@@ -1,4 +1,5 @@
-"""ZeRO-3 partitioned over 2 ranks that share ONE MI355X (gloo host collectives; RCCL needs one GPU
+"""ZeRO-3 partitioned over 2 ranks that share ONE MI355X (also with the deferred reduce-scatter and
+params retained across micro-steps, as bench.py runs it) (gloo host collectives; RCCL needs one GPU
 per rank): exercises the GPU side of stage 3 -- all-gather / reduce-scatter side streams, events,
 record_stream fencing, kept-for-backward units, TN weight-gradient path into bf16 staging -- and
 compares with the single-rank result on the same GPU."""
@@ -25,7 +26,8 @@ def _case(rank, world, reuse, stage=3, se=None, defer=False):
         model = LlamaForCausalLM(cfg)
     ds = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": 2, "bf16": {"enabled": True},
           "zero_optimization": {"stage": stage, "stage3_param_persistence_threshold": 0,
-                                "stage3_max_reuse_distance": reuse, "stage3_defer_reduce": defer},
+                                "stage3_max_reuse_distance": reuse, "stage3_defer_reduce": defer,
+                                "stage3_retain_params_in_step": defer},
           "optimizer": {"type": "SGD", "params": {"lr": 0.05}}}
     eng, _, _, _ = sxe.initialize(model=model, config=ds, **(se or {}))
     g = torch.Generator().manual_seed(7)

@@ -201,3 +201,15 @@ def test_zero3_deferred_reduce_scatter_matches_per_microstep():
     assert n[0]["rs"] == gas * d[0]["rs"], (n[0]["rs"], d[0]["rs"])
     for k, v in n[0]["params"].items():
         torch.testing.assert_close(d[0]["params"][k], v, atol=1e-4, rtol=1e-3)  # Adam amplifies sum order
+
+
+def test_zero3_retain_params_in_step_gathers_once_per_step():
+    """stage3_retain_params_in_step: gathered units stay resident across the micro-steps of one
+    optimizer step -> one all-gather per unit per step; same parameters."""
+    world, steps, mbs, gas, seq = 2, 2, 2, 3, 16
+    r = run_dist(C.case_zero3_defer, world, True, steps, mbs, gas, seq, True)
+    n = run_dist(C.case_zero3_defer, world, True, steps, mbs, gas, seq, False)
+    assert r[0]["ag"] <= steps * (r[0]["n_units"] + 1), (r[0]["ag"], r[0]["n_units"])
+    assert n[0]["ag"] >= 2 * r[0]["ag"], (n[0]["ag"], r[0]["ag"])  # 16 vs 6 per step at gas 3
+    for k, v in n[0]["params"].items():
+        torch.testing.assert_close(r[0]["params"][k], v, atol=1e-6, rtol=1e-5)
