@@ -78,7 +78,8 @@ def init_distributed(dist_backend=None, auto_mpi_discovery=True, distributed_por
     env.setdefault("LOCAL_RANK", "0")
     env.setdefault("MASTER_ADDR", "127.0.0.1")
     env.setdefault("MASTER_PORT", str(distributed_port))
-    backend = dist_backend or get_accelerator().communication_backend_name()
+    # SXE_DIST_BACKEND=gloo: multi-rank rehearsals on a single GPU (RCCL needs one GPU per rank)
+    backend = dist_backend or env.get("SXE_DIST_BACKEND") or get_accelerator().communication_backend_name()
     if timeout is None:
         timeout = datetime.timedelta(minutes=int(env.get("SXE_TIMEOUT_MIN", env.get("DEEPSPEED_TIMEOUT", "30"))))
     kw = {}
