@@ -173,6 +173,10 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         self._build(unit_classes)
         self._init_master()
         self._register()
+        for units in self.units:  # accumulators start zeroed: every slot counts as written
+            for u in units:
+                u.acc_valid = [True] * len(u.params)
+                u.rs_valid = True
         # deferred reduce-scatter (zero_optimization.stage3_defer_reduce): units keep an fp32
         # gradient sum across micro-steps (4 B/param of HBM) and reduce-scatter at the boundary
         self.defer_reduce = bool(defer_reduce) and self.S > 1 and not self.qgz
@@ -308,7 +312,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         i = u.param_index[id(p)]
         o, n = u.offsets[i], u.numels[i]
         if u.persistent and self.S == 1:
-            return u.grad[o:o + n].view(p.shape), True
+            return u.grad[o:o + n].view(p.shape), u.acc_valid[i]
         if u.staging is None:
             u.staging = torch.empty(u.padded, dtype=u.staging_dtype or u.dtype, device=u.device)
             if u.padded > u.numel:
@@ -320,6 +324,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         i = u.param_index[id(p)]
         if u.persistent and self.S == 1:
             u.filled[i] = True
+            u.acc_valid[i] = True
             return
         if not u.filled[i]:
             u.filled[i] = True
@@ -411,7 +416,11 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             if unit.persistent and self.S == 1:
                 i = unit.param_index[id(p)]
                 o, n = unit.offsets[i], unit.numels[i]
-                unit.grad[o:o + n].add_(p.grad.reshape(-1))
+                if unit.acc_valid[i]:
+                    unit.grad[o:o + n].add_(p.grad.reshape(-1))
+                else:
+                    unit.grad[o:o + n].copy_(p.grad.reshape(-1))
+                    unit.acc_valid[i] = True
                 if not unit.filled[i]:
                     unit.filled[i] = True
                     unit.pending -= 1
@@ -542,7 +551,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             want = self.comm_dtype or (u.dtype if self.defer_reduce else None)
             send = st if (want is None or st.dtype == want) else st.to(want)
             if self.S == 1:
-                u.grad.add_(send)
+                self._accumulate(u, send, 1.0)
             elif self.qgz and not self.mics:
                 self._quantized_reduce_scatter(u, st)
             else:
@@ -550,14 +559,46 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 dist.reduce_scatter_tensor(out, send, group=self.topo.slice_group)
                 if self.mics:
                     dist.all_reduce(out, group=self._mics_replica)
-                    u.grad.add_(out, alpha=self.sp_scale / (self.S * self.topo.num_slices))
+                    self._accumulate(u, out, self.sp_scale / (self.S * self.topo.num_slices))
                 else:
-                    u.grad.add_(out, alpha=self.sp_scale / self.S)
+                    self._accumulate(u, out, self.sp_scale / self.S)
                 if rs is not None:
                     out.record_stream(rs)
             if rs is not None:
                 st.record_stream(rs)
                 send.record_stream(rs)
+
+    def _accumulate(self, u, x, alpha):
+        """u.grad += alpha * x, or = alpha * x for the first reduction of the step (no memset of
+        the fp32 accumulators between steps, see zero_grad_buffers)."""
+        if u.rs_valid:
+            u.grad.add_(x, alpha=alpha)
+        else:
+            torch.mul(x, alpha, out=u.grad) if x.dtype == u.grad.dtype else u.grad.copy_(x).mul_(alpha)
+            u.rs_valid = True
+
+    def zero_grad_buffers(self):
+        """Mark the fp32 gradient accumulators stale instead of zeroing them (a 32 GB memset per
+        step on an 8B model at dp=1): each slot's first write of the next step overwrites (GEMMs
+        with beta = 0, copy_ in the hooks, assignment after the reduce-scatter) and slots no
+        gradient reached are zeroed right before the step (_zero_stale)."""
+        for units in self.units:
+            for u in units:
+                u.acc_valid = [False] * len(u.params)
+                u.rs_valid = False
+
+    def _zero_stale(self):
+        for units in self.units:
+            for u in units:
+                if u.persistent and self.S == 1:
+                    for i, ok in enumerate(u.acc_valid):
+                        if not ok:
+                            o, n = u.offsets[i], u.numels[i]
+                            u.grad[o:o + n].zero_()
+                    u.acc_valid = [True] * len(u.params)
+                elif not u.rs_valid:
+                    u.grad.zero_()
+                    u.rs_valid = True
 
     def _quantized_reduce_scatter(self, u, staging):
         """qgZ: quantize the full gradient unit per destination chunk, all-to-all the packed
@@ -568,7 +609,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         rq, rs = torch.empty_like(q), torch.empty_like(sc)
         dist.all_to_all_single(rq, q, group=self.topo.slice_group)
         dist.all_to_all_single(rs, sc, group=self.topo.slice_group)
-        dequant_reduce(rq, rs, self.S, qg, self.gbits, u.grad, alpha=self.sp_scale / self.S, accumulate=True)
+        dequant_reduce(rq, rs, self.S, qg, self.gbits, u.grad, alpha=self.sp_scale / self.S, accumulate=u.rs_valid)
+        u.rs_valid = True
         if self.rs_stream is not None:
             for t in (q, sc, rq, rs):
                 t.record_stream(self.rs_stream)
@@ -617,6 +659,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             torch.cuda.current_stream().wait_stream(self.rs_stream)
         if self.se is not None and self.se.method == "Gossip":
             self.se.pre_step([u.shard for units in self.units for u in units])
+        self._zero_stale()
         coef, skip = self._grad_norm_and_flags()
         if getattr(self.loss_scaler, "dynamic", False) and self._handle_overflow_host():
             self.zero_grad_buffers()

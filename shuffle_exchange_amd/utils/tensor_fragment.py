@@ -26,6 +26,8 @@ def _loc(param):
 def _fragment(param, which, key=None):
     """(fragment tensor of this rank's chunk, (param_lo, param_hi)) or (None, None)."""
     opt, g, u, i = _loc(param)
+    if which == "grad" and hasattr(opt, "_zero_stale"):
+        opt._zero_stale()  # ZeRO-3 zeroes accumulator slots lazily: settle them before reading
     rng = u.param_range_in_shard(i)
     if rng is None:
         return None, None
