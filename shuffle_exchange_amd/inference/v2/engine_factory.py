@@ -13,8 +13,9 @@ from .model_implementations.hf_decoder import load_hf_decoder
 
 
 def build_hf_engine(path_or_model, engine_config: RaggedInferenceEngineConfig = None, dtype=torch.bfloat16,
-                    device=None, debug_level=None):
+                    device=None, debug_level=None, weight_quant=None):
+    """``weight_quant='fp8'``: row-scaled e4m3 projection / LM-head weights (ops/fp_quantizer.FP8Weight)."""
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
-    model = load_hf_decoder(path_or_model, dtype=dtype, device=device)
+    model = load_hf_decoder(path_or_model, dtype=dtype, device=device, weight_quant=weight_quant)
     return InferenceEngineV2(model, engine_config)

@@ -61,13 +61,14 @@ class RaggedInferenceEngineConfig:
     num_kv_blocks: Optional[int] = None
     tensor_parallel: dict = field(default_factory=lambda: {"tp_size": 1})
     decode_graphs: bool = True  # replay pure-decode steps from captured HIP graphs (decode_graphs.py)
+    weight_quant: Optional[str] = None  # "fp8": row-scaled e4m3 projection / LM-head weights (W8A16 decode GEMMs)
 
 
 class InferenceEngineV2:
     def __init__(self, model, config: RaggedInferenceEngineConfig = None):
         from .model_implementations import ragged_model_for
         self._config = config or RaggedInferenceEngineConfig()
-        self._model = ragged_model_for(model)
+        self._model = ragged_model_for(model, weight_quant=self._config.weight_quant)
         sm = self._config.state_manager
         dev = self._model.device
         bs = self._config.kv_block_size

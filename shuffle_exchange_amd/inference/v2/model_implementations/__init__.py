@@ -10,15 +10,16 @@ from .hf_decoder import RaggedDecoder, load_hf_decoder, spec_from_hf_config  # n
 from .llama import RaggedLlama  # noqa: F401
 
 
-def ragged_model_for(model):
-    """Pick the ragged implementation for a model object."""
+def ragged_model_for(model, weight_quant=None):
+    """Pick the ragged implementation for a model object (``weight_quant='fp8'``: row-scaled e4m3
+    projection / LM-head weights for the decode GEMMs)."""
     if isinstance(model, (RaggedDecoder, RaggedLlama)):
         return model
     if hasattr(model, "config") and hasattr(model.config, "model_type") and hasattr(model.config, "to_dict"):
         p = next(model.parameters())
         dtype = p.dtype if p.dtype in (__import__("torch").bfloat16, __import__("torch").float16,
                                        __import__("torch").float32) else None
-        return load_hf_decoder(model, dtype=dtype, device=p.device)
+        return load_hf_decoder(model, dtype=dtype, device=p.device, weight_quant=weight_quant)
     if hasattr(model, "layers") and hasattr(model.layers[0], "self_attn") and hasattr(model, "embed_tokens"):
-        return RaggedLlama(model)
+        return RaggedLlama(model, weight_quant=weight_quant)
     raise NotImplementedError(f"no ragged inference implementation for {type(model).__name__}")

@@ -405,7 +405,9 @@ class RaggedDecoder:
     """Engine-facing model (InferenceEngineV2 protocol: num_layers / nkv / head_dim / dtype /
     device / vocab_size / forward(batch, kv_cache) -> last-token fp32 logits)."""
 
-    def __init__(self, spec: DecoderSpec, weights, dtype=torch.bfloat16, device=None):
+    QUANT_KEYS = ("qkv_w", "o_w", "gu_w", "down_w", "fc1_w", "fc2_w", "sh_gu", "sh_down")
+
+    def __init__(self, spec: DecoderSpec, weights, dtype=torch.bfloat16, device=None, weight_quant=None):
         self.spec = spec
         device = torch.device(device) if device is not None else torch.device("cpu")
 
@@ -413,6 +415,17 @@ class RaggedDecoder:
             return t.to(device=device, dtype=dtype).contiguous() if torch.is_tensor(t) else t
         self.w = {k: mv(v) for k, v in weights.items() if k != "layers"}
         self.w["layers"] = [{k: mv(v) for k, v in L.items()} for L in weights["layers"]]
+        if weight_quant:
+            # weight-only FP8 (row-scaled e4m3) projections and LM head: decode GEMMs stream half
+            # the bytes through the skinny MFMA kernel (reference: FP6-LLM QuantizedWf6Af16Linear)
+            assert weight_quant == "fp8", "weight_quant: 'fp8'"
+            from ....ops.fp_quantizer import FP8Weight
+            for L in self.w["layers"]:
+                for k in self.QUANT_KEYS:
+                    if torch.is_tensor(L.get(k)) and L[k].dim() == 2:
+                        L[k] = FP8Weight(L[k])
+            self.w["lm_head"] = FP8Weight(self.w["lm_head"])
+        self.weight_quant = weight_quant
         self.num_layers, self.nq, self.nkv, self.head_dim = spec.n_layers, spec.nq, spec.nkv, spec.head_dim
         self.vocab_size = spec.vocab_size
         self._dtype, self._device = dtype, device
@@ -489,7 +502,7 @@ class RaggedDecoder:
         return linear(h, W["lm_head"], W.get("lm_head_b")).float()
 
 
-def load_hf_decoder(model_or_path, dtype=torch.bfloat16, device=None):
+def load_hf_decoder(model_or_path, dtype=torch.bfloat16, device=None, weight_quant=None):
     """A transformers model instance or a local checkpoint directory (config.json + safetensors /
     pytorch_model*.bin, loaded without executing pickled code) -> RaggedDecoder."""
     if isinstance(model_or_path, (str, os.PathLike)):
@@ -500,4 +513,4 @@ def load_hf_decoder(model_or_path, dtype=torch.bfloat16, device=None):
         cfg = model_or_path.config.to_dict()
         sd = {k: v.detach() for k, v in model_or_path.state_dict().items()}
     spec = spec_from_hf_config(cfg)
-    return RaggedDecoder(spec, convert_hf_weights(spec, sd, cfg), dtype=dtype, device=device)
+    return RaggedDecoder(spec, convert_hf_weights(spec, sd, cfg), dtype=dtype, device=device, weight_quant=weight_quant)

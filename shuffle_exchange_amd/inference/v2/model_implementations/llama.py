@@ -27,8 +27,20 @@ FLASH_PREFILL_MIN = 128
 
 
 class RaggedLlama:
-    def __init__(self, model):
+    def __init__(self, model, weight_quant=None):
         self.model = model
+        self.qw = None
+        if weight_quant:
+            assert weight_quant == "fp8", "weight_quant: 'fp8'"
+            from ....ops.fp_quantizer import FP8Weight
+            self.qw = []
+            for layer in model.layers:
+                d = {"qkv": FP8Weight(layer.self_attn.qkv_proj.weight), "o": FP8Weight(layer.self_attn.o_proj.weight)}
+                if hasattr(layer, "mlp"):
+                    d["gu"] = FP8Weight(layer.mlp.gate_up_proj.weight)
+                    d["down"] = FP8Weight(layer.mlp.down_proj.weight)
+                self.qw.append(d)
+            self.qhead = FP8Weight(model.lm_head.weight)
         self.cfg = model.cfg
         self.is_moe = hasattr(model.layers[0], "block_sparse_moe") or hasattr(model.layers[0], "moe")
         a0 = model.layers[0].self_attn
@@ -80,10 +92,15 @@ class RaggedLlama:
                 out[s:s + n] = o[s:s + n]
         return out
 
-    def _mlp(self, layer, m):
+    def _proj(self, mod, x, li, key):
+        if self.qw is not None and key in self.qw[li]:
+            return linear(x, self.qw[li][key], mod.bias)
+        return mod(x)
+
+    def _mlp(self, layer, m, li=0):
         if hasattr(layer, "mlp"):
             mlp = layer.mlp
-            return mlp.down_proj(swiglu(mlp.gate_up_proj(m)))
+            return self._proj(mlp.down_proj, swiglu(self._proj(mlp.gate_up_proj, m, li, "gu")), li, "down")
         moe = layer.block_sparse_moe if hasattr(layer, "block_sparse_moe") else layer.moe
         return self._moe_dropless(moe.deepspeed_moe, m)
 
@@ -127,14 +144,14 @@ class RaggedLlama:
             else:
                 a, h = layer.input_layernorm(x, res)
             attn = layer.self_attn
-            qkv = attn.qkv_proj(a).view(T, self.nq + 2 * self.nkv, self.head_dim)
+            qkv = self._proj(attn.qkv_proj, a, li, "qkv").view(T, self.nq + 2 * self.nkv, self.head_dim)
             apply_rope_tokens_(qkv, rope, self.nq + self.nkv, batch.positions)
             kv_layer = kv_cache.layer(li)
             kv_cache_append(qkv, kv_layer, batch.slots, self.nq, self.nkv)
             o = self._attention(qkv, kv_layer, batch)
-            o = attn.o_proj(o.reshape(T, self.nq * self.head_dim))
+            o = self._proj(attn.o_proj, o.reshape(T, self.nq * self.head_dim), li, "o")
             m, h2 = layer.post_attention_layernorm(o, h)
-            x, res = self._mlp(layer, m), h2
+            x, res = self._mlp(layer, m, li), h2
         last = batch.last_idx
         h = model.norm(x.index_select(0, last), res.index_select(0, last))[0]
-        return linear(h, model.lm_head.weight).float()
+        return linear(h, self.qhead if self.qw is not None else model.lm_head.weight).float()

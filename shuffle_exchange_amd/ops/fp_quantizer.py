@@ -156,6 +156,32 @@ def matmul_fp8(inp, weight, scale, quantization_group_size):
     return torch.matmul(inp, wd.view(weight.shape))
 
 
+class FP8Weight:
+    """Row-scaled FP8 (e4m3) weight of a linear layer, [N, K] -> used through ``ops.linear.linear``:
+    decode-sized inputs (<= 16 rows) stream the FP8 bytes through the skinny MFMA kernel
+    (skinny_gemm.hip, W8A16: weights converted to bf16 in registers, half the HBM bytes of bf16);
+    larger inputs run ``fp8_linear`` on the FP8 matrix cores (activations quantized per row)."""
+
+    def __init__(self, w):
+        self.q, self.scale = quantize_weight_fp8_rowwise(w.detach())
+        self.shape = tuple(w.shape)
+        self.dtype = w.dtype
+
+    def linear(self, x, bias=None):
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        if (x2.is_cuda and x2.dtype == torch.bfloat16 and 0 < x2.shape[0] <= 16 and K % 16 == 0
+                and x2.stride(-1) == 1 and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0):
+            native.require_hip()
+            b = bias.to(torch.bfloat16).contiguous() if bias is not None else None
+            y = torch.ops.sxe.skinny_gemm_fp8w(x2, self.q.view(torch.uint8), self.scale, b)
+            return y.view(*x.shape[:-1], self.q.shape[0])
+        return fp8_linear(x, self.q, self.scale, bias, out_dtype=x.dtype)
+
+    def dequantize(self):
+        return (self.q.float() * self.scale.view(-1, 1)).to(self.dtype)
+
+
 class FP8Linear(torch.nn.Module):
     """Inference linear with an FP8 (row-scaled) weight; the GEMM runs on the FP8 matrix cores."""
 

@@ -121,6 +121,8 @@ class _Linear(torch.autograd.Function):
 
 
 def linear(x, weight, bias=None):
+    if not isinstance(weight, torch.Tensor):  # quantized inference weight (ops/fp_quantizer.FP8Weight)
+        return weight.linear(x, bias)
     grad = torch.is_grad_enabled() and (weight.requires_grad or x.requires_grad)
     if grad and weight.requires_grad and hasattr(weight, "_sxe_grad_target"):
         return _Linear.apply(x, weight, bias)

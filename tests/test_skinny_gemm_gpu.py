@@ -38,3 +38,38 @@ def test_linear_dispatches_skinny_under_no_grad():
     xg = x.clone().requires_grad_()
     linear(xg, w).sum().backward()  # autograd path still works (F.linear)
     assert xg.grad is not None
+
+
+@pytest.mark.parametrize("M", [1, 4, 16])
+@pytest.mark.parametrize("N,K", [(16, 64), (100, 576), (4104, 4096), (1000, 14336)])
+def test_skinny_gemm_fp8_weights_matches_fp32(M, N, K):
+    from shuffle_exchange_amd.ops.fp_quantizer import quantize_weight_fp8_rowwise
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    b = torch.randn(N, device="cuda", dtype=torch.bfloat16, generator=g)
+    q, s = quantize_weight_fp8_rowwise(w)
+    y = torch.ops.sxe.skinny_gemm_fp8w(x, q.view(torch.uint8), s, b)
+    ref = x.float() @ (q.float() * s[:, None]).t() + b.float()  # exact dequantized weights
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item() + 1e-2, err
+
+
+def test_hf_engine_fp8_weights_close_to_bf16():
+    transformers = pytest.importorskip("transformers")
+    from shuffle_exchange_amd.inference.v2.engine_factory import build_hf_engine
+    from shuffle_exchange_amd.inference.v2.engine_v2 import RaggedInferenceEngineConfig
+    torch.manual_seed(0)
+    T = transformers
+    model = T.LlamaForCausalLM(T.LlamaConfig(hidden_size=512, intermediate_size=1024, num_attention_heads=4,
+                                             num_key_value_heads=2, vocab_size=512, num_hidden_layers=2)).eval()
+    cfg = RaggedInferenceEngineConfig(kv_block_size=64, num_kv_blocks=32)
+    e16 = build_hf_engine(model, cfg, device="cuda")
+    e8 = build_hf_engine(model, RaggedInferenceEngineConfig(kv_block_size=64, num_kv_blocks=32), device="cuda",
+                         weight_quant="fp8")
+    p = torch.randint(0, 512, (40,)).tolist()
+    a, b = e16.put([0], [p]), e8.put([0], [p])
+    for t in (5, 9, 11):
+        a, b = e16.put([0], [[t]]), e8.put([0], [[t]])  # decode steps: skinny FP8-weight kernel
+        cos = torch.nn.functional.cosine_similarity(a.float(), b.float()).item()
+        assert cos > 0.99, cos

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--ctx", type=int, default=1024)
     ap.add_argument("--batches", default="1,8,32,64")
     ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--modes", default="eager,graphs,graphs+fp8",
+                    help="comma list of eager | graphs | graphs+fp8 (FP8 row-scaled weights, W8A16)")
     a = ap.parse_args()
     from shuffle_exchange_amd.inference.v2 import RaggedInferenceEngineConfig, build_engine
     from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
@@ -31,9 +33,11 @@ def main():
     torch.set_default_dtype(torch.float32)
     nparam = sum(p.numel() for p in model.parameters())
     rows = []
-    for graphs in (False, True):
+    for mode in a.modes.split(","):
+        graphs = mode.startswith("graphs")
         eng = build_engine(model, RaggedInferenceEngineConfig(kv_block_size=64, num_kv_blocks=4096,
-                                                              decode_graphs=graphs))
+                                                              decode_graphs=graphs,
+                                                              weight_quant="fp8" if "fp8" in mode else None))
         for B in [int(x) for x in a.batches.split(",")]:
             uids = list(range(B))
             g = torch.Generator().manual_seed(B)
@@ -50,7 +54,7 @@ def main():
             ms = (time.perf_counter() - t0) / a.steps * 1e3
             hbm_gb = (nparam * 2 + B * (a.ctx + a.steps) * cfg.num_hidden_layers * 2 * cfg.num_key_value_heads *
                       (cfg.hidden_size // cfg.num_attention_heads) * 2) / 1e9
-            rows.append({"graphs": graphs, "batch": B, "ctx": a.ctx, "ms_per_step": round(ms, 3),
+            rows.append({"mode": mode, "batch": B, "ctx": a.ctx, "ms_per_step": round(ms, 3),
                          "tokens_per_s": round(B / ms * 1e3, 1), "hbm_GB_per_step": round(hbm_gb, 2),
                          "eff_TB_per_s": round(hbm_gb / ms, 2)})
             print(json.dumps(rows[-1]), flush=True)

@@ -48,11 +48,19 @@ def main():
             def bl():
                 i[0] = (i[0] + 1) % 4
                 F.linear(x, ws[i[0]])
-            t_sk, t_bl = timeit(sk), timeit(bl)
+            from shuffle_exchange_amd.ops.fp_quantizer import quantize_weight_fp8_rowwise
+            qs = [quantize_weight_fp8_rowwise(wi) for wi in ws]
+
+            def f8():
+                i[0] = (i[0] + 1) % 4
+                torch.ops.sxe.skinny_gemm_fp8w(x, qs[i[0]][0].view(torch.uint8), qs[i[0]][1], None)
+            t_sk, t_bl, t_f8 = timeit(sk), timeit(bl), timeit(f8)
             gb = N * K * 2 / 1e9
             print(json.dumps({"shape": name, "N": N, "K": K, "M": M, "skinny_us": round(t_sk, 2),
-                              "hipblaslt_us": round(t_bl, 2), "skinny_TBps": round(gb / t_sk * 1e3, 2),
-                              "hipblaslt_TBps": round(gb / t_bl * 1e3, 2)}), flush=True)
+                              "hipblaslt_us": round(t_bl, 2), "skinny_fp8w_us": round(t_f8, 2),
+                              "skinny_TBps": round(gb / t_sk * 1e3, 2), "hipblaslt_TBps": round(gb / t_bl * 1e3, 2),
+                              "fp8w_weight_TBps": round(gb / 2 / t_f8 * 1e3, 2)}), flush=True)
+            del qs
         del ws
 
 
