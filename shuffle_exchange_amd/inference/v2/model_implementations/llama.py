@@ -93,7 +93,9 @@ class RaggedLlama:
         return out
 
     def _proj(self, mod, x, li, key):
-        if self.qw is not None and key in self.qw[li]:
+        # FP8 weights pay off where the GEMM is weight-streaming bound (<= 16 rows: W8A16 skinny
+        # kernel); larger batches keep the module's bf16 weight on hipBLASLt
+        if self.qw is not None and key in self.qw[li] and x.shape[0] <= 16:
             return linear(x, self.qw[li][key], mod.bias)
         return mod(x)
 
@@ -154,4 +156,5 @@ class RaggedLlama:
             x, res = self._mlp(layer, m, li), h2
         last = batch.last_idx
         h = model.norm(x.index_select(0, last), res.index_select(0, last))[0]
-        return linear(h, self.qhead if self.qw is not None else model.lm_head.weight).float()
+        use_q = self.qw is not None and h.shape[0] <= 16
+        return linear(h, self.qhead if use_q else model.lm_head.weight).float()
