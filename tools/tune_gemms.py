@@ -2,8 +2,8 @@
 solution search only, bounded per solution) and report tuned-vs-default TFLOP/s per shape.
 
 Standalone (no model): every shape is issued exactly like ops/linear.py issues it -- forward
-``x @ W.T``, input grad ``gy @ W``, weight grad ``gy.T @ x`` (bf16 out, and the fp32-accumulating
-``addmm.dtype_out`` the ZeRO buffers use). Writes the TunableOp CSV that
+``x @ W.T``, input grad on a transposed weight ``gy @ (W^T)^T`` (data_grad), weight grad as
+transposes + forward-layout GEMM (TN path) or the fp32-accumulating ``addmm.dtype_out``. Writes the TunableOp CSV that
 runtime/gemm_tuning.py loads (SXE_TUNABLEOP_FILE or the packaged tuning/ file).
 
 usage: python tools/tune_gemms.py OUT.csv [tokens] [--max-ms 8] [--iters 10]
@@ -55,6 +55,11 @@ def timeit(fn, n=10):
 
 
 cases = []
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from shuffle_exchange_amd.ops import native  # noqa: E402
+from shuffle_exchange_amd.ops.linear import DGRAD_WT_MIN_ELEMS, TN_MIN_ELEMS  # noqa: E402
+native.require_hip()
+tr = torch.ops.sxe.transpose16
 for name, (N, K) in layers.items():
     x = torch.randn(T, K, device=dev, dtype=torch.bfloat16)
     w = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
@@ -62,11 +67,18 @@ for name, (N, K) in layers.items():
     acc = torch.zeros(N, K, device=dev, dtype=torch.float32)
     fl = 2.0 * T * N * K
     cases.append((f"{name} fwd", fl, lambda x=x, w=w: x @ w.t()))
-    cases.append((f"{name} dgrad", fl, lambda gy=gy, w=w: gy @ w))
-    cases.append((f"{name} wgrad-bf16", fl, lambda gy=gy, x=x: gy.t() @ x))
-    cases.append((f"{name} wgrad-fp32acc", fl,
-                  lambda gy=gy, x=x, acc=acc: torch.ops.aten.addmm.dtype_out(acc, gy.t(), x, torch.float32, beta=1,
-                                                                              alpha=1, out=acc)))
+    if N * K >= DGRAD_WT_MIN_ELEMS:  # ops/linear.data_grad: forward-layout GEMM on a transposed weight
+        wt = tr(w)
+        cases.append((f"{name} dgrad-wT", fl, lambda gy=gy, wt=wt: gy @ wt.t()))
+    else:
+        cases.append((f"{name} dgrad", fl, lambda gy=gy, w=w: gy @ w))
+    if N * K >= TN_MIN_ELEMS:  # ops/linear.write_weight_grad TN path: transposes + forward-layout GEMM
+        gyt, xt = tr(gy), tr(x)
+        cases.append((f"{name} wgrad-TN", fl, lambda gyt=gyt, xt=xt: gyt @ xt.t()))
+    else:
+        cases.append((f"{name} wgrad-fp32acc", fl,
+                      lambda gy=gy, x=x, acc=acc: torch.ops.aten.addmm.dtype_out(acc, gy.t(), x, torch.float32,
+                                                                                  beta=1, alpha=1, out=acc)))
 
 base = {}
 for nm, fl, fn in cases:
