@@ -69,6 +69,16 @@ def dequant_reduce(q, scales, W, group_size, bits, out, alpha=1.0, accumulate=Fa
     return out
 
 
+def loco_quantize(x, err, err_beta, group_size=128, bits=8):
+    """LoCo error-feedback quantization (reference runtime/comm/coalesced_collectives.py
+    ``all_to_all_loco_quant_reduce`` / ``loco_swizzle_quant``): quantize x + err_beta * err and
+    return (q, scales, new_err) with new_err = compensated - dequant(q) (fp32)."""
+    comp = x.float().reshape(-1) if err is None else x.float().reshape(-1).add(err.float().reshape(-1), alpha=err_beta)
+    q, sc = quantize(comp, group_size, bits)
+    deq = dequantize(q, sc, group_size, bits, numel=comp.numel(), dtype=torch.float32)
+    return q, sc, comp - deq
+
+
 def quantize_fp8(x, group_size=128):
     x = x.contiguous().reshape(-1)
     if native.use_hip(x):

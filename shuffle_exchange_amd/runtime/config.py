@@ -80,6 +80,7 @@ class ZeroConfig(ConfigModel):
     zero_quantized_weights: bool = False
     zero_quantized_nontrainable_weights: bool = False
     zero_quantized_gradients: bool = False
+    zeropp_loco_param: Optional[Dict[str, Any]] = None  # {"err_beta": 0.8, "reset_T": 1024}: LoCo error feedback
     mics_shard_size: int = -1
     mics_hierarchical_params_gather: bool = False
     memory_efficient_linear: bool = True

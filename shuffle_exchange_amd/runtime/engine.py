@@ -358,7 +358,7 @@ class SXEEngine(nn.Module):
                 host_step=host_step, offload_param=offload_param, quantized_weights=zc.zero_quantized_weights,
                 quantized_gradients=zc.zero_quantized_gradients, hpz_partition_size=zc.zero_hpz_partition_size,
                 max_reuse_distance=zc.max_reuse_distance, max_live_parameters=zc.max_live_parameters,
-                defer_reduce=zc.defer_reduce, retain_params=zc.retain_params)
+                defer_reduce=zc.defer_reduce, retain_params=zc.retain_params, loco_param=zc.zeropp_loco_param)
         elif stage in (1, 2):
             self.optimizer = ZeroStage12Optimizer(
                 basic, stage=stage, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks,

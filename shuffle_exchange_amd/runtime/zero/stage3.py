@@ -109,7 +109,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                  average_master=False, host_step=None, offload_param=False, quantized_weights=False,
                  quantized_gradients=False, hpz_partition_size=1, quant_group_size=128, grad_quant_bits=8,
                  max_reuse_distance=1_000_000_000, max_live_parameters=1_000_000_000, defer_reduce=False,
-                 retain_params=False):
+                 retain_params=False, loco_param=None):
         acc = get_accelerator()
         device = torch.device(acc.current_device_name())
         self.module = module
@@ -142,6 +142,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         # ZeRO++ knobs
         self.qwz = bool(quantized_weights) and self.S > 1
         self.qgz = bool(quantized_gradients) and self.S > 1
+        self.loco = dict(loco_param) if (loco_param and self.qgz) else None  # zeropp_loco_param
+        self._loco_idx = 0
         self.qgroup = int(quant_group_size)
         self.gbits = int(grad_quant_bits)
         self.hpz = int(hpz_partition_size or 1)
@@ -605,7 +607,20 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         chunks, dequantize + reduce the W received chunks straight into this rank's accumulator."""
         from ...ops.quantizer import dequant_reduce, quantize
         qg = self._qgroup(u)
-        q, sc = quantize(staging, qg, self.gbits)
+        if self.loco is not None:
+            # LoCo error feedback (reference coalesced_collectives.all_to_all_loco_quant_reduce):
+            # quantize grad + err_beta * (previous quantization error) and keep the new error,
+            # reset every reset_T reductions; the error buffer is stored in the gradient dtype
+            from ...ops.quantizer import loco_quantize
+            beta, reset_t = float(self.loco.get("err_beta", 0.8)), int(self.loco.get("reset_T", 1024))
+            err = getattr(u, "loco_err", None)
+            if self._loco_idx > reset_t:
+                err, self._loco_idx = None, 0
+            q, sc, new_err = loco_quantize(staging, err, beta, qg, self.gbits)
+            u.loco_err = new_err.to(staging.dtype)
+            self._loco_idx += 1
+        else:
+            q, sc = quantize(staging, qg, self.gbits)
         rq, rs = torch.empty_like(q), torch.empty_like(sc)
         dist.all_to_all_single(rq, q, group=self.topo.slice_group)
         dist.all_to_all_single(rs, sc, group=self.topo.slice_group)

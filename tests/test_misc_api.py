@@ -114,3 +114,22 @@ def test_nhwc_bias_add_variants():
     torch.testing.assert_close(nhwc_bias_add(x, b, o, ob), x + bb + o + ob.view(1, 8, 1, 1))
     y = torch.randn(2, 4, 4, 8)  # plain NHWC tensor
     torch.testing.assert_close(nhwc_bias_add(y, b), y + b)
+
+
+def test_loco_error_feedback_bounds_accumulated_quantization_error():
+    """LoCo (ops/quantizer.loco_quantize): with error feedback (beta = 1) the sum of the dequantized
+    gradients over many steps stays within one quantization step of the true sum, while plain
+    quantization accumulates its bias linearly."""
+    from shuffle_exchange_amd.ops.quantizer import dequantize, loco_quantize, quantize
+    torch.manual_seed(0)
+    g = torch.randn(1024) * 1e-3 + 0.37e-3  # constant gradient, biased w.r.t. the int4 grid
+    steps, tot_plain, tot_loco, err = 50, torch.zeros(1024), torch.zeros(1024), None
+    for _ in range(steps):
+        q, s = quantize(g, 128, 4)
+        tot_plain += dequantize(q, s, 128, 4, numel=1024, dtype=torch.float32)
+        q, s, err = loco_quantize(g, err, 1.0, 128, 4)
+        tot_loco += dequantize(q, s, 128, 4, numel=1024, dtype=torch.float32)
+    true = g * steps
+    e_plain = (tot_plain - true).abs().max().item()
+    e_loco = (tot_loco - true).abs().max().item()
+    assert e_loco < 0.2 * e_plain, (e_loco, e_plain)

@@ -115,9 +115,12 @@ def test_collectives_and_fingerprint():
 
 @pytest.mark.parametrize("knobs,tol", [({"zero_quantized_weights": True}, 5e-2),
                                        ({"zero_quantized_gradients": True}, 5e-2),
+                                       ({"zero_quantized_gradients": True,
+                                         "zeropp_loco_param": {"err_beta": 0.8, "reset_T": 2}}, 5e-2),
                                        ({"zero_hpz_partition_size": 2}, 1e-5)])
 def test_zeropp_matches_zero3(knobs, tol):
-    """ZeRO++ qwZ / qgZ (int8) track plain ZeRO-3 closely; hpZ (secondary intra-group shards) is exact."""
+    """ZeRO++ qwZ / qgZ (int8, with and without LoCo error feedback) track plain ZeRO-3 closely; hpZ
+    (secondary intra-group shards) is exact."""
     world, mbs, seq, steps = 4, 1, 16, 3
     base = {"stage": 3, "stage3_param_persistence_threshold": 0}
     SGD = {"type": "SGD", "params": {"lr": 0.05}}
