@@ -347,6 +347,10 @@ class SXEEngine(nn.Module):
             assert stage > 0, "optimizer offload needs ZeRO stage 1, 2 or 3"
             from .zero.offload import HostOptimizerStep
             host_step = HostOptimizerStep(off, aio_config=cfg.model.aio, rank=dist.get_rank())
+            from .zero.base import _kind
+            if host_step.ratio < 1.0 and _kind(basic)[0] != "generic":
+                from .zero.offload import split_param_groups
+                split_param_groups(basic, host_step.ratio)  # Twin-Flow: part of every group stays in HBM
         offload_param = bool(zc.offload_param is not None and zc.offload_param.device in ("cpu", "nvme"))
         if stage == 3:
             self.optimizer = ZeroStage3Optimizer(

@@ -66,9 +66,12 @@ class ZeroOptimizerBase:
             for u in units:
                 for i, p in enumerate(u.params):
                     p._sxe_zero = (self, g, u, i)
-        if self.host_step is not None:
-            return self.host_step.init_master(self)
+        G = len(self.units)
+        self.master, self.grads = [None] * G, [None] * G
+        host = self.host_step.host_groups(self) if self.host_step is not None else set()
         for g, units in enumerate(self.units):
+            if g in host:
+                continue  # masters / state on the host tier (offload.py)
             total = sum(u.chunk for u in units)
             m = torch.empty(total, dtype=torch.float32, device=self.device)
             gr = torch.zeros(total, dtype=torch.float32, device=self.device)
@@ -79,9 +82,11 @@ class ZeroOptimizerBase:
                 u.master.copy_(u.shard.float())
                 off += u.chunk
             m = torch.nn.Parameter(m, requires_grad=False)
-            self.master.append(m)
-            self.grads.append(gr)
+            self.master[g] = m
+            self.grads[g] = gr
             self.optimizer.param_groups[g]["params"] = [m]
+        if self.host_step is not None:
+            return self.host_step.init_master(self)  # also initialises the state of every group
         self.optimizer.state.clear()
         self._init_state()
 
@@ -130,9 +135,15 @@ class ZeroOptimizerBase:
 
     def _fused_update(self, coef, skip):
         """One optimizer step over every unit chunk; writes the bit16 chunks in the same pass."""
+        host = set()
         if self.host_step is not None:
-            return self.host_step.update(self, coef, skip)
+            self.host_step.update(self, coef, skip)
+            host = self.host_step.groups
+            if len(host) == len(self.units):
+                return
         for g, units in enumerate(self.units):
+            if g in host:
+                continue  # Twin-Flow: this group was stepped on the host
             pg = self.optimizer.param_groups[g]
             m = self.master[g]
             st = self.optimizer.state[m]
@@ -266,13 +277,17 @@ class ZeroOptimizerBase:
         def back(t):
             return t.to(dev, non_blocking=non_blocking) if torch.is_tensor(t) and t.device != dev else t
 
-        if "hp_params" in inc and self.host_step is None:
-            for m in self.master:
-                m.data = back(m.data)
+        host = self.host_step.groups if self.host_step is not None else set()
+        if "hp_params" in inc:
+            for g, m in enumerate(self.master):
+                if g not in host:
+                    m.data = back(m.data)
         if "lp_grads" in inc:
             self.grads = [back(g) for g in self.grads]
-        if "optim_states" in inc and self.host_step is None:
-            for m in self.master:
+        if "optim_states" in inc:
+            for g, m in enumerate(self.master):
+                if g in host:
+                    continue
                 st = self.optimizer.state[m]
                 for k, v in list(st.items()):
                     if torch.is_tensor(v) and v.numel() > 1:

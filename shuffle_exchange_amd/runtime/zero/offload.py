@@ -115,9 +115,14 @@ class HostOptimizerStep:
         self.pin = bool(offload_config.pin_memory) or self.device == "nvme"
         self.nvme_path = offload_config.nvme_path
         self.buffer_count = max(3, int(offload_config.buffer_count))
+        # Twin-Flow partial offload: the first `ratio` of every param group's elements lives on the
+        # host, the rest keeps its masters / state / update in HBM (split_param_groups below)
         self.ratio = float(offload_config.ratio)
-        if self.ratio < 1.0:
-            log_dist("offload_optimizer.ratio < 1 is not supported yet: offloading the whole optimizer", ranks=[0])
+        if self.ratio < 1.0 and self.device == "nvme":
+            log_dist("offload_optimizer.ratio < 1 applies to device=cpu only: offloading the whole optimizer",
+                     ranks=[0])
+            self.ratio = 1.0
+        self.groups = set()
         self.aio_config = aio_config
         self.rank = rank
         self.swapper = None
@@ -134,16 +139,22 @@ class HostOptimizerStep:
     def _kinds(self, opt):
         return {"adam": 3, "lion": 2, "adagrad": 2}.get(opt.kind, 1)
 
+    def host_groups(self, opt):
+        """Indices of the param groups this tier owns (all of them unless Twin-Flow split them)."""
+        return {g for g, pg in enumerate(opt.optimizer.param_groups) if pg.get("sxe_offload", True)}
+
     def init_master(self, opt):
         if opt.kind == "generic" and self.device == "nvme":
             raise ValueError("NVMe optimizer offload supports Adam/AdamW/Lion/Adagrad")
-        opt.grad_host, opt.lp_host = [], []
+        self.groups = self.host_groups(opt)
+        G = len(opt.units)
+        opt.grad_host, opt.lp_host = [None] * G, [None] * G
         # Host staging of gradients (fp32, D2H) and updated bit16 params (H2D): a ring of
         # STAGE_SLOTS unit-sized pinned slots instead of full-model mirrors (6 B/param less on the
         # host -- the host tier is what bounds the trainable model size); generic torch optimizers
         # step whole groups and keep the full mirrors.
         self.streamed = opt.kind != "generic"
-        all_units = [u for units in opt.units for u in units]
+        all_units = [u for g in sorted(self.groups) for u in opt.units[g]]
         if self.streamed and all_units:
             maxc = max(u.chunk for u in all_units)
             self.gslots = [_pinned(maxc, torch.float32) for _ in range(self.STAGE_SLOTS)]
@@ -151,11 +162,13 @@ class HostOptimizerStep:
             self.lslots = [_pinned(maxc, lp_dtype) for _ in range(self.STAGE_SLOTS)] if lp_dtype else None
             self._lslot_ev = [None] * self.STAGE_SLOTS
         for g, units in enumerate(opt.units):
+            if g not in self.groups:
+                continue  # Twin-Flow device group: initialised by the ZeRO optimizer itself
             total = sum(u.chunk for u in units)
             gr = torch.zeros(total, dtype=torch.float32, device=opt.device)  # GPU accumulator
             needs_lp = any(u.shard.is_cuda for u in units)
-            opt.grad_host.append(None if self.streamed else _pinned(total, torch.float32))
-            opt.lp_host.append(_pinned(total, units[0].dtype) if needs_lp and not self.streamed else None)
+            opt.grad_host[g] = None if self.streamed else _pinned(total, torch.float32)
+            opt.lp_host[g] = _pinned(total, units[0].dtype) if needs_lp and not self.streamed else None
             if self.device == "cpu":
                 m = _pinned(total, torch.float32) if self.pin else torch.empty(total, dtype=torch.float32)
             else:
@@ -170,8 +183,8 @@ class HostOptimizerStep:
                     u.master = None
                 off += u.chunk
             m = torch.nn.Parameter(m, requires_grad=False)
-            opt.master.append(m)
-            opt.grads.append(gr)
+            opt.master[g] = m
+            opt.grads[g] = gr
             opt.optimizer.param_groups[g]["params"] = [m]
         opt.optimizer.state.clear()
         if self.device == "cpu":
@@ -226,6 +239,8 @@ class HostOptimizerStep:
         return []
 
     def update(self, opt, coef_t, skip_t):
+        if not self.groups:
+            return  # Twin-Flow ratio 0: everything is stepped in device memory
         flags = torch.cat([coef_t.reshape(1).float(), skip_t.reshape(1).float()]).cpu()  # the one sync
         coef, skip = float(flags[0]), float(flags[1])
         if skip != 0.0:
@@ -237,7 +252,7 @@ class HostOptimizerStep:
             return self._update_mirrored(opt, cur, coef)
         # units in step order; unit k's gradient lands in staging slot k % NS, so at most NS units'
         # copies are in flight ahead of the CPU update
-        flat = [(g, i, u, off) for g, units in enumerate(opt.units)
+        flat = [(g, i, u, off) for g, units in enumerate(opt.units) if g in self.groups
                 for i, u, off in zip(range(len(units)), units, _offsets(units))]
         NS = len(self.gslots)
         d2h_ev = {}
@@ -260,7 +275,7 @@ class HostOptimizerStep:
             issue_d2h(k)
         nvme = self.device == "nvme"
         nslot = len(self.swapper.slots) if nvme else 0
-        for g, units in enumerate(opt.units):
+        for g in self.groups:
             st = opt.optimizer.state[opt.master[g]]
             if opt.kind in ("adam", "adagrad"):
                 st["step"] = int(st.get("step", 0)) + 1
@@ -419,6 +434,31 @@ class HostOptimizerStep:
         sw.views(0, u.chunk)[0].copy_(u.shard.float().cpu() if u.shard.is_cuda else u.shard.float())
         sw.write(0, g, i, u.chunk)
         sw.drain()
+
+
+def split_param_groups(optimizer, ratio):
+    """Twin-Flow partial offload (reference runtime/zero/stage3.py:867-876 puts the first
+    int(ratio * n) optimizer sub-groups on the CPU, the rest on the accelerator): every param group
+    is cut, in parameter order, into a host part -- the parameters starting within the first
+    ``ratio`` of the group's elements -- and a device part. Both parts keep the group's
+    hyper-parameters (LR schedules and clipping see them as ordinary groups) and carry the
+    ``sxe_offload`` tag that ``HostOptimizerStep.host_groups`` reads. The device part's masters,
+    Adam moments and update stay in HBM (fused HIP Adam), so HBM holds 6 + 12 (1 - ratio) bytes per
+    trainable parameter and the host 12 ratio + staging: the ratio trades host RAM for HBM."""
+    ratio = min(max(float(ratio), 0.0), 1.0)
+    out = []
+    for pg in optimizer.param_groups:
+        params = list(pg["params"])
+        total = sum(p.numel() for p in params)
+        host, dev, start = [], [], 0
+        for p in params:
+            (host if start < ratio * total else dev).append(p)
+            start += p.numel()
+        for part, flag in ((host, True), (dev, False)):
+            if part:
+                out.append(dict(pg, params=part, sxe_offload=flag))
+    optimizer.param_groups[:] = out
+    return optimizer
 
 
 def OffloadOptimizer(*a, **kw):  # pragma: no cover - kept for the reference's class name

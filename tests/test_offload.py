@@ -12,9 +12,9 @@ from .dist_utils import run_dist
 ADAM = {"type": "AdamW", "params": {"lr": 1e-2, "weight_decay": 0.01}}
 
 
-def _cfg(stage, device="cpu", nvme_path=None, offload_param=False, clip=0.0):
+def _cfg(stage, device="cpu", nvme_path=None, offload_param=False, clip=0.0, ratio=1.0):
     z = {"stage": stage, "reduce_bucket_size": 20000,
-         "offload_optimizer": {"device": device, "nvme_path": nvme_path, "pin_memory": True}}
+         "offload_optimizer": {"device": device, "nvme_path": nvme_path, "pin_memory": True, "ratio": ratio}}
     if offload_param:
         z["offload_param"] = {"device": "cpu", "pin_memory": True}
         z["stage3_param_persistence_threshold"] = 10
@@ -55,10 +55,28 @@ def test_zero3_param_and_optimizer_offload(tmp_path):
     _check(res, reference_train(ADAM, 3, 2, 2, 16))
 
 
-def _case_offload_ckpt(rank, world, device, nvme, ckdir):
+@pytest.mark.parametrize("stage", [2, 3])
+@pytest.mark.parametrize("ratio", [0.0, 0.4])
+def test_twin_flow_partial_offload_matches_reference(stage, ratio):
+    """offload_optimizer.ratio < 1 (Twin-Flow): part of every param group is stepped on the host,
+    the rest in device memory; together they equal one AdamW over the global batch."""
+    res = run_dist(case_train, 2, _cfg(stage, ratio=ratio), 3, 2, 16)
+    _check(res, reference_train(ADAM, 3, 2, 2, 16))
+
+
+def test_split_param_groups_by_ratio():
+    from shuffle_exchange_amd.runtime.zero.offload import split_param_groups
+    ps = [torch.nn.Parameter(torch.zeros(n)) for n in (10, 30, 20, 40)]
+    opt = torch.optim.AdamW([{"params": ps[:3], "weight_decay": 0.1}, {"params": ps[3:], "weight_decay": 0.0}])
+    split_param_groups(opt, 0.5)
+    got = [([p.numel() for p in g["params"]], g["sxe_offload"], g["weight_decay"]) for g in opt.param_groups]
+    assert got == [([10, 30], True, 0.1), ([20], False, 0.1), ([40], True, 0.0)]
+
+
+def _case_offload_ckpt(rank, world, device, nvme, ckdir, ratio=1.0):
     import shuffle_exchange_amd as sxe
     from ._dist_cases import full_params, global_batches, tiny_llama
-    cfg_a = _cfg(2, device, nvme)
+    cfg_a = _cfg(2, device, nvme, ratio=ratio)
     model, cfg = tiny_llama(0)
     eng, _, _, _ = sxe.initialize(model=model, config=cfg_a)
     batches = global_batches(cfg, world, 2, 16, 4)
@@ -81,10 +99,10 @@ def _case_offload_ckpt(rank, world, device, nvme, ckdir):
     return {"ok": all(torch.allclose(want[k], got[k], atol=1e-6) for k in want)}
 
 
-@pytest.mark.parametrize("device", ["cpu", "nvme"])
-def test_offload_checkpoint_resume(tmp_path, device):
+@pytest.mark.parametrize("device,ratio", [("cpu", 1.0), ("nvme", 1.0), ("cpu", 0.5)])
+def test_offload_checkpoint_resume(tmp_path, device, ratio):
     nv = str(tmp_path / "nvme") if device == "nvme" else None
-    res = run_dist(_case_offload_ckpt, 2, device, nv, str(tmp_path / "ck"))
+    res = run_dist(_case_offload_ckpt, 2, device, nv, str(tmp_path / "ck"), ratio)
     assert all(r["ok"] for r in res)
 
 

@@ -23,8 +23,8 @@ def _case(rank, world, stage, offload, nvme_dir=None):
     with sxe.zero.Init(dtype=torch.bfloat16):
         model = LlamaForCausalLM(cfg)
     zc = {"stage": stage, "stage3_param_persistence_threshold": 0}
-    if offload == "cpu":
-        zc["offload_optimizer"] = {"device": "cpu", "pin_memory": True}
+    if offload in ("cpu", "twin_flow"):
+        zc["offload_optimizer"] = {"device": "cpu", "pin_memory": True, "ratio": 0.5 if offload == "twin_flow" else 1.0}
         if stage == 3:
             zc["offload_param"] = {"device": "cpu", "pin_memory": True}
     elif offload == "nvme":
@@ -44,7 +44,7 @@ def _case(rank, world, stage, offload, nvme_dir=None):
     return C.full_params(eng)
 
 
-@pytest.mark.parametrize("stage,offload", [(2, "cpu"), (3, "cpu"), (3, "nvme")])
+@pytest.mark.parametrize("stage,offload", [(2, "cpu"), (3, "cpu"), (3, "nvme"), (3, "twin_flow")])
 def test_offload_matches_hbm_adam(stage, offload):
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
         off = run_dist(_case, 1, stage, offload, d)[0]

@@ -8,6 +8,8 @@ fresh child processes, and reports the largest model that trains. Modes:
   cpu_offload  ZeRO-Infinity host tier: fp32 master/m/v + bf16 staging in pinned host DRAM
                (14 B/param on the host, 6 B/param in HBM); sizes whose host need exceeds
                --host-gb are skipped, never attempted (the host must not run out of memory)
+  --ratio r    Twin-Flow partial offload (cpu_offload only): the first r of every param group on the
+               host (12 r B/param there), the rest stepped in HBM (6 + 12 (1 - r) B/param)
 Usage: python tools/peak_params.py --mode hbm --layers 12,14,15
 """
 import argparse
@@ -26,7 +28,7 @@ def params_for(L):
     return L * per_layer + 2 * v * h + h
 
 
-def child(L, mode, seq, steps):
+def child(L, mode, seq, steps, ratio=1.0):
     sys.path.insert(0, ROOT)
     import torch
     import shuffle_exchange_amd as sxe
@@ -38,7 +40,7 @@ def child(L, mode, seq, steps):
         model = LlamaForCausalLM(cfg)
     zc = {"stage": 3, "stage3_param_persistence_threshold": 100_000, "reduce_bucket_size": 500_000_000}
     if mode == "cpu_offload":
-        zc["offload_optimizer"] = {"device": "cpu", "pin_memory": True}
+        zc["offload_optimizer"] = {"device": "cpu", "pin_memory": True, "ratio": ratio}
     ds = {"train_micro_batch_size_per_gpu": 1, "gradient_accumulation_steps": 1, "bf16": {"enabled": True},
           "gradient_clipping": 1.0, "zero_optimization": zc,
           "optimizer": {"type": "AdamW", "params": {"lr": 1e-4, "weight_decay": 0.1}}, "steps_per_print": 10**9}
@@ -59,6 +61,7 @@ def child(L, mode, seq, steps):
     dt = (time.perf_counter() - t0) / steps
     import psutil
     print("RESULT " + json.dumps({"layers": L, "params": n, "params_B": round(n / 1e9, 2), "mode": mode,
+                                  "offload_ratio": ratio if mode == "cpu_offload" else None,
                                   "peak_hbm_GB": round(torch.cuda.max_memory_allocated() / 1e9, 1),
                                   "host_rss_GB": round(psutil.Process().memory_info().rss / 1e9, 1),
                                   "s_per_step": round(dt, 2), "tokens_per_s": round(seq / dt, 1),
@@ -72,22 +75,24 @@ def main():
     ap.add_argument("--seq", type=int, default=2048)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--host-gb", type=float, default=200.0)
+    ap.add_argument("--ratio", type=float, default=1.0)
     ap.add_argument("--timeout", type=int, default=420)
     ap.add_argument("--child", type=int, default=None)
     a = ap.parse_args()
     if a.child is not None:
-        return child(a.child, a.mode, a.seq, a.steps)
+        return child(a.child, a.mode, a.seq, a.steps, a.ratio)
     best = None
     for L in [int(x) for x in a.layers.split(",")]:
         n = params_for(L)
-        if a.mode == "cpu_offload" and 14 * n / 1e9 > a.host_gb:
+        host_need = (12 * a.ratio * n + 20e9) / 1e9  # masters + moments (+ runtime) on the host
+        if a.mode == "cpu_offload" and host_need > a.host_gb:
             print(json.dumps({"layers": L, "params_B": round(n / 1e9, 2), "skipped": "host memory estimate "
-                              f"{14 * n / 1e9:.0f} GB > --host-gb {a.host_gb}"}), flush=True)
+                              f"{host_need:.0f} GB > --host-gb {a.host_gb}"}), flush=True)
             continue
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29700 + L), RANK="0", WORLD_SIZE="1",
                    LOCAL_RANK="0")
         proc = subprocess.Popen([sys.executable, "-u", __file__, "--mode", a.mode, "--seq", str(a.seq), "--steps",
-                                 str(a.steps), "--child", str(L)], env=env, stdout=subprocess.PIPE,
+                                 str(a.steps), "--ratio", str(a.ratio), "--child", str(L)], env=env, stdout=subprocess.PIPE,
                                 stderr=subprocess.STDOUT, text=True)
         lines = []
         t_start = time.time()
