@@ -67,6 +67,11 @@ class InferenceEngine(torch.nn.Module):
         if config.weight_quantization:
             from .quantization import _init_group_wise_weight_quantization
             _init_group_wise_weight_quantization(model, {"weight_quantization": config.weight_quantization})
+        self.injected_layers = 0
+        if config.replace_with_kernel_inject:
+            # Hugging Face layers with an injection policy -> fused gfx950 layers (replace_module.py)
+            from ..module_inject.replace_module import replace_transformer_layer
+            self.injected_layers = replace_transformer_layer(model)
         self.device = dev
         self._graphs = {}
         self._ragged = None

@@ -1,0 +1,160 @@
+"""v1 kernel injection: swap Hugging Face transformer layers for fused gfx950 layers in place.
+
+Parity: reference module_inject/replace_module.py (``replace_transformer_layer`` /
+``replace_with_policy``: walk the model, match each layer class against the injection policies,
+build the fused inference layer from the policy's weights) and the per-architecture containers
+module_inject/containers/{bert.py, gpt2.py, distil_bert.py} (``HFBertLayerPolicy``,
+``HFGPT2LayerPolicy``: HF parameter names -> qkv / attn-out / mlp / norm tensors).
+
+MI355X-first layer: the policy packs q/k/v into ONE [3H, H] weight (one hipBLASLt GEMM instead of
+three), keeps every projection in the ``y = x W^T`` layout ``ops.linear`` dispatches (hipBLASLt, or
+the skinny-M gfx950 kernel for decode-sized inputs), runs bias+GELU as one elementwise kernel
+(``ops.activation.bias_act``) and folds every residual add into the following LayerNorm kernel
+(``ops.norm.layer_norm(..., residual=)``). Attention is the HIP flash kernel where it applies
+(bf16, head dim 128, no padding mask) and SDPA otherwise. Decoder blocks keep Hugging Face's
+``Cache`` protocol (``past_key_values.update``), so ``model.generate`` works on injected models.
+Anything a fused layer does not cover (cross-attention, head masks, attention-probability outputs)
+is delegated to the original module, which the fused layer keeps without re-registering its
+parameters.
+"""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.activation import bias_act
+from ..ops.attention import attention, hip_supported
+from ..ops.linear import linear
+from ..ops.norm import layer_norm
+
+
+def _act_name(hf_act):
+    # Hugging Face "gelu" is the exact (erf) GELU; the framework's "gelu" is the tanh form
+    return {"gelu": "gelu_exact"}.get(hf_act, hf_act) if isinstance(hf_act, str) else "gelu_exact"
+
+
+def _attend(q, k, v, mask, causal, scale):
+    """q [B, Sq, H, D], k/v [B, Sk, H, D] -> [B, Sq, H, D]."""
+    if mask is None and q.shape[1] == k.shape[1] and hip_supported(q, k, v):
+        return attention(q, k, v, causal=causal, softmax_scale=scale)
+    qt, kt, vt = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+    if causal and mask is None and qt.shape[2] != kt.shape[2]:
+        # new tokens after a cached prefix: bottom-right aligned causal mask
+        sq, sk = qt.shape[2], kt.shape[2]
+        mask = torch.ones(sq, sk, dtype=torch.bool, device=q.device).tril(sk - sq)
+        causal = False
+    if mask is not None and mask.dtype != torch.bool:
+        mask = mask.to(q.dtype)
+    o = F.scaled_dot_product_attention(qt, kt, vt, attn_mask=mask, is_causal=causal and mask is None,
+                                       scale=scale)
+    return o.transpose(1, 2)
+
+
+class _Fused(nn.Module):
+    def __init__(self, orig):
+        super().__init__()
+        self.__dict__["orig"] = orig  # not a submodule: its parameters stay out of this layer's state
+
+    @staticmethod
+    def _p(t):
+        return nn.Parameter(t.detach().clone().contiguous(), requires_grad=False)
+
+
+class FusedEncoderLayer(_Fused):
+    """Post-LayerNorm encoder layer (BERT / RoBERTa): self-attention, out-proj + residual LN,
+    bias-GELU MLP + residual LN."""
+
+    def __init__(self, layer, config):
+        super().__init__(layer)
+        sa, ao = layer.attention.self, layer.attention.output
+        self.nh = sa.num_attention_heads
+        self.hd = sa.attention_head_size
+        self.w_qkv = self._p(torch.cat([sa.query.weight, sa.key.weight, sa.value.weight]))
+        self.b_qkv = self._p(torch.cat([sa.query.bias, sa.key.bias, sa.value.bias]))
+        self.w_o, self.b_o = self._p(ao.dense.weight), self._p(ao.dense.bias)
+        self.ln1_w, self.ln1_b, self.eps1 = self._p(ao.LayerNorm.weight), self._p(ao.LayerNorm.bias), ao.LayerNorm.eps
+        self.w_fc, self.b_fc = self._p(layer.intermediate.dense.weight), self._p(layer.intermediate.dense.bias)
+        self.w_out, self.b_out = self._p(layer.output.dense.weight), self._p(layer.output.dense.bias)
+        ln2 = layer.output.LayerNorm
+        self.ln2_w, self.ln2_b, self.eps2 = self._p(ln2.weight), self._p(ln2.bias), ln2.eps
+        self.act = _act_name(getattr(config, "hidden_act", "gelu"))
+
+    def forward(self, hidden_states, attention_mask=None, encoder_hidden_states=None, *args, **kwargs):
+        if encoder_hidden_states is not None or kwargs.get("output_attentions"):
+            return self.orig(hidden_states, attention_mask, encoder_hidden_states, *args, **kwargs)
+        x = hidden_states
+        B, S, H = x.shape
+        qkv = linear(x, self.w_qkv, self.b_qkv).view(B, S, 3, self.nh, self.hd)
+        o = _attend(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], attention_mask, False, 1.0 / math.sqrt(self.hd))
+        a = linear(o.reshape(B, S, H), self.w_o, self.b_o)
+        h, _ = layer_norm(a, self.ln1_w, self.ln1_b, self.eps1, residual=x)
+        m = linear(bias_act(linear(h, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
+        y, _ = layer_norm(m, self.ln2_w, self.ln2_b, self.eps2, residual=h)
+        return y
+
+
+class FusedGPT2Block(_Fused):
+    """Pre-LayerNorm decoder block (GPT-2): LN -> fused QKV -> causal attention (KV cache through
+    the HF Cache protocol) -> out-proj; residual folded into LN2; bias-GELU MLP."""
+
+    def __init__(self, block, config):
+        super().__init__(block)
+        at = block.attn
+        self.nh, self.hd = at.num_heads, at.head_dim
+        self.layer_idx = at.layer_idx
+        t = lambda conv: conv.weight.t()  # HF Conv1D stores [in, out]
+        self.w_qkv, self.b_qkv = self._p(t(at.c_attn)), self._p(at.c_attn.bias)
+        self.w_o, self.b_o = self._p(t(at.c_proj)), self._p(at.c_proj.bias)
+        self.ln1_w, self.ln1_b, self.eps1 = self._p(block.ln_1.weight), self._p(block.ln_1.bias), block.ln_1.eps
+        self.ln2_w, self.ln2_b, self.eps2 = self._p(block.ln_2.weight), self._p(block.ln_2.bias), block.ln_2.eps
+        self.w_fc, self.b_fc = self._p(t(block.mlp.c_fc)), self._p(block.mlp.c_fc.bias)
+        self.w_out, self.b_out = self._p(t(block.mlp.c_proj)), self._p(block.mlp.c_proj.bias)
+        self.act = _act_name(getattr(config, "activation_function", "gelu_new"))
+        scale = 1.0 / math.sqrt(self.hd) if getattr(at, "scale_attn_weights", True) else 1.0
+        if getattr(at, "scale_attn_by_inverse_layer_idx", False):
+            scale /= float(self.layer_idx + 1)
+        self.scale = scale
+        self.cross = getattr(block, "crossattention", None) is not None
+
+    def forward(self, hidden_states, past_key_values=None, attention_mask=None, encoder_hidden_states=None,
+                *args, **kwargs):
+        if self.cross or encoder_hidden_states is not None or kwargs.get("output_attentions"):
+            return self.orig(hidden_states, past_key_values, attention_mask, encoder_hidden_states, *args,
+                             **kwargs)
+        x = hidden_states
+        B, S, H = x.shape
+        y = layer_norm(x, self.ln1_w, self.ln1_b, self.eps1)
+        qkv = linear(y, self.w_qkv, self.b_qkv).view(B, S, 3, self.nh, self.hd)
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        if past_key_values is not None:
+            kt, vt = past_key_values.update(k.transpose(1, 2), v.transpose(1, 2), self.layer_idx)
+            k, v = kt.transpose(1, 2), vt.transpose(1, 2)
+        o = _attend(q, k, v, attention_mask, attention_mask is None, self.scale)
+        a = linear(o.reshape(B, S, H), self.w_o, self.b_o)
+        h2, h = layer_norm(a, self.ln2_w, self.ln2_b, self.eps2, residual=x)
+        m = linear(bias_act(linear(h2, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
+        return h + m
+
+
+# layer class name -> fused layer constructor (reference containers/__init__.py policy list)
+POLICIES = {
+    "BertLayer": FusedEncoderLayer,
+    "RobertaLayer": FusedEncoderLayer,
+    "GPT2Block": FusedGPT2Block,
+}
+
+
+def replace_transformer_layer(model, config=None):
+    """Replace every layer with an injection policy by its fused counterpart; returns the number of
+    replaced layers (0 = the model's layers have no policy, e.g. this framework's own models,
+    which already run the gfx950 kernels)."""
+    config = config if config is not None else getattr(model, "config", None)
+    n = 0
+    for parent in list(model.modules()):
+        for name, child in list(parent.named_children()):
+            ctor = POLICIES.get(type(child).__name__)
+            if ctor is not None:
+                setattr(parent, name, ctor(child, config))
+                n += 1
+    return n
