@@ -137,11 +137,72 @@ class FusedGPT2Block(_Fused):
         return h + m
 
 
+def _rope_partial(x, cos, sin):
+    """NeoX-style (rotate-half) rotary on the first cos.shape[-1] dims of x [B, S, H, D]; cos/sin
+    [B, S, rot] as the HF model's rotary embedding hands them to its layers."""
+    cos, sin = cos.unsqueeze(2).to(x.dtype), sin.unsqueeze(2).to(x.dtype)
+    rot = cos.shape[-1]
+    xr, xp = x[..., :rot], x[..., rot:]
+    rotated = torch.cat([-xr[..., rot // 2:], xr[..., :rot // 2]], -1)
+    return torch.cat([xr * cos + rotated * sin, xp], -1)
+
+
+class FusedGPTNeoXLayer(_Fused):
+    """GPT-NeoX / Pythia layer (reference containers/gptneox.py): pre-LN, per-head interleaved QKV
+    re-packed to [3, heads, D] rows at injection, partial rotary, parallel (or sequential) residual
+    with the residual add folded into the post-attention LayerNorm in the sequential form."""
+
+    def __init__(self, layer, config):
+        super().__init__(layer)
+        at = layer.attention
+        self.nh, self.hd = at.num_attention_heads if hasattr(at, "num_attention_heads") else config.num_attention_heads, \
+            at.head_size
+        self.layer_idx, self.scale = at.layer_idx, float(at.scaling)
+        H = at.query_key_value.weight.shape[1]
+        w = at.query_key_value.weight.view(self.nh, 3, self.hd, H).transpose(0, 1).reshape(-1, H)
+        b = at.query_key_value.bias.view(self.nh, 3, self.hd).transpose(0, 1).reshape(-1)
+        self.w_qkv, self.b_qkv = self._p(w), self._p(b)
+        self.w_o, self.b_o = self._p(at.dense.weight), self._p(at.dense.bias)
+        li, lp = layer.input_layernorm, layer.post_attention_layernorm
+        self.ln1_w, self.ln1_b, self.eps1 = self._p(li.weight), self._p(li.bias), li.eps
+        self.ln2_w, self.ln2_b, self.eps2 = self._p(lp.weight), self._p(lp.bias), lp.eps
+        self.w_fc, self.b_fc = self._p(layer.mlp.dense_h_to_4h.weight), self._p(layer.mlp.dense_h_to_4h.bias)
+        self.w_out, self.b_out = self._p(layer.mlp.dense_4h_to_h.weight), self._p(layer.mlp.dense_4h_to_h.bias)
+        self.act = _act_name(getattr(config, "hidden_act", "gelu"))
+        self.parallel = bool(layer.use_parallel_residual)
+
+    def _mlp(self, y):
+        return linear(bias_act(linear(y, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
+
+    def forward(self, hidden_states, attention_mask=None, position_ids=None, use_cache=False, layer_past=None,
+                position_embeddings=None, **kwargs):
+        if position_embeddings is None or kwargs.get("output_attentions"):
+            return self.orig(hidden_states, attention_mask=attention_mask, position_ids=position_ids,
+                             use_cache=use_cache, layer_past=layer_past, position_embeddings=position_embeddings,
+                             **kwargs)
+        x = hidden_states
+        B, S, H = x.shape
+        qkv = linear(layer_norm(x, self.ln1_w, self.ln1_b, self.eps1), self.w_qkv, self.b_qkv)
+        qkv = qkv.view(B, S, 3, self.nh, self.hd)
+        cos, sin = position_embeddings
+        q, k, v = _rope_partial(qkv[:, :, 0], cos, sin), _rope_partial(qkv[:, :, 1], cos, sin), qkv[:, :, 2]
+        if layer_past is not None:
+            kt, vt = layer_past.update(k.transpose(1, 2), v.transpose(1, 2), self.layer_idx)
+            k, v = kt.transpose(1, 2), vt.transpose(1, 2)
+        o = _attend(q, k, v, attention_mask, attention_mask is None, self.scale)
+        a = linear(o.reshape(B, S, H), self.w_o, self.b_o)
+        if self.parallel:
+            return self._mlp(layer_norm(x, self.ln2_w, self.ln2_b, self.eps2)) + a + x
+        y2, h = layer_norm(a, self.ln2_w, self.ln2_b, self.eps2, residual=x)
+        return self._mlp(y2) + h
+
+
 # layer class name -> fused layer constructor (reference containers/__init__.py policy list)
 POLICIES = {
     "BertLayer": FusedEncoderLayer,
     "RobertaLayer": FusedEncoderLayer,
     "GPT2Block": FusedGPT2Block,
+    "GPTNeoXLayer": FusedGPTNeoXLayer,
 }
 
 

@@ -7,7 +7,16 @@ import torch
 
 transformers = pytest.importorskip("transformers")
 
-from shuffle_exchange_amd.module_inject.replace_module import replace_transformer_layer  # noqa: E402
+from shuffle_exchange_amd.module_inject import replace_module as rm  # noqa: E402
+
+
+def replace_transformer_layer(model):
+    """Inject, then drop the originals: a fused layer that silently delegated would fail."""
+    n = rm.replace_transformer_layer(model)
+    for m in model.modules():
+        if isinstance(m, rm._Fused):
+            m.__dict__["orig"] = None
+    return n
 
 
 def _bert(cls_name="Bert"):
@@ -84,3 +93,22 @@ def test_gpt2_injection_gpu_bf16_flash_path():
     rel = ((got - ref).norm() / ref.norm()).item()
     assert rel < 2e-2, rel
     assert gen.shape == (2, 20)
+
+
+@pytest.mark.parametrize("parallel", [True, False])
+def test_gpt_neox_injection_logits_and_generate(parallel):
+    cfg = transformers.GPTNeoXConfig(vocab_size=300, hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
+                                     intermediate_size=128, max_position_embeddings=64, rotary_pct=0.5,
+                                     use_parallel_residual=parallel)
+    torch.manual_seed(0)
+    model = transformers.GPTNeoXForCausalLM(cfg).eval()
+    ids = torch.randint(0, 300, (2, 10))
+    with torch.no_grad():
+        ref = model(ids, use_cache=False).logits
+        ref_gen = model.generate(ids, max_new_tokens=6, do_sample=False, pad_token_id=0)
+        n = replace_transformer_layer(model)
+        got = model(ids, use_cache=False).logits
+        got_gen = model.generate(ids, max_new_tokens=6, do_sample=False, pad_token_id=0)
+    assert n == 2
+    torch.testing.assert_close(got, ref, atol=5e-5, rtol=1e-4)
+    assert torch.equal(got_gen, ref_gen)
