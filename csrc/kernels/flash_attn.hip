@@ -183,7 +183,7 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const unsigned short* __res
                                                      const unsigned short* __restrict__ v, Strides vs,
                                                      unsigned short* __restrict__ o, Strides os,
                                                      float* __restrict__ lse, int B, int H, int Hk, int S,
-                                                     float scale, int causal, Sparse sp) {
+                                                     float scale, int causal, Sparse sp, int kvlen) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BUF = 2 * KT * ROWB;  // one ring slot = K tile + V tile
   int* tlist = reinterpret_cast<int*>(smem + 4 * KT * ROWB) + 1;
@@ -241,6 +241,7 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const unsigned short* __res
         for (int t2 = 0; t2 < D / 16; ++t2) s[j] = mfma(lds_row16(kt, 32 * j + r, 2 * t2 + h), qf[t2], s[j]);
       }
       const bool diag = causal && (kbase + KT - 1 > q0);
+      const bool tail = kbase + KT > kvlen;  // keys past the valid length (sequence padded to 128)
       float mx = -INFINITY;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -253,6 +254,7 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const unsigned short* __res
         for (int i = 0; i < 16; ++i) {
           float x = s[j][i] * c;
           if (diag && (kbase + 32 * j + acc_row(i, h) > q0 + r)) x = -INFINITY;
+          if (tail && (kbase + 32 * j + acc_row(i, h) >= kvlen)) x = -INFINITY;
           if (!(acc_row(i, h) < 16 ? b0 : b1)) x = -INFINITY;
           s[j][i] = x;
           mx = fmaxf(mx, x);
@@ -374,7 +376,7 @@ __global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __rest
                                                     const unsigned short* __restrict__ dout, Strides dos,
                                                     const float* __restrict__ lse, const float* __restrict__ delta,
                                                     unsigned short* __restrict__ dq, Strides dqs, int B, int H,
-                                                    int Hk, int S, float scale, int causal, Sparse sp) {
+                                                    int Hk, int S, float scale, int causal, Sparse sp, int kvlen) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BUF = 2 * KT * ROWB;
   int* tlist = reinterpret_cast<int*>(smem + 4 * KT * ROWB) + 1;
@@ -426,6 +428,7 @@ __global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __rest
       const char* kt = smem + cur * BUF;
       const char* vt = smem + cur * BUF + KT * ROWB;
       const bool diag = causal && (kbase + KT - 1 > q0);
+      const bool tail = kbase + KT > kvlen;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         f32x16 s = zero16(), dp = zero16();
@@ -443,6 +446,7 @@ __global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __rest
         for (int i = 0; i < 16; ++i) {
           float p = fast_exp2(s[i] * c - lse2);
           if (diag && (kbase + 32 * j + acc_row(i, h) > q0 + r)) p = 0.f;
+          if (tail && (kbase + 32 * j + acc_row(i, h) >= kvlen)) p = 0.f;
           if (!(acc_row(i, h) < 16 ? b0 : b1)) p = 0.f;
           s[i] = p * (dp[i] - dlt);  // dS^T
         }
@@ -691,9 +695,11 @@ static fa::Sparse sparse_of(const c10::optional<at::Tensor>& layout, int64_t blo
 constexpr size_t kListBytes = (1 + 2048) * sizeof(int) + 16;  // tile list + scratch flags (sparse mode)
 
 static std::vector<at::Tensor> fwd_impl(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, double scale,
-                                        fa::Sparse sp) {
+                                        fa::Sparse sp, int64_t kv_len = -1) {
   check_qkv(q, k, v);
   const int B = q.size(0), S = q.size(1), H = q.size(2), Hk = k.size(2);
+  const int kvlen = kv_len < 0 ? S : (int)kv_len;
+  SXE_CHECK(kvlen >= 1 && kvlen <= S, "flash_attn: kv_len must be in [1, seq_len]");
   c10::DeviceGuard guard(q.device());
   auto o = at::empty({B, S, H, fa::D}, q.options());
   auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
@@ -710,16 +716,19 @@ static std::vector<at::Tensor> fwd_impl(at::Tensor q, at::Tensor k, at::Tensor v
                      reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
                      reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),
                      reinterpret_cast<unsigned short*>(o.data_ptr()), strides_of(o), lse.data_ptr<float>(), B, H, Hk,
-                     S, (float)scale, causal ? 1 : 0, sp);
+                     S, (float)scale, causal ? 1 : 0, sp, kvlen);
   SXE_LAUNCH_CHECK();
   return {o, lse};
 }
 
 // dq/dk/dv are caller-provided (possibly strided views of one dqkv buffer).
 static void bwd_impl(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
-                     at::Tensor dq, at::Tensor dk, at::Tensor dv, bool causal, double scale, fa::Sparse sp) {
+                     at::Tensor dq, at::Tensor dk, at::Tensor dv, bool causal, double scale, fa::Sparse sp,
+                     int64_t kv_len = -1) {
   check_qkv(q, k, v);
   check_qkv(dq, dk, dv);
+  const int kvlen = kv_len < 0 ? (int)q.size(1) : (int)kv_len;
+  SXE_CHECK(kvlen >= 1 && kvlen <= q.size(1), "flash_attn_bwd: kv_len must be in [1, seq_len]");
   SXE_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && dout.stride(3) == 1 && o.stride(3) == 1,
             "flash_attn_bwd: dout/o shapes");
   SXE_CHECK(dq.sizes() == q.sizes() && dk.sizes() == k.sizes() && dv.sizes() == v.sizes(), "flash_attn_bwd: grad shapes");
@@ -751,7 +760,7 @@ static void bwd_impl(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, 
                      reinterpret_cast<const unsigned short*>(dout.data_ptr()), strides_of(dout),
                      lse.data_ptr<float>(), delta.data_ptr<float>(),
                      reinterpret_cast<unsigned short*>(dq.data_ptr()), strides_of(dq), B, H, Hk, S, (float)scale,
-                     causal ? 1 : 0, sp);
+                     causal ? 1 : 0, sp, kvlen);
   SXE_LAUNCH_CHECK();
   // sparse: always one workgroup per query head (per-head tile lists); with GQA the per-head fp32
   // partials are reduced; causal GQA: split to remove the key-block-0 tail (see dkdv_kernel)
@@ -790,13 +799,14 @@ static void bwd_impl(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, 
   SXE_LAUNCH_CHECK();
 }
 
-std::vector<at::Tensor> flash_attn_fwd(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, double scale) {
-  return fwd_impl(q, k, v, causal, scale, fa::Sparse{nullptr, 0, 0});
+std::vector<at::Tensor> flash_attn_fwd(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, double scale,
+                                       int64_t kv_len) {
+  return fwd_impl(q, k, v, causal, scale, fa::Sparse{nullptr, 0, 0}, kv_len);
 }
 
 void flash_attn_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
-                    at::Tensor dq, at::Tensor dk, at::Tensor dv, bool causal, double scale) {
-  bwd_impl(dout, q, k, v, o, lse, dq, dk, dv, causal, scale, fa::Sparse{nullptr, 0, 0});
+                    at::Tensor dq, at::Tensor dk, at::Tensor dv, bool causal, double scale, int64_t kv_len) {
+  bwd_impl(dout, q, k, v, o, lse, dq, dk, dv, causal, scale, fa::Sparse{nullptr, 0, 0}, kv_len);
 }
 
 std::vector<at::Tensor> flash_attn_fwd_sparse(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor layout,
@@ -813,9 +823,9 @@ void flash_attn_bwd_sparse(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tens
 }  // namespace sxe
 
 TORCH_LIBRARY_FRAGMENT(sxe, m) {
-  m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> Tensor[]");
+  m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, int kv_len=-1) -> Tensor[]");
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, "
-        "Tensor(c!) dv, bool causal, float scale) -> ()");
+        "Tensor(c!) dv, bool causal, float scale, int kv_len=-1) -> ()");
   m.def("flash_attn_fwd_sparse(Tensor q, Tensor k, Tensor v, Tensor layout, int block, bool causal, float scale) -> Tensor[]");
   m.def("flash_attn_bwd_sparse(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, "
         "Tensor(b!) dk, Tensor(c!) dv, Tensor layout, int block, bool causal, float scale) -> ()");

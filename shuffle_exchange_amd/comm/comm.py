@@ -45,6 +45,7 @@ class _State:
     logger_prof_all = True
     logger_prof_ops = []
     comms = defaultdict(lambda: defaultdict(list))  # op -> msg_size -> [latency_ms...]
+    op_counts = defaultdict(int)  # log_name -> collectives issued (always counted, no sync)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -264,6 +265,12 @@ def get_comms_stats():
 
 def reset_comms_stats():
     _State.comms.clear()
+    _State.op_counts.clear()
+
+
+def get_op_counts():
+    """Collectives issued per ``log_name`` since the last ``reset_comms_stats()``."""
+    return dict(_State.op_counts)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -275,6 +282,7 @@ def _skip(kind):
 def all_reduce(tensor, op=ReduceOp.SUM, group=None, async_op=False, prof=False, log_name="all_reduce"):
     if _skip("ALL_REDUCE") or get_world_size(group) == 1:
         return None
+    _State.op_counts[log_name] += 1
     return _timed("all_reduce", lambda: tdist.all_reduce(tensor, op=op, group=group, async_op=async_op), tensor,
                   group, async_op)
 

@@ -4,8 +4,12 @@ fixed-shape forwards, and KV-cached ``generate`` through the ragged v2 engine.
 Parity: reference inference/engine.py -- ``InferenceEngine`` :40 (``_create_model_parallel_group``
 :247, ``_apply_injection_policy`` :378 / AutoTP, ``_create_cuda_graph`` :494, ``forward`` :554,
 ``_generate``), config inference/config.py ``DeepSpeedInferenceConfig``.
-"Kernel injection" is implicit: the framework's models already run the gfx950 kernels, so
-``replace_with_kernel_inject`` only toggles the ragged/KV-cached generation path.
+The framework's own models always run the gfx950 kernels. ``replace_with_kernel_inject`` (default
+False, as in the reference) swaps Hugging Face layers that have an injection policy for fused gfx950
+layers (module_inject/replace_module.py); it is skipped -- with a log line -- under AutoTP
+(tp_size > 1) and post-init weight quantization, whose sharded / quantized weights the fused
+layers cannot take. ``generate`` uses the ragged KV-cached engine whenever the architecture has a
+v2 implementation, independent of injection.
 """
 from dataclasses import dataclass, field
 from typing import Optional
@@ -23,7 +27,7 @@ _DT = {"fp32": torch.float32, "float32": torch.float32, "fp16": torch.float16, "
 class InferenceConfig:
     dtype: object = torch.bfloat16
     tensor_parallel: dict = field(default_factory=lambda: {"tp_size": 1})
-    replace_with_kernel_inject: bool = True
+    replace_with_kernel_inject: bool = False
     enable_cuda_graph: bool = False
     max_out_tokens: int = 1024
     max_tokens: Optional[int] = None
@@ -68,10 +72,16 @@ class InferenceEngine(torch.nn.Module):
             from .quantization import _init_group_wise_weight_quantization
             _init_group_wise_weight_quantization(model, {"weight_quantization": config.weight_quantization})
         self.injected_layers = 0
+        self.injection_skipped = None
         if config.replace_with_kernel_inject:
-            # Hugging Face layers with an injection policy -> fused gfx950 layers (replace_module.py)
-            from ..module_inject.replace_module import replace_transformer_layer
-            self.injected_layers = replace_transformer_layer(model)
+            if config.tp_size > 1 or config.weight_quantization:
+                self.injection_skipped = "tp_size > 1" if config.tp_size > 1 else "weight_quantization"
+                log_dist(f"kernel injection skipped ({self.injection_skipped}): fused layers need whole, dense "
+                         f"weights", ranks=[0])
+            else:
+                # Hugging Face layers with an injection policy -> fused gfx950 layers (replace_module.py)
+                from ..module_inject.replace_module import replace_transformer_layer
+                self.injected_layers = replace_transformer_layer(model)
         self.device = dev
         self._graphs = {}
         self._ragged = None
@@ -128,7 +138,8 @@ class InferenceEngine(torch.nn.Module):
         max_new = max_new_tokens or kw.get("max_length", self._config.max_out_tokens)
         prompts = [list(map(int, r)) for r in (input_ids.tolist() if torch.is_tensor(input_ids) else input_ids)]
         try:
-            eng = self._ragged_engine() if self._config.replace_with_kernel_inject else None
+            # AutoTP-sharded models decode through their own (all-reducing) forward
+            eng = self._ragged_engine() if self._config.tp_size == 1 else None
         except NotImplementedError:
             eng = None
         if eng is not None:

@@ -15,6 +15,7 @@ from ..ops.attention import attention
 from ..ops.cross_entropy import cross_entropy
 from ..ops.linear import Linear
 from ..ops.norm import LayerNorm
+from ..runtime.zero.partition_parameters import local_shard
 
 
 @dataclass
@@ -91,9 +92,9 @@ class GPT2LMHeadModel(nn.Module):
     def reset_parameters(self):
         for m in self.modules():
             if isinstance(m, (nn.Linear, nn.Embedding)):
-                m.weight.normal_(0.0, self.cfg.initializer_range)
+                local_shard(m.weight).normal_(0.0, self.cfg.initializer_range)
             if isinstance(m, nn.Linear) and m.bias is not None:
-                m.bias.zero_()
+                local_shard(m.bias).zero_()
 
     def forward(self, input_ids, labels=None):
         B, S = input_ids.shape

@@ -23,6 +23,7 @@ import torch.nn.functional as F
 
 from ..ops.activation import swiglu
 from ..runtime.activation_checkpointing.checkpointing import checkpoint
+from ..runtime.zero.partition_parameters import local_shard
 from ..ops.attention import attention_qkv_rope
 from ..ops.cross_entropy import fused_linear_cross_entropy
 from ..ops.linear import Linear, linear
@@ -205,12 +206,14 @@ class LlamaForCausalLM(nn.Module):
 
     @torch.no_grad()
     def reset_parameters(self):
+        # element-wise i.i.d. init: under a partitioning zero.Init each rank initialises its own
+        # construction partition (local_shard), which is the same distribution as the full tensor
         std = self.cfg.initializer_range
         for m in self.modules():
             if isinstance(m, (nn.Linear, nn.Embedding)):
-                m.weight.normal_(0.0, std)
+                local_shard(m.weight).normal_(0.0, std)
         if not self.cfg.tie_word_embeddings:
-            self.lm_head.weight.normal_(0.0, std)
+            local_shard(self.lm_head.weight).normal_(0.0, std)
 
     def rope(self, device):
         if self._rope is None or self._rope.cos.device != device:

@@ -15,7 +15,12 @@ the skinny-M gfx950 kernel for decode-sized inputs), runs bias+GELU as one eleme
 ``Cache`` protocol (``past_key_values.update``), so ``model.generate`` works on injected models.
 Anything a fused layer does not cover (cross-attention, head masks, attention-probability outputs)
 is delegated to the original module, which the fused layer keeps without re-registering its
-parameters.
+parameters. The original module holds no weight memory of its own: its parameters are re-pointed
+at views of the fused tensors (row slices of the packed QKV, transposed views for GPT-2's
+Conv1D), and re-pointed again after every ``.to()`` / ``.half()`` of the fused layer; a layout that
+has no view (NeoX's head-interleaved QKV) is rebuilt only for the duration of a delegated call.
+Encoder layers configured as decoders (BERT/RoBERTa ``is_decoder``: causal self-attention, a KV
+cache, optional cross-attention) are not injected.
 """
 import math
 
@@ -24,7 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.activation import bias_act
-from ..ops.attention import attention, hip_supported
+from ..ops.attention import attention, hip_paddable, hip_supported
 from ..ops.linear import linear
 from ..ops.norm import layer_norm
 
@@ -36,7 +41,7 @@ def _act_name(hf_act):
 
 def _attend(q, k, v, mask, causal, scale):
     """q [B, Sq, H, D], k/v [B, Sk, H, D] -> [B, Sq, H, D]."""
-    if mask is None and q.shape[1] == k.shape[1] and hip_supported(q, k, v):
+    if mask is None and q.shape[1] == k.shape[1] and (hip_supported(q, k, v) or hip_paddable(q, k, v)):
         return attention(q, k, v, causal=causal, softmax_scale=scale)
     qt, kt, vt = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
     if causal and mask is None and qt.shape[2] != kt.shape[2]:
@@ -58,7 +63,27 @@ class _Fused(nn.Module):
 
     @staticmethod
     def _p(t):
-        return nn.Parameter(t.detach().clone().contiguous(), requires_grad=False)
+        """Fused parameter from an HF tensor: shares its storage when already contiguous."""
+        t = t.detach()
+        return nn.Parameter(t if t.is_contiguous() else t.contiguous(), requires_grad=False)
+
+    def _links(self):
+        """(orig parameter, view of a fused tensor) pairs; see the module docstring."""
+        return []
+
+    def _link(self):
+        if self.__dict__.get("orig") is None:
+            return
+        for param, view in self._links():
+            param.data = view
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        self._link()
+        return out
+
+    def _delegate(self, *args, **kwargs):
+        return self.orig(*args, **kwargs)
 
 
 class FusedEncoderLayer(_Fused):
@@ -79,10 +104,24 @@ class FusedEncoderLayer(_Fused):
         ln2 = layer.output.LayerNorm
         self.ln2_w, self.ln2_b, self.eps2 = self._p(ln2.weight), self._p(ln2.bias), ln2.eps
         self.act = _act_name(getattr(config, "hidden_act", "gelu"))
+        self._link()
+
+    def _links(self):
+        L, H = self.orig, self.nh * self.hd
+        sa, ao = L.attention.self, L.attention.output
+        out = []
+        for i, lin in enumerate((sa.query, sa.key, sa.value)):
+            out += [(lin.weight, self.w_qkv[i * H:(i + 1) * H]), (lin.bias, self.b_qkv[i * H:(i + 1) * H])]
+        out += [(ao.dense.weight, self.w_o), (ao.dense.bias, self.b_o), (ao.LayerNorm.weight, self.ln1_w),
+                (ao.LayerNorm.bias, self.ln1_b), (L.intermediate.dense.weight, self.w_fc),
+                (L.intermediate.dense.bias, self.b_fc), (L.output.dense.weight, self.w_out),
+                (L.output.dense.bias, self.b_out), (L.output.LayerNorm.weight, self.ln2_w),
+                (L.output.LayerNorm.bias, self.ln2_b)]
+        return out
 
     def forward(self, hidden_states, attention_mask=None, encoder_hidden_states=None, *args, **kwargs):
         if encoder_hidden_states is not None or kwargs.get("output_attentions"):
-            return self.orig(hidden_states, attention_mask, encoder_hidden_states, *args, **kwargs)
+            return self._delegate(hidden_states, attention_mask, encoder_hidden_states, *args, **kwargs)
         x = hidden_states
         B, S, H = x.shape
         qkv = linear(x, self.w_qkv, self.b_qkv).view(B, S, 3, self.nh, self.hd)
@@ -116,12 +155,21 @@ class FusedGPT2Block(_Fused):
             scale /= float(self.layer_idx + 1)
         self.scale = scale
         self.cross = getattr(block, "crossattention", None) is not None
+        self._link()
+
+    def _links(self):
+        b = self.orig
+        return [(b.attn.c_attn.weight, self.w_qkv.t()), (b.attn.c_attn.bias, self.b_qkv),
+                (b.attn.c_proj.weight, self.w_o.t()), (b.attn.c_proj.bias, self.b_o),
+                (b.ln_1.weight, self.ln1_w), (b.ln_1.bias, self.ln1_b), (b.ln_2.weight, self.ln2_w),
+                (b.ln_2.bias, self.ln2_b), (b.mlp.c_fc.weight, self.w_fc.t()), (b.mlp.c_fc.bias, self.b_fc),
+                (b.mlp.c_proj.weight, self.w_out.t()), (b.mlp.c_proj.bias, self.b_out)]
 
     def forward(self, hidden_states, past_key_values=None, attention_mask=None, encoder_hidden_states=None,
                 *args, **kwargs):
         if self.cross or encoder_hidden_states is not None or kwargs.get("output_attentions"):
-            return self.orig(hidden_states, past_key_values, attention_mask, encoder_hidden_states, *args,
-                             **kwargs)
+            return self._delegate(hidden_states, past_key_values, attention_mask, encoder_hidden_states, *args,
+                                  **kwargs)
         x = hidden_states
         B, S, H = x.shape
         y = layer_norm(x, self.ln1_w, self.ln1_b, self.eps1)
@@ -170,6 +218,28 @@ class FusedGPTNeoXLayer(_Fused):
         self.w_out, self.b_out = self._p(layer.mlp.dense_4h_to_h.weight), self._p(layer.mlp.dense_4h_to_h.bias)
         self.act = _act_name(getattr(config, "hidden_act", "gelu"))
         self.parallel = bool(layer.use_parallel_residual)
+        self._link()
+
+    def _links(self):
+        L = self.orig
+        at = L.attention
+        empty = self.w_qkv.new_empty(0)  # head-interleaved QKV has no view: rebuilt per delegated call
+        return [(at.query_key_value.weight, empty), (at.query_key_value.bias, self.b_qkv.new_empty(0)),
+                (at.dense.weight, self.w_o), (at.dense.bias, self.b_o), (L.input_layernorm.weight, self.ln1_w),
+                (L.input_layernorm.bias, self.ln1_b), (L.post_attention_layernorm.weight, self.ln2_w),
+                (L.post_attention_layernorm.bias, self.ln2_b), (L.mlp.dense_h_to_4h.weight, self.w_fc),
+                (L.mlp.dense_h_to_4h.bias, self.b_fc), (L.mlp.dense_4h_to_h.weight, self.w_out),
+                (L.mlp.dense_4h_to_h.bias, self.b_out)]
+
+    def _delegate(self, *args, **kwargs):
+        at = self.orig.attention
+        H = self.w_qkv.shape[1]
+        at.query_key_value.weight.data = self.w_qkv.view(3, self.nh, self.hd, H).transpose(0, 1).reshape(-1, H)
+        at.query_key_value.bias.data = self.b_qkv.view(3, self.nh, self.hd).transpose(0, 1).reshape(-1)
+        try:
+            return self.orig(*args, **kwargs)
+        finally:
+            self._link()
 
     def _mlp(self, y):
         return linear(bias_act(linear(y, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
@@ -177,9 +247,9 @@ class FusedGPTNeoXLayer(_Fused):
     def forward(self, hidden_states, attention_mask=None, position_ids=None, use_cache=False, layer_past=None,
                 position_embeddings=None, **kwargs):
         if position_embeddings is None or kwargs.get("output_attentions"):
-            return self.orig(hidden_states, attention_mask=attention_mask, position_ids=position_ids,
-                             use_cache=use_cache, layer_past=layer_past, position_embeddings=position_embeddings,
-                             **kwargs)
+            return self._delegate(hidden_states, attention_mask=attention_mask, position_ids=position_ids,
+                                  use_cache=use_cache, layer_past=layer_past, position_embeddings=position_embeddings,
+                                  **kwargs)
         x = hidden_states
         B, S, H = x.shape
         qkv = linear(layer_norm(x, self.ln1_w, self.ln1_b, self.eps1), self.w_qkv, self.b_qkv)
@@ -206,6 +276,13 @@ POLICIES = {
 }
 
 
+def _is_decoder_layer(layer, config):
+    sa = getattr(getattr(layer, "attention", None), "self", None)
+    return bool(getattr(config, "is_decoder", False) or getattr(layer, "is_decoder", False)
+                or getattr(sa, "is_causal", False) or getattr(sa, "is_decoder", False)
+                or getattr(layer, "add_cross_attention", False))
+
+
 def replace_transformer_layer(model, config=None):
     """Replace every layer with an injection policy by its fused counterpart; returns the number of
     replaced layers (0 = the model's layers have no policy, e.g. this framework's own models,
@@ -215,6 +292,8 @@ def replace_transformer_layer(model, config=None):
     for parent in list(model.modules()):
         for name, child in list(parent.named_children()):
             ctor = POLICIES.get(type(child).__name__)
+            if ctor is FusedEncoderLayer and _is_decoder_layer(child, config):
+                continue  # causal self-attention + KV cache: the encoder fusion does not apply
             if ctor is not None:
                 setattr(parent, name, ctor(child, config))
                 n += 1

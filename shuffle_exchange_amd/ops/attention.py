@@ -5,8 +5,13 @@ Backends:
 * ``hip``  -- this repo's gfx950 flash-attention kernels (csrc/kernels/flash_attn.hip): MFMA bf16,
   online softmax, LSE output; deterministic backward (dK/dV kernel + dQ kernel, no atomics);
 * ``sdpa`` -- ``torch.nn.functional.scaled_dot_product_attention``: used on CPU (plumbing tests) and
-  for shapes the HIP kernel does not cover (head dim != 128, seq % 128 != 0); on GPU this is
-  logged once so a silent fallback cannot hide in a benchmark.
+  for head dims above 128 on GPU (logged once so a silent fallback cannot hide in a benchmark).
+
+Shapes outside the kernel's native tile (head dim 128, sequence a multiple of 128) run the same
+kernels on padded copies: the sequence is zero-padded to the next multiple of 128 (padded keys
+are masked with the kernels' ``kv_len``; padded query rows are dropped) and head dims below 128
+(64, 80, 96, ...) are zero-padded to 128 (zero q/k columns leave the scores unchanged, zero v
+columns produce zero output columns that are dropped). The softmax scale is the true head dim's.
 ``SXE_ATTN_BACKEND=sdpa`` forces the stopgap for A/B comparisons.
 
 ``attention_qkv_rope`` is the training entry point of the Llama family: it takes the fused QKV
@@ -36,11 +41,61 @@ def _sdpa(q, k, v, causal, scale):
     return o.transpose(1, 2)
 
 
+TILE, HEAD_DIM = 128, 128
+
+
+def _aligned(t):
+    return (t.stride(-1) == 1 and t.stride(0) % 8 == 0 and t.stride(1) % 8 == 0 and t.stride(2) % 8 == 0
+            and t.data_ptr() % 16 == 0)
+
+
 def hip_supported(q, k, v):
+    """The kernels run these tensors in place (no padding copies)."""
     if os.environ.get("SXE_ATTN_BACKEND") == "sdpa":
         return False
-    return (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] == 128 and q.shape[1] % 128 == 0
-            and q.shape[2] % k.shape[2] == 0 and q.stride(-1) == 1 and k.stride(-1) == 1 and v.stride(-1) == 1)
+    return (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] == HEAD_DIM and q.shape[1] % TILE == 0
+            and q.shape[1] == k.shape[1] and q.shape[2] % k.shape[2] == 0 and all(_aligned(t) for t in (q, k, v)))
+
+
+def hip_paddable(q, k, v):
+    """The kernels run these tensors on padded copies (sequence and/or head dim)."""
+    if os.environ.get("SXE_ATTN_BACKEND") == "sdpa":
+        return False
+    return (q.is_cuda and q.dtype in (torch.bfloat16, torch.float16, torch.float32) and q.shape[-1] <= HEAD_DIM
+            and q.shape[-1] % 8 == 0 and q.shape[1] == k.shape[1] and q.shape[2] % k.shape[2] == 0)
+
+
+def _pad(t, S_pad, D_pad):
+    B, S, H, D = t.shape
+    if S == S_pad and D == D_pad and t.dtype == torch.bfloat16 and _aligned(t):
+        return t
+    out = torch.zeros(B, S_pad, H, D_pad, dtype=torch.bfloat16, device=t.device)
+    out[:, :S, :, :D].copy_(t)
+    return out
+
+
+class _FlashAttnPadded(torch.autograd.Function):
+    """Flash attention on padded copies (see the module docstring)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale):
+        S, D = q.shape[1], q.shape[-1]
+        Sp = -(-S // TILE) * TILE
+        qp, kp, vp = _pad(q, Sp, HEAD_DIM), _pad(k, Sp, HEAD_DIM), _pad(v, Sp, HEAD_DIM)
+        o, lse = torch.ops.sxe.flash_attn_fwd(qp, kp, vp, bool(causal), float(scale), S)
+        ctx.save_for_backward(qp, kp, vp, o, lse)
+        ctx.meta = (causal, scale, S, D, q.dtype)
+        return o[:, :S, :, :D].to(q.dtype)
+
+    @staticmethod
+    def backward(ctx, do):
+        qp, kp, vp, o, lse = ctx.saved_tensors
+        causal, scale, S, D, dtype = ctx.meta
+        dop = _pad(do, qp.shape[1], HEAD_DIM)
+        dq, dk, dv = torch.empty_like(qp), torch.empty_like(kp), torch.empty_like(vp)
+        torch.ops.sxe.flash_attn_bwd(dop, qp, kp, vp, o, lse, dq, dk, dv, bool(causal), float(scale), S)
+        sl = (slice(None), slice(0, S), slice(None), slice(0, D))
+        return dq[sl].to(dtype), dk[sl].to(dtype), dv[sl].to(dtype), None, None
 
 
 class _FlashAttn(torch.autograd.Function):
@@ -67,6 +122,8 @@ def attention(q, k, v, causal=True, softmax_scale=None):
         native.require_hip()
         if hip_supported(q, k, v):
             return _FlashAttn.apply(q, k, v, causal, scale)
+        if hip_paddable(q, k, v):
+            return _FlashAttnPadded.apply(q, k, v, causal, scale)
         warning_once(f"sxe attention: HIP flash kernel does not cover dtype={q.dtype} D={q.shape[-1]} "
                      f"S={q.shape[1]}; using SDPA")
     return _sdpa(q, k, v, causal, scale)
@@ -112,13 +169,11 @@ def attention_qkv_rope(qkv, nq, nkv, rope=None, position_ids=None, causal=True, 
             cos = rope.cos if rope is not None else None
             sin = rope.sin if rope is not None else None
             return _FlashAttnQKVRope.apply(qkv, cos, sin, nq, nkv, causal, scale, pos)
-        warning_once(f"sxe attention: HIP flash kernel does not cover dtype={qkv.dtype} D={D} S={qkv.shape[1]}; "
-                     f"using RoPE kernel + SDPA")
     if rope is not None:
         from .rope import apply_rope_qkv_
         qkv = apply_rope_qkv_(qkv, rope, nq + nkv, position_ids)
     q, k, v = qkv[:, :, :nq], qkv[:, :, nq:nq + nkv], qkv[:, :, nq + nkv:]
-    return _sdpa(q, k, v, causal, scale)
+    return attention(q, k, v, causal, scale)
 
 
 def attention_with_lse(q, k, v, causal=True, softmax_scale=None):
@@ -126,6 +181,12 @@ def attention_with_lse(q, k, v, causal=True, softmax_scale=None):
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if q.is_cuda and hip_supported(q, k, v) and q.shape[1] == k.shape[1]:
         return torch.ops.sxe.flash_attn_fwd(q, k, v, bool(causal), float(scale))
+    if q.is_cuda and hip_paddable(q, k, v):
+        S, D = q.shape[1], q.shape[-1]
+        Sp = -(-S // TILE) * TILE
+        o, lse = torch.ops.sxe.flash_attn_fwd(_pad(q, Sp, HEAD_DIM), _pad(k, Sp, HEAD_DIM), _pad(v, Sp, HEAD_DIM),
+                                              bool(causal), float(scale), S)
+        return o[:, :S, :, :D].to(q.dtype), lse[:, :, :S].contiguous()
     return reference_attention(q, k, v, causal, scale, return_lse=True)
 
 

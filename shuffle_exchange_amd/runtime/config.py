@@ -387,6 +387,37 @@ class SXEConfig:
         self.scheduler_params = dict(m.scheduler.params) if m.scheduler else {}
         self.comms_logger = m.comms_logger
         self.seed = m.seed
+        self.ignored_knobs = self._check_ignored_knobs()
+
+    # Reference knobs that are accepted for config compatibility but have no effect here, with the
+    # reason. Setting one explicitly logs a warning (never silent); ``ignored_knobs`` lists them.
+    IGNORED_ZERO_KNOBS = {
+        "sub_group_size": "the fused optimizer step is ONE multi-tensor HIP launch over all fp32 chunks "
+                          "(the host tier streams its own fixed-size buffers)",
+        "round_robin_gradients": "gradient partitions are flat units reduce-scattered straight into their owner",
+        "mics_hierarchical_params_gather": "single-node xGMI: the MiCS shard group is gathered in one step",
+        "allgather_bucket_size": "ZeRO-1/2 all-gather one flat unit at a time (units are sized by reduce_bucket_size)",
+        "zero_quantized_nontrainable_weights": "frozen weights are not partitioned by ZeRO-3 here (kept resident)",
+        "contiguous_gradients": "gradients always land in contiguous flat units",
+        "use_multi_rank_bucket_allreduce": "ZeRO-1/2 always use a true reduce-scatter",
+        "legacy_stage1": "one ZeRO-1/2 implementation",
+        "memory_efficient_linear": "ops/linear.py always writes weight gradients into the ZeRO buffers",
+        "pipeline_loading_checkpoint": "checkpoint loading is not pipelined",
+    }
+
+    def _check_ignored_knobs(self):
+        zc = self.zero_config
+        set_ = set(getattr(zc, "model_fields_set", set()))
+        out = []
+        for k, why in self.IGNORED_ZERO_KNOBS.items():
+            if k in set_:
+                out.append((f"zero_optimization.{k}", why))
+        if self.model.sparse_gradients:
+            out.append(("sparse_gradients", "embedding gradients are reduced densely inside the flat units "
+                                            "(same numerics; one large collective instead of a sparse all-gather)"))
+        for k, why in out:
+            logger.warning(f"config: '{k}' is accepted but has no effect: {why}")
+        return out
 
     def _solve_batch(self):
         m = self.model

@@ -48,6 +48,46 @@ _DTYPE = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16, 
           "float16": torch.float16, "bfloat16": torch.bfloat16}
 
 
+def broadcast_coalesced(tensors, src, group, bucket_bytes):
+    """Broadcast every tensor from ``src``: tensors of at least ``bucket_bytes`` in place, smaller
+    ones packed per dtype into flat buckets of at most ``bucket_bytes`` (one collective per bucket).
+    Returns the number of collectives issued."""
+    n_coll = 0
+    pending = {}
+
+    def flush(ts):
+        nonlocal n_coll
+        flat = torch.cat([t.reshape(-1) for t in ts])
+        dist.broadcast(flat, src=src, group=group)
+        n_coll += 1
+        o = 0
+        for t in ts:
+            k = t.numel()
+            t.copy_(flat[o:o + k].view_as(t))
+            o += k
+
+    for t in tensors:
+        nbytes = t.numel() * t.element_size()
+        if nbytes >= bucket_bytes or not t.is_contiguous():
+            c = t.contiguous()
+            dist.broadcast(c, src=src, group=group)
+            if c is not t:
+                t.copy_(c)
+            n_coll += 1
+            continue
+        key = (t.dtype, t.device)
+        lst, size = pending.get(key, ([], 0))
+        if size + nbytes > bucket_bytes:
+            flush(lst)
+            lst, size = [], 0
+        lst.append(t)
+        pending[key] = (lst, size + nbytes)
+    for lst, _ in pending.values():
+        if lst:
+            flush(lst)
+    return n_coll
+
+
 def _split_tp_replicated(model_parameters, tp):
     """Separate TP-sharded from TP-replicated parameters so the global gradient norm counts the
     replicated ones once (their grads are identical on every TP rank)."""
@@ -116,6 +156,9 @@ class SXEEngine(nn.Module):
         self._configure_distributed_model(model, dont_change_device)
         self.tput_timer = ThroughputTimer(batch_size=cfg.train_batch_size, steps_per_output=cfg.steps_per_print,
                                           seq_len=None)
+        self.tput_timer.world_size = groups.get_data_parallel_world_size()
+        self._n_params = sum(getattr(p, "ds_numel", p.numel()) for p in model.parameters())
+        self._loss_acc = None
         self.training_dataloader = self.deepspeed_io(training_data) if training_data is not None else None
         self.optimizer = None
         self.basic_optimizer = None
@@ -237,11 +280,22 @@ class SXEEngine(nn.Module):
     def _configure_distributed_model(self, model, dont_change_device):
         dtype = self.model_dtype()
         tp = groups.get_tensor_model_parallel_world_size()
+        zero_init = any(hasattr(p, "ds_tensor") for p in model.parameters())
+        if zero_init and self._config.zero_optimization_stage < 3:
+            # zero.Init partitions belong to ZeRO-3; lower stages keep whole parameters on every rank
+            from .zero.partition_parameters import release_construction_partition
+            for p in model.parameters():
+                if hasattr(p, "ds_tensor_full"):
+                    p.data = p.ds_tensor_full().to(self.device)
+                    release_construction_partition(p)
+            zero_init = False
         if tp > 1 and groups._Registry.mpu is None and not getattr(model, "_sxe_tp_size", 0):
+            if zero_init:
+                raise ValueError("AutoTP training shards whole weights: build the model outside zero.Init "
+                                 "(or with zero.Init(partition=False)) when tensor_parallel.autotp_size > 1")
             # AutoTP training (reference engine.py:450-516 _configure_tensor_parallel)
             from ..module_inject.auto_tp import tp_model_init
             tp_model_init(model, tp, tp_group=groups.get_tensor_model_parallel_group())
-        zero_init = any(hasattr(p, "ds_tensor") for p in model.parameters())
         if not zero_init:
             if dtype != torch.float32:
                 model.to(dtype)
@@ -249,9 +303,15 @@ class SXEEngine(nn.Module):
                 model.to(self.device)
             self._broadcast_model()
 
+    # tensors up to this size are coalesced into one broadcast; larger ones go in place
+    BROADCAST_BUCKET_BYTES = 64 << 20
+
     def _broadcast_model(self):
         """Identical initial weights on every data-parallel replica (reference engine.py:1242-1261).
-        Coalesced per dtype into one flat broadcast to avoid per-parameter collectives."""
+        Large tensors are broadcast in place; small ones are coalesced into buckets of at most
+        ``BROADCAST_BUCKET_BYTES`` (no full-model staging copy: the extra HBM is one bucket).
+        Models built under a partitioning ``zero.Init`` never get here: their parameters were
+        broadcast one module at a time during construction."""
         if self.world_size == 1:
             return
         group = groups.get_sequence_data_parallel_group()
@@ -276,17 +336,7 @@ class SXEEngine(nn.Module):
                         dist.broadcast(p.data, src=edp_ranks[0], group=groups.get_expert_data_parallel_group(name))
         tensors = [p.data for p in self.module.parameters() if not is_moe_param(p)] + \
             [b for b in self.module.buffers()]
-        by_dtype = {}
-        for t in tensors:
-            by_dtype.setdefault(t.dtype, []).append(t)
-        for dt, ts in by_dtype.items():
-            flat = torch.cat([t.reshape(-1) for t in ts])
-            dist.broadcast(flat, src=src, group=group)
-            o = 0
-            for t in ts:
-                n = t.numel()
-                t.copy_(flat[o:o + n].view_as(t))
-                o += n
+        broadcast_coalesced(tensors, src, group, self.BROADCAST_BUCKET_BYTES)
 
     # ------------------------------------------------------------------------------- optimizer
     def _configure_basic_optimizer(self, model_parameters):
@@ -362,13 +412,18 @@ class SXEEngine(nn.Module):
                 host_step=host_step, offload_param=offload_param, quantized_weights=zc.zero_quantized_weights,
                 quantized_gradients=zc.zero_quantized_gradients, hpz_partition_size=zc.zero_hpz_partition_size,
                 max_reuse_distance=zc.max_reuse_distance, max_live_parameters=zc.max_live_parameters,
-                defer_reduce=zc.defer_reduce, retain_params=zc.retain_params, loco_param=zc.zeropp_loco_param)
+                defer_reduce=zc.defer_reduce, retain_params=zc.retain_params, loco_param=zc.zeropp_loco_param,
+                prefetch_bucket_size=(zc.prefetch_bucket_size if "prefetch_bucket_size" in zc.model_fields_set
+                                      and "prefetch_depth" not in zc.model_fields_set else None),
+                model_persistence_threshold=zc.model_persistence_threshold)
         elif stage in (1, 2):
             self.optimizer = ZeroStage12Optimizer(
                 basic, stage=stage, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks,
                 dp_group=dp_group, reduce_bucket_size=zc.reduce_bucket_size,
-                communication_data_type=self.communication_data_type, overlap_comm=True, shuffle_exchange_cfg=se,
-                mp_group=mp_group, timers=self.timers, host_step=host_step)
+                communication_data_type=self.communication_data_type, overlap_comm=zc.overlap_comm,
+                shuffle_exchange_cfg=se, mp_group=mp_group, timers=self.timers, host_step=host_step)
+            if zc.overlap_comm:
+                self.optimizer.attach_module(self.module)
         else:
             from .zero.stage0 import DataParallelOptimizer
             self.optimizer = DataParallelOptimizer(
@@ -387,7 +442,10 @@ class SXEEngine(nn.Module):
             if callable(client_lr_scheduler) and not hasattr(client_lr_scheduler, "step"):
                 self.lr_scheduler = client_lr_scheduler(self.basic_optimizer)
             else:
-                self.lr_scheduler = client_lr_scheduler
+                # built on the optimizer before initialize(): Twin-Flow offload may have split its
+                # param groups since (zero/offload.py split_param_groups)
+                from .zero.offload import expand_scheduler_groups
+                self.lr_scheduler = expand_scheduler_groups(client_lr_scheduler, self.basic_optimizer)
             return
         if self._config.scheduler_name:
             self.lr_scheduler = build_scheduler(self._config.scheduler_name, self.optimizer,
@@ -413,6 +471,8 @@ class SXEEngine(nn.Module):
                 and all(a.is_cuda for a in inputs if torch.is_tensor(a))):
             return self._graph_forward(inputs)
         self.timers(FORWARD_MICRO_TIMER).start()
+        if self.module.training and torch.is_grad_enabled():
+            self._tput_start(inputs, kwargs)
         if self.optimizer is not None and hasattr(self.optimizer, "forward_prologue"):
             self.optimizer.forward_prologue()
         if self.progressive_layer_drop is not None:
@@ -453,6 +513,8 @@ class SXEEngine(nn.Module):
         opt = self.optimizer
         opt.set_gradient_accumulation_boundary(boundary and not self._in_no_sync)
         opt.backward_prologue()
+        ld = loss.detach()
+        self._loss_acc = ld if self._loss_acc is None else self._loss_acc + ld
         scaled = loss * opt.loss_scale if self.fp16_enabled() else loss
         scaled.backward(retain_graph=retain_graph)
         if not self._in_no_sync:
@@ -479,8 +541,54 @@ class SXEEngine(nn.Module):
         self.micro_steps += 1
         self._boundary_override = None
         self.timers(STEP_MICRO_TIMER).stop()
+        rep = self.tput_timer.stop(global_step=boundary, report_speed=True)
+        if boundary:
+            self._write_monitor(rep)
         if boundary and self.wall_clock_breakdown() and self.global_steps % self.steps_per_print() == 0:
             self.timers.log([FORWARD_MICRO_TIMER, BACKWARD_MICRO_TIMER, STEP_MICRO_TIMER])
+
+    def _tput_start(self, inputs, kwargs):
+        """Start the throughput timer; learn tokens per sample and model FLOPs per sample from
+        the first token-id input (reference engine.py:2068 tput_timer.start)."""
+        t = self.tput_timer
+        if t.seq_len is None:
+            x = inputs[0] if inputs and torch.is_tensor(inputs[0]) else kwargs.get("input_ids")
+            if torch.is_tensor(x) and x.dim() >= 2 and not x.is_floating_point():
+                t.seq_len = int(x.shape[-1]) * max(1, self._config.sequence_parallel_size)
+                cfg = getattr(self.module, "cfg", None)
+                if cfg is not None and hasattr(cfg, "flops_per_token"):
+                    t.flops_per_sample = float(cfg.flops_per_token(t.seq_len)) * t.seq_len
+                else:
+                    t.flops_per_sample = 6.0 * self._n_params * t.seq_len
+        t.start()
+
+    def _write_monitor(self, rep):
+        """Monitor events at the optimizer step (reference engine.py:2204, 2459-2575): train loss,
+        lr, loss scale, throughput at each report, fwd/bwd/step times with wall_clock_breakdown.
+        Reading the loss is the one host sync, and it happens only when a monitor is enabled."""
+        loss, self._loss_acc = self._loss_acc, None
+        mon = self.monitor
+        if mon is None or not mon.enabled or self.global_rank != 0:
+            return
+        s = self.global_samples
+        ev = [("Train/Samples/lr", self.get_lr()[0], s)]
+        if loss is not None:
+            ev.append(("Train/Samples/train_loss", float(loss.float().reshape(-1)[0]), s))
+        if self.optimizer is not None and hasattr(self.optimizer, "loss_scale"):
+            ev.append(("Train/Samples/loss_scale", float(self.optimizer.loss_scale), s))
+        if rep:
+            ev.append(("Train/Samples/samples_per_sec", rep["samples_per_sec"], s))
+            if "tokens_per_sec" in rep:
+                ev.append(("Train/Samples/tokens_per_sec", rep["tokens_per_sec"], s))
+            if "tflops" in rep:
+                ev.append(("Train/Samples/tflops_per_gpu", rep["tflops"], s))
+        if self.wall_clock_breakdown():
+            for name, key in ((FORWARD_MICRO_TIMER, "forward"), (BACKWARD_MICRO_TIMER, "backward"),
+                              (STEP_MICRO_TIMER, "step")):
+                tm = self.timers.get_timers().get(name)
+                if tm is not None:
+                    ev.append((f"Train/Samples/elapsed_time_ms_{key}", tm.mean() * 1000.0, s))
+        mon.write_events(ev)
 
     def _autotuning_probe(self):
         """Autotuning experiments: time steps (start, end] and write the metric file, then exit
@@ -533,8 +641,6 @@ class SXEEngine(nn.Module):
             self.shuffle_exchange()
         if se.enabled and se.sync_period > 0 and self.global_steps % se.sync_period == 0:
             self.synchronization()
-        if self.monitor is not None and self.monitor.enabled and self.global_rank == 0:
-            self.monitor.write_events([("Train/Samples/lr", self.get_lr()[0], self.global_samples)])
 
     def train(self, mode=True):
         self.module.train(mode)
@@ -660,6 +766,8 @@ class SXEEngine(nn.Module):
         return d, model, optim
 
     def module_state_dict(self, exclude_frozen_parameters=False):
+        if hasattr(self.optimizer, "wait_params"):
+            self.optimizer.wait_params()
         if self.zero_optimization_stage() == 3:
             if self._config.zero_config.gather_16bit_weights_on_model_save:
                 return self._zero3_consolidated_16bit_state_dict()

@@ -104,9 +104,48 @@ class ZeroOptimizerBase:
                 st["step"] = 0
 
     # --------------------------------------------------------------------------------------------
+    def _norm_domains(self):
+        """Step-metadata layout, built once (collectively) on the first step.
+
+        The gradient norm of a rank is summed over its *norm domain*: the ranks holding different
+        pieces of the same model replica's gradients -- the connected closure of its partition
+        group (ZeRO chunks, or a Shuffle-exchange slice) and its model-parallel group (TP x PP).
+        The non-finite flag is agreed world-wide (the fork's world overflow check, reference
+        stage_1_and_2.py:2071-2073). Both travel in ONE all-reduce of a [D + 1] fp32 vector over
+        the world: slot ``domain`` carries this rank's sum of squares, slot D the non-finite count
+        (reference: a norm all-reduce per group plus a separate overflow all-reduce)."""
+        if getattr(self, "_meta", None) is not None:
+            return self._meta
+        W = dist.get_world_size()
+        if W == 1:
+            self._meta = (0, 1)
+            return self._meta
+        part = dist.group_ranks(self.partition_group) if self.partition_group is not None else [dist.get_rank()]
+        mp = dist.group_ranks(self.mp_group) if self.mp_group is not None else [dist.get_rank()]
+        extra = getattr(self, "extra_norm_group", None)
+        mp = list(mp) + (dist.group_ranks(extra) if extra is not None else [])
+        objs = [None] * W
+        import torch.distributed as tdist
+        tdist.all_gather_object(objs, (tuple(part), tuple(mp)))
+        parent = list(range(W))
+
+        def find(a):
+            while parent[a] != a:
+                parent[a] = parent[parent[a]]
+                a = parent[a]
+            return a
+        for r, (pr, mr) in enumerate(objs):
+            for q in list(pr) + list(mr):
+                ra, rb = find(r), find(q)
+                if ra != rb:
+                    parent[max(ra, rb)] = min(ra, rb)
+        roots = sorted({find(r) for r in range(W)})
+        self._meta = (roots.index(find(dist.get_rank())), len(roots))
+        return self._meta
+
     def _grad_norm_and_flags(self):
-        """Device-side: global grad norm over the partition group (unscaled), the clip/unscale
-        coefficient and the skip (non-finite) flag. No host synchronisation."""
+        """Device-side: global grad norm (unscaled), the clip/unscale coefficient and the skip
+        (non-finite) flag, with ONE small all-reduce for all step metadata. No host sync."""
         sq = None
         for g, gr in enumerate(self.grads):
             s = fused.sumsq(gr)
@@ -115,16 +154,17 @@ class ZeroOptimizerBase:
                 s = s * w
             sq = s if sq is None else sq + s
         sq = sq.reshape(1).float()
-        if self.partition_group is not None:  # None = unpartitioned (replicated) optimizer state
-            dist.all_reduce(sq, group=self.partition_group)
-        if self.mp_group is not None:
-            dist.all_reduce(sq, group=self.mp_group)
+        domain, D = self._norm_domains()
+        if D > 1 or dist.get_world_size() > 1:
+            meta = torch.zeros(D + 1, dtype=torch.float32, device=sq.device)
+            meta[domain:domain + 1] = torch.nan_to_num(sq, nan=0.0, posinf=0.0)
+            meta[D:] = (~torch.isfinite(sq)).float()
+            dist.all_reduce(meta, group=None, log_name="step_meta")
+            # a non-finite gradient anywhere in the world -> inf norm -> every rank skips the step
+            sq = torch.where(meta[D:] > 0, torch.full_like(sq, float("inf")), meta[domain:domain + 1])
         ls = float(self.loss_scaler.loss_scale)
         norm = sq.sqrt() / ls
         skip = (~torch.isfinite(norm)).float()
-        if self.overflow_group is not None:
-            # the fork's world-wide overflow agreement (reference stage_1_and_2.py:2071-2073)
-            dist.all_reduce(skip, op=dist.ReduceOp.MAX, group=self.overflow_group)
         coef = torch.full((1,), 1.0 / ls, dtype=torch.float32, device=norm.device)
         if self.clip_grad > 0:
             clip = torch.clamp(self.clip_grad / (torch.nan_to_num(norm, nan=0.0, posinf=0.0) + 1e-6), max=1.0)

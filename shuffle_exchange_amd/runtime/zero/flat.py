@@ -36,8 +36,9 @@ class FlatUnit:
         self.rank = rank_in_group
         self.dtype = dtype
         self.device = device
-        self.numels = [p.numel() for p in self.params]
-        self.shapes = [tuple(p.shape) for p in self.params]
+        # zero.Init-partitioned parameters carry their logical shape in ds_shape (p.data is empty)
+        self.shapes = [tuple(getattr(p, "ds_shape", p.shape)) for p in self.params]
+        self.numels = [math.prod(s) for s in self.shapes]
         self.offsets = []
         off = 0
         for n in self.numels:

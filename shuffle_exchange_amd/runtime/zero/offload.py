@@ -446,8 +446,8 @@ def split_param_groups(optimizer, ratio):
     Adam moments and update stay in HBM (fused HIP Adam), so HBM holds 6 + 12 (1 - ratio) bytes per
     trainable parameter and the host 12 ratio + staging: the ratio trades host RAM for HBM."""
     ratio = min(max(float(ratio), 0.0), 1.0)
-    out = []
-    for pg in optimizer.param_groups:
+    out, origin = [], []
+    for gi, pg in enumerate(optimizer.param_groups):
         params = list(pg["params"])
         total = sum(p.numel() for p in params)
         host, dev, start = [], [], 0
@@ -457,8 +457,27 @@ def split_param_groups(optimizer, ratio):
         for part, flag in ((host, True), (dev, False)):
             if part:
                 out.append(dict(pg, params=part, sxe_offload=flag))
+                origin.append(gi)
+    n_orig = len(optimizer.param_groups)
     optimizer.param_groups[:] = out
+    optimizer._sxe_group_origin = (n_orig, origin)
     return optimizer
+
+
+def expand_scheduler_groups(scheduler, optimizer):
+    """A client LR scheduler built before ``split_param_groups`` holds one entry per ORIGINAL
+    param group (``base_lrs``, ``_last_lr``, ``lr_lambdas`` ...): expand every such per-group list to
+    the split groups, so both parts of a group follow the group's schedule."""
+    info = getattr(optimizer, "_sxe_group_origin", None)
+    if info is None or scheduler is None:
+        return scheduler
+    n_orig, origin = info
+    if getattr(scheduler, "optimizer", None) is not None:
+        scheduler.optimizer = optimizer
+    for k, v in list(vars(scheduler).items()):
+        if isinstance(v, list) and len(v) == n_orig and k != "optimizer":
+            setattr(scheduler, k, [v[i] for i in origin])
+    return scheduler
 
 
 def OffloadOptimizer(*a, **kw):  # pragma: no cover - kept for the reference's class name

@@ -48,6 +48,22 @@ class DataParallelOptimizer(ZeroOptimizerBase):
                         self.param_unit[p] = u
             self.units.append(units)
         self._init_master()
+        # MoE: expert gradients differ across the expert-parallel group (each rank holds other
+        # experts) while dense gradients are identical there after the all-reduce. The norm domain
+        # therefore spans the EP group, with dense groups weighted 1/ep so they count once --
+        # otherwise ranks clip by different norms and the replicated dense weights drift apart.
+        moe_names = sorted({pg["name"] for pg in init_optimizer.param_groups if pg.get("moe", False)})
+        if moe_names:
+            from ...parallel import groups
+            eps = {groups.get_expert_parallel_world_size(n) for n in moe_names}
+            if len(eps) > 1:
+                raise NotImplementedError("ZeRO-0 with several expert-parallel sizes")
+            ep = eps.pop()
+            if ep > 1:
+                self.extra_norm_group = groups.get_expert_parallel_group(moe_names[0])
+                for pg in init_optimizer.param_groups:
+                    if not pg.get("moe", False):
+                        pg["norm_weight"] = pg.get("norm_weight", 1.0) / ep
         if hasattr(self.optimizer, "set_segments"):  # layer-wise optimizers (LAMB) on flat masters
             for g, units in enumerate(self.units):
                 segs, base = [], 0

@@ -90,6 +90,8 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
             self.partition_group = dp_group
         self._init_master()
         self._register_hooks()
+        self._module_units = None  # module -> units of its own params (set by attach_module)
+        self._pending_events = {}  # unit -> HIP event of its post-step gather (consumed by forward)
         log_dist(f"ZeRO-{stage}: {sum(len(u) for u in self.units)} units, slice_count={S}, "
                  f"slices={self.topo.num_slices}, shuffle_exchange="
                  f"{self.method if self.shuffle_exchange_enabled else 'off'}", ranks=[0])
@@ -209,6 +211,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                     self._reduce_unit(u)
 
     def _wait_comm(self):
+        self._drain_pending()
         if self.comm_stream is not None:
             torch.cuda.current_stream().wait_stream(self.comm_stream)
 
@@ -224,13 +227,74 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                 return
         self._fused_update(coef, skip)
         self.zero_grad_buffers()
-        if self.se is not None:
-            shards = [u.shard for units in self.units for u in units]
-            self.se.sync(shards, self._device_masters())
-        self._allgather_params()
+        self._post_step_exchange()
         self.global_step += 1
 
+    def attach_module(self, module):
+        """Let the next forward overlap the post-step parameter exchange: every module that owns
+        parameters gets a pre-forward hook that waits (on the device, no host sync) for the
+        events of its own units only, so layer 0 computes while later units still gather."""
+        mu = {}
+        for m in module.modules():
+            us = []
+            for p in m.parameters(recurse=False):
+                u = self.param_unit.get(p)
+                if u is not None and u not in us:
+                    us.append(u)
+            if us:
+                mu[m] = us
+                self._hooks.append(m.register_forward_pre_hook(self._make_wait_hook(us)))
+        self._module_units = mu
+
+    def _make_wait_hook(self, units):
+        def pre(mod, args):
+            if not self._pending_events:
+                return
+            cur = torch.cuda.current_stream()
+            for u in units:
+                ev = self._pending_events.pop(u, None)
+                if ev is not None:
+                    cur.wait_event(ev)
+        return pre
+
+    def _post_step_exchange(self):
+        """Inter-slice synchronisation (Shuffle-exchange) and the in-slice all-gather, unit by unit
+        on the comm stream: the Shuffle-exchange all-reduce of unit k+1 overlaps nothing on the
+        comm stream but the all-gather of unit k is already done, and the compute stream is free
+        to start the next forward (it waits per unit via ``attach_module``'s hooks)."""
+        units = [u for us in self.units for u in us]
+        masters = self._device_masters()
+        stream = self.comm_stream if self._module_units is not None else None
+        if stream is not None:
+            stream.wait_stream(torch.cuda.current_stream())
+        with get_accelerator().stream(stream):
+            gossip = self.se is not None and self.se.method == "Gossip"
+            if gossip:  # push-sum draws its senders once per step for all chunks together
+                self.se.sync([u.shard for u in units], masters)
+            for i, u in enumerate(units):
+                if self.se is not None and not gossip:
+                    self.se.sync([u.shard], [masters[i]] if masters is not None else None)
+                if u.topo.S > 1:
+                    dist.all_gather_into_tensor(u.flat, u.shard, group=u.topo.slice_group)
+                if stream is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(stream)
+                    self._pending_events[u] = ev
+        # units no forward hook consumed are waited for by the next step / checkpoint at the latest
+
+    def wait_params(self):
+        """Make the compute stream wait for every in-flight post-step parameter exchange."""
+        self._drain_pending()
+
+    def _drain_pending(self):
+        if self._pending_events:
+            cur = torch.cuda.current_stream()
+            for ev in self._pending_events.values():
+                cur.wait_event(ev)
+            self._pending_events.clear()
+
     def _allgather_params(self):
+        self._drain_pending()
         for units in self.units:
             for u in units:
                 if u.topo.S > 1:

@@ -32,6 +32,7 @@ from ...accelerator import get_accelerator
 from ...utils.logging import log_dist
 from .base import ZeroOptimizerBase
 from .flat import FlatUnit
+from .partition_parameters import release_construction_partition
 from .shuffle_exchange import ShuffleExchange, SliceTopology
 
 RELEASED, INFLIGHT, AVAILABLE = 0, 1, 2
@@ -109,7 +110,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                  average_master=False, host_step=None, offload_param=False, quantized_weights=False,
                  quantized_gradients=False, hpz_partition_size=1, quant_group_size=128, grad_quant_bits=8,
                  max_reuse_distance=1_000_000_000, max_live_parameters=1_000_000_000, defer_reduce=False,
-                 retain_params=False, loco_param=None):
+                 retain_params=False, loco_param=None, prefetch_bucket_size=None,
+                 model_persistence_threshold=2**63 - 1):
         acc = get_accelerator()
         device = torch.device(acc.current_device_name())
         self.module = module
@@ -160,7 +162,13 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         else:
             self.hpz = 1
         self.prefetch_depth = max(0, int(prefetch_depth))
+        # stage3_prefetch_bucket_size (when given instead of prefetch_depth): prefetch the next
+        # fetch groups until this many elements are in flight (at least one group)
+        self.prefetch_numel = int(prefetch_bucket_size) if prefetch_bucket_size else None
         self.persist_thr = int(param_persistence_threshold)
+        # stage3_model_persistence_threshold: cap on the total elements kept persistent
+        self.model_persist_thr = int(model_persistence_threshold)
+        self._persist_total = 0
         self.max_reuse_distance = int(max_reuse_distance)
         self.max_live_parameters = int(max_live_parameters)
         self._kept_numel = 0
@@ -266,12 +274,20 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         u = FlatUnit(params, self.S, self.topo.offset, dtype, self.device, name=name, materialize_full=False)
         u.fg = fg
         u.owner = self
-        u.persistent = (self.S == 1 and not self.offload_param) or (u.numel < self.persist_thr)
+        u.persistent = (self.S == 1 and not self.offload_param) or (
+            u.numel < self.persist_thr and self._persist_total + u.numel <= self.model_persist_thr)
+        if u.persistent:
+            self._persist_total += u.numel
         flat = torch.zeros(u.padded, dtype=dtype, device=self.device)
         with torch.no_grad():
             for p, o, n in zip(u.params, u.offsets, u.numels):
-                src = p.ds_tensor_full() if hasattr(p, "ds_tensor_full") else p.data
-                flat[o:o + n].copy_(src.reshape(-1))
+                if hasattr(p, "ds_tensor_full"):
+                    # zero.Init construction partition: gather this one parameter, then drop the
+                    # per-parameter chunk (the unit shard below replaces it)
+                    flat[o:o + n].copy_(p.ds_tensor_full().reshape(-1))
+                    release_construction_partition(p)
+                else:
+                    flat[o:o + n].copy_(p.data.reshape(-1))
         u.flat = flat
         u.link_params()
         if u.persistent:
@@ -526,6 +542,15 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         if fg.idx not in order:
             return
         i = order.index(fg.idx)
+        if self.prefetch_numel is not None:
+            acc = 0
+            for j in order[i + 1:]:
+                if acc >= self.prefetch_numel:
+                    break
+                nxt = self.fgroups[j]
+                self._fetch(nxt, wait=False)
+                acc += sum(u.padded for u in nxt.units if not u.persistent)
+            return
         for j in order[i + 1:i + 1 + self.prefetch_depth]:
             self._fetch(self.fgroups[j], wait=False)
 

@@ -139,7 +139,10 @@ class NoopTimer:
 
 
 class ThroughputTimer:
-    """samples/s, tokens/s and model TFLOPs per GPU over the steps since start."""
+    """samples/s, tokens/s and model TFLOPs per GPU over the global steps since ``start_step``
+    (reference utils/timer.py:199). Each micro-step's [forward .. step] segment is bracketed by
+    HIP events: nothing synchronises the host until a report is due (the reference synchronises
+    the device at every start/stop)."""
 
     def __init__(self, batch_size, seq_len=None, flops_per_sample=None, start_step=2, steps_per_output=50,
                  monitor_memory=False, logging_fn=None):
@@ -150,50 +153,79 @@ class ThroughputTimer:
         self.steps_per_output = steps_per_output
         self.logging = logging_fn or (lambda m: log_dist(m, ranks=[0]))
         self.monitor_memory = monitor_memory
+        self.use_events = get_accelerator().gpu
         self.global_step_count = 0
         self.micro_step_count = 0
         self.total_elapsed_time = 0.0
         self.step_elapsed_time = 0.0
         self._t = None
+        self._pending = []
         self.started = False
+        self.last_report = None
 
     def update_epoch_count(self):
         pass
 
+    def _now(self):
+        if self.use_events:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
     def start(self):
+        if self.started:
+            return
         self.started = True
         if self.global_step_count >= self.start_step:
-            get_accelerator().synchronize()
-            self._t = time.perf_counter()
+            self._t = self._now()
+
+    def _drain(self):
+        if not self._pending:
+            return
+        if self.use_events:
+            self._pending[-1][1].synchronize()
+            dt = sum(a.elapsed_time(b) for a, b in self._pending) / 1000.0
+        else:
+            dt = sum(b - a for a, b in self._pending)
+        self._pending = []
+        self.total_elapsed_time += dt
+        self.step_elapsed_time += dt
 
     def stop(self, global_step=False, report_speed=True):
         if not self.started:
-            return
+            return None
         self.started = False
         self.micro_step_count += 1
         if global_step:
             self.global_step_count += 1
         if self._t is not None:
-            get_accelerator().synchronize()
-            dt = time.perf_counter() - self._t
+            self._pending.append((self._t, self._now()))
             self._t = None
-            self.total_elapsed_time += dt
-            self.step_elapsed_time += dt
-            if global_step and report_speed and self.global_step_count % self.steps_per_output == 0:
-                msg = (f"step={self.global_step_count} samples/s={self.avg_samples_per_sec():.2f}")
-                if self.seq_len:
-                    msg += f" tokens/s={self.avg_tokens_per_sec():.1f}"
-                if self.flops_per_sample:
-                    msg += f" TFLOPs={self.avg_tflops():.1f}"
-                if self.monitor_memory:
-                    msg += f" mem_alloc_GB={get_accelerator().memory_allocated() / 2**30:.2f}"
-                self.logging(msg)
-                self.step_elapsed_time = 0.0
+        if global_step and report_speed and self.steps_per_output and \
+                self.global_step_count % self.steps_per_output == 0 and self._timed_steps() > 0:
+            self._drain()
+            rep = {"samples_per_sec": self.avg_samples_per_sec()}
+            msg = f"step={self.global_step_count} samples/s={rep['samples_per_sec']:.2f}"
+            if self.seq_len:
+                rep["tokens_per_sec"] = self.avg_tokens_per_sec()
+                msg += f" tokens/s={rep['tokens_per_sec']:.1f}"
+            if self.flops_per_sample:
+                rep["tflops"] = self.avg_tflops()
+                msg += f" TFLOPs/GPU={rep['tflops']:.1f}"
+            if self.monitor_memory:
+                msg += f" mem_alloc_GB={get_accelerator().memory_allocated() / 2**30:.2f}"
+            self.logging(msg)
+            self.step_elapsed_time = 0.0
+            self.last_report = rep
+            return rep
+        return None
 
     def _timed_steps(self):
         return max(0, self.global_step_count - self.start_step)
 
     def avg_samples_per_sec(self):
+        self._drain()
         n = self._timed_steps()
         return (n * self.batch_size / self.total_elapsed_time) if n > 0 and self.total_elapsed_time > 0 else 0.0
 
@@ -201,4 +233,7 @@ class ThroughputTimer:
         return self.avg_samples_per_sec() * (self.seq_len or 1)
 
     def avg_tflops(self):
-        return self.avg_samples_per_sec() * (self.flops_per_sample or 0) / 1e12
+        """Model TFLOP/s per GPU (``flops_per_sample`` is the whole-model cost of one sample;
+        ``batch_size`` is the global batch, so divide by the data-parallel world)."""
+        ws = max(1, getattr(self, "world_size", 1))
+        return self.avg_samples_per_sec() * (self.flops_per_sample or 0) / ws / 1e12

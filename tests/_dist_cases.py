@@ -309,3 +309,84 @@ def case_zero3_defer(rank, world, defer, steps, mbs, gas, seq, retain=False):
     opt._launch_gather = orig_gather
     return {"params": full_params(eng), "rs": n_rs[0], "ag": n_ag[0], "defer": eng.optimizer.defer_reduce,
             "n_units": sum(len(us) for us in opt.units)}
+
+
+def case_zero_init(rank, world, layers, steps):
+    """zero.Init partitions at construction (different RNG per rank), ZeRO-3 trains from it."""
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+    torch.manual_seed(100 + rank)  # deliberately different per rank
+    cfg = llama_config("llama-tiny", num_hidden_layers=layers)
+    init = sxe.zero.Init(dtype=torch.float32)
+    with init:
+        model = LlamaForCausalLM(cfg)
+    empty = all(p.data.numel() == 0 for p in model.parameters())
+    full_numel = cfg.num_params()
+    layer_numel = sum(p.ds_numel for p in model.layers[0].parameters())
+    emb_numel = model.embed_tokens.weight.ds_numel
+    # whole-tensor edit between construction and initialize(): rank 0's value must win everywhere
+    w = model.norm.weight
+    with sxe.zero.GatheredParameters([w], modifier_rank=0):
+        w.data.fill_(1.5 if rank == 0 else -7.0)
+    ds = {"train_micro_batch_size_per_gpu": 1, "zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 0},
+          "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    left = sum(1 for p in model.parameters() if hasattr(p, "ds_tensor"))
+    before = full_params(eng)
+    g = torch.Generator().manual_seed(7)
+    losses = []
+    for _ in range(steps):
+        b = torch.randint(0, cfg.vocab_size, (world, 16), generator=g)[rank:rank + 1]
+        loss = eng(b, labels=b)
+        eng.backward(loss)
+        eng.step()
+        losses.append(float(loss.detach()))
+    return {"stats": dict(init.stats), "empty": empty, "full_numel": full_numel, "layer_numel": layer_numel,
+            "emb_numel": emb_numel, "left": left, "before": before, "after": full_params(eng), "losses": losses}
+
+
+def case_broadcast_coalesced(rank, world):
+    from shuffle_exchange_amd.runtime.engine import broadcast_coalesced
+    torch.manual_seed(rank)
+    ts = [torch.randn(1000), torch.randn(10), torch.randn(300, 3).t(), torch.randn(5000).double(), torch.randn(7)]
+    n = broadcast_coalesced(ts, 0, None, bucket_bytes=4096)
+    torch.manual_seed(0)
+    ref = [torch.randn(1000), torch.randn(10), torch.randn(300, 3).t(), torch.randn(5000).double(), torch.randn(7)]
+    return {"ok": all(torch.equal(a, b) for a, b in zip(ts, ref)), "n": n}
+
+
+def case_step_meta(rank, world, stage, se_kwargs, steps):
+    """Count the collectives of the optimizer step: one fused step-metadata all-reduce per step."""
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd import comm
+    model, cfg = tiny_llama(0)
+    ds = {"train_micro_batch_size_per_gpu": 1, "gradient_clipping": 1.0,
+          "zero_optimization": {"stage": stage, "stage3_param_persistence_threshold": 0},
+          "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds, **(se_kwargs or {}))
+    b = torch.randint(0, cfg.vocab_size, (1, 16), generator=torch.Generator().manual_seed(rank))
+    comm.reset_comms_stats()
+    for _ in range(steps):
+        loss = eng(b, labels=b)
+        eng.backward(loss)
+        eng.step()
+    return comm.get_op_counts()
+
+
+def case_mixtral_dense_sync(rank, world):
+    """ZeRO-0 + expert parallelism with clipping: dense weights stay identical across ranks."""
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd.models.mixtral import MixtralForCausalLM, mixtral_config
+    torch.manual_seed(0)
+    cfg = mixtral_config("mixtral-tiny", ep_size=2)
+    model = MixtralForCausalLM(cfg)
+    ds = {"train_micro_batch_size_per_gpu": 2, "zero_optimization": {"stage": 0},
+          "optimizer": {"type": "AdamW", "params": {"lr": 3e-3}}, "gradient_clipping": 0.01}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    ids = torch.randint(0, cfg.vocab_size, (2, 32), generator=torch.Generator().manual_seed(7 + rank))
+    for _ in range(3):
+        loss = eng(ids, labels=ids)
+        eng.backward(loss)
+        eng.step()
+    from shuffle_exchange_amd.moe.utils import is_moe_param
+    return {n: p.detach().float().clone() for n, p in model.named_parameters() if not is_moe_param(p)}

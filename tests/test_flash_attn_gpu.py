@@ -98,3 +98,42 @@ def test_flash_perf_report():
     torch.cuda.synchronize()
     tfb = 3.5 * flops / (e0.elapsed_time(e1) / 10 / 1e3) / 1e12
     print(f"\n[flash] fwd {tf:.0f} TFLOP/s, fwd+bwd {tfb:.0f} TFLOP/s (model FLOPs, 3.5x fwd)")
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("B,S,H,Hk,D", [(2, 100, 4, 4, 64), (1, 200, 8, 2, 128), (2, 128, 4, 2, 80),
+                                        (1, 77, 2, 1, 96), (2, 300, 12, 12, 64)])
+def test_flash_padded_shapes_run_hip(causal, B, S, H, Hk, D, monkeypatch):
+    """Head dims below 128 and sequence lengths that are not multiples of 128 run the HIP kernels on
+    padded copies (kv_len masks the padded keys) -- never SDPA -- and match the fp32 reference."""
+    import torch.nn.functional as F
+    from shuffle_exchange_amd.ops import attention as A
+    calls = []
+    monkeypatch.setattr(A, "_sdpa", lambda *a, **k: calls.append(1) or F.scaled_dot_product_attention(*a))
+    torch.manual_seed(0)
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    o = A.attention(q, k, v, causal=causal)
+    assert not calls
+    q2, k2, v2 = (t.detach().float().requires_grad_() for t in (q, k, v))
+    o2 = A.reference_attention(q2, k2, v2, causal=causal)
+    assert o.shape == o2.shape
+    assert _rel(o, o2) < 1e-2
+    do = torch.randn_like(o2)
+    (o.float() * do).sum().backward()
+    (o2 * do).sum().backward()
+    for a, b in ((q.grad, q2.grad), (k.grad, k2.grad), (v.grad, v2.grad)):
+        assert a.shape == b.shape and _rel(a, b) < 2e-2
+
+
+def test_smoke_shape_llama_d64_uses_hip():
+    """The driver's smoke shape (hidden 256, 4 heads -> D = 64, S = 128) runs the HIP kernels."""
+    from shuffle_exchange_amd.ops import attention as A
+    from shuffle_exchange_amd.ops.rope import RopeCache
+    B, S, nq, nkv, D = 2, 128, 4, 2, 64
+    cache = RopeCache(D, 256, 10000.0, device="cuda")
+    qkv = torch.randn(B, S, nq + 2 * nkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    o = A.attention_qkv_rope(qkv * 1.0, nq, nkv, cache)
+    o.float().square().mean().backward()
+    assert o.shape == (B, S, nq, D) and torch.isfinite(qkv.grad).all()

@@ -112,3 +112,103 @@ def test_gpt_neox_injection_logits_and_generate(parallel):
     assert n == 2
     torch.testing.assert_close(got, ref, atol=5e-5, rtol=1e-4)
     assert torch.equal(got_gen, ref_gen)
+
+
+def test_decoder_bert_is_not_injected():
+    """BERT/RoBERTa configured as decoders (causal self-attention + KV cache) keep their HF layers."""
+    cfg = transformers.BertConfig(vocab_size=200, hidden_size=64, num_hidden_layers=2, num_attention_heads=4,
+                                  intermediate_size=128, max_position_embeddings=64, is_decoder=True)
+    torch.manual_seed(0)
+    model = transformers.BertLMHeadModel(cfg).eval()
+    ids = torch.randint(3, 200, (2, 10))
+    with torch.no_grad():
+        ref = model(ids).logits
+        n = rm.replace_transformer_layer(model)
+        got = model(ids).logits
+    assert n == 0
+    torch.testing.assert_close(got, ref)
+
+
+def test_fused_layers_share_weight_memory_and_delegate_after_to():
+    """The original module's parameters are views of the fused tensors (no second copy of the
+    weights), delegation still matches HF, also after a dtype move of the model."""
+    model = _bert("Bert")
+    ids = torch.randint(3, 200, (2, 12))
+    with torch.no_grad():
+        ref = model(ids, output_attentions=True)
+        n = rm.replace_transformer_layer(model)
+    assert n == 2
+    layer = model.encoder.layer[0]
+    orig = layer.orig
+    assert orig.attention.self.query.weight.data_ptr() == layer.w_qkv.data_ptr()
+    assert orig.output.dense.weight.data_ptr() == layer.w_out.data_ptr()
+    with torch.no_grad():
+        got = model(ids, output_attentions=True)  # delegated path
+    torch.testing.assert_close(got.last_hidden_state, ref.last_hidden_state, atol=2e-5, rtol=1e-4)
+    model.double()
+    assert orig.attention.self.key.weight.dtype == torch.float64
+    assert orig.attention.self.key.weight.data_ptr() == layer.w_qkv.data_ptr() + 64 * 64 * 8
+    with torch.no_grad():
+        got64 = model(ids, output_attentions=True).last_hidden_state
+    torch.testing.assert_close(got64.float(), ref.last_hidden_state, atol=1e-4, rtol=1e-4)
+
+
+def test_gpt2_left_padded_batched_generate():
+    model = _gpt2()
+    ids = torch.randint(1, 300, (2, 9))
+    mask = torch.ones_like(ids)
+    ids[1, :3] = 0
+    mask[1, :3] = 0  # left padding
+    with torch.no_grad():
+        ref = model.generate(ids, attention_mask=mask, max_new_tokens=5, do_sample=False, pad_token_id=0)
+        rm.replace_transformer_layer(model)
+        got = model.generate(ids, attention_mask=mask, max_new_tokens=5, do_sample=False, pad_token_id=0)
+    assert torch.equal(got, ref)
+
+
+def test_init_inference_skips_injection_under_quantization():
+    import shuffle_exchange_amd as sxe
+    model = _gpt2()
+    ids = torch.randint(0, 300, (1, 8))
+    eng = sxe.init_inference(model, dtype=torch.float32, replace_with_kernel_inject=True,
+                             weight_quantization={"post_init_quant": {"c_fc": {"num_bits": 8, "group_size": 64}}})
+    assert eng.injected_layers == 0 and eng.injection_skipped == "weight_quantization"
+    assert not any(isinstance(m, rm._Fused) for m in model.modules())
+    with torch.no_grad():
+        out = eng(ids.to(eng.device), use_cache=False).logits
+    assert torch.isfinite(out).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arch", ["gpt2", "bert"])
+def test_real_head_dim_injection_runs_hip_flash(arch, monkeypatch):
+    """Real GPT-2 / BERT-base geometry (768 hidden, 12 heads -> D = 64, S = 200): the injected layers
+    run the HIP flash kernels (padded head dim / sequence), not SDPA."""
+    from shuffle_exchange_amd.ops import attention as A
+    from shuffle_exchange_amd.ops import native
+    native.require_hip()
+    calls = {"hip": 0}
+    real = torch.ops.sxe.flash_attn_fwd
+
+    class _Spy:
+        def __call__(self, *a, **k):
+            calls["hip"] += 1
+            return real(*a, **k)
+    monkeypatch.setattr(A, "_sdpa", lambda *a, **k: (_ for _ in ()).throw(AssertionError("SDPA fallback")))
+    torch.manual_seed(0)
+    if arch == "gpt2":
+        cfg = transformers.GPT2Config(vocab_size=512, n_positions=256, n_embd=768, n_layer=2, n_head=12)
+        model = transformers.GPT2LMHeadModel(cfg).eval().to("cuda", torch.bfloat16)
+    else:
+        cfg = transformers.BertConfig(vocab_size=512, hidden_size=768, num_hidden_layers=2, num_attention_heads=12,
+                                      intermediate_size=3072, max_position_embeddings=256)
+        model = transformers.BertModel(cfg).eval().to("cuda", torch.bfloat16)
+    ids = torch.randint(0, 512, (2, 200), device="cuda")
+    with torch.no_grad():
+        ref = model(ids).logits.float() if arch == "gpt2" else model(ids).last_hidden_state.float()
+        replace_transformer_layer(model)
+        monkeypatch.setattr(torch.ops.sxe, "flash_attn_fwd", _Spy(), raising=False)
+        got = model(ids).logits.float() if arch == "gpt2" else model(ids).last_hidden_state.float()
+    assert calls["hip"] == 2
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel < 2e-2, rel

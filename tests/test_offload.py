@@ -127,3 +127,18 @@ def test_aio_roundtrip(tmp_path):
     assert torch.equal(back, big[4096:])
     with pytest.raises(RuntimeError):
         h.sync_pread(torch.empty(10), tmp_path / "missing.bin")
+
+
+def test_client_scheduler_survives_twin_flow_split():
+    """A torch LR scheduler built on the client optimizer before initialize() keeps driving every
+    split part of its groups (ADVICE: strict zip over base_lrs raised after the split)."""
+    from shuffle_exchange_amd.runtime.zero.offload import expand_scheduler_groups, split_param_groups
+    ps = [torch.nn.Parameter(torch.zeros(n)) for n in (10, 30, 20, 40)]
+    opt = torch.optim.AdamW([{"params": ps[:3], "lr": 1.0}, {"params": ps[3:], "lr": 2.0}])
+    sch = torch.optim.lr_scheduler.LambdaLR(opt, [lambda s: 0.5 ** s, lambda s: 0.1 * s])
+    split_param_groups(opt, 0.5)
+    expand_scheduler_groups(sch, opt)
+    for _ in range(2):
+        opt.step()
+        sch.step()
+    assert [g["lr"] for g in opt.param_groups] == [0.25, 0.25, 2.0 * 0.2]

@@ -216,3 +216,54 @@ def test_zero3_retain_params_in_step_gathers_once_per_step():
     assert n[0]["ag"] >= 2 * r[0]["ag"], (n[0]["ag"], r[0]["ag"])  # 16 vs 6 per step at gas 3
     for k, v in n[0]["params"].items():
         torch.testing.assert_close(r[0]["params"][k], v, atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_zero_init_partitions_at_construction(world):
+    """zero.Init: per-rank construction memory is ~full/W + one module, ranks agree on the weights
+    even with different seeds, GatheredParameters(modifier_rank=0) edits propagate, and ZeRO-3
+    trains from the partitioned model (reference partition_parameters.py:1141, :1109-1116)."""
+    layers = 4
+    res = run_dist(C.case_zero_init, world, layers, 2)
+    r0 = res[0]
+    st = r0["stats"]
+    full = r0["full_numel"]
+    assert r0["empty"] and r0["left"] == 0
+    # one module's own parameters whole at a time: the largest is a decoder layer or the embedding
+    assert st["peak_full_numel"] <= max(r0["layer_numel"], r0["emb_numel"])
+    assert st["peak_full_numel"] < full / 2
+    for r in res:
+        assert abs(r["stats"]["partition_numel"] - full / world) <= 64 * st["params"]
+    for r in res[1:]:
+        for k in r0["before"]:
+            assert torch.equal(r["before"][k], r0["before"][k]), k
+            assert torch.allclose(r["after"][k], r0["after"][k], atol=1e-6), k
+    assert torch.all(r0["before"]["norm.weight"] == 1.5)
+    assert all(l == l for l in r0["losses"])
+
+
+def test_broadcast_coalesced_in_place_and_bucketed():
+    res = run_dist(C.case_broadcast_coalesced, 2)
+    for r in res:
+        assert r["ok"]
+    # 5000 doubles (40 KB) and the non-contiguous one go alone; the 1000+10+7 floats share a bucket
+    assert res[0]["n"] == 3
+
+
+@pytest.mark.parametrize("stage,se", [(0, None), (2, None), (3, None), (2, {"method": "RR", "slice_count": 2}),
+                                      (1, {"method": "H-RR", "slice_count": 1})])
+def test_one_step_metadata_collective_per_step(stage, se):
+    """Gradient norm and the world-wide overflow flag travel in ONE all-reduce per optimizer step
+    (the reference issues a norm all-reduce per group plus a separate overflow all-reduce)."""
+    steps = 3
+    res = run_dist(C.case_step_meta, 4, stage, se, steps)
+    for counts in res:
+        assert counts.get("step_meta", 0) == steps, counts
+        if se is None:
+            assert counts.get("all_reduce", 0) == (0 if stage else counts.get("all_reduce", 0)), counts
+
+
+def test_moe_zero0_clipping_keeps_dense_weights_in_sync():
+    a, b = run_dist(C.case_mixtral_dense_sync, 2)
+    for k in a:
+        assert torch.allclose(a[k], b[k], atol=1e-6), k
