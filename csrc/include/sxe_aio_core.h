@@ -5,7 +5,9 @@
 // <-> file range) is split into `block_size` pieces served with positional pread/pwrite, so one
 // large swap is spread over `num_threads` concurrent NVMe queues. O_DIRECT when buffer address,
 // size and offset are 4 KiB aligned and the filesystem accepts it; buffered I/O otherwise.
-// Errors are reported by wait()/wait_request() as std::runtime_error (first error wins).
+// Errors are kept per request: wait_request(id) throws only that request's error (a failing read
+// of one client never surfaces in another client's wait); wait() throws the first outstanding one
+// and clears them all. Both report std::runtime_error.
 //
 // Kept free of torch so the same code builds into the sanitizer stress test
 // (csrc/tests/aio_stress.cpp, -fsanitize=thread / address,undefined; tests/test_sanitizers.py).
@@ -25,6 +27,7 @@
 #include <sys/stat.h>
 #include <thread>
 #include <unistd.h>
+#include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
@@ -109,7 +112,11 @@ class Engine {
     done_cv_.wait(lk, [this] { return inflight_tasks_ == 0; });
     const int64_t n = completed_requests_;
     completed_requests_ = 0;
-    throw_pending_error_locked();
+    if (!errors_.empty()) {
+      std::string e = errors_.begin()->second;
+      errors_.clear();
+      throw std::runtime_error(e);
+    }
     return n;
   }
 
@@ -117,7 +124,12 @@ class Engine {
   void wait_request(int64_t id) {
     std::unique_lock<std::mutex> lk(mu_);
     done_cv_.wait(lk, [&] { return live_.count(id) == 0; });
-    throw_pending_error_locked();
+    auto it = errors_.find(id);
+    if (it != errors_.end()) {
+      std::string e = std::move(it->second);
+      errors_.erase(it);
+      throw std::runtime_error(e);
+    }
   }
 
   int64_t pending() {
@@ -126,14 +138,6 @@ class Engine {
   }
 
  private:
-  void throw_pending_error_locked() {
-    if (!error_.empty()) {
-      std::string e = error_;
-      error_.clear();
-      throw std::runtime_error(e);
-    }
-  }
-
   void run(Task& t) {
     int64_t done = 0;
     while (done < t.nbytes) {
@@ -151,7 +155,7 @@ class Engine {
       if (r <= 0) {
         const std::string why = (r == 0 ? std::string("unexpected end of file") : std::string(std::strerror(errno)));
         std::lock_guard<std::mutex> g(mu_);
-        if (error_.empty()) error_ = std::string(t.write ? "pwrite " : "pread ") + t.file->path + ": " + why;
+        errors_.emplace(t.file->id, std::string(t.write ? "pwrite " : "pread ") + t.file->path + ": " + why);
         return;
       }
       done += r;
@@ -195,7 +199,7 @@ class Engine {
   int64_t completed_requests_ = 0;
   std::atomic<int64_t> request_id_{0};
   std::unordered_set<int64_t> live_;
-  std::string error_;
+  std::unordered_map<int64_t, std::string> errors_;  // request id -> its first I/O error
 };
 
 }  // namespace sxe_aio

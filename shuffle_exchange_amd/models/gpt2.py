@@ -13,7 +13,7 @@ import torch.nn.functional as F
 from ..ops.activation import bias_gelu
 from ..ops.attention import attention
 from ..ops.cross_entropy import cross_entropy
-from ..ops.linear import Linear
+from ..ops.linear import Embedding, Linear
 from ..ops.norm import LayerNorm
 from ..runtime.zero.partition_parameters import local_shard
 
@@ -55,11 +55,12 @@ class GPT2Block(nn.Module):
         self.n_head = cfg.n_head
         self.head_dim = h // cfg.n_head
         self.ln_1 = LayerNorm(h, cfg.layer_norm_epsilon)
-        self.c_attn = Linear(h, 3 * h)
-        self.c_proj = Linear(h, h)
+        std = cfg.initializer_range
+        self.c_attn = Linear(h, 3 * h, init_std=std)
+        self.c_proj = Linear(h, h, init_std=std)
         self.ln_2 = LayerNorm(h, cfg.layer_norm_epsilon)
-        self.c_fc = Linear(h, 4 * h)
-        self.mlp_proj = Linear(4 * h, h)
+        self.c_fc = Linear(h, 4 * h, init_std=std)
+        self.mlp_proj = Linear(4 * h, h, init_std=std)
         self.c_attn._tp_layout = ("chunks", 3)
         self.c_proj._tp_row_parallel = True
         self.mlp_proj._tp_row_parallel = True
@@ -82,11 +83,11 @@ class GPT2LMHeadModel(nn.Module):
     def __init__(self, cfg: GPT2Config):
         super().__init__()
         self.cfg = cfg
-        self.wte = nn.Embedding(cfg.vocab_size, cfg.n_embd)
-        self.wpe = nn.Embedding(cfg.n_positions, cfg.n_embd)
+        self.wte = Embedding(cfg.vocab_size, cfg.n_embd, init_std=cfg.initializer_range)
+        self.wpe = Embedding(cfg.n_positions, cfg.n_embd, init_std=cfg.initializer_range)
         self.h = nn.ModuleList([GPT2Block(cfg) for _ in range(cfg.n_layer)])
         self.ln_f = LayerNorm(cfg.n_embd, cfg.layer_norm_epsilon)
-        self.reset_parameters()
+        # weights initialise themselves in their constructors (world-size invariant under zero.Init)
 
     @torch.no_grad()
     def reset_parameters(self):

@@ -26,7 +26,7 @@ from ..runtime.activation_checkpointing.checkpointing import checkpoint
 from ..runtime.zero.partition_parameters import local_shard
 from ..ops.attention import attention_qkv_rope
 from ..ops.cross_entropy import fused_linear_cross_entropy
-from ..ops.linear import Linear, linear
+from ..ops.linear import Embedding, Linear, linear
 from ..ops.norm import RMSNorm
 from ..ops.rope import RopeCache
 from ..sequence.layer import ulysses_qkv_attention
@@ -102,8 +102,9 @@ class LlamaAttention(nn.Module):
         super().__init__()
         self.cfg = cfg
         self.nq, self.nkv, self.d = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
-        self.qkv_proj = Linear(cfg.hidden_size, (self.nq + 2 * self.nkv) * self.d, bias=False)
-        self.o_proj = Linear(self.nq * self.d, cfg.hidden_size, bias=False)
+        std = cfg.initializer_range
+        self.qkv_proj = Linear(cfg.hidden_size, (self.nq + 2 * self.nkv) * self.d, bias=False, init_std=std)
+        self.o_proj = Linear(self.nq * self.d, cfg.hidden_size, bias=False, init_std=std)
         # AutoTP: split q|k|v by heads (GQA-aware); nq/nkv become per-rank counts
         self.qkv_proj._tp_layout = ("heads", [self.nq, self.nkv, self.nkv], self.d)
         self.o_proj._tp_row_parallel = True
@@ -133,8 +134,9 @@ class LlamaAttention(nn.Module):
 class LlamaMLP(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
-        self.gate_up_proj = Linear(cfg.hidden_size, 2 * cfg.intermediate_size, bias=False)
-        self.down_proj = Linear(cfg.intermediate_size, cfg.hidden_size, bias=False)
+        std = cfg.initializer_range
+        self.gate_up_proj = Linear(cfg.hidden_size, 2 * cfg.intermediate_size, bias=False, init_std=std)
+        self.down_proj = Linear(cfg.intermediate_size, cfg.hidden_size, bias=False, init_std=std)
         self.gate_up_proj._tp_layout = ("chunks", 2)
         self.down_proj._tp_row_parallel = True
 
@@ -170,6 +172,8 @@ class LMHeadLoss(nn.Module):
         self.cfg = cfg
         if weight is None:
             self.weight = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden_size))
+            with torch.no_grad():
+                self.weight.normal_(0.0, cfg.initializer_range)
         else:
             self.weight = weight
 
@@ -197,12 +201,23 @@ class LlamaForCausalLM(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
         self.cfg = cfg
-        self.embed_tokens = nn.Embedding(cfg.vocab_size, cfg.hidden_size)
+        self.embed_tokens = Embedding(cfg.vocab_size, cfg.hidden_size, init_std=cfg.initializer_range)
         self.layers = nn.ModuleList([LlamaDecoderLayer(cfg) for _ in range(cfg.num_hidden_layers)])
         self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         self.lm_head = LMHeadLoss(cfg, self.embed_tokens.weight if cfg.tie_word_embeddings else None)
         self._rope = None
-        self.reset_parameters()
+        # every weight was initialised N(0, std) by its own constructor, i.e. on the whole tensor
+        # before a partitioning zero.Init cut it: the model depends on the seed, not on the world size
+        self._init_remaining()
+
+    @torch.no_grad()
+    def _init_remaining(self):
+        """N(0, std) for Linear/Embedding modules that did not initialise themselves (e.g. MoE
+        routers): on this rank's construction partition when zero.Init partitioned them."""
+        std = self.cfg.initializer_range
+        for m in self.modules():
+            if isinstance(m, (nn.Linear, nn.Embedding)) and not getattr(m, "_sxe_inited", False):
+                local_shard(m.weight).normal_(0.0, std)
 
     @torch.no_grad()
     def reset_parameters(self):

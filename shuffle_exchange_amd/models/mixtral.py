@@ -11,6 +11,7 @@ import torch
 import torch.nn as nn
 
 from ..moe.layer import MoE
+from ..ops.linear import Embedding
 from ..runtime.activation_checkpointing.checkpointing import checkpoint
 from ..ops.norm import RMSNorm
 from .llama import LlamaAttention, LlamaConfig, LlamaForCausalLM, LMHeadLoss
@@ -80,12 +81,12 @@ class MixtralForCausalLM(LlamaForCausalLM):
     def __init__(self, cfg: MixtralConfig):
         nn.Module.__init__(self)
         self.cfg = cfg
-        self.embed_tokens = nn.Embedding(cfg.vocab_size, cfg.hidden_size)
+        self.embed_tokens = Embedding(cfg.vocab_size, cfg.hidden_size, init_std=cfg.initializer_range)
         self.layers = nn.ModuleList([MixtralDecoderLayer(cfg) for _ in range(cfg.num_hidden_layers)])
         self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         self.lm_head = LMHeadLoss(cfg, None)
         self._rope = None
-        self.reset_parameters()
+        self._init_remaining()
 
     def forward(self, input_ids, labels=None, position_ids=None):
         x = self.embed_tokens(input_ids)

@@ -135,7 +135,31 @@ def linear(x, weight, bias=None):
 
 class Linear(torch.nn.Linear):
     """``nn.Linear`` whose GEMMs go through ``linear`` (fused weight-grad into ZeRO buffers).
-    AutoTP swaps it for a column/row-parallel layer with the same call signature."""
+    AutoTP swaps it for a column/row-parallel layer with the same call signature.
+
+    ``init_std``: initialise the weight N(0, init_std) (bias zero) inside the constructor, i.e.
+    on the whole tensor before a partitioning ``zero.Init`` cuts it -- the initial model then
+    depends only on the seed, not on the number of ranks."""
+
+    def __init__(self, in_features, out_features, bias=True, device=None, dtype=None, init_std=None):
+        super().__init__(in_features, out_features, bias=bias, device=device, dtype=dtype)
+        if init_std is not None:
+            with torch.no_grad():
+                self.weight.normal_(0.0, init_std)
+                if self.bias is not None:
+                    self.bias.zero_()
+            self._sxe_inited = True
 
     def forward(self, x, skip_bias=False):
         return linear(x, self.weight, None if skip_bias else self.bias)
+
+
+class Embedding(torch.nn.Embedding):
+    """``nn.Embedding`` with the constructor-time N(0, init_std) init of ``Linear``."""
+
+    def __init__(self, num_embeddings, embedding_dim, init_std=None, **kw):
+        super().__init__(num_embeddings, embedding_dim, **kw)
+        if init_std is not None:
+            with torch.no_grad():
+                self.weight.normal_(0.0, init_std)
+            self._sxe_inited = True

@@ -31,11 +31,8 @@ def load_tuned_gemms(path=None):
     tun = torch.cuda.tunable
     tun.enable(True)
     tun.tuning_enable(False)
-    # PyTorch registers the ROCBLAS_VERSION validator lazily, with the first rocBLAS-backed
-    # TunableOp; reading the table before any GEMM has run fails that validator ("Failed
-    # validator: ROCBLAS_VERSION") and drops every entry. One tiny GEMM registers it.
-    a = torch.ones(64, 64, device="cuda", dtype=torch.bfloat16)
-    torch.mm(a, a)
+    # the table must have LF line endings: with CRLF the last validator's value carries a '\r'
+    # and TunableOp rejects the whole file ("Failed validator: ROCBLAS_VERSION")
     ok = tun.read_file(path)
     if not ok:
         have = dict(tun.get_validators())

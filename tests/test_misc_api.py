@@ -133,3 +133,15 @@ def test_loco_error_feedback_bounds_accumulated_quantization_error():
     e_plain = (tot_plain - true).abs().max().item()
     e_loco = (tot_loco - true).abs().max().item()
     assert e_loco < 0.2 * e_plain, (e_loco, e_plain)
+
+
+def test_packaged_gemm_table_is_lf_and_has_validators():
+    """TunableOp rejects a results file whose lines end in CRLF (the last validator's value then
+    carries a carriage return): the packaged MI355X table must be LF-only."""
+    import os
+    from shuffle_exchange_amd.runtime.gemm_tuning import PACKAGED
+    raw = open(PACKAGED, "rb").read()
+    assert b"\r" not in raw
+    keys = [ln.split(",")[1] for ln in raw.decode().splitlines() if ln.startswith("Validator,")]
+    assert {"PT_VERSION", "HIP_VERSION", "HIPBLASLT_VERSION", "GCN_ARCH_NAME", "ROCBLAS_VERSION"} <= set(keys)
+    assert os.path.getsize(PACKAGED) > 0

@@ -56,7 +56,7 @@ def _case_engine(rank, world, name, freeze, steps, lr=1e-3, fixed=False):
     model, cfg = tiny_llama(0)
     params = {"lr": lr}
     if name == "ZeroOneAdam":
-        params.update(var_freeze_step=freeze, var_update_scaler=1, local_step_scaler=1000, local_step_clipper=2)
+        params.update(var_freeze_step=freeze, var_update_scaler=16, local_step_scaler=1000, local_step_clipper=2)
     else:
         params["freeze_step"] = freeze
     ds = {"train_micro_batch_size_per_gpu": 2, "zero_optimization": {"stage": 0},

@@ -69,3 +69,31 @@ def test_shuffle_exchange_rr_four_ranks_one_gpu(stage):
     for k in four[0]["params"]:
         for r in range(1, 4):
             assert torch.equal(four[0]["params"][k], four[r]["params"][k]), (k, r)
+
+
+def _case_init_mem(rank, world):
+    os.environ["LOCAL_RANK"] = "0"
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+    torch.cuda.set_device(0)
+    torch.manual_seed(0)
+    cfg = llama_config("llama-tiny", hidden_size=1024, intermediate_size=4096, num_attention_heads=8,
+                       num_key_value_heads=2, vocab_size=8192, num_hidden_layers=8)
+    torch.cuda.reset_peak_memory_stats()
+    base = torch.cuda.memory_allocated()
+    with sxe.zero.Init(dtype=torch.bfloat16):
+        model = LlamaForCausalLM(cfg)
+    peak = torch.cuda.max_memory_allocated() - base
+    held = torch.cuda.memory_allocated() - base
+    layer = sum(p.ds_numel for p in model.layers[0].parameters()) * 2
+    return {"peak": peak, "held": held, "full": cfg.num_params() * 2, "layer": layer}
+
+
+def test_zero_init_gpu_memory_two_ranks():
+    """zero.Init on the GPU: each of 2 ranks holds ~half the model after construction and never more
+    than its half plus one module's whole parameters (+ allocator slack) while building it."""
+    res = run_dist(_case_init_mem, 2)
+    for r in res:
+        assert r["held"] <= r["full"] / 2 + (4 << 20), r
+        assert r["peak"] <= r["full"] / 2 + 2 * max(r["layer"], 8192 * 1024 * 2) + (16 << 20), r
+        assert r["peak"] < 0.75 * r["full"], r

@@ -28,7 +28,9 @@ def test_zero_matches_single_process_adamw(stage):
     res = run_dist(C.case_train, world, ds, steps, mbs, seq)
     ref = C.reference_train(ADAMW, steps, world, mbs, seq)
     for r in res:
-        _close(r["params"], ref)
+        # Adam normalises each element by its own gradient scale: a near-zero gradient summed in a
+        # different order (2-rank reduce vs one process) moves its update by up to a fraction of lr
+        _close(r["params"], ref, tol=1e-4)
 
 
 def test_zero2_grad_accumulation_and_clipping():
@@ -175,7 +177,7 @@ def test_zero3_reuse_distance_skips_backward_gathers():
     drop = run_dist(C.case_zero3_reuse, world, 0, steps, mbs, seq)
     ref = C.reference_train(ADAMW, steps, world, mbs, seq)
     for r in keep + drop:
-        _close(r["params"], ref)
+        _close(r["params"], ref, tol=1e-4)
     assert keep[0]["gathers"] < drop[0]["gathers"], (keep[0]["gathers"], drop[0]["gathers"])
 
 
@@ -240,6 +242,14 @@ def test_zero_init_partitions_at_construction(world):
             assert torch.allclose(r["after"][k], r0["after"][k], atol=1e-6), k
     assert torch.all(r0["before"]["norm.weight"] == 1.5)
     assert all(l == l for l in r0["losses"])
+    # world-size invariant: every weight was initialised whole (by its constructor) on rank 0 and
+    # broadcast, so the partitioned model equals the unpartitioned one built from rank 0's seed
+    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+    torch.manual_seed(100)
+    ref = LlamaForCausalLM(llama_config("llama-tiny", num_hidden_layers=layers))
+    for n, p in ref.named_parameters():
+        if n != "norm.weight":
+            assert torch.equal(r0["before"][n], p.detach().float()), n
 
 
 def test_broadcast_coalesced_in_place_and_bucketed():
