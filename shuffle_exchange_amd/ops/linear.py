@@ -79,6 +79,10 @@ def write_weight_grad(w, gy2, x2):
         a, b = torch.ops.sxe.transpose16(gy2), torch.ops.sxe.transpose16(x2).t()
         if buf.dtype == gy2.dtype and not accumulate:
             torch.mm(a, b, out=buf)  # the reduce-scatter staging slot of a multi-rank unit
+        elif buf.dtype == torch.float32:
+            # fp32-out TN GEMM accumulating in its epilogue (beta = 1): no bf16 dW round trip and no
+            # separate fp32 add pass (28672x4096 at 8192 tokens: 1.62 vs 1.74 ms, wgrad_tn_fp32_exp)
+            torch.ops.aten.addmm.dtype_out(buf, a, b, torch.float32, beta=1 if accumulate else 0, alpha=1, out=buf)
         else:
             dw = torch.mm(a, b)
             buf.add_(dw) if accumulate else buf.copy_(dw)

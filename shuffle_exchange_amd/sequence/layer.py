@@ -4,7 +4,10 @@ Parity: reference deepspeed/sequence/layer.py -- ``DistributedAttention`` :331-4
 ``_SeqAllToAll`` :277, ``single_all_to_all`` :221-254 -- and the ALST HF path
 (runtime/sequence_parallel/ulysses_sp.py:47 ``UlyssesSPAttentionHF``, GQA kv replication :117-138).
 
-Layout here is batch-first [B, S, H, D] (what the QKV projection produces), so the exchange is:
+``DistributedAttention`` takes any layout (reference default: sequence-first [s/p, b, h, d],
+scatter_idx=2 / gather_idx=0) and uneven head counts through one general flat-range all-to-all
+(``all_to_all_dims``). The model-internal fused path is batch-first [B, S, H, D] (what the QKV
+projection produces):
   [B, S/p, H, D] --a2a--> [B, S, H/p, D]   (scatter heads, gather sequence)
 and back for the output. MI355X-first differences:
 * the fused QKV path (``ulysses_qkv_attention``) moves q, k and v in ONE all_to_all_single (the
@@ -15,6 +18,8 @@ and back for the output. MI355X-first differences:
   same HIP kernel call that rotates q and k;
 * on one 8-GPU node an all-to-all is a full-mesh exchange: every GPU drives all 7 xGMI links.
 """
+import math
+
 import torch
 import torch.nn as nn
 
@@ -61,21 +66,160 @@ class _SeqAllToAll(torch.autograd.Function):
         return None, (head_to_seq(g, ctx.group) if ctx.to_heads else seq_to_head(g, ctx.group)), None
 
 
-class DistributedAttention(nn.Module):
-    """Wrap any local attention ``fn(q, k, v, *args, **kw) -> [B, S, H/p, D]`` (batch-first)."""
+def shard_sizes(total, p):
+    """Near-even split of ``total`` items over ``p`` ranks (the first ``total % p`` get one more):
+    the head partition of the uneven-heads all-to-all (reference module_inject/tp_shard.py:42-74
+    without the kv-head grain, which callers express by passing kv heads as ``total``)."""
+    return [total // p + (1 if r < total % p else 0) for r in range(p)]
 
-    def __init__(self, local_attention, sequence_process_group, scatter_idx=2, gather_idx=1, sp_stream=None):
+
+def all_to_all_dims(x, scatter_dim, gather_dim, send_sizes, recv_sizes, group, stream=None):
+    """General all-to-all over ``group``: slice ``send_sizes[j]`` of ``x`` along ``scatter_dim``
+    goes to rank j; the pieces received from ranks 0..p-1 (``recv_sizes[i]`` long along
+    ``gather_dim``) are concatenated along ``gather_dim``. Any layout (batch- or sequence-first),
+    any scatter/gather axes, uneven sizes on either side. One ``all_to_all_single`` on flat
+    element ranges (so pieces of different shapes travel in one collective).
+
+    Parity: reference sequence/layer.py:221-254 ``single_all_to_all`` and :111-218
+    ``uneven_heads_all2all`` -- one routine here instead of per-layout permute tables."""
+    p = dist.get_world_size(group)
+    me = dist.get_rank(group)
+    nd = x.dim()
+    sd, gd = scatter_dim % nd, gather_dim % nd
+    assert sd != gd and sum(send_sizes) == x.shape[sd] and len(send_sizes) == p == len(recv_sizes)
+    send = x.movedim(sd, 0).contiguous()  # [T, rest...]: piece j is a contiguous row range
+    rest = list(send.shape[1:])
+    row = math.prod(rest)
+    g_in_rest = gd if gd < sd else gd - 1  # gather axis within `rest`
+    per_row_wo_g = row // rest[g_in_rest] if rest[g_in_rest] else 0
+    # every rank cuts the scatter axis with the same partition, so each sends us send_sizes[me]
+    # rows, each holding recv_sizes[i] elements along the gather axis
+    recv_t = send_sizes[me]
+    in_splits = [n * row for n in send_sizes]
+    out_splits = [recv_t * per_row_wo_g * n for n in recv_sizes]
+    out = torch.empty(sum(out_splits), dtype=x.dtype, device=x.device)
+    ctx = torch.cuda.stream(stream) if stream is not None else _nullctx()
+    with ctx:
+        dist.all_to_all_single(out, send.reshape(-1), output_split_sizes=out_splits, input_split_sizes=in_splits,
+                               group=group)
+        pieces = []
+        for i, flat in enumerate(out.split(out_splits)):
+            shp = [recv_t] + rest
+            shp[1 + g_in_rest] = recv_sizes[i]
+            pieces.append(flat.view(shp))
+        y = torch.cat(pieces, dim=1 + g_in_rest) if p > 1 else pieces[0]
+        y = y.movedim(0, sd).contiguous()
+    return y
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+class _AllToAllDims(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, group, x, sd, gd, send_sizes, recv_sizes, stream):
+        ctx.args = (group, sd, gd, send_sizes, recv_sizes, stream)
+        return all_to_all_dims(x, sd, gd, send_sizes, recv_sizes, group, stream)
+
+    @staticmethod
+    def backward(ctx, g):
+        group, sd, gd, send_sizes, recv_sizes, stream = ctx.args
+        # the adjoint exchange: scatter back along the gathered axis, gather along the scattered one
+        if stream is not None:
+            stream.wait_stream(torch.cuda.current_stream(g.device))
+        dx = all_to_all_dims(g, gd, sd, recv_sizes, send_sizes, group, stream)
+        if stream is not None:
+            torch.cuda.current_stream(g.device).wait_stream(stream)
+            dx.record_stream(torch.cuda.current_stream(g.device))
+        return None, dx, None, None, None, None, None
+
+
+def _rotate_half(x):
+    x1, x2 = x.chunk(2, dim=-1)
+    return torch.cat((-x2, x1), dim=-1)
+
+
+def _apply_rotary(t, cos, sin):
+    rd = cos.shape[-1]
+    head, tail = t[..., :rd], t[..., rd:]
+    head = head * cos + _rotate_half(head) * sin
+    return head if tail.shape[-1] == 0 else torch.cat((head, tail), dim=-1)
+
+
+class DistributedAttention(nn.Module):
+    """Ulysses attention around any local attention callable.
+
+    ``forward(query, key, value, batch_dim_idx, rotary_pos_emb=None, *args, **kwargs)`` with inputs
+    holding the local sequence chunk: sequence-first ``[s/p, b, h, d]`` for the defaults
+    ``scatter_idx=2, gather_idx=0`` (``batch_dim_idx=1``), or batch-first ``[b, s/p, h, d]`` with
+    ``gather_idx=1`` (``batch_dim_idx=0``). The local attention sees the full sequence and ``h/p``
+    heads in the same layout; the output is returned in the input layout. Head counts that do not
+    divide by the SP degree use the near-even uneven-heads exchange (:func:`shard_sizes`) with the kv
+    head as the grain, so every rank keeps whole GQA groups.
+
+    ``sp_stream``: q, k and v travel on that HIP stream, each exchange issued as soon as its input
+    is ready, and the compute stream waits on an event only right before the local attention (and,
+    in backward, the three gradient exchanges run there back to back) -- the permute/copy work of
+    one tensor overlaps the transfer of the next.
+
+    Parity: reference sequence/layer.py:331-440 (``DistributedAttention``; defaults :341-347,
+    rotary after the exchange :425-428, overlap :392-426)."""
+
+    def __init__(self, local_attention, sequence_process_group, scatter_idx=2, gather_idx=0, sp_stream=None):
         super().__init__()
         self.local_attn = local_attention
         self.spg = sequence_process_group
         self.scatter_idx, self.gather_idx = scatter_idx, gather_idx
+        self.sp_stream = sp_stream
+        self.sp_overlap_comm = sp_stream is not None
 
-    def forward(self, query, key, value, *args, **kwargs):
-        q = _SeqAllToAll.apply(self.spg, query, True)
-        k = _SeqAllToAll.apply(self.spg, key, True)
-        v = _SeqAllToAll.apply(self.spg, value, True)
-        o = self.local_attn(q, k, v, *args, **kwargs)
-        return _SeqAllToAll.apply(self.spg, o, False)
+    def _exchange(self, t, fwd, head_sizes):
+        p = dist.get_world_size(self.spg)
+        if p == 1:
+            return t
+        stream = self.sp_stream if (self.sp_stream is not None and t.is_cuda) else None
+        if stream is not None:
+            stream.wait_stream(torch.cuda.current_stream(t.device))
+        if fwd:  # scatter heads, gather sequence
+            seq = [t.shape[self.gather_idx]] * p
+            return _AllToAllDims.apply(self.spg, t, self.scatter_idx, self.gather_idx, head_sizes, seq, stream)
+        seq = [t.shape[self.gather_idx] // p] * p  # scatter sequence, gather heads
+        return _AllToAllDims.apply(self.spg, t, self.gather_idx, self.scatter_idx, seq, head_sizes, stream)
+
+    def forward(self, query, key, value, batch_dim_idx=None, rotary_pos_emb=None, *args, **kwargs):
+        if batch_dim_idx is None:
+            batch_dim_idx = 0 if self.gather_idx == 1 else 1
+        assert batch_dim_idx in (0, 1)
+        p = dist.get_world_size(self.spg)
+        hq, hkv = query.shape[self.scatter_idx], key.shape[self.scatter_idx]
+        assert hq % hkv == 0, f"query heads ({hq}) must be a multiple of kv heads ({hkv})"
+        # kv heads are the partition grain: rank r gets kv_sizes[r] kv heads and the q heads of
+        # exactly those kv groups, so GQA stays intact on every rank even when p does not divide
+        kv_sizes = shard_sizes(hkv, p)
+        q_sizes = [n * (hq // hkv) for n in kv_sizes]
+        q = self._exchange(query, True, q_sizes)
+        k = self._exchange(key, True, kv_sizes)
+        v = self._exchange(value, True, kv_sizes)
+        if self.sp_stream is not None and q.is_cuda:
+            torch.cuda.current_stream(q.device).wait_stream(self.sp_stream)
+            for t in (q, k, v):
+                t.record_stream(torch.cuda.current_stream(q.device))
+        if rotary_pos_emb is not None:
+            cos, sin = rotary_pos_emb[0], rotary_pos_emb[1]
+            if batch_dim_idx == 1:  # reference layout: freqs arrive [b, s, 1, d] -> [s, b, 1, d]
+                cos, sin = cos.permute(1, 0, 2, 3), sin.permute(1, 0, 2, 3)
+            q, k = _apply_rotary(q, cos, sin), _apply_rotary(k, cos, sin)
+        ctx = self.local_attn(q, k, v, *args, **kwargs)
+        out = self._exchange(ctx, False, q_sizes)
+        if self.sp_stream is not None and out.is_cuda:
+            torch.cuda.current_stream(out.device).wait_stream(self.sp_stream)
+            out.record_stream(torch.cuda.current_stream(out.device))
+        return out
 
 
 # ------------------------------------------------------------------------------------------------

@@ -78,3 +78,78 @@ def test_ulysses_sp_matches_full_sequence(stage):
             assert a == pytest.approx(b, rel=1e-5)
         for k, v in ref["params"].items():
             assert torch.allclose(r["params"][k], v, atol=2e-5), k
+
+
+def _sdpa_seq_first(q, k, v):
+    # q/k/v [s, b, h, d] (heads may differ for GQA) -> [s, b, h, d]
+    rep = q.shape[2] // k.shape[2]
+    k, v = k.repeat_interleave(rep, 2), v.repeat_interleave(rep, 2)
+    o = torch.nn.functional.scaled_dot_product_attention(q.permute(1, 2, 0, 3), k.permute(1, 2, 0, 3),
+                                                         v.permute(1, 2, 0, 3), is_causal=True)
+    return o.permute(2, 0, 1, 3)
+
+
+def _sdpa_batch_first(q, k, v):
+    o = _sdpa_seq_first(q.transpose(0, 1), k.transpose(0, 1), v.transpose(0, 1))
+    return o.transpose(0, 1)
+
+
+def _case_dist_attn_layouts(rank, world, layout, hq, hkv, rotary):
+    from shuffle_exchange_amd.parallel import groups
+    from shuffle_exchange_amd.sequence.layer import DistributedAttention
+    groups.initialize(sequence_parallel_size=world)
+    g = groups.get_sequence_parallel_group()
+    torch.manual_seed(0)
+    S, B, D = 8 * world, 2, 16
+    qf, kf, vf = (torch.randn(S, B, h, D, dtype=torch.float64) for h in (hq, hkv, hkv))
+    freqs = None
+    if rotary:
+        ang = torch.arange(S, dtype=torch.float64)[:, None] * torch.rand(D // 2, dtype=torch.float64)
+        cos, sin = torch.cat([ang.cos()] * 2, -1), torch.cat([ang.sin()] * 2, -1)
+        freqs = (cos[None, :, None, :].expand(B, S, 1, D), sin[None, :, None, :].expand(B, S, 1, D))
+    chunk = slice(rank * S // world, (rank + 1) * S // world)
+
+    if layout == "seq_first":
+        attn = DistributedAttention(_sdpa_seq_first, g)  # reference defaults: scatter 2, gather 0
+        ins = [t[chunk].clone().requires_grad_() for t in (qf, kf, vf)]
+        out = attn(*ins, 1, freqs)
+    else:
+        attn = DistributedAttention(_sdpa_batch_first, g, scatter_idx=2, gather_idx=1)
+        ins = [t.transpose(0, 1)[:, chunk].clone().requires_grad_() for t in (qf, kf, vf)]
+        fb = None if freqs is None else (freqs[0], freqs[1])
+        out = attn(*ins, 0, fb)
+    go = torch.randn(out.shape, dtype=out.dtype, generator=torch.Generator().manual_seed(5 + rank))
+    (out * go).sum().backward()
+    return {"out": out.detach(), "go": go, "grads": [t.grad for t in ins]}
+
+
+@pytest.mark.parametrize("layout,hq,hkv,rotary", [("seq_first", 4, 4, False), ("seq_first", 4, 2, True),
+                                                   ("batch_first", 4, 4, True), ("seq_first", 6, 3, False),
+                                                   ("batch_first", 3, 3, False)])
+def test_distributed_attention_layouts_and_uneven_heads(layout, hq, hkv, rotary):
+    """DistributedAttention (reference sequence/layer.py:331) == full-sequence causal attention, for the
+    reference's sequence-first default, batch-first input, GQA, rotary after the exchange, and head
+    counts not divisible by sp (uneven-heads all-to-all, :111): forward and input gradients."""
+    world = 2
+    res = run_dist(_case_dist_attn_layouts, world, layout, hq, hkv, rotary)
+    torch.manual_seed(0)
+    S, B, D = 8 * world, 2, 16
+    qf, kf, vf = (torch.randn(S, B, h, D, dtype=torch.float64).requires_grad_() for h in (hq, hkv, hkv))
+    q, k = qf, kf
+    if rotary:
+        ang = torch.arange(S, dtype=torch.float64)[:, None] * torch.rand(D // 2, dtype=torch.float64)
+        cos, sin = torch.cat([ang.cos()] * 2, -1)[:, None, None, :], torch.cat([ang.sin()] * 2, -1)[:, None, None, :]
+
+        def rot(t):
+            a, b = t.chunk(2, -1)
+            return t * cos + torch.cat((-b, a), -1) * sin
+        q, k = rot(qf), rot(kf)
+    full = _sdpa_seq_first(q, k, vf)
+    bf = layout == "batch_first"
+    out = torch.cat([r["out"].transpose(0, 1) if bf else r["out"] for r in res], 0)
+    assert torch.allclose(out, full, atol=1e-10), (out - full).abs().max()
+    go = torch.cat([r["go"].transpose(0, 1) if bf else r["go"] for r in res], 0)
+    (full * go).sum().backward()
+    for i, ref in enumerate((qf, kf, vf)):
+        got = torch.cat([r["grads"][i].transpose(0, 1) if bf else r["grads"][i] for r in res], 0)
+        assert torch.allclose(got, ref.grad, atol=1e-10), (i, (got - ref.grad).abs().max())
