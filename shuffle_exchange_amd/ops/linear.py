@@ -47,6 +47,26 @@ def _skinny(x, weight, bias):
     return torch.ops.sxe.skinny_gemm(x2, weight, bias).view(*x.shape[:-1], weight.shape[0])
 
 
+# Hand-written weight-gradient GEMM (csrc/kernels/gemm_wgrad.hip: k-major operands read through LDS
+# with ds_read_b64_tr_b16, fp32 accumulate in the epilogue): no transposed copies of dY / X at all.
+# Measured on MI355X at 8192 tokens (tools/wgrad_exp.py, profiles/wgrad_kernel.log): 28672x4096
+# 1.59 ms vs 1.63 (transposes + hipBLASLt TN fp32-out), 4096x14336 0.84 vs 0.89, 4096x4096 0.24 vs
+# 0.25 (NT fp32-out); it loses where its 256x256 tile grid leaves a partial last wave of blocks
+# (6144x4096: 1.5 waves over 256 CUs) and on the LM head, which keep the library paths.
+SXE_WGRAD = os.environ.get("SXE_WGRAD", "1") == "1"
+
+
+def _sxe_wgrad_ok(gy2, x2, buf):
+    if not (SXE_WGRAD and gy2.is_cuda and buf.dtype == torch.float32 and gy2.dtype == torch.bfloat16
+            and x2.dtype == torch.bfloat16 and buf.is_contiguous() and gy2.stride(1) == 1 and x2.stride(1) == 1):
+        return False
+    K, M, N = gy2.shape[0], gy2.shape[1], x2.shape[1]
+    if K % 128 or M % 256 or N % 256 or gy2.stride(0) % 8 or x2.stride(0) % 8 or M * N >= 2 ** 27:
+        return False
+    tiles = (M // 256) * (N // 256)
+    return tiles % 256 == 0 or tiles >= 3 * 256
+
+
 def _tn_ok(gy2, x2):
     return (gy2.is_cuda and gy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and TN_MIN_ELEMS > 0
             and gy2.shape[1] * x2.shape[1] >= TN_MIN_ELEMS and gy2.shape[0] % 64 == 0 and gy2.shape[1] % 64 == 0
@@ -75,7 +95,9 @@ def write_weight_grad(w, gy2, x2):
     if tgt is None:
         return False
     buf, accumulate = tgt(w)
-    if _tn_ok(gy2, x2) and buf.is_contiguous():
+    if _sxe_wgrad_ok(gy2, x2, buf):
+        torch.ops.sxe.wgrad_gemm_(gy2, x2, buf, 1.0, bool(accumulate))
+    elif _tn_ok(gy2, x2) and buf.is_contiguous():
         a, b = torch.ops.sxe.transpose16(gy2), torch.ops.sxe.transpose16(x2).t()
         if buf.dtype == gy2.dtype and not accumulate:
             torch.mm(a, b, out=buf)  # the reduce-scatter staging slot of a multi-rank unit

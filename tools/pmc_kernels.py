@@ -23,7 +23,7 @@ def main():
     k = torch.randn(4, 2048, 8, 128, device=dev, dtype=bf, requires_grad=True)
     v = torch.randn(4, 2048, 8, 128, device=dev, dtype=bf, requires_grad=True)
     g = torch.randn(4, 2048, 32, 128, device=dev, dtype=bf)
-    for _ in range(3):
+    for _ in range(0 if os.environ.get("PMC_ONLY_GEMM") else 3):
         torch.autograd.grad(attention(q, k, v), (q, k, v), g)
     x1 = torch.randn(1, 14336, device=dev, dtype=bf)
     w = torch.randn(4096, 14336, device=dev, dtype=bf)
@@ -50,6 +50,14 @@ def main():
     lp = torch.empty(n, device=dev, dtype=bf)
     for s in range(1, 4):
         adam_flat_(p, gr, m, vv, lp, lr=1e-3, step=s)
+    # weight-gradient GEMM (k-major operands, fp32 accumulate) vs hipBLASLt's forward-layout GEMM
+    gy = torch.randn(8192, 28672, device=dev, dtype=bf)
+    xw = torch.randn(8192, 4096, device=dev, dtype=bf)
+    accw = torch.zeros(28672, 4096, device=dev)
+    gyt, xwt = gy.t().contiguous(), xw.t().contiguous()
+    for _ in range(3):
+        torch.ops.sxe.wgrad_gemm_variant_(gy, xw, accw, 1.0, True, 0)
+        torch.mm(gyt, xwt.t())
     torch.cuda.synchronize()
     print("pmc workload done", flush=True)
 

@@ -12,16 +12,23 @@ def t(fn, n=10):
     torch.cuda.synchronize(); return (time.perf_counter() - t0) / n
 
 torch.manual_seed(0)
-# correctness on a small case against an fp64 reference
-K, M, N = 512, 512, 768
-a = torch.randn(K, M, device="cuda", dtype=torch.bfloat16)
-b = torch.randn(K, N, device="cuda", dtype=torch.bfloat16)
-c = torch.randn(M, N, device="cuda")
-ref = c.double() + 0.5 * (a.double().t() @ b.double())
-torch.ops.sxe.wgrad_gemm_(a, b, c, 0.5, True)
-err = ((c.double() - ref).norm() / ref.norm()).item()
-print(f"correctness rel err {err:.2e}", flush=True)
-assert err < 1e-3
+from shuffle_exchange_amd.runtime.gemm_tuning import load_tuned_gemms
+load_tuned_gemms()
+# correctness against an fp64 reference (accumulate into a random C, alpha != 1, several shapes)
+for K, M, N in [(128, 256, 256), (512, 512, 768), (1024, 768, 512), (8192, 256, 1024)]:
+    a = torch.randn(K, M, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(K, N, device="cuda", dtype=torch.bfloat16)
+    c = torch.randn(M, N, device="cuda")
+    ref = c.double() + 0.5 * (a.double().t() @ b.double())
+    for v in (0, 1, 2):
+        cc = c.clone()
+        torch.ops.sxe.wgrad_gemm_variant_(a, b, cc, 0.5, True, v)
+        err = ((cc.double() - ref).norm() / ref.norm()).item()
+        c2 = torch.empty(M, N, device="cuda")
+        torch.ops.sxe.wgrad_gemm_variant_(a, b, c2, 1.0, False, v)
+        err2 = ((c2.double() - a.double().t() @ b.double()).norm() / (a.double().t() @ b.double()).norm()).item()
+        print(f"correctness v{v} K={K} M={M} N={N}: accumulate rel err {err:.2e}, overwrite {err2:.2e}", flush=True)
+        assert err < 1e-5 and err2 < 1e-5
 T = 8192
 for (Mo, Ni) in [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)]:
     gy = torch.randn(T, Mo, device="cuda", dtype=torch.bfloat16)
@@ -32,7 +39,21 @@ for (Mo, Ni) in [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (1282
     torch.ops.aten.addmm.dtype_out(acc2, gy.t(), x, torch.float32, beta=1, alpha=1, out=acc2)
     e = ((acc - acc2).norm() / acc2.norm()).item()
     fl = 2.0 * T * Mo * Ni
-    t1 = t(lambda: torch.ops.sxe.wgrad_gemm_(gy, x, acc, 1.0, True))
-    t2 = t(lambda: torch.ops.aten.addmm.dtype_out(acc2, gy.t(), x, torch.float32, beta=1, alpha=1, out=acc2))
-    print(f"[{Mo}x{Ni}] K={T}: sxe {t1*1e3:.3f} ms {fl/t1/1e12:.0f} TF | hipBLASLt {t2*1e3:.3f} ms {fl/t2/1e12:.0f} TF | err {e:.1e}", flush=True)
+
+    def tn_fp32():
+        d1, x1 = torch.ops.sxe.transpose16(gy), torch.ops.sxe.transpose16(x)
+        torch.ops.aten.addmm.dtype_out(acc2, d1, x1.t(), torch.float32, beta=1, alpha=1, out=acc2)
+    arms = {"v0 accum": lambda: torch.ops.sxe.wgrad_gemm_variant_(gy, x, acc, 1.0, True, 0),
+            "v1 accum": lambda: torch.ops.sxe.wgrad_gemm_variant_(gy, x, acc, 1.0, True, 1),
+            "v2 accum": lambda: torch.ops.sxe.wgrad_gemm_variant_(gy, x, acc, 1.0, True, 2),
+            "v2 overwrite": lambda: torch.ops.sxe.wgrad_gemm_variant_(gy, x, acc, 1.0, False, 2),
+            "hipBLASLt NT fp32": lambda: torch.ops.aten.addmm.dtype_out(acc2, gy.t(), x, torch.float32, beta=1,
+                                                                         alpha=1, out=acc2),
+            "transposes+TN fp32": tn_fp32}
+    best = {k: 1e9 for k in arms}
+    for _ in range(3):  # interleaved rounds in one process; keep the best of each arm
+        for k, fn in arms.items():
+            best[k] = min(best[k], t(fn, 5))
+    print(f"[{Mo}x{Ni}] K={T} err {e:.1e}: " + " | ".join(f"{k} {v*1e3:.3f} ms {fl/v/1e12:.0f} TF"
+                                                       for k, v in best.items()), flush=True)
     del gy, x, acc, acc2
