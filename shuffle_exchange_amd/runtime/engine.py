@@ -402,6 +402,12 @@ class SXEEngine(nn.Module):
                 from .zero.offload import split_param_groups
                 split_param_groups(basic, host_step.ratio)  # Twin-Flow: part of every group stays in HBM
         offload_param = bool(zc.offload_param is not None and zc.offload_param.device in ("cpu", "nvme"))
+        param_swap = None
+        if offload_param and zc.offload_param.device == "nvme":
+            if stage != 3:
+                raise ValueError("offload_param needs ZeRO stage 3")
+            param_swap = dict(nvme_path=zc.offload_param.nvme_path, rank=dist.get_rank(), dtype=dtype,
+                              aio_config=cfg.model.aio, buffer_count=zc.offload_param.buffer_count)
         if stage == 3:
             self.optimizer = ZeroStage3Optimizer(
                 self.module, basic, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks,
@@ -415,7 +421,7 @@ class SXEEngine(nn.Module):
                 defer_reduce=zc.defer_reduce, retain_params=zc.retain_params, loco_param=zc.zeropp_loco_param,
                 prefetch_bucket_size=(zc.prefetch_bucket_size if "prefetch_bucket_size" in zc.model_fields_set
                                       and "prefetch_depth" not in zc.model_fields_set else None),
-                model_persistence_threshold=zc.model_persistence_threshold)
+                model_persistence_threshold=zc.model_persistence_threshold, param_swap=param_swap)
         elif stage in (1, 2):
             self.optimizer = ZeroStage12Optimizer(
                 basic, stage=stage, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks,

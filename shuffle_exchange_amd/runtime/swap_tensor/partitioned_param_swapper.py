@@ -35,12 +35,16 @@ class AsyncPartitionedParameterSwapper:
     every dirty buffer back. Eviction takes the least recently used unpinned buffer, writing it back
     first if dirty and waiting for the HIP event of its last reader."""
 
+    _count = 0
+
     def __init__(self, nvme_path, rank, dtype, aio_config=None, buffer_count=5):
         from ...ops.aio import AsyncIOHandle
         assert nvme_path, "offload_param.device=nvme needs nvme_path"
         self.dir = os.path.join(nvme_path, f"sxe_param_swap_rank{rank}")
         os.makedirs(self.dir, exist_ok=True)
-        self.file = os.path.join(self.dir, "params.swp")
+        # one file per swapper instance (several engines may share an nvme_path in one process)
+        AsyncPartitionedParameterSwapper._count += 1
+        self.file = os.path.join(self.dir, f"params_{os.getpid()}_{AsyncPartitionedParameterSwapper._count}.swp")
         open(self.file, "wb").close()
         self.dtype = dtype
         self.esize = torch.tensor([], dtype=dtype).element_size()
@@ -196,6 +200,11 @@ class AsyncPartitionedParameterSwapper:
         self.dirty.add(key)
         return self._view(key)
 
+    def read_copy(self, key):
+        """A standalone host copy of the shard (checkpointing); does not mark it dirty."""
+        self._resident(key)
+        return self._view(key).clone()
+
     def flush(self):
         """Write every dirty shard back and wait for all I/O."""
         for key in list(self.dirty):
@@ -208,3 +217,15 @@ class AsyncPartitionedParameterSwapper:
     def synchronize_reads(self):
         self.rd.wait()
         self.reads.clear()
+
+    def close(self):
+        """Drain all I/O and delete the swap file."""
+        try:
+            self.rd.wait()
+            self.wr.wait()
+            os.remove(self.file)
+        except (OSError, RuntimeError):
+            pass
+
+    def __del__(self):
+        self.close()

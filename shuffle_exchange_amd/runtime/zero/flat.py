@@ -51,6 +51,7 @@ class FlatUnit:
         self.lo = self.rank * self.chunk
         self.hi = self.lo + self.chunk
         self.flat = None           # full bit16 buffer (stage 1/2 always; stage 3 while fetched)
+        self.swap = None           # NVMe parameter tier (ZeRO-Infinity): the shard lives in a swap file
         self.shard = None          # this rank's chunk (a view of `flat` for stage 1/2; own storage stage 3)
         self.master = None         # fp32 chunk (view into the group master buffer)
         self.grad = None           # fp32 chunk gradient accumulator (view into group grad buffer)
@@ -64,6 +65,27 @@ class FlatUnit:
             self._build_full()
 
     # ------------------------------------------------------------------------------------------
+    @property
+    def shard(self):
+        """This rank's bit16 chunk. With the NVMe tier: the swap cache's resident pinned buffer,
+        read in on demand and marked dirty (any in-place edit is written back on eviction/flush)."""
+        if self.swap is not None:
+            return self.swap.access(self)
+        return self._shard
+
+    @shard.setter
+    def shard(self, v):
+        self._shard = v
+
+    def shard_for_overwrite(self):
+        """The chunk to receive a whole new value (optimizer step): no swap-in read first."""
+        if self.swap is not None:
+            return self.swap.overwrite(self)
+        return self._shard
+
+    def shard_is_cuda(self):
+        return self.swap is None and self._shard is not None and self._shard.is_cuda
+
     def _build_full(self):
         flat = torch.zeros(self.padded, dtype=self.dtype, device=self.device)
         with torch.no_grad():

@@ -158,7 +158,7 @@ class HostOptimizerStep:
         if self.streamed and all_units:
             maxc = max(u.chunk for u in all_units)
             self.gslots = [_pinned(maxc, torch.float32) for _ in range(self.STAGE_SLOTS)]
-            lp_dtype = next((u.dtype for u in all_units if u.shard.is_cuda), None)
+            lp_dtype = next((u.dtype for u in all_units if u.shard_is_cuda()), None)
             self.lslots = [_pinned(maxc, lp_dtype) for _ in range(self.STAGE_SLOTS)] if lp_dtype else None
             self._lslot_ev = [None] * self.STAGE_SLOTS
         for g, units in enumerate(opt.units):
@@ -166,7 +166,7 @@ class HostOptimizerStep:
                 continue  # Twin-Flow device group: initialised by the ZeRO optimizer itself
             total = sum(u.chunk for u in units)
             gr = torch.zeros(total, dtype=torch.float32, device=opt.device)  # GPU accumulator
-            needs_lp = any(u.shard.is_cuda for u in units)
+            needs_lp = any(u.shard_is_cuda() for u in units)
             opt.grad_host[g] = None if self.streamed else _pinned(total, torch.float32)
             opt.lp_host[g] = _pinned(total, units[0].dtype) if needs_lp and not self.streamed else None
             if self.device == "cpu":
@@ -299,18 +299,18 @@ class HostOptimizerStep:
                 master, states = views[0], views[1:]
             else:
                 master, states = u.master, self._state_views(opt, g, off, u.chunk)
-            if u.shard.is_cuda:
+            if u.shard_is_cuda():
                 if self._lslot_ev[slot] is not None:
                     self._lslot_ev[slot].synchronize()  # its previous H2D has drained
                 lp = self.lslots[slot][:u.chunk]
             else:
-                lp = u.shard
+                lp = u.shard_for_overwrite()  # pinned host shard, or an NVMe swap buffer
             self._host_kernel(opt, pg, st, master, grad, states, lp, coef)
             if nvme:
                 self.swapper.write(k % nslot, g, i, u.chunk)
             if k + NS < len(flat):
                 issue_d2h(k + NS)  # this grad slot is free again
-            if u.shard.is_cuda:
+            if u.shard_is_cuda():
                 with get_accelerator().stream(self.h2d):
                     u.shard.copy_(lp, non_blocking=True)
                     ev = torch.cuda.Event()
@@ -318,6 +318,8 @@ class HostOptimizerStep:
                     self._lslot_ev[slot] = ev
         if nvme:
             self.swapper.drain()
+        if getattr(opt, "pswap", None) is not None:
+            opt.pswap.flush()  # updated NVMe-tier shards back to their swap file
         if cur is not None:
             cur.wait_stream(self.d2h)  # zero_grad_buffers() must not overtake the copies
             cur.wait_stream(self.h2d)
@@ -367,14 +369,16 @@ class HostOptimizerStep:
         m.grad = None
         off = 0
         for u in units:
-            if u.shard.is_cuda:
+            if u.shard_is_cuda():
                 lp = opt.lp_host[g][off:off + u.chunk]
                 lp.copy_(u.master)
                 with get_accelerator().stream(self.h2d):
                     u.shard.copy_(lp, non_blocking=True)
             else:
-                u.shard.copy_(u.master)
+                u.shard_for_overwrite().copy_(u.master)
             off += u.chunk
+        if getattr(opt, "pswap", None) is not None:
+            opt.pswap.flush()
 
     # ------------------------------------------------------------------------- checkpoint support
     def materialize(self, opt):

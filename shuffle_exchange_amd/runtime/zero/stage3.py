@@ -111,7 +111,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                  quantized_gradients=False, hpz_partition_size=1, quant_group_size=128, grad_quant_bits=8,
                  max_reuse_distance=1_000_000_000, max_live_parameters=1_000_000_000, defer_reduce=False,
                  retain_params=False, loco_param=None, prefetch_bucket_size=None,
-                 model_persistence_threshold=2**63 - 1):
+                 model_persistence_threshold=2**63 - 1, param_swap=None):
         acc = get_accelerator()
         device = torch.device(acc.current_device_name())
         self.module = module
@@ -140,6 +140,18 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         self.offload_param = bool(offload_param)
         if self.offload_param and self.se is not None:
             raise NotImplementedError("offload_param with shuffle-exchange slices is not supported")
+        # offload_param.device = nvme: non-persistent shards live in a swap file (ZeRO-Infinity),
+        # cached in a few pinned buffers (runtime/swap_tensor/partitioned_param_swapper.py)
+        self.pswap = None
+        if param_swap is not None:
+            if host_step is None:
+                raise ValueError("offload_param.device=nvme needs offload_optimizer (cpu or nvme): the "
+                                 "optimizer step writes the updated shards on the host")
+            if quantized_weights:
+                raise ValueError("offload_param.device=nvme does not combine with zero_quantized_weights")
+            from ..swap_tensor.partitioned_param_swapper import AsyncPartitionedParameterSwapper
+            self.pswap = AsyncPartitionedParameterSwapper(**param_swap)
+            self.offload_param = True
         self.S = self.topo.S
         # ZeRO++ knobs
         self.qwz = bool(quantized_weights) and self.S > 1
@@ -294,7 +306,11 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             u.shard = flat[u.lo:u.hi]
             u.state = AVAILABLE
         else:
-            if self.offload_param:
+            if self.pswap is not None:
+                self.pswap.register(u, flat[u.lo:u.hi].cpu())
+                u.shard = None
+                u.swap = self.pswap
+            elif self.offload_param:
                 if flat.is_cuda:
                     from .offload import pinned_empty  # exact-size pinned (no power-of-2 rounding)
                     u.shard = pinned_empty(u.chunk, dtype)
@@ -460,11 +476,18 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             st.wait_stream(cur)
         with get_accelerator().stream(st):
             u.flat.untyped_storage().resize_(u.padded * u.flat.element_size())
-            src = u.shard
+            swapped = u.swap is not None
+            src = u.swap.acquire(u) if swapped else u.shard
             if src.device != u.flat.device:
                 src = src.to(u.flat.device, non_blocking=True)
                 if st is not None:
                     src.record_stream(st)
+            if swapped:  # the pinned swap buffer may be reused once this H2D copy has run
+                ev = None
+                if u.flat.is_cuda:
+                    ev = torch.cuda.Event()
+                    ev.record(st if st is not None else cur)
+                u.swap.release(u, ev)
             if self.S == 1:
                 u.flat.copy_(src)
             elif self.hpz > 1 and self._in_bwd and u.sec_valid:
@@ -553,6 +576,12 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             return
         for j in order[i + 1:i + 1 + self.prefetch_depth]:
             self._fetch(self.fgroups[j], wait=False)
+        if self.pswap is not None:
+            # NVMe read-ahead beyond the gather window, into whatever swap buffers are free now
+            for j in order[i + 1 + self.prefetch_depth:i + 1 + 2 * self.prefetch_depth + 2]:
+                for u in self.fgroups[j].units:
+                    if u.swap is not None and u.state == RELEASED:
+                        self.pswap.prefetch(u)
 
     def _pre_backward(self, fg):
         self._in_bwd = True
@@ -794,7 +823,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             "clip_grad": self.clip_grad,
             "optimizer_state_dict": self.optimizer.state_dict(),
             "fp32_flat_groups": [m.data for m in self.master],
-            "bit16_partitions": [[u.shard for u in units] for units in self.units],
+            "bit16_partitions": [[u.swap.read_copy(u) if u.swap is not None else u.shard for u in units]
+                                 for units in self.units],
             "zero_stage": 3,
             "partition_count": self.S,
             "shuffle_exchange": self.se.state_dict() if self.se is not None else None,
@@ -815,7 +845,9 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             m.data.copy_(saved.to(m.device))
         for units in self.units:
             for u in units:
-                u.shard.copy_(u.master)
+                u.shard_for_overwrite().copy_(u.master)
+        if self.pswap is not None:
+            self.pswap.flush()
         self._host_flush()
         self._refresh_persistent()
         if self.se is not None and sd.get("shuffle_exchange"):
