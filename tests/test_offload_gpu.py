@@ -29,6 +29,9 @@ def _case(rank, world, stage, offload, nvme_dir=None):
             zc["offload_param"] = {"device": "cpu", "pin_memory": True}
     elif offload == "nvme":
         zc["offload_optimizer"] = {"device": "nvme", "nvme_path": nvme_dir}
+    elif offload == "nvme_params":  # ZeRO-Infinity: parameter shards AND optimizer state on NVMe
+        zc["offload_optimizer"] = {"device": "nvme", "nvme_path": nvme_dir}
+        zc["offload_param"] = {"device": "nvme", "nvme_path": nvme_dir, "buffer_count": 3}
     ds = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": 2, "bf16": {"enabled": True},
           "gradient_clipping": 1.0, "zero_optimization": zc,
           "optimizer": {"type": "AdamW", "params": {"lr": 1e-3, "weight_decay": 0.01}}}
@@ -44,7 +47,8 @@ def _case(rank, world, stage, offload, nvme_dir=None):
     return C.full_params(eng)
 
 
-@pytest.mark.parametrize("stage,offload", [(2, "cpu"), (3, "cpu"), (3, "nvme"), (3, "twin_flow")])
+@pytest.mark.parametrize("stage,offload", [(2, "cpu"), (3, "cpu"), (3, "nvme"), (3, "twin_flow"),
+                                           (3, "nvme_params")])
 def test_offload_matches_hbm_adam(stage, offload):
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
         off = run_dist(_case, 1, stage, offload, d)[0]
