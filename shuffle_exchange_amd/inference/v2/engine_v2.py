@@ -64,11 +64,31 @@ class RaggedInferenceEngineConfig:
     weight_quant: Optional[str] = None  # "fp8": row-scaled e4m3 projection / LM-head weights (W8A16 decode GEMMs)
 
 
+def _tp_group(tp):
+    """Consecutive blocks of `tp` ranks (the ranks of one node share one xGMI mesh)."""
+    from ... import comm as dist
+    assert dist.is_initialized(), "tensor_parallel.tp_size > 1 needs torch.distributed"
+    world, me = dist.get_world_size(), dist.get_rank()
+    assert world % tp == 0, f"world size {world} must be a multiple of tp_size {tp}"
+    if tp == world:
+        return None  # the world group
+    mine = None
+    for i in range(0, world, tp):
+        g = dist.new_group(list(range(i, i + tp)))  # every rank creates every group
+        if i <= me < i + tp:
+            mine = g
+    return mine
+
+
 class InferenceEngineV2:
     def __init__(self, model, config: RaggedInferenceEngineConfig = None):
         from .model_implementations import ragged_model_for
         self._config = config or RaggedInferenceEngineConfig()
-        self._model = ragged_model_for(model, weight_quant=self._config.weight_quant)
+        tp = int((self._config.tensor_parallel or {}).get("tp_size", 1))
+        self._tp = tp
+        self._tp_group = _tp_group(tp) if tp > 1 else None
+        self._model = ragged_model_for(model, weight_quant=self._config.weight_quant, tp_group=self._tp_group,
+                                       tp_size=tp)
         sm = self._config.state_manager
         dev = self._model.device
         bs = self._config.kv_block_size
@@ -138,7 +158,8 @@ class InferenceEngineV2:
             m = self._model
             dense = not getattr(m, "is_moe", False) and not any(
                 "router" in L for L in getattr(m, "w", {}).get("layers", []))
-            ok = (self._config.decode_graphs and m.device.type == "cuda" and dense and self._kv.free_blocks > 1)
+            ok = (self._config.decode_graphs and m.device.type == "cuda" and dense and self._kv.free_blocks > 1
+                  and self._tp == 1)  # collectives stay outside graph capture
             if ok:
                 from .decode_graphs import DecodeGraphRunner
                 sm = self._config.state_manager

@@ -13,6 +13,13 @@ BLAS linear, cutlass MoE GEMM) replaced by this framework's gfx950 kernels:
   * only the last token of every sequence goes through the final norm + LM head.
 The weights are the training modules' own parameters (no copy): a trained LlamaForCausalLM /
 MixtralForCausalLM serves directly.
+
+Tensor parallelism (``tp_group`` of size t; reference llama_v2/model.py:156 all-reduce after the
+attention output and MLP down projections, :191 all-gather of the vocab-parallel logits): each rank
+holds q heads / kv heads / FFN columns / vocab rows of its 1/t share (kv heads replicated when t
+exceeds their count), its KV cache holds only its kv heads, and per layer exactly two all-reduces
+(o_proj, down_proj) plus one logits all-gather per forward cross xGMI. The embedding and norms stay
+replicated. Dense models only (experts run locally, ``ep_size == 1``).
 """
 import torch
 import torch.nn.functional as F
@@ -26,10 +33,55 @@ from ....ops.rope import apply_rope_tokens_
 FLASH_PREFILL_MIN = 128
 
 
+class _TPShards:
+    """This rank's slices of every projection (copied once; the full weights can then be freed)."""
+
+    def __init__(self, model, t, r, nq, nkv, D):
+        assert nq % t == 0, f"query heads ({nq}) must divide by tp_size ({t})"
+        assert nkv % t == 0 or t % nkv == 0, f"kv heads ({nkv}) and tp_size ({t}) must divide one another"
+        self.nq = nq // t
+        if nkv % t == 0:
+            self.nkv, kv0 = nkv // t, r * (nkv // t)
+        else:  # fewer kv heads than ranks: each rank keeps the kv head its q heads attend to
+            self.nkv, kv0 = 1, (r * nq // t) // (nq // nkv)
+        q0 = r * self.nq
+        self.layers = []
+        for layer in model.layers:
+            a = layer.self_attn
+            w = a.qkv_proj.weight
+            q = w[q0 * D:(q0 + self.nq) * D]
+            k = w[(nq + kv0) * D:(nq + kv0 + self.nkv) * D]
+            v = w[(nq + nkv + kv0) * D:(nq + nkv + kv0 + self.nkv) * D]
+            d = {"qkv": torch.cat([q, k, v]).contiguous(),
+                 "o": a.o_proj.weight[:, q0 * D:(q0 + self.nq) * D].contiguous()}
+            mlp = layer.mlp
+            inter = mlp.gate_up_proj.weight.shape[0] // 2
+            assert inter % t == 0, f"intermediate size ({inter}) must divide by tp_size ({t})"
+            c = inter // t
+            gu = mlp.gate_up_proj.weight
+            d["gu"] = torch.cat([gu[r * c:(r + 1) * c], gu[inter + r * c:inter + (r + 1) * c]]).contiguous()
+            d["down"] = mlp.down_proj.weight[:, r * c:(r + 1) * c].contiguous()
+            self.layers.append(d)
+        V = model.lm_head.weight.shape[0]
+        self.vshard = -(-V // t)
+        self.vocab = V
+        lo, hi = min(r * self.vshard, V), min((r + 1) * self.vshard, V)
+        head = model.lm_head.weight[lo:hi]
+        if hi - lo < self.vshard:  # pad the last shard so every rank gathers the same size
+            head = torch.cat([head, head.new_zeros(self.vshard - (hi - lo), head.shape[1])])
+        self.head = head.contiguous()
+
+
 class RaggedLlama:
-    def __init__(self, model, weight_quant=None):
+    def __init__(self, model, weight_quant=None, tp_group=None, tp_size=1):
         self.model = model
         self.qw = None
+        from .... import comm as dist
+        self.tp_group = tp_group  # None with tp_size > 1: the world group
+        self.tp = int(tp_size)
+        if self.tp > 1:
+            assert dist.get_world_size(tp_group) == self.tp, "tp_group size != tp_size"
+        self.tp_rank = dist.get_rank(tp_group) if self.tp > 1 else 0
         if weight_quant:
             assert weight_quant == "fp8", "weight_quant: 'fp8'"
             from ....ops.fp_quantizer import FP8Weight
@@ -47,6 +99,14 @@ class RaggedLlama:
         self.nq, self.nkv, self.head_dim = a0.nq, a0.nkv, a0.d
         self.num_layers = len(model.layers)
         self.vocab_size = self.cfg.vocab_size
+        self.tps = None
+        if self.tp > 1:
+            if self.is_moe:
+                raise NotImplementedError("ragged tensor parallelism covers dense Llama-family models")
+            if weight_quant:
+                raise NotImplementedError("weight_quant with tensor_parallel")
+            self.tps = _TPShards(model, self.tp, self.tp_rank, self.nq, self.nkv, self.head_dim)
+            self.nq, self.nkv = self.tps.nq, self.tps.nkv
 
     @property
     def device(self):
@@ -93,6 +153,12 @@ class RaggedLlama:
         return out
 
     def _proj(self, mod, x, li, key):
+        if self.tps is not None:
+            y = linear(x, self.tps.layers[li][key])
+            if key in ("o", "down"):  # row-parallel: partial sums over this rank's heads / FFN columns
+                from .... import comm as dist
+                dist.all_reduce(y, group=self.tp_group)
+            return y
         # FP8 weights pay off where the GEMM is weight-streaming bound (<= 16 rows: W8A16 skinny
         # kernel); larger batches keep the module's bf16 weight on hipBLASLt
         if self.qw is not None and key in self.qw[li] and x.shape[0] <= 16:
@@ -156,5 +222,11 @@ class RaggedLlama:
             x, res = self._mlp(layer, m, li), h2
         last = batch.last_idx
         h = model.norm(x.index_select(0, last), res.index_select(0, last))[0]
+        if self.tps is not None:  # vocab-parallel head: gather every rank's logit columns
+            from .... import comm as dist
+            part = linear(h, self.tps.head).float()
+            full = torch.empty(self.tp * part.shape[0], part.shape[1], dtype=part.dtype, device=part.device)
+            dist.all_gather_into_tensor(full, part, group=self.tp_group)
+            return full.view(self.tp, -1, part.shape[1]).permute(1, 0, 2).reshape(part.shape[0], -1)[:, :self.tps.vocab]
         use_q = self.qw is not None and h.shape[0] <= 16
         return linear(h, self.qhead if use_q else model.lm_head.weight).float()

@@ -71,3 +71,38 @@ def test_init_inference_generate_matches_recompute():
             nxt = m(ids)[:, -1].argmax(-1, keepdim=True)
         ids = torch.cat([ids, nxt], dim=1)
     assert torch.equal(out.cpu(), ids)
+
+
+def _case_v2_tp(rank, world, tp, nq, nkv):
+    import torch
+    from shuffle_exchange_amd.inference.v2 import RaggedInferenceEngineConfig, build_engine
+    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+    torch.manual_seed(0)
+    cfg = llama_config("llama-tiny", num_attention_heads=nq, num_key_value_heads=nkv, hidden_size=128,
+                       intermediate_size=256, vocab_size=301, num_hidden_layers=2)
+    m = LlamaForCausalLM(cfg)
+    eng = build_engine(m, RaggedInferenceEngineConfig(kv_block_size=8, num_kv_blocks=64,
+                                                      tensor_parallel={"tp_size": tp}))
+    g = torch.Generator().manual_seed(3)
+    prompts = [torch.randint(0, 301, (n,), generator=g) for n in (5, 11, 3)]
+    first = eng.put([1, 2, 3], prompts)  # ragged prefill
+    nxt = first.argmax(-1)
+    second = eng.put([1, 2, 3], [t.view(1) for t in nxt])  # one decode step each
+    gen = eng.generate([prompts[0].tolist()], max_new_tokens=4)
+    return {"first": first, "second": second, "gen": gen, "kv_heads": eng.model.nkv}
+
+
+@pytest.mark.parametrize("nq,nkv", [(4, 2), (4, 1)])
+def test_v2_tensor_parallel_matches_tp1(nq, nkv):
+    """InferenceEngineV2 with tensor_parallel.tp_size = 2 on gloo (reference llama_v2/model.py:156-191:
+    all-reduce after o_proj / down_proj, all-gather of vocab-parallel logits; an odd vocab pads the
+    last shard; kv heads replicated when tp exceeds them) == the tp = 1 engine: prefill + decode logits
+    and greedy generation."""
+    from .dist_utils import run_dist
+    one = run_dist(_case_v2_tp, 1, 1, nq, nkv)[0]
+    two = run_dist(_case_v2_tp, 2, 2, nq, nkv)
+    for r in two:
+        assert r["kv_heads"] == max(1, nkv // 2)
+        assert torch.allclose(r["first"], one["first"], atol=1e-4), (r["first"] - one["first"]).abs().max()
+        assert torch.allclose(r["second"], one["second"], atol=1e-4)
+        assert r["gen"] == one["gen"]
