@@ -86,11 +86,12 @@ def _max_capacity(exp_counts, ep_group, num_tokens):
 
 def top1gating(logits, capacity_factor, min_capacity, used_token=None, noisy_gate_policy=None, drop_tokens=True,
                use_rts=True, ep_group=None):
+    from ..ops.moe import topk_softmax
     logits_w_noise = logits + gumbel_rsample(logits.shape, logits.device) if noisy_gate_policy == "RSample" else None
-    gates = F.softmax(logits, dim=1)
+    gates, top = topk_softmax(logits, 1)
     S, E = gates.shape
     capacity = _capacity(S, E, capacity_factor, min_capacity)
-    idx1 = torch.argmax(logits_w_noise if logits_w_noise is not None else gates, dim=1)
+    idx1 = torch.argmax(logits_w_noise, dim=1) if logits_w_noise is not None else top[:, 0]
     mask1 = F.one_hot(idx1, E)
     if used_token is not None:
         mask1 = mask1 * used_token.unsqueeze(1).to(mask1.dtype)
@@ -140,8 +141,9 @@ def top2gating(logits, capacity_factor, min_capacity, drop_tokens=True, ep_group
 
 
 def topkgating(logits, k, capacity_factor, min_capacity, drop_tokens=True, ep_group=None, drop_policy="probs"):
-    top_gate, top_idx = torch.topk(logits, k=k, dim=1)
-    gates = F.softmax(logits, dim=1)
+    from ..ops.moe import topk_softmax
+    gates, top_idx = topk_softmax(logits, k)  # one HIP launch on GPU (softmax + top-k per token)
+    top_gate = torch.gather(logits, 1, top_idx)
     S, E = gates.shape
     mask = torch.zeros_like(gates, dtype=torch.bool).scatter_(1, top_idx, True)
     exp_counts = mask.sum(0).detach()
@@ -258,11 +260,11 @@ class MOELayer(nn.Module):
         E = self.ep_size * self.num_local_experts
         C = r.capacity
         k = r.expert.shape[1]
-        keep = r.keep.reshape(-1)
-        tok = torch.arange(S, device=x.device).repeat_interleave(k)[keep]
-        slots = r.slots().reshape(-1)[keep]
-        # dispatch: rows of x into their expert/capacity slot (dropped slots stay zero)
-        disp = xt.new_zeros(E * C, H).index_copy(0, slots, xt.index_select(0, tok))
+        from ..ops.moe import combine, dispatch, routing_tables
+        # slots[t, c] = expert * C + position (-1 dropped) and its inverse slot_src[E * C]: dispatch
+        # and combine are then atomic-free row gathers (csrc/kernels/moe.hip on the GPU)
+        slots, slot_src = routing_tables(r.expert, r.location, r.keep, C, E)
+        disp = dispatch(xt, slots, slot_src)
         # [E, C, H] -> a2a over EP: rank j receives, from every rank, the rows for its local experts
         disp = all_to_all(self.ep_group, disp.view(self.ep_size, self.num_local_experts * C, H))
         # local experts see [E_local, ep*C, H]
@@ -272,8 +274,7 @@ class MOELayer(nn.Module):
         out = out.view(self.num_local_experts, self.ep_size, C, H).transpose(0, 1).reshape(self.ep_size,
                                                                                               self.num_local_experts * C, H)
         out = all_to_all(self.ep_group, out).reshape(E * C, H)
-        w = r.weight.reshape(-1)[keep].to(out.dtype)
-        comb = xt.new_zeros(S, H).index_add(0, tok, out.index_select(0, slots) * w.unsqueeze(1))
+        comb = combine(out, slots, slot_src, r.weight)
         self.l_aux = r.l_aux
         self.exp_counts = r.exp_counts
         return comb.view(shape)

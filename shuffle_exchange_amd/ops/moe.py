@@ -1,0 +1,106 @@
+"""MoE routing ops on the gfx950 kernels of csrc/kernels/moe.hip, with autograd.
+
+* ``topk_softmax(logits, k)`` -> (probs, top_idx): fused softmax + top-k per token (one wave per
+  token); ``probs`` is differentiable (softmax backward), ``top_idx`` int64;
+* ``routing_tables(expert, location, keep, capacity, E)`` -> (slots [S, k], slot_src [E*C]): the
+  forward map (assignment -> capacity slot, -1 = dropped) and its inverse (slot -> assignment,
+  -1 = empty) that make dispatch / combine atomic-free gathers;
+* ``dispatch(x, slots, slot_src)``: [S, H] -> [E*C, H] expert-ordered rows (empty slots zero);
+* ``combine(expert_out, slots, slot_src, w)``: [E*C, H] -> [S, H], weighted by the fp32 gate
+  weights ``w`` [S, k] (differentiable in both ``expert_out`` and ``w``).
+
+Parity: reference inference/v2/kernels/ragged_ops/top_k_gating (:15), moe_scatter (:23),
+moe_gather (:21); training dispatch/combine of runtime moe/sharded_moe.py:587-678. CPU tensors
+(gloo plumbing tests) take the equivalent PyTorch ops.
+"""
+import torch
+import torch.nn.functional as F
+
+from . import native
+
+
+def _hip(t):
+    return t.is_cuda and native.use_hip(t)
+
+
+class _TopKSoftmax(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, k):
+        probs, _, topi = torch.ops.sxe.moe_topk_softmax(logits.contiguous(), int(k))
+        ctx.save_for_backward(probs)
+        ctx.mark_non_differentiable(topi)
+        return probs, topi
+
+    @staticmethod
+    def backward(ctx, gprobs, _gtopi):
+        (p,) = ctx.saved_tensors
+        return p * (gprobs - (gprobs * p).sum(-1, keepdim=True)), None
+
+
+def topk_softmax(logits, k):
+    """(softmax(logits) [S, E] fp32, indices of the k largest [S, k] int64)."""
+    logits = logits.float()
+    if _hip(logits) and logits.dim() == 2 and logits.shape[1] <= 512:
+        return _TopKSoftmax.apply(logits, k)
+    probs = F.softmax(logits, dim=1)
+    return probs, torch.topk(logits, k=k, dim=1).indices
+
+
+def routing_tables(expert, location, keep, capacity, num_experts):
+    slots = torch.where(keep, expert * capacity + location, torch.full_like(expert, -1)).contiguous()
+    flat = slots.reshape(-1)
+    kept = flat >= 0
+    slot_src = torch.full((num_experts * capacity,), -1, dtype=torch.int64, device=expert.device)
+    slot_src.index_copy_(0, flat[kept], torch.arange(flat.numel(), device=expert.device)[kept])
+    return slots, slot_src
+
+
+class _Dispatch(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, slots, slot_src):
+        ctx.save_for_backward(slots)
+        return torch.ops.sxe.moe_dispatch(x.contiguous(), slot_src, slots.shape[1])
+
+    @staticmethod
+    def backward(ctx, g):
+        (slots,) = ctx.saved_tensors
+        return torch.ops.sxe.moe_gather_sum(g.contiguous(), slots, None), None, None
+
+
+class _Combine(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, out, slots, slot_src, w):
+        out = out.contiguous()
+        w = w.float().contiguous()
+        ctx.save_for_backward(out, slot_src, w, slots)
+        return torch.ops.sxe.moe_gather_sum(out, slots, w)
+
+    @staticmethod
+    def backward(ctx, gy):
+        out, slot_src, w, slots = ctx.saved_tensors
+        gout, gw = torch.ops.sxe.moe_combine_bwd(gy.contiguous(), out, slot_src, w)
+        return gout, None, None, gw
+
+
+def _kernel_ok(x):
+    return _hip(x) and x.dim() == 2 and x.shape[1] % 8 == 0 and x.dtype in (torch.bfloat16, torch.float16,
+                                                                            torch.float32)
+
+
+def dispatch(x, slots, slot_src):
+    if _kernel_ok(x):
+        return _Dispatch.apply(x, slots, slot_src)
+    k = slots.shape[1]
+    src = slot_src.clamp(min=0) // k
+    rows = x.index_select(0, src)
+    return rows * (slot_src >= 0).unsqueeze(1).to(rows.dtype)
+
+
+def combine(expert_out, slots, slot_src, w):
+    if _kernel_ok(expert_out):
+        return _Combine.apply(expert_out, slots, slot_src, w)
+    S, k = slots.shape
+    idx = slots.clamp(min=0).reshape(-1)
+    rows = expert_out.index_select(0, idx).view(S, k, -1)
+    ww = (w.float() * (slots >= 0)).to(rows.dtype).unsqueeze(-1)
+    return (rows * ww).sum(1)
