@@ -85,9 +85,12 @@ class _GroupedMM(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             tgt = getattr(w, "_sxe_grad_target", None)
             if tgt is not None:
+                from ..ops.linear import _sxe_wgrad_ok
                 buf, acc = tgt(w)
                 for e in range(E):
-                    if buf.dtype == torch.float32 and dy.dtype != torch.float32 and dy.is_cuda:
+                    if _sxe_wgrad_ok(x[e], dy[e], buf[e]):  # hand-written k-major wgrad GEMM (gemm_wgrad.hip)
+                        torch.ops.sxe.wgrad_gemm_(x[e], dy[e], buf[e], 1.0, bool(acc))
+                    elif buf.dtype == torch.float32 and dy.dtype != torch.float32 and dy.is_cuda:
                         torch.ops.aten.addmm.dtype_out(buf[e], x[e].t(), dy[e], torch.float32, beta=1 if acc else 0,
                                                        alpha=1, out=buf[e])
                     elif buf.dtype != dy.dtype:

@@ -15,7 +15,15 @@ def main():
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
-    step = rows[idx[-2] + 1:idx[-1] + 1]
+    # an optimizer step may launch the marker several times back to back (one per param group):
+    # cluster adjacent launches; the step is everything after the second-to-last cluster
+    clusters = []
+    for i in idx:
+        if clusters and i - clusters[-1][-1] <= 2:
+            clusters[-1].append(i)
+        else:
+            clusters.append([i])
+    step = rows[clusters[-2][-1] + 1:clusters[-1][-1] + 1]
     t0, t1 = int(step[0]["Start_Timestamp"]), int(step[-1]["End_Timestamp"])
     c, n = collections.Counter(), collections.Counter()
     for r in step:
