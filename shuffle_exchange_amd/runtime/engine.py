@@ -869,6 +869,17 @@ class SXEEngine(nn.Module):
         if self._config.model.checkpoint.load_universal:
             return self.load_universal_checkpoint(os.path.join(load_dir, str(tag)), load_optimizer_states,
                                                   load_lr_scheduler_states)
+        from ..checkpoint.reference_format import is_reference_checkpoint, load_reference_checkpoint
+        if not load_module_only and is_reference_checkpoint(load_dir, tag):
+            # written by the reference's ZeRO (its key schema and pickled classes): merge the fp32
+            # partitions and Adam moments and scatter them into this engine's own layout
+            ck = load_reference_checkpoint(self, load_dir, tag, load_optimizer_states, load_lr_scheduler_states,
+                                           strict=load_module_strict)
+            dist.barrier()
+            skip = {"module", "buffer_names", "optimizer", "param_shapes", "frozen_param_shapes", "lr_scheduler",
+                    "sparse_tensor_module_names", "skipped_steps", "global_steps", "global_samples",
+                    "dp_world_size", "mp_world_size", "ds_config", "ds_version", "shared_params"}
+            return os.path.join(load_dir, str(tag)), {k: v for k, v in ck["model_states"].items() if k not in skip}
         d, model_path, optim_path = self._ckpt_names(load_dir, tag)
         ce = self.checkpoint_engine
         state = ce.load(model_path, map_location="cpu")

@@ -49,6 +49,9 @@ def _optim_files(d):
 
 
 def get_fp32_state_dict_from_zero_checkpoint(checkpoint_dir, tag=None, exclude_frozen_parameters=False):
+    from ..checkpoint.reference_format import is_reference_checkpoint, read_reference_checkpoint
+    if is_reference_checkpoint(checkpoint_dir, tag):  # written in the reference's ZeRO layout
+        return dict(read_reference_checkpoint(checkpoint_dir, tag)["fp32"])
     d = _tag_dir(checkpoint_dir, tag)
     files = _optim_files(d)
     if not files:
