@@ -76,10 +76,11 @@ _SAFE = [
 ]
 
 
-def load_file(path):
-    """torch.load(weights_only=True) with the reference's pickled classes mapped to stand-ins."""
+def load_file(path, mmap=True):
+    """torch.load(weights_only=True) with the reference's pickled classes mapped to stand-ins;
+    memory-mapped, so merging touches only the slices it copies."""
     with torch.serialization.safe_globals(_SAFE):
-        return torch.load(path, map_location="cpu", weights_only=True)
+        return torch.load(path, map_location="cpu", weights_only=True, mmap=mmap)
 
 
 # ------------------------------------------------------------------------------- discovery

@@ -6,7 +6,10 @@ states) and the engine's ``load_universal_checkpoint`` path (runtime/engine.py, 
 {load_universal: true}``), which re-partitions those tensors for the *current* data-parallel /
 Shuffle-exchange layout -- so a run saved on 8 GPUs resumes on 4 or 16.
 
-Writing is offline (CPU, no process group); loading slices each parameter's fp32 tensor and
+Writing is offline (CPU, no process group) and streaming: the rank files are memory-mapped and
+consumed one unit at a time, so peak host memory is about one unit's full fp32 tensors (not every
+rank's whole state: ~840 GB for a 70B model). Checkpoints in the reference's own ZeRO layout are
+converted too (checkpoint/reference_format.py). Loading slices each parameter's fp32 tensor and
 moments straight into this rank's chunk of its flat unit (no full-model materialisation per rank).
 """
 import argparse
@@ -29,9 +32,33 @@ def _numel(shape):
     return n
 
 
+def _convert_reference(checkpoint_dir, output_dir, tag):
+    from .reference_format import _tag_dir as ref_tag_dir
+    from .reference_format import read_reference_checkpoint
+    ck = read_reference_checkpoint(checkpoint_dir, tag)
+    zdir = os.path.join(output_dir, "zero")
+    for name, t in ck["fp32"].items():
+        pdir = os.path.join(zdir, name)
+        os.makedirs(pdir, exist_ok=True)
+        torch.save(t.clone(), os.path.join(pdir, "fp32.pt"))
+        for k, v in ck["state"].get(name, {}).items():
+            if k in STATE_KEYS:
+                torch.save(v.clone(), os.path.join(pdir, f"{k}.pt"))
+    with open(os.path.join(output_dir, "universal_meta.json"), "w") as f:
+        json.dump({"step": ck["step"], "source_zero_stage": ck["zero_stage"], "source_format": "reference",
+                   "source_dp": ck["dp_world_size"]}, f)
+    d = ref_tag_dir(checkpoint_dir, tag)
+    for mf in glob.glob(os.path.join(d, "*model_states.pt")):
+        shutil.copy(mf, output_dir)
+    return output_dir
+
+
 def convert_to_universal(checkpoint_dir, output_dir, tag=None):
+    from .reference_format import is_reference_checkpoint
+    if is_reference_checkpoint(checkpoint_dir, tag):
+        return _convert_reference(checkpoint_dir, output_dir, tag)
     d = _tag_dir(checkpoint_dir, tag)
-    states = [_load(f)["optimizer_state_dict"] for f in _optim_files(d)]
+    states = [_load(f, mmap=True)["optimizer_state_dict"] for f in _optim_files(d)]
     s0 = states[0]
     stage = s0.get("zero_stage", 0)
     layout = s0["unit_layout"]

@@ -913,7 +913,11 @@ class SXEEngine(nn.Module):
         state = {}
         files = sorted(f for f in os.listdir(universal_dir) if f.endswith("model_states.pt"))
         if files:
-            state = torch.load(os.path.join(universal_dir, files[0]), map_location="cpu", weights_only=False)
+            from ..checkpoint.reference_format import load_file
+            try:  # weights_only (reference-written model states map their classes to stand-ins)
+                state = load_file(os.path.join(universal_dir, files[0]), mmap=False)
+            except Exception:  # this framework's own model states (client objects)
+                state = torch.load(os.path.join(universal_dir, files[0]), map_location="cpu", weights_only=False)
         if load_lr_scheduler_states and self.lr_scheduler is not None and state.get("lr_scheduler"):
             self.lr_scheduler.load_state_dict(state["lr_scheduler"])
         self.global_steps = state.get("global_steps", meta.get("step", 0))

@@ -22,8 +22,10 @@ import re
 import torch
 
 
-def _load(path):
-    return torch.load(path, map_location="cpu", weights_only=False)  # files written by this framework
+def _load(path, mmap=False):
+    # files written by this framework; mmap=True maps the tensors instead of reading them, so a
+    # consumer that slices one unit at a time only pages in that unit (streaming conversion)
+    return torch.load(path, map_location="cpu", weights_only=False, mmap=mmap)
 
 
 def _tag_dir(checkpoint_dir, tag=None):

@@ -194,3 +194,28 @@ def test_reference_files_load_with_weights_only(tmp_path):
     osd = load_file(f)["optimizer_state_dict"]
     assert osd["loss_scaler"].state()["cur_scale"] == 1024.0
     assert int(osd["zero_stage"]) == 2
+
+
+def _case_universal(rank, world, udir):
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd.utils.tensor_fragment import safe_get_full_fp32_param, safe_get_full_optimizer_state
+    model, _ = tiny_llama(5)
+    ds = {"train_micro_batch_size_per_gpu": 1, "zero_optimization": {"stage": 2},
+          "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}}, "checkpoint": {"load_universal": True}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    eng.load_checkpoint(os.path.dirname(udir), tag=os.path.basename(udir))
+    return {n: (safe_get_full_fp32_param(p).clone(), safe_get_full_optimizer_state(p, "exp_avg").clone())
+            for n, p in eng.module.named_parameters()}
+
+
+def test_reference_checkpoint_to_universal_and_resume(tmp_path):
+    """ds_to_universal on a reference-layout ZeRO-3 checkpoint (dp 3), resumed as ZeRO-2 on 2 ranks."""
+    from shuffle_exchange_amd.checkpoint.universal import convert_to_universal
+    fp32, m, _ = write_reference_checkpoint(str(tmp_path / "ck"), 3, 3)
+    udir = tmp_path / "uni" / "global_step7"
+    convert_to_universal(str(tmp_path / "ck"), str(udir))
+    assert (udir / "zero" / "lm_head.weight" / "fp32.pt").exists()
+    for r in run_dist(_case_universal, 2, str(udir)):
+        for n in fp32:
+            assert torch.allclose(r[n][0], fp32[n], atol=1e-7), n
+            assert torch.allclose(r[n][1], m[n], atol=1e-9), n
