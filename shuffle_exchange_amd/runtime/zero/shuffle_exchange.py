@@ -202,12 +202,14 @@ class ShuffleExchange:
             for t in tensors:
                 self._mean_allreduce(t, self.group, len(self.group_ranks))
         elif m == "H-RR":
+            # sum up the hierarchy, divide ONCE at the top (pre-dividing every bit16 chunk by n
+            # before the sums would round each contribution in bf16 first)
             n = self.topo.num_slices
             for t in tensors:
-                t.div_(n)
                 dist.reduce(t, dst=self.top_node, group=self.group)
                 if self.in_top:
                     dist.all_reduce(t, group=self.top_group)
+                    t.div_(n)
                 dist.broadcast(t, src=self.top_node, group=self.group)
         elif m == "Gossip":
             self._gossip(shards)
