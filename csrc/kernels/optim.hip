@@ -356,6 +356,116 @@ at::Tensor sumsq(at::Tensor x) {
   return partial.sum();
 }
 
+// ---------------------------------------------------------------------------------------------
+// LAMB over a flat fp32 master with PER-PARAMETER trust ratios (reference ops/lamb/fused_lamb.py:14,
+// csrc/lamb/fused_lamb_cuda_kernel.cu): the flat is cut into segments (this rank's fragment of each
+// original parameter); `blk` maps every block to (segment, begin, end) so a block never straddles
+// two parameters. Stage 1 updates m / v and accumulates, per segment, ||p||^2 and ||u||^2 of the
+// Adam direction u = m^ / (sqrt(v^) + eps) + wd p into `sums` [nseg, 2] (one atomic per block and
+// segment). The caller all-reduces `sums` over the partition group when a parameter is split across
+// ranks, so the ratio is the whole parameter's. Stage 2 recomputes u (p, m, v unchanged since) and
+// applies p -= lr * clamp(||p|| / ||u||, min_coeff, max_coeff) * u, writing the bit16 copy too.
+struct LambHP {
+  float lr, b1, b2, eps, wd, bc1, bc2, min_coeff, max_coeff;
+};
+
+template <DT G>
+__global__ void __launch_bounds__(256) lamb_stage1_kernel(const float* __restrict__ p,
+                                                          const typename dt_traits<G>::storage* __restrict__ g,
+                                                          float* __restrict__ m, float* __restrict__ v,
+                                                          const int64_t* __restrict__ blk, const int64_t* __restrict__ seg_id,
+                                                          float* __restrict__ sums, LambHP hp, float gscale,
+                                                          const float* __restrict__ scale_t, const float* __restrict__ skip_t) {
+  __shared__ float red[4];
+  if (skip_t && *skip_t != 0.f) return;
+  if (scale_t) gscale *= *scale_t;
+  const int64_t b0 = blk[2 * blockIdx.x], b1e = blk[2 * blockIdx.x + 1];
+  float pn = 0.f, un = 0.f;
+  for (int64_t i = b0 + threadIdx.x; i < b1e; i += blockDim.x) {
+    const float gi = to_f32<G>(g[i]) * gscale;
+    const float mi = hp.b1 * m[i] + (1.f - hp.b1) * gi;
+    const float vi = hp.b2 * v[i] + (1.f - hp.b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float pi = p[i];
+    const float u = (mi / hp.bc1) / (sqrtf(vi / hp.bc2) + hp.eps) + hp.wd * pi;
+    pn += pi * pi;
+    un += u * u;
+  }
+  pn = block_sum<4>(pn, red);
+  un = block_sum<4>(un, red);
+  if (threadIdx.x == 0) {
+    const int64_t sidx = seg_id[blockIdx.x];
+    atomicAdd(sums + 2 * sidx, pn);
+    atomicAdd(sums + 2 * sidx + 1, un);
+  }
+}
+
+template <DT L>
+__global__ void __launch_bounds__(256) lamb_stage2_kernel(float* __restrict__ p, const float* __restrict__ m,
+                                                          const float* __restrict__ v,
+                                                          typename dt_traits<L>::storage* __restrict__ lp,
+                                                          const int64_t* __restrict__ blk, const int64_t* __restrict__ seg_id,
+                                                          const float* __restrict__ sums, float* __restrict__ coeffs,
+                                                          LambHP hp, const float* __restrict__ skip_t) {
+  if (skip_t && *skip_t != 0.f) return;
+  const int64_t sidx = seg_id[blockIdx.x];
+  const float wn = sqrtf(sums[2 * sidx]), un = sqrtf(sums[2 * sidx + 1]);
+  float coeff = (wn > 0.f && un > 0.f) ? wn / un : 1.f;
+  coeff = fminf(fmaxf(coeff, hp.min_coeff), hp.max_coeff);
+  if (coeffs && threadIdx.x == 0) coeffs[sidx] = coeff;
+  const float step = hp.lr * coeff;
+  const int64_t b0 = blk[2 * blockIdx.x], b1e = blk[2 * blockIdx.x + 1];
+  for (int64_t i = b0 + threadIdx.x; i < b1e; i += blockDim.x) {
+    const float pi = p[i];
+    const float u = (m[i] / hp.bc1) / (sqrtf(v[i] / hp.bc2) + hp.eps) + hp.wd * pi;
+    const float np = pi - step * u;
+    p[i] = np;
+    if (lp) lp[i] = from_f32<L>(np);
+  }
+}
+
+// blk: [nblk, 2] int64 (begin, end) element ranges, seg_id: [nblk] int64, sums: [nseg, 2] fp32 (zeroed)
+void lamb_stage1_(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tensor blk, at::Tensor seg_id,
+                  at::Tensor sums, c10::optional<at::Tensor> scale_t, c10::optional<at::Tensor> skip_t, double lr,
+                  double b1, double b2, double eps, double wd, double bc1, double bc2, double grad_scale) {
+  SXE_CHECK(p.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat &&
+                sums.scalar_type() == at::kFloat && blk.scalar_type() == at::kLong && seg_id.scalar_type() == at::kLong,
+            "lamb_stage1_: dtypes");
+  const int64_t nblk = seg_id.numel();
+  if (nblk == 0) return;
+  c10::DeviceGuard guard(p.device());
+  LambHP hp{(float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2, 0.f, 0.f};
+  SXE_DISPATCH_DT(dtype_of(g), GT, {
+    using GS = typename dt_traits<GT>::storage;
+    hipLaunchKernelGGL((lamb_stage1_kernel<GT>), dim3(nblk), dim3(256), 0, cur_stream(), p.data_ptr<float>(),
+                       reinterpret_cast<const GS*>(g.data_ptr()), m.data_ptr<float>(), v.data_ptr<float>(),
+                       blk.data_ptr<int64_t>(), seg_id.data_ptr<int64_t>(), sums.data_ptr<float>(), hp,
+                       (float)grad_scale, opt_f32_ptr(scale_t), opt_f32_ptr(skip_t));
+  });
+  SXE_LAUNCH_CHECK();
+}
+
+void lamb_stage2_(at::Tensor p, at::Tensor m, at::Tensor v, c10::optional<at::Tensor> lp, at::Tensor blk,
+                  at::Tensor seg_id, at::Tensor sums, c10::optional<at::Tensor> coeffs, c10::optional<at::Tensor> skip_t,
+                  double lr, double eps, double wd, double bc1, double bc2, double min_coeff, double max_coeff) {
+  const int64_t nblk = seg_id.numel();
+  if (nblk == 0) return;
+  const bool has_lp = lp.has_value() && lp->defined();
+  c10::DeviceGuard guard(p.device());
+  LambHP hp{(float)lr, 0.f, 0.f, (float)eps, (float)wd, (float)bc1, (float)bc2, (float)min_coeff, (float)max_coeff};
+  float* cp = (coeffs.has_value() && coeffs->defined()) ? coeffs->data_ptr<float>() : nullptr;
+  DT ld = has_lp ? dtype_of(*lp) : DT::BF16;
+  SXE_DISPATCH_DT(ld, LT, {
+    using LS = typename dt_traits<LT>::storage;
+    hipLaunchKernelGGL((lamb_stage2_kernel<LT>), dim3(nblk), dim3(256), 0, cur_stream(), p.data_ptr<float>(),
+                       m.data_ptr<float>(), v.data_ptr<float>(), has_lp ? reinterpret_cast<LS*>(lp->data_ptr()) : nullptr,
+                       blk.data_ptr<int64_t>(), seg_id.data_ptr<int64_t>(), sums.data_ptr<float>(), cp, hp,
+                       opt_f32_ptr(skip_t));
+  });
+  SXE_LAUNCH_CHECK();
+}
+
 }  // namespace sxe
 
 TORCH_LIBRARY_FRAGMENT(sxe, m) {
@@ -370,6 +480,12 @@ TORCH_LIBRARY_FRAGMENT(sxe, m) {
   m.def("adagrad_flat_(Tensor(a!) p, Tensor g, Tensor(b!) s, Tensor(d!)? lp, Tensor? scale, Tensor? skip, float lr, "
         "float eps, float weight_decay, float grad_scale) -> ()");
   m.def("sumsq(Tensor x) -> Tensor");
+  m.def("lamb_stage1_(Tensor p, Tensor g, Tensor(a!) m, Tensor(b!) v, Tensor blk, Tensor seg_id, Tensor(c!) sums, "
+        "Tensor? scale, Tensor? skip, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1, "
+        "float bc2, float grad_scale) -> ()");
+  m.def("lamb_stage2_(Tensor(a!) p, Tensor m, Tensor v, Tensor(b!)? lp, Tensor blk, Tensor seg_id, Tensor sums, "
+        "Tensor(c!)? coeffs, Tensor? skip, float lr, float eps, float weight_decay, float bc1, float bc2, "
+        "float min_coeff, float max_coeff) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(sxe, CUDA, m) {
@@ -378,4 +494,6 @@ TORCH_LIBRARY_IMPL(sxe, CUDA, m) {
   m.impl("lion_flat_", &sxe::lion_flat_);
   m.impl("adagrad_flat_", &sxe::adagrad_flat_);
   m.impl("sumsq", &sxe::sumsq);
+  m.impl("lamb_stage1_", &sxe::lamb_stage1_);
+  m.impl("lamb_stage2_", &sxe::lamb_stage2_);
 }

@@ -191,9 +191,69 @@ class FusedAdagrad(torch.optim.Optimizer):
         return loss
 
 
+LAMB_BLOCK_ELEMS = 8192  # elements per HIP block of the LAMB kernels (one segment per block)
+
+
+def lamb_block_table(segments, device):
+    """(blk [nblk, 2] int64 element ranges, seg_id [nblk] int64) for segments [(seg_index, start,
+    numel)] of a flat buffer: no block straddles two segments (each segment = one parameter)."""
+    rows, ids = [], []
+    for sid, start, n in segments:
+        for b in range(start, start + n, LAMB_BLOCK_ELEMS):
+            rows.append((b, min(b + LAMB_BLOCK_ELEMS, start + n)))
+            ids.append(sid)
+    blk = torch.tensor(rows, dtype=torch.int64).reshape(-1, 2).to(device)
+    return blk, torch.tensor(ids, dtype=torch.int64).to(device)
+
+
+def lamb_flat_(p, g, m, v, lp, table, nseg, *, lr, beta1, beta2, eps, weight_decay, step, bias_correction=True,
+               min_coeff=0.01, max_coeff=10.0, scale_t=None, skip_t=None, norm_group=None, coeffs=None):
+    """LAMB on a flat fp32 master whose segments are (fragments of) separate parameters: per-segment
+    trust ratios (csrc/kernels/optim.hip lamb_stage1_/lamb_stage2_). ``norm_group``: all-reduce the
+    per-segment norms over the ranks that hold the other fragments of the same parameters."""
+    bc1 = 1 - beta1 ** step if bias_correction else 1.0
+    bc2 = 1 - beta2 ** step if bias_correction else 1.0
+    blk, seg_id = table
+    sums = torch.zeros(nseg, 2, dtype=torch.float32, device=p.device)
+    if p.is_cuda and native.use_hip(p):
+        torch.ops.sxe.lamb_stage1_(p, g, m, v, blk, seg_id, sums, scale_t, skip_t, float(lr), float(beta1),
+                                   float(beta2), float(eps), float(weight_decay), float(bc1), float(bc2), 1.0)
+        if norm_group is not None:
+            from .. import comm as dist
+            dist.all_reduce(sums, group=norm_group)
+        torch.ops.sxe.lamb_stage2_(p, m, v, lp, blk, seg_id, sums, coeffs, skip_t, float(lr), float(eps),
+                                   float(weight_decay), float(bc1), float(bc2), float(min_coeff), float(max_coeff))
+        return
+    # CPU reference path (gloo plumbing): the same two stages in torch
+    if skip_t is not None and float(skip_t.reshape(-1)[0]) != 0.0:
+        return
+    gs = g.float() * (scale_t.reshape(()) if scale_t is not None else 1.0)
+    m.mul_(beta1).add_(gs, alpha=1 - beta1)
+    v.mul_(beta2).addcmul_(gs, gs, value=1 - beta2)
+    u = (m / bc1) / ((v / bc2).sqrt() + eps) + weight_decay * p
+    rows = blk.cpu().tolist()
+    ids = seg_id.cpu().tolist()
+    for (b, e), sid in zip(rows, ids):
+        sums[sid, 0] += p[b:e].pow(2).sum()
+        sums[sid, 1] += u[b:e].pow(2).sum()
+    if norm_group is not None:
+        from .. import comm as dist
+        dist.all_reduce(sums, group=norm_group)
+    wn, un = sums[:, 0].sqrt(), sums[:, 1].sqrt()
+    coeff = torch.where((wn > 0) & (un > 0), wn / un.clamp(min=1e-30), torch.ones_like(wn)).clamp(min_coeff, max_coeff)
+    if coeffs is not None:
+        coeffs.copy_(coeff)
+    for (b, e), sid in zip(rows, ids):
+        p[b:e].sub_(u[b:e] * (lr * coeff[sid]))
+    if lp is not None:
+        lp.copy_(p)
+
+
 class FusedLamb(torch.optim.Optimizer):
     """LAMB (reference deepspeed/ops/lamb/fused_lamb.py:14): Adam direction scaled per tensor by
-    the trust ratio ||p|| / ||update||, clamped to [min_coeff, max_coeff]."""
+    the trust ratio ||p|| / ||update||, clamped to [min_coeff, max_coeff]. GPU tensors run the
+    two-stage HIP kernels (one segment per parameter); under ZeRO the engine runs the same kernels
+    over the flat partitions with the trust ratio of each WHOLE parameter (runtime/zero/base.py)."""
 
     def __init__(self, params, lr=1e-3, bias_correction=True, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
                  max_grad_norm=0.0, max_coeff=10.0, min_coeff=0.01):
@@ -216,6 +276,17 @@ class FusedLamb(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros(p.shape, dtype=torch.float32, device=p.device)
                     st["exp_avg_sq"] = torch.zeros(p.shape, dtype=torch.float32, device=p.device)
                 st["step"] += 1
+                if p.is_cuda and p.dtype == torch.float32 and p.is_contiguous():
+                    if "table" not in st:
+                        st["table"] = lamb_block_table([(0, 0, p.numel())], p.device)
+                    coeff = torch.empty(1, device=p.device)
+                    lamb_flat_(p.view(-1), p.grad.contiguous().view(-1), st["exp_avg"].view(-1),
+                               st["exp_avg_sq"].view(-1), None, st["table"], 1, lr=group["lr"], beta1=b1, beta2=b2,
+                               eps=group["eps"], weight_decay=group["weight_decay"], step=st["step"],
+                               bias_correction=group["bias_correction"], min_coeff=group["min_coeff"],
+                               max_coeff=group["max_coeff"], coeffs=coeff)
+                    self.lamb_coeffs.append(coeff[0])
+                    continue
                 g = p.grad.float()
                 m, v = st["exp_avg"], st["exp_avg_sq"]
                 m.mul_(b1).add_(g, alpha=1 - b1)

@@ -398,7 +398,7 @@ class SXEEngine(nn.Module):
             from .zero.offload import HostOptimizerStep
             host_step = HostOptimizerStep(off, aio_config=cfg.model.aio, rank=dist.get_rank())
             from .zero.base import _kind
-            if host_step.ratio < 1.0 and _kind(basic)[0] != "generic":
+            if host_step.ratio < 1.0 and _kind(basic)[0] in ("adam", "lion", "adagrad"):
                 from .zero.offload import split_param_groups
                 split_param_groups(basic, host_step.ratio)  # Twin-Flow: part of every group stays in HBM
         offload_param = bool(zc.offload_param is not None and zc.offload_param.device in ("cpu", "nvme"))

@@ -27,6 +27,8 @@ def _kind(opt):
         return "lion", None
     if isinstance(opt, (fused.FusedAdagrad, Adagrad)):
         return "adagrad", None
+    if isinstance(opt, fused.FusedLamb):
+        return "lamb", None
     return "generic", None
 
 
@@ -93,7 +95,7 @@ class ZeroOptimizerBase:
     def _init_state(self):
         for g, m in enumerate(self.master):
             st = self.optimizer.state[m]
-            if self.kind == "adam":
+            if self.kind in ("adam", "lamb"):
                 st["step"] = 0
                 st["exp_avg"] = torch.zeros_like(m.data)
                 st["exp_avg_sq"] = torch.zeros_like(m.data)
@@ -218,6 +220,19 @@ class ZeroOptimizerBase:
                     fused.adagrad_flat_(u.master, u.grad, st["sum"][o:o + u.chunk], u.shard, lr=pg["lr"],
                                         eps=pg.get("eps", 1e-10), weight_decay=pg.get("weight_decay", 0.0),
                                         scale_t=coef, skip_t=skip)
+            elif self.kind == "lamb":
+                st["step"] = int(st.get("step", 0)) + 1
+                b1, b2 = pg["betas"]
+                table, nseg = self._lamb_segments(g)
+                lp = units[0].shard if len(units) == 1 else None
+                fused.lamb_flat_(m.data, self.grads[g], st["exp_avg"], st["exp_avg_sq"], lp, table, nseg, lr=pg["lr"],
+                                 beta1=b1, beta2=b2, eps=pg["eps"], weight_decay=pg["weight_decay"], step=st["step"],
+                                 bias_correction=pg.get("bias_correction", True), min_coeff=pg.get("min_coeff", 0.01),
+                                 max_coeff=pg.get("max_coeff", 10.0), scale_t=coef, skip_t=skip,
+                                 norm_group=self.partition_group if any(u.S > 1 for u in units) else None)
+                if lp is None:  # several units: refresh each unit's bit16 shard from its master chunk
+                    for u in units:
+                        u.shard.copy_(u.master)
         if self.kind == "generic":
             # any torch.optim optimizer: fp32 grads -> .grad of the master, step, copy back.
             # (host-synchronising on skip; the fused kinds above never do)
@@ -230,6 +245,24 @@ class ZeroOptimizerBase:
                 self.master[g].grad = None
                 for u in units:
                     u.shard.copy_(u.master)
+
+    def _lamb_segments(self, g):
+        """Per-parameter segments of group g's flat master on this rank (cached): LAMB's trust
+        ratio is per ORIGINAL parameter, and a parameter split across the partition has its
+        fragments' norms summed over the partition group."""
+        cache = self.__dict__.setdefault("_lamb_tables", {})
+        if g not in cache:
+            segs, gi, base = [], 0, 0
+            for u in self.units[g]:
+                for i in range(len(u.params)):
+                    rng = u.param_range_in_shard(i)
+                    if rng is not None:
+                        plo, phi, slo = rng
+                        segs.append((gi, base + slo, phi - plo))
+                    gi += 1
+                base += u.chunk
+            cache[g] = (fused.lamb_block_table(segs, self.master[g].device), gi)
+        return cache[g]
 
     def _unit_offsets(self, g):
         offs, o = [], 0

@@ -27,6 +27,9 @@ from ...ops import native
 from ...utils.logging import log_dist
 
 
+HOST_KINDS = ("adam", "lion", "adagrad")  # optimizers with a streamed C++ host kernel
+
+
 def _pinned(n, dtype):
     return pinned_empty(n, dtype)
 
@@ -144,7 +147,7 @@ class HostOptimizerStep:
         return {g for g, pg in enumerate(opt.optimizer.param_groups) if pg.get("sxe_offload", True)}
 
     def init_master(self, opt):
-        if opt.kind == "generic" and self.device == "nvme":
+        if opt.kind not in HOST_KINDS and self.device == "nvme":
             raise ValueError("NVMe optimizer offload supports Adam/AdamW/Lion/Adagrad")
         self.groups = self.host_groups(opt)
         G = len(opt.units)
@@ -153,7 +156,7 @@ class HostOptimizerStep:
         # STAGE_SLOTS unit-sized pinned slots instead of full-model mirrors (6 B/param less on the
         # host -- the host tier is what bounds the trainable model size); generic torch optimizers
         # step whole groups and keep the full mirrors.
-        self.streamed = opt.kind != "generic"
+        self.streamed = opt.kind in HOST_KINDS  # C++ CPU kernels; others step torch-side on mirrors
         all_units = [u for g in sorted(self.groups) for u in opt.units[g]]
         if self.streamed and all_units:
             maxc = max(u.chunk for u in all_units)

@@ -307,3 +307,38 @@ def test_linear_weight_grad_uses_wgrad_kernel_and_matches():
         ref += gy.reshape(-1, 4096).float().t() @ x.detach().reshape(-1, 4096).float()
     assert state["done"] == 2 and w.grad is None
     assert _rel(buf, ref) < 1e-5
+
+
+def test_lamb_kernels_vs_torch_reference():
+    """optim.hip lamb_stage1_/lamb_stage2_ (per-segment trust ratios, bf16 copy) == fp32 torch LAMB."""
+    from shuffle_exchange_amd.ops.optim import lamb_block_table, lamb_flat_
+    torch.manual_seed(0)
+    sizes = [1, 37, 8192, 8193, 100_000, 3]
+    n = sum(sizes)
+    p = torch.randn(n, device="cuda")
+    g = torch.randn(n, device="cuda").bfloat16()
+    m = torch.randn(n, device="cuda") * 0.01
+    v = torch.rand(n, device="cuda") * 0.01
+    lp = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+    segs, off = [], 0
+    for i, s in enumerate(sizes):
+        segs.append((i, off, s))
+        off += s
+    ref_p, ref_m, ref_v = p.clone().cpu(), m.clone().cpu(), v.clone().cpu()
+    coeffs = torch.empty(len(sizes), device="cuda")
+    scale = torch.tensor([0.5], device="cuda")
+    lamb_flat_(p, g, m, v, lp, lamb_block_table(segs, "cuda"), len(sizes), lr=1e-2, beta1=0.9, beta2=0.99, eps=1e-6,
+               weight_decay=0.05, step=4, scale_t=scale, coeffs=coeffs)
+    gf = g.float().cpu() * 0.5
+    ref_m = 0.9 * ref_m + 0.1 * gf
+    ref_v = 0.99 * ref_v + 0.01 * gf * gf
+    u = (ref_m / (1 - 0.9 ** 4)) / ((ref_v / (1 - 0.99 ** 4)).sqrt() + 1e-6) + 0.05 * ref_p
+    out = ref_p.clone()
+    for i, s0, s in segs:
+        wn, un = ref_p[s0:s0 + s].norm(), u[s0:s0 + s].norm()
+        c = float((wn / un).clamp(0.01, 10.0)) if wn > 0 and un > 0 else 1.0
+        assert abs(float(coeffs[i]) - c) < 1e-4 * max(1.0, c)
+        out[s0:s0 + s] -= 1e-2 * c * u[s0:s0 + s]
+    assert _rel(m.cpu(), ref_m) < 1e-6 and _rel(v.cpu(), ref_v) < 1e-6
+    assert _rel(p.cpu(), out) < 1e-6
+    assert torch.equal(lp, p.bfloat16())
