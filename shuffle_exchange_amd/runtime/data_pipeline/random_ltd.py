@@ -52,14 +52,30 @@ def scatter_tokens(full, part, idx):
 
 
 class RandomLayerTokenDrop(nn.Module):
-    """Wraps a layer f([B, S, H], ...) so that during training it only processes ``k`` random
-    tokens per sequence (the rest pass through unchanged)."""
+    """Wraps a layer f(x [B, S, H], ...) so that during training it only processes ``k`` random
+    tokens per sequence (sorted, so causal order is kept); the other tokens pass through unchanged.
+
+    Positional arguments shaped like the hidden states (this framework's fused-residual stream:
+    ``layer(x, res, rope, position_ids)`` -> ``(x, res)``) are gathered and scattered alongside, so
+    a dropped token keeps x + res; a ``position_ids`` of None becomes the kept tokens' ORIGINAL
+    positions (RoPE must not see the compacted order). Parity: reference
+    data_routing/basic_layer.py ``RandomLayerTokenDrop``."""
 
     def __init__(self, layer, scheduler=None):
         super().__init__()
         self.layer = layer
         self.scheduler = scheduler
         self.reserved_length = None
+        import inspect
+        try:
+            names = list(inspect.signature(layer.forward).parameters)
+        except (TypeError, ValueError):
+            names = []
+        self._pos_arg = names.index("position_ids") if "position_ids" in names else None
+
+    def init_config(self, config, scheduler, layer_id=0):
+        self.scheduler = scheduler
+        self.layer_id = layer_id
 
     def forward(self, x, *args, **kwargs):
         k = self.reserved_length if self.reserved_length is not None else (
@@ -68,6 +84,47 @@ class RandomLayerTokenDrop(nn.Module):
             return self.layer(x, *args, **kwargs)
         B, S, _ = x.shape
         idx = token_sort_(torch.rand(B, S, device=x.device).topk(k, dim=1).indices)
-        part = self.layer(gather_tokens(x, idx), *args, **kwargs)
-        part = part[0] if isinstance(part, tuple) else part
-        return scatter_tokens(x, part, idx)
+        args = list(args)
+        full = {0: x}
+        for j, a in enumerate(args):
+            if torch.is_tensor(a) and a.dim() == 3 and a.shape[:2] == (B, S):
+                full[j + 1] = a
+                args[j] = gather_tokens(a, idx)
+        pj = self._pos_arg
+        if pj is not None and pj - 1 < len(args) and pj >= 1:
+            pos = args[pj - 1]
+            if pos is None:
+                pos = torch.arange(S, device=x.device).unsqueeze(0).expand(B, S)
+            if torch.is_tensor(pos) and pos.shape[-1] == S:
+                args[pj - 1] = torch.gather(pos.expand(B, S), 1, idx)
+        elif "position_ids" in kwargs or pj is not None:
+            pos = kwargs.get("position_ids")
+            if pos is None:
+                pos = torch.arange(S, device=x.device).unsqueeze(0).expand(B, S)
+            kwargs["position_ids"] = torch.gather(pos.expand(B, S), 1, idx)
+        out = self.layer(gather_tokens(x, idx), *args, **kwargs)
+        if torch.is_tensor(out):
+            return scatter_tokens(x, out, idx)
+        outs = list(out)
+        for j, o in enumerate(outs):
+            src = full.get(j, x if j == 0 else None)
+            if src is not None and torch.is_tensor(o) and o.shape[:2] == (B, k):
+                outs[j] = scatter_tokens(src, o, idx)
+        return type(out)(outs) if isinstance(out, tuple) else outs
+
+
+def convert_to_random_ltd(model, layer_ids, scheduler):
+    """Wrap the decoder layers ``layer_ids`` (indices into the model's first ModuleList) with
+    ``RandomLayerTokenDrop`` in place; returns the wrapped count (reference
+    data_routing/helper.py ``convert_to_random_ltd``)."""
+    for mod in model.modules():
+        for name, child in mod.named_children():
+            if isinstance(child, nn.ModuleList) and len(child) > 0:
+                n = 0
+                for i in sorted(layer_ids):
+                    if not isinstance(child[i], RandomLayerTokenDrop):
+                        child[i] = RandomLayerTokenDrop(child[i], scheduler)
+                        child[i].layer_id = i
+                    n += 1
+                return n
+    return 0

@@ -159,6 +159,7 @@ class SXEEngine(nn.Module):
         self.tput_timer.world_size = groups.get_data_parallel_world_size()
         self._n_params = sum(getattr(p, "ds_numel", p.numel()) for p in model.parameters())
         self._loss_acc = None
+        self._configure_data_efficiency()  # random-LTD wraps layers before any optimizer sees them
         self.training_dataloader = self.deepspeed_io(training_data) if training_data is not None else None
         self.optimizer = None
         self.basic_optimizer = None
@@ -186,6 +187,23 @@ class SXEEngine(nn.Module):
         self._auto_se_steps = 0
         self._configure_training_aux()
 
+    def _configure_data_efficiency(self):
+        raw = self._config._param_dict
+        # data_efficiency (reference engine.py:384-388, 698-741, 1954-1962, 2064-2065): curriculum
+        # data sampling over per-sample difficulty metrics + random layerwise token drop
+        de = raw.get("data_efficiency", {}) or {}
+        self._de = de if de.get("enabled") else {}
+        self.random_ltd_scheduler = None
+        rltd = self._de.get("data_routing", {}).get("random_ltd", {}) if self._de.get("data_routing", {}).get(
+            "enabled", True) else {}
+        if rltd.get("enabled"):
+            from .data_pipeline import RandomLTDScheduler, convert_to_random_ltd
+            self.random_ltd_scheduler = RandomLTDScheduler(rltd)
+            ids = list(rltd.get("random_ltd_layer_id", []))
+            n = convert_to_random_ltd(self.module, ids, self.random_ltd_scheduler)
+            if rltd.get("random_ltd_layer_num", n) != n:
+                raise ValueError(f"random_ltd_layer_num {rltd['random_ltd_layer_num']} != {n} wrapped layers")
+
     def _configure_training_aux(self):
         """Progressive layer drop, legacy curriculum learning and MoQ from the raw config
         (reference engine.py _configure_progressive_layer_drop / curriculum / quantizer)."""
@@ -211,6 +229,45 @@ class SXEEngine(nn.Module):
                                        "stochastic"), q_start_bits=bits.get("start_bits", 16),
                                        q_target_bits=bits.get("target_bits", 8),
                                        q_period=sch.get("quantize_period", 100))
+
+    def data_efficiency_enabled(self):
+        return bool(self._de)
+
+    def data_efficiency_config(self):
+        return self._de
+
+    def data_sampling_enabled(self):
+        return bool(self._de.get("data_sampling", {}).get("enabled", False))
+
+    def curriculum_learning_enabled(self):
+        ds = self._de.get("data_sampling", {})
+        return bool(ds.get("enabled", True) and ds.get("curriculum_learning", {}).get("enabled", False))
+
+    def random_ltd_enabled(self):
+        return self.random_ltd_scheduler is not None
+
+    def _curriculum_sampler(self, dataset):
+        """DeepSpeedDataSampler analogue: one metric's per-sample difficulties (``index_to_metric_path``
+        .npy, or a ``metric_values`` array in the config) + its difficulty schedule."""
+        import numpy as np
+        from .data_pipeline import CurriculumDataSampler, CurriculumScheduler
+        cl = self._de["data_sampling"]["curriculum_learning"]
+        metrics = cl.get("curriculum_metrics", {})
+        if len(metrics) != 1:
+            raise NotImplementedError("curriculum data sampling supports exactly one curriculum metric")
+        name, mc = next(iter(metrics.items()))
+        if "metric_values" in mc:
+            vals = np.asarray(mc["metric_values"])
+        else:
+            path = mc["index_to_metric_path"]
+            vals = np.load(path if path.endswith(".npy") else path + ".npy", allow_pickle=False)
+        if len(vals) != len(dataset):
+            raise ValueError(f"curriculum metric {name}: {len(vals)} values for {len(dataset)} samples")
+        sched = CurriculumScheduler(mc)
+        return CurriculumDataSampler(vals, sched, self.train_batch_size() // self.gradient_accumulation_steps(),
+                                     dp_rank=groups.get_data_parallel_rank(),
+                                     dp_size=groups.get_data_parallel_world_size(),
+                                     seed=self._de.get("seed", 1234))
 
     def curriculum_enabled_legacy(self):
         return self.curriculum_scheduler_legacy is not None
@@ -460,6 +517,9 @@ class SXEEngine(nn.Module):
     # ------------------------------------------------------------------------------------- data
     def deepspeed_io(self, dataset, batch_size=None, route=None, pin_memory=True, data_sampler=None,
                      collate_fn=None, num_local_io_workers=None):
+        if data_sampler is None and route is None and self.curriculum_learning_enabled():
+            data_sampler = self._curriculum_sampler(dataset)
+            self.curriculum_sampler = data_sampler
         return SXEDataLoader(dataset, batch_size=batch_size or self.train_micro_batch_size_per_gpu(),
                              pin_memory=pin_memory and get_accelerator().gpu, collate_fn=collate_fn or self.collate_fn,
                              num_workers=num_local_io_workers or 0, data_parallel_world_size=groups.get_data_parallel_world_size(),
@@ -485,6 +545,8 @@ class SXEEngine(nn.Module):
             kwargs.update(self.progressive_layer_drop.get_state())
         if self.curriculum_scheduler_legacy is not None:
             kwargs["curriculum_seqlen"] = self.curriculum_scheduler_legacy.update_difficulty(self.global_steps + 1)
+        if self.random_ltd_scheduler is not None and self.module.training:
+            self.random_ltd_scheduler.update_seq(self.global_steps)
         fp = self._config.model.flops_profiler
         prof = None
         if fp.enabled and self.global_steps + 1 == fp.profile_step and self.micro_steps % max(
