@@ -267,12 +267,256 @@ class FusedGPTNeoXLayer(_Fused):
         return self._mlp(y2) + h
 
 
+def _rope_half(x, cos, sin):
+    """HF Llama-style rotate-half rotary on x [B, S, H, D] with cos/sin [B, S, D]."""
+    cos, sin = cos.unsqueeze(2).to(x.dtype), sin.unsqueeze(2).to(x.dtype)
+    d = x.shape[-1] // 2
+    return x * cos + torch.cat([-x[..., d:], x[..., :d]], -1) * sin
+
+
+def _attend_gqa(q, k, v, mask, causal, scale):
+    """_attend for grouped-query heads (q heads a multiple of kv heads)."""
+    if q.shape[2] != k.shape[2] and (mask is not None or q.shape[1] != k.shape[1]
+                                     or not (hip_supported(q, k, v) or hip_paddable(q, k, v))):
+        rep = q.shape[2] // k.shape[2]
+        k, v = k.repeat_interleave(rep, dim=2), v.repeat_interleave(rep, dim=2)
+    return _attend(q, k, v, mask, causal, scale)
+
+
+class FusedLlamaLayer(_Fused):
+    """Llama / Mistral / Qwen2 decoder layer (reference containers/llama.py, llama2.py): RMSNorm ->
+    one packed [q | k | v] GEMM (GQA, optional biases) -> rotate-half RoPE from the model's
+    ``position_embeddings`` -> causal attention with the HF Cache -> o_proj; the residual add is
+    folded into the post-attention RMSNorm; gate|up as ONE GEMM -> SwiGLU kernel -> down."""
+
+    def __init__(self, layer, config):
+        super().__init__(layer)
+        at, mlp = layer.self_attn, layer.mlp
+        self.hd = at.head_dim
+        self.nq = at.q_proj.weight.shape[0] // self.hd
+        self.nkv = at.k_proj.weight.shape[0] // self.hd
+        self.layer_idx, self.scale = at.layer_idx, float(at.scaling)
+        self.w_qkv = self._p(torch.cat([at.q_proj.weight, at.k_proj.weight, at.v_proj.weight]))
+        self.b_qkv = (self._p(torch.cat([at.q_proj.bias, at.k_proj.bias, at.v_proj.bias]))
+                      if at.q_proj.bias is not None else None)
+        self.w_o = self._p(at.o_proj.weight)
+        self.w_gu = self._p(torch.cat([mlp.gate_proj.weight, mlp.up_proj.weight]))
+        self.w_down = self._p(mlp.down_proj.weight)
+        li, lp = layer.input_layernorm, layer.post_attention_layernorm
+        self.ln1_w, self.eps1 = self._p(li.weight), float(getattr(li, "variance_epsilon", getattr(li, "eps", 1e-6)))
+        self.ln2_w, self.eps2 = self._p(lp.weight), float(getattr(lp, "variance_epsilon", getattr(lp, "eps", 1e-6)))
+        act = getattr(config, "hidden_act", "silu")
+        self.swiglu = act in ("silu", "swish")
+        self.act = act
+        self._link()
+
+    def _links(self):
+        L, D = self.orig, self.hd
+        at, mlp = L.self_attn, L.mlp
+        q, kv = self.nq * D, self.nkv * D
+        out = [(at.q_proj.weight, self.w_qkv[:q]), (at.k_proj.weight, self.w_qkv[q:q + kv]),
+               (at.v_proj.weight, self.w_qkv[q + kv:]), (at.o_proj.weight, self.w_o),
+               (mlp.gate_proj.weight, self.w_gu[:self.w_gu.shape[0] // 2]),
+               (mlp.up_proj.weight, self.w_gu[self.w_gu.shape[0] // 2:]), (mlp.down_proj.weight, self.w_down),
+               (L.input_layernorm.weight, self.ln1_w), (L.post_attention_layernorm.weight, self.ln2_w)]
+        if self.b_qkv is not None:
+            out += [(at.q_proj.bias, self.b_qkv[:q]), (at.k_proj.bias, self.b_qkv[q:q + kv]),
+                    (at.v_proj.bias, self.b_qkv[q + kv:])]
+        return out
+
+    def forward(self, hidden_states, attention_mask=None, position_ids=None, past_key_values=None, use_cache=False,
+                position_embeddings=None, **kwargs):
+        if position_embeddings is None or kwargs.get("output_attentions") or not self.swiglu:
+            return self._delegate(hidden_states, attention_mask=attention_mask, position_ids=position_ids,
+                                  past_key_values=past_key_values, use_cache=use_cache,
+                                  position_embeddings=position_embeddings, **kwargs)
+        from ..ops.activation import swiglu
+        from ..ops.norm import rms_norm
+        x = hidden_states
+        B, S, H = x.shape
+        qkv = linear(rms_norm(x, self.ln1_w, self.eps1), self.w_qkv, self.b_qkv)
+        qkv = qkv.view(B, S, self.nq + 2 * self.nkv, self.hd)
+        cos, sin = position_embeddings
+        q = _rope_half(qkv[:, :, :self.nq], cos, sin)
+        k = _rope_half(qkv[:, :, self.nq:self.nq + self.nkv], cos, sin)
+        v = qkv[:, :, self.nq + self.nkv:]
+        if past_key_values is not None:
+            kt, vt = past_key_values.update(k.transpose(1, 2), v.transpose(1, 2), self.layer_idx)
+            k, v = kt.transpose(1, 2), vt.transpose(1, 2)
+        o = _attend_gqa(q, k, v, attention_mask, attention_mask is None, self.scale)
+        a = linear(o.reshape(B, S, self.nq * self.hd), self.w_o)
+        y2, h = rms_norm(a, self.ln2_w, self.eps2, residual=x)
+        return h + linear(swiglu(linear(y2, self.w_gu)), self.w_down)
+
+
+class FusedOPTLayer(_Fused):
+    """OPT decoder layer (reference containers/opt.py): packed biased QKV (q pre-scaled by
+    head_dim^-0.5 as HF does), causal attention with the HF Cache, out-proj with the residual folded
+    into the final LayerNorm (pre-LN models), bias + ReLU MLP."""
+
+    def __init__(self, layer, config):
+        super().__init__(layer)
+        at = layer.self_attn
+        self.nh, self.hd = at.num_heads, at.head_dim
+        self.layer_idx, self.scaling = at.layer_idx, float(at.scaling)
+        self.w_qkv = self._p(torch.cat([at.q_proj.weight, at.k_proj.weight, at.v_proj.weight]))
+        self.b_qkv = self._p(torch.cat([at.q_proj.bias, at.k_proj.bias, at.v_proj.bias]))
+        self.w_o, self.b_o = self._p(at.out_proj.weight), self._p(at.out_proj.bias)
+        l1, l2 = layer.self_attn_layer_norm, layer.final_layer_norm
+        self.ln1_w, self.ln1_b, self.eps1 = self._p(l1.weight), self._p(l1.bias), l1.eps
+        self.ln2_w, self.ln2_b, self.eps2 = self._p(l2.weight), self._p(l2.bias), l2.eps
+        self.w_fc1, self.b_fc1 = self._p(layer.fc1.weight), self._p(layer.fc1.bias)
+        self.w_fc2, self.b_fc2 = self._p(layer.fc2.weight), self._p(layer.fc2.bias)
+        self.pre_ln = bool(layer.do_layer_norm_before)
+        self.act = getattr(config, "activation_function", "relu")
+        self._link()
+
+    def _links(self):
+        L, H = self.orig, self.nh * self.hd
+        at = L.self_attn
+        out = []
+        for i, lin in enumerate((at.q_proj, at.k_proj, at.v_proj)):
+            out += [(lin.weight, self.w_qkv[i * H:(i + 1) * H]), (lin.bias, self.b_qkv[i * H:(i + 1) * H])]
+        return out + [(at.out_proj.weight, self.w_o), (at.out_proj.bias, self.b_o),
+                      (L.self_attn_layer_norm.weight, self.ln1_w), (L.self_attn_layer_norm.bias, self.ln1_b),
+                      (L.final_layer_norm.weight, self.ln2_w), (L.final_layer_norm.bias, self.ln2_b),
+                      (L.fc1.weight, self.w_fc1), (L.fc1.bias, self.b_fc1), (L.fc2.weight, self.w_fc2),
+                      (L.fc2.bias, self.b_fc2)]
+
+    def forward(self, hidden_states, attention_mask=None, past_key_values=None, use_cache=False, position_ids=None,
+                **kwargs):
+        if kwargs.get("output_attentions") or not self.pre_ln or self.act not in ("relu", "gelu", "gelu_new"):
+            return self._delegate(hidden_states, attention_mask=attention_mask, past_key_values=past_key_values,
+                                  use_cache=use_cache, position_ids=position_ids, **kwargs)
+        x = hidden_states
+        B, S, H = x.shape
+        qkv = linear(layer_norm(x, self.ln1_w, self.ln1_b, self.eps1), self.w_qkv, self.b_qkv).view(
+            B, S, 3, self.nh, self.hd)
+        q, k, v = qkv[:, :, 0] * self.scaling, qkv[:, :, 1], qkv[:, :, 2]
+        if past_key_values is not None:
+            kt, vt = past_key_values.update(k.transpose(1, 2), v.transpose(1, 2), self.layer_idx)
+            k, v = kt.transpose(1, 2), vt.transpose(1, 2)
+        o = _attend(q, k, v, attention_mask, attention_mask is None, 1.0)
+        a = linear(o.reshape(B, S, H), self.w_o, self.b_o)
+        y2, h = layer_norm(a, self.ln2_w, self.ln2_b, self.eps2, residual=x)
+        return h + linear(bias_act(linear(y2, self.w_fc1), self.b_fc1, _act_name(self.act)), self.w_fc2, self.b_fc2)
+
+
+class FusedGPTJBlock(_Fused):
+    """GPT-J block (reference containers/gptj.py): one LayerNorm feeding attention and MLP in
+    parallel; packed bias-free QKV; interleaved (rotate-every-two) rotary on the first
+    ``rotary_dim`` dims from the model's sinusoid table; attention + MLP + residual summed."""
+
+    def __init__(self, block, config):
+        super().__init__(block)
+        at = block.attn
+        self.nh, self.hd = at.num_attention_heads, at.head_dim
+        self.layer_idx, self.rot = at.layer_idx, at.rotary_dim
+        self.w_qkv = self._p(torch.cat([at.q_proj.weight, at.k_proj.weight, at.v_proj.weight]))
+        self.w_o = self._p(at.out_proj.weight)
+        self.ln_w, self.ln_b, self.eps = self._p(block.ln_1.weight), self._p(block.ln_1.bias), block.ln_1.eps
+        self.w_in, self.b_in = self._p(block.mlp.fc_in.weight), self._p(block.mlp.fc_in.bias)
+        self.w_out, self.b_out = self._p(block.mlp.fc_out.weight), self._p(block.mlp.fc_out.bias)
+        self.act = getattr(config, "activation_function", "gelu_new")
+        self.register_buffer("embed_positions", at.embed_positions.detach().clone(), persistent=False)  # sin | cos
+        self._link()
+
+    def _links(self):
+        b, H = self.orig, self.nh * self.hd
+        at = b.attn
+        return [(at.q_proj.weight, self.w_qkv[:H]), (at.k_proj.weight, self.w_qkv[H:2 * H]),
+                (at.v_proj.weight, self.w_qkv[2 * H:]), (at.out_proj.weight, self.w_o), (b.ln_1.weight, self.ln_w),
+                (b.ln_1.bias, self.ln_b), (b.mlp.fc_in.weight, self.w_in), (b.mlp.fc_in.bias, self.b_in),
+                (b.mlp.fc_out.weight, self.w_out), (b.mlp.fc_out.bias, self.b_out)]
+
+    def _rotary(self, x, sin, cos):
+        r = self.rot or x.shape[-1]
+        xr, xp = x[..., :r], x[..., r:]
+        sin = sin.repeat_interleave(2, -1).unsqueeze(2).to(x.dtype)
+        cos = cos.repeat_interleave(2, -1).unsqueeze(2).to(x.dtype)
+        rot = torch.stack((-xr[..., 1::2], xr[..., ::2]), dim=-1).flatten(-2)
+        return torch.cat([xr * cos + rot * sin, xp], -1)
+
+    def forward(self, hidden_states, layer_past=None, attention_mask=None, position_ids=None, use_cache=False,
+                output_attentions=False, **kwargs):
+        if output_attentions or position_ids is None:
+            return self._delegate(hidden_states, layer_past=layer_past, attention_mask=attention_mask,
+                                  position_ids=position_ids, use_cache=use_cache, output_attentions=output_attentions,
+                                  **kwargs)
+        x = hidden_states
+        B, S, H = x.shape
+        y = layer_norm(x, self.ln_w, self.ln_b, self.eps)
+        qkv = linear(y, self.w_qkv).view(B, S, 3, self.nh, self.hd)
+        sincos = self.embed_positions[position_ids].to(x.dtype)  # [B, S, rot]
+        sin, cos = torch.split(sincos, sincos.shape[-1] // 2, dim=-1)
+        q, k, v = self._rotary(qkv[:, :, 0], sin, cos), self._rotary(qkv[:, :, 1], sin, cos), qkv[:, :, 2]
+        if layer_past is not None:
+            kt, vt = layer_past.update(k.transpose(1, 2), v.transpose(1, 2), self.layer_idx)
+            k, v = kt.transpose(1, 2), vt.transpose(1, 2)
+        o = _attend(q.float(), k.float(), v.float(), attention_mask, attention_mask is None,
+                    1.0 / math.sqrt(self.hd)).to(x.dtype)  # GPT-J attends in fp32
+        a = linear(o.reshape(B, S, H), self.w_o)
+        m = linear(bias_act(linear(y, self.w_in), self.b_in, _act_name(self.act)), self.w_out, self.b_out)
+        return a + m + x, None
+
+
+class FusedDistilBertBlock(_Fused):
+    """DistilBERT encoder block (reference containers/distil_bert.py): packed biased QKV,
+    bidirectional attention, residual-fused post-LayerNorms, bias-GELU FFN."""
+
+    def __init__(self, block, config):
+        super().__init__(block)
+        at = block.attention
+        self.nh = at.n_heads
+        self.hd = at.dim // at.n_heads
+        self.w_qkv = self._p(torch.cat([at.q_lin.weight, at.k_lin.weight, at.v_lin.weight]))
+        self.b_qkv = self._p(torch.cat([at.q_lin.bias, at.k_lin.bias, at.v_lin.bias]))
+        self.w_o, self.b_o = self._p(at.out_lin.weight), self._p(at.out_lin.bias)
+        l1, l2 = block.sa_layer_norm, block.output_layer_norm
+        self.ln1_w, self.ln1_b, self.eps1 = self._p(l1.weight), self._p(l1.bias), l1.eps
+        self.ln2_w, self.ln2_b, self.eps2 = self._p(l2.weight), self._p(l2.bias), l2.eps
+        self.w1, self.b1 = self._p(block.ffn.lin1.weight), self._p(block.ffn.lin1.bias)
+        self.w2, self.b2 = self._p(block.ffn.lin2.weight), self._p(block.ffn.lin2.bias)
+        self.act = _act_name(getattr(config, "activation", "gelu"))
+        self._link()
+
+    def _links(self):
+        b, H = self.orig, self.nh * self.hd
+        at = b.attention
+        out = []
+        for i, lin in enumerate((at.q_lin, at.k_lin, at.v_lin)):
+            out += [(lin.weight, self.w_qkv[i * H:(i + 1) * H]), (lin.bias, self.b_qkv[i * H:(i + 1) * H])]
+        return out + [(at.out_lin.weight, self.w_o), (at.out_lin.bias, self.b_o), (b.sa_layer_norm.weight, self.ln1_w),
+                      (b.sa_layer_norm.bias, self.ln1_b), (b.output_layer_norm.weight, self.ln2_w),
+                      (b.output_layer_norm.bias, self.ln2_b), (b.ffn.lin1.weight, self.w1), (b.ffn.lin1.bias, self.b1),
+                      (b.ffn.lin2.weight, self.w2), (b.ffn.lin2.bias, self.b2)]
+
+    def forward(self, hidden_states, attention_mask=None, **kwargs):
+        if kwargs.get("output_attentions"):
+            return self._delegate(hidden_states, attention_mask=attention_mask, **kwargs)
+        x = hidden_states
+        B, S, H = x.shape
+        qkv = linear(x, self.w_qkv, self.b_qkv).view(B, S, 3, self.nh, self.hd)
+        o = _attend(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], attention_mask, False, 1.0 / math.sqrt(self.hd))
+        a = linear(o.reshape(B, S, H), self.w_o, self.b_o)
+        h, _ = layer_norm(a, self.ln1_w, self.ln1_b, self.eps1, residual=x)
+        f = linear(bias_act(linear(h, self.w1), self.b1, self.act), self.w2, self.b2)
+        y, _ = layer_norm(f, self.ln2_w, self.ln2_b, self.eps2, residual=h)
+        return y
+
+
 # layer class name -> fused layer constructor (reference containers/__init__.py policy list)
 POLICIES = {
     "BertLayer": FusedEncoderLayer,
     "RobertaLayer": FusedEncoderLayer,
     "GPT2Block": FusedGPT2Block,
     "GPTNeoXLayer": FusedGPTNeoXLayer,
+    "LlamaDecoderLayer": FusedLlamaLayer,
+    "MistralDecoderLayer": FusedLlamaLayer,
+    "Qwen2DecoderLayer": FusedLlamaLayer,
+    "OPTDecoderLayer": FusedOPTLayer,
+    "GPTJBlock": FusedGPTJBlock,
+    "TransformerBlock": FusedDistilBertBlock,  # DistilBERT
 }
 
 
@@ -292,6 +536,8 @@ def replace_transformer_layer(model, config=None):
     for parent in list(model.modules()):
         for name, child in list(parent.named_children()):
             ctor = POLICIES.get(type(child).__name__)
+            if ctor is FusedDistilBertBlock and not hasattr(child, "sa_layer_norm"):
+                continue  # another library's "TransformerBlock"
             if ctor is FusedEncoderLayer and _is_decoder_layer(child, config):
                 continue  # causal self-attention + KV cache: the encoder fusion does not apply
             if ctor is not None:

@@ -212,3 +212,82 @@ def test_real_head_dim_injection_runs_hip_flash(arch, monkeypatch):
     assert calls["hip"] == 2
     rel = ((got - ref).norm() / ref.norm()).item()
     assert rel < 2e-2, rel
+
+
+def _decoder(arch):
+    torch.manual_seed(0)
+    if arch == "llama":
+        cfg = transformers.LlamaConfig(vocab_size=300, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                                       num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=64)
+        return transformers.LlamaForCausalLM(cfg).eval()
+    if arch == "qwen2":
+        cfg = transformers.Qwen2Config(vocab_size=300, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                                       num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=64)
+        return transformers.Qwen2ForCausalLM(cfg).eval()
+    if arch == "mistral":
+        cfg = transformers.MistralConfig(vocab_size=300, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                                         num_attention_heads=4, num_key_value_heads=1, max_position_embeddings=64,
+                                         sliding_window=None)
+        return transformers.MistralForCausalLM(cfg).eval()
+    if arch == "opt":
+        cfg = transformers.OPTConfig(vocab_size=300, hidden_size=64, ffn_dim=128, num_hidden_layers=2,
+                                     num_attention_heads=4, max_position_embeddings=64, word_embed_proj_dim=64)
+        return transformers.OPTForCausalLM(cfg).eval()
+    if arch == "gptj":
+        cfg = transformers.GPTJConfig(vocab_size=300, n_embd=64, n_layer=2, n_head=4, rotary_dim=8, n_positions=64)
+        return transformers.GPTJForCausalLM(cfg).eval()
+    raise ValueError(arch)
+
+
+@pytest.mark.parametrize("arch", ["llama", "qwen2", "mistral", "opt", "gptj"])
+def test_decoder_injection_logits_and_generate(arch):
+    """Llama / Qwen2 / Mistral (GQA, RoPE, SwiGLU), OPT (biased QKV, pre-LN, ReLU) and GPT-J (parallel
+    residual, interleaved partial rotary) injection: logits and greedy generation through the HF
+    cache match the original modules (reference module_inject/containers/{llama,llama2,opt,gptj}.py)."""
+    model = _decoder(arch)
+    ids = torch.randint(3, 300, (2, 10))
+    with torch.no_grad():
+        ref = model(ids, use_cache=False).logits
+        ref_gen = model.generate(ids, max_new_tokens=6, do_sample=False, pad_token_id=0)
+        n = replace_transformer_layer(model)
+        got = model(ids, use_cache=False).logits
+        got_gen = model.generate(ids, max_new_tokens=6, do_sample=False, pad_token_id=0)
+    assert n == 2
+    torch.testing.assert_close(got, ref, atol=5e-5, rtol=1e-4)
+    assert torch.equal(got_gen, ref_gen)
+
+
+def test_distilbert_injection_matches_hf():
+    cfg = transformers.DistilBertConfig(vocab_size=200, dim=64, n_layers=2, n_heads=4, hidden_dim=128,
+                                        max_position_embeddings=64)
+    torch.manual_seed(0)
+    model = transformers.DistilBertModel(cfg).eval()
+    ids = torch.randint(3, 200, (2, 12))
+    mask = torch.ones(2, 12, dtype=torch.long)
+    mask[1, 8:] = 0
+    with torch.no_grad():
+        ref = model(ids, attention_mask=mask).last_hidden_state
+        n = replace_transformer_layer(model)
+        got = model(ids, attention_mask=mask).last_hidden_state
+    assert n == 2
+    torch.testing.assert_close(got[0], ref[0], atol=2e-5, rtol=1e-4)
+    torch.testing.assert_close(got[1, :8], ref[1, :8], atol=2e-5, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arch", ["llama", "opt", "gptj"])
+def test_decoder_injection_gpu_bf16(arch):
+    """The new decoder policies on the MI355X in bf16 (HIP norm / GEMM / activation / flash kernels):
+    logits close to the HF modules, greedy generation runs through the HF cache."""
+    from shuffle_exchange_amd.ops import native
+    native.require_hip()
+    model = _decoder(arch).to("cuda", torch.bfloat16)
+    ids = torch.randint(3, 300, (2, 130), device="cuda")
+    with torch.no_grad():
+        ref = model(ids, use_cache=False).logits.float()
+        assert replace_transformer_layer(model) == 2
+        got = model(ids, use_cache=False).logits.float()
+        gen = model.generate(ids[:, :16], max_new_tokens=4, do_sample=False, pad_token_id=0)
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel < 3e-2, rel
+    assert gen.shape == (2, 20)
