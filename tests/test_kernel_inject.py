@@ -214,27 +214,27 @@ def test_real_head_dim_injection_runs_hip_flash(arch, monkeypatch):
     assert rel < 2e-2, rel
 
 
-def _decoder(arch):
+def _decoder(arch, max_pos=64):
     torch.manual_seed(0)
     if arch == "llama":
         cfg = transformers.LlamaConfig(vocab_size=300, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
-                                       num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=64)
+                                       num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=max_pos)
         return transformers.LlamaForCausalLM(cfg).eval()
     if arch == "qwen2":
         cfg = transformers.Qwen2Config(vocab_size=300, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
-                                       num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=64)
+                                       num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=max_pos)
         return transformers.Qwen2ForCausalLM(cfg).eval()
     if arch == "mistral":
         cfg = transformers.MistralConfig(vocab_size=300, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
-                                         num_attention_heads=4, num_key_value_heads=1, max_position_embeddings=64,
+                                         num_attention_heads=4, num_key_value_heads=1, max_position_embeddings=max_pos,
                                          sliding_window=None)
         return transformers.MistralForCausalLM(cfg).eval()
     if arch == "opt":
         cfg = transformers.OPTConfig(vocab_size=300, hidden_size=64, ffn_dim=128, num_hidden_layers=2,
-                                     num_attention_heads=4, max_position_embeddings=64, word_embed_proj_dim=64)
+                                     num_attention_heads=4, max_position_embeddings=max_pos, word_embed_proj_dim=64)
         return transformers.OPTForCausalLM(cfg).eval()
     if arch == "gptj":
-        cfg = transformers.GPTJConfig(vocab_size=300, n_embd=64, n_layer=2, n_head=4, rotary_dim=8, n_positions=64)
+        cfg = transformers.GPTJConfig(vocab_size=300, n_embd=64, n_layer=2, n_head=4, rotary_dim=8, n_positions=max_pos)
         return transformers.GPTJForCausalLM(cfg).eval()
     raise ValueError(arch)
 
@@ -281,8 +281,9 @@ def test_decoder_injection_gpu_bf16(arch):
     logits close to the HF modules, greedy generation runs through the HF cache."""
     from shuffle_exchange_amd.ops import native
     native.require_hip()
-    model = _decoder(arch).to("cuda", torch.bfloat16)
+    model = _decoder(arch, max_pos=256).to("cuda", torch.bfloat16)  # positions must cover the 130 tokens
     ids = torch.randint(3, 300, (2, 130), device="cuda")
+    assert ids.shape[1] + 8 <= 256
     with torch.no_grad():
         ref = model(ids, use_cache=False).logits.float()
         assert replace_transformer_layer(model) == 2
