@@ -27,8 +27,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--seq", type=int, default=int(os.environ.get("SXE_BENCH_SEQ", 2048)))
-    ap.add_argument("--mbs", type=int, default=int(os.environ.get("SXE_BENCH_MBS", 4)))
-    ap.add_argument("--gas", type=int, default=int(os.environ.get("SXE_BENCH_GAS", 4)))
+    # global batch 16 per GPU as 8 x 2 micro-steps: 288 GB HBM holds the activations of 8 x 2048
+    # tokens (peak 211 GB); half the weight-gradient accumulation passes of 4 x 4 and larger GEMM M
+    # (measured 24,254 vs 23,799 tok/s, profiles/bench_1gpu_r02.log)
+    ap.add_argument("--mbs", type=int, default=int(os.environ.get("SXE_BENCH_MBS", 8)))
+    ap.add_argument("--gas", type=int, default=int(os.environ.get("SXE_BENCH_GAS", 2)))
     ap.add_argument("--stage", type=int, default=3)
     ap.add_argument("--ac", action="store_true", help="activation checkpointing")
     ap.add_argument("--layers", type=int, default=None, help="override layer count (debug only; invalid for the metric)")
