@@ -64,6 +64,7 @@ struct Args {
   float* part_o;   // [splits, T, nq, D]
   float* part_ml;  // [splits, T, nq, 2]
   int T;
+  int window;      // sliding window (Mistral / Qwen2): keys older than `window` positions are masked; 0 = off
 };
 
 // R = query rows (token x head-in-group) per pass: 4 / 8 / 16 picked on the host from the GQA group
@@ -108,6 +109,13 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(Args a) {
     __syncthreads();
     const int max_pos = kl - ql + (row0 + nrows - 1) / G;  // causal horizon of this tile
     const int k_hi = min(k_end, max_pos + 1);
+    // sliding window: keys below the oldest row's window are masked for every row of the pass --
+    // start at the 64-key chunk holding the first visible key (the waves keep their interleave)
+    int k_start = k_begin;
+    if (a.window > 0) {
+      const int k_lo = kl - ql + row0 / G - a.window + 1;
+      if (k_lo > k_begin) k_start = k_begin + ((k_lo - k_begin) / 64) * 64;
+    }
     float m[R], l[R], acc[R][4];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -116,7 +124,7 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(Args a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[r][e] = 0.f;
     }
-    for (int kb = k_begin + wave * 64; kb < k_hi; kb += kWaves * 64) {
+    for (int kb = k_start + wave * 64; kb < k_hi; kb += kWaves * 64) {
       // q rows are re-read from LDS every chunk: without this fence LICM hoists all R x D of them
       // into registers (R = 4 alone would need 512 VGPRs and spill to scratch)
       asm volatile("" ::: "memory");
@@ -153,7 +161,8 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(Args a) {
       for (int r = 0; r < R; ++r) {
         if (r < nrows) {
           const int pos = kl - ql + (row0 + r) / G;
-          const float sv = (valid && key <= pos) ? s[r] : -INFINITY;
+          const bool vis = valid && key <= pos && (a.window <= 0 || key > pos - a.window);
+          const float sv = vis ? s[r] : -INFINITY;
           const float mx = wave_max(sv);
           const float mn = fmaxf(m[r], mx);
           float p = 0.f, alpha = 1.f;
@@ -287,15 +296,18 @@ void kv_cache_append(const at::Tensor& qkv, at::Tensor cache, const at::Tensor& 
   else if (D == 64)
     hipLaunchKernelGGL(pa::kv_append_kernel<64>, dim3(T), dim3(256), 0, cur_stream(), q, qkv.stride(0), (int)nq,
                        (int)nkv, slots.data_ptr<int64_t>(), c, bs);
+  else if (D == 256)
+    hipLaunchKernelGGL(pa::kv_append_kernel<256>, dim3(T), dim3(256), 0, cur_stream(), q, qkv.stride(0), (int)nq,
+                       (int)nkv, slots.data_ptr<int64_t>(), c, bs);
   else
-    SXE_CHECK(false, "kv_cache_append: head_dim must be 64 or 128");
+    SXE_CHECK(false, "kv_cache_append: head_dim must be 64, 128 or 256");
   SXE_LAUNCH_CHECK();
 }
 
 // q: [T, nq, D] (token stride free); returns out [T, nq, D] bf16
 at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const at::Tensor& block_table,
                            const at::Tensor& q_start, const at::Tensor& q_len, const at::Tensor& kv_len, double scale,
-                           int64_t max_kv_len, int64_t splits) {
+                           int64_t max_kv_len, int64_t splits, int64_t window) {
   SXE_CHECK_CUDA(q);
   SXE_CHECK(q.scalar_type() == at::kBFloat16 && cache.scalar_type() == at::kBFloat16, "bf16 only");
   SXE_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == q.size(2), "q must be [T, nq, D] with head stride D");
@@ -337,6 +349,7 @@ at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const a
   a.T = T;
   a.part_o = nullptr;
   a.part_ml = nullptr;
+  a.window = (int)std::max<int64_t>(0, window);
   if (splits > 1) {
     part_o = at::empty({splits, T, nq, D}, q.options().dtype(at::kFloat));
     part_ml = at::empty({splits, T, nq, 2}, q.options().dtype(at::kFloat));
@@ -345,12 +358,15 @@ at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const a
   }
   dim3 grid(S * nkv, splits);
   const int G = nq / nkv;
-  SXE_CHECK(D == 128 || D == 64, "paged_attention: head_dim must be 64 or 128");
+  SXE_CHECK(D == 128 || D == 64 || D == 256, "paged_attention: head_dim must be 64, 128 or 256");
 #define SXE_PA_LAUNCH(DD, RR) hipLaunchKernelGGL((pa::paged_attn_kernel<DD, RR>), grid, dim3(256), 0, cur_stream(), a)
   if (D == 128) {
     if (G <= 4) SXE_PA_LAUNCH(128, 4);
     else if (G <= 8) SXE_PA_LAUNCH(128, 8);
     else SXE_PA_LAUNCH(128, 16);
+  } else if (D == 256) {  // 64 lanes per V row: one row per load; R <= 8 keeps LDS + VGPRs in budget
+    if (G <= 4) SXE_PA_LAUNCH(256, 4);
+    else SXE_PA_LAUNCH(256, 8);
   } else {
     if (G <= 4) SXE_PA_LAUNCH(64, 4);
     else if (G <= 8) SXE_PA_LAUNCH(64, 8);
@@ -361,6 +377,9 @@ at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const a
   if (splits > 1) {
     if (D == 128)
       hipLaunchKernelGGL(pa::merge_kernel<128>, dim3(T * nq), dim3(128), 0, cur_stream(), a.part_o, a.part_ml,
+                         (int)splits, T, nq, a.out, a.out_tok_stride);
+    else if (D == 256)
+      hipLaunchKernelGGL(pa::merge_kernel<256>, dim3(T * nq), dim3(256), 0, cur_stream(), a.part_o, a.part_ml,
                          (int)splits, T, nq, a.out, a.out_tok_stride);
     else
       hipLaunchKernelGGL(pa::merge_kernel<64>, dim3(T * nq), dim3(64), 0, cur_stream(), a.part_o, a.part_ml,
@@ -375,7 +394,7 @@ at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const a
 TORCH_LIBRARY_FRAGMENT(sxe, m) {
   m.def("kv_cache_append(Tensor qkv, Tensor(a!) cache, Tensor slots, int nq, int nkv) -> ()");
   m.def("paged_attention(Tensor q, Tensor cache, Tensor block_table, Tensor q_start, Tensor q_len, Tensor kv_len, "
-        "float scale, int max_kv_len, int splits) -> Tensor");
+        "float scale, int max_kv_len, int splits, int window=0) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(sxe, CUDA, m) {
   m.impl("kv_cache_append", &sxe::kv_cache_append);

@@ -74,15 +74,16 @@ def choose_splits(num_seqs, nkv, max_kv_len, target_wgs=512):
 
 def paged_attention(q, cache, block_table, q_start, q_len, kv_len, scale, max_kv_len, splits=None, window=None):
     """q: [T, nq, D] (head stride D); metadata int32 [S]; returns [T, nq, D]. ``window``: sliding
-    window length (keys older than ``window`` positions are masked); the HIP kernel covers head dims
-    64/128 with the window wider than every context."""
+    window length (keys older than ``window`` positions are masked, Mistral / Qwen2). The HIP kernel
+    covers head dims 64 / 128 / 256, with or without a window (the window also skips the key chunks
+    it masks entirely)."""
     if window is not None and max_kv_len <= window:
         window = None
-    if native.use_hip(q) and window is None and q.shape[-1] in (64, 128):
+    if native.use_hip(q) and q.shape[-1] in (64, 128, 256):
         if splits is None:
             splits = choose_splits(block_table.shape[0], cache.shape[2], max_kv_len)
         return torch.ops.sxe.paged_attention(q, cache, block_table, q_start, q_len, kv_len, float(scale),
-                                             int(max_kv_len), int(splits))
+                                             int(max_kv_len), int(splits), int(window or 0))
     if q.is_cuda:
         from ..utils.logging import warning_once
         warning_once(f"paged_attention: head_dim={q.shape[-1]} window={window} not covered by the HIP kernel; "

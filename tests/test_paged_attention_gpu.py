@@ -57,3 +57,23 @@ def test_paged_attention(seqs, nq, nkv, D, bs, splits):
     ref = paged_attention_reference(q.float(), cache.float(), bt, qs, ql, kl, scale)
     err = ((out.float() - ref).norm() / ref.norm()).item()
     assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("seqs", [[(37, 1), (500, 1), (0, 5)], [(130, 3), (1, 20), (2000, 1)], [(4100, 1)] * 2])
+@pytest.mark.parametrize("nq,nkv,D,bs,window", [(8, 2, 128, 64, 256), (4, 1, 64, 16, 100), (8, 4, 256, 32, 0),
+                                                (16, 2, 256, 64, 300)])
+@pytest.mark.parametrize("splits", [None, 2])
+def test_paged_attention_window_and_d256(seqs, nq, nkv, D, bs, window, splits):
+    """Sliding-window decode / chunked rows (Mistral, Qwen2) and head dim 256 on the HIP kernel ==
+    the fp32 reference with the same window."""
+    from shuffle_exchange_amd.ops.paged_attention import (kv_cache_append, paged_attention,
+                                                          paged_attention_reference)
+    qkv, cache, bt, qs, ql, kl, slots, maxkv = _setup(seqs, nq, nkv, D, bs, seed=3)
+    kv_cache_append(qkv, cache, slots, nq, nkv)
+    q = qkv[:, :nq]
+    scale = D ** -0.5
+    w = window or None
+    out = paged_attention(q, cache, bt, qs, ql, kl, scale, maxkv, splits, window=w)
+    ref = paged_attention_reference(q.float(), cache.float(), bt, qs, ql, kl, scale, w)
+    err = ((out.float() - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
