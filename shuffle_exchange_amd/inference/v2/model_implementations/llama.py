@@ -105,8 +105,15 @@ class RaggedLlama:
                 raise NotImplementedError("ragged tensor parallelism covers dense Llama-family models")
             if weight_quant:
                 raise NotImplementedError("weight_quant with tensor_parallel")
+            self._full_heads = (self.nq, self.nkv)
             self.tps = _TPShards(model, self.tp, self.tp_rank, self.nq, self.nkv, self.head_dim)
             self.nq, self.nkv = self.tps.nq, self.tps.nkv
+
+    def refresh_shards(self):
+        """Re-slice the tensor-parallel shards from the (updated) module weights -- the hybrid
+        engine calls this before each generation, after training steps changed the weights."""
+        if self.tps is not None:
+            self.tps = _TPShards(self.model, self.tp, self.tp_rank, *self._full_heads, self.head_dim)
 
     @property
     def device(self):

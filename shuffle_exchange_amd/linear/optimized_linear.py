@@ -116,7 +116,22 @@ class LoRAOptimizedLinear(nn.Module):
             w = parts
         return w
 
+    @torch.no_grad()
+    def fuse_lora(self):
+        """Inference (hybrid-engine generation): one GEMM with W + scaling * B A instead of the base
+        GEMM plus the two rank-r GEMMs. The fused weight is a separate tensor (the frozen base stays
+        bit-exact for training; reference hybrid_engine.py:132 ``_fuse_lora_layer``)."""
+        w = self.full_weight().detach().float().clone()
+        w.add_(self.lora_weight_2.float() @ self.lora_weight_1.float(), alpha=self.lora_scaling)
+        self._fused = w.to(self.dtype)
+
+    def unfuse_lora(self):
+        self._fused = None
+
     def forward(self, x):
+        fused = self.__dict__.get("_fused")
+        if fused is not None:
+            return F.linear(x, fused.to(x.dtype), self.bias)
         w = self.full_weight().detach()
         y = F.linear(x, w.to(x.dtype), self.bias)
         lora = linear(linear(x, self.lora_weight_1), self.lora_weight_2)
