@@ -52,6 +52,36 @@ class InferenceConfig:
         return int(self.tensor_parallel.get("tp_size", 1))
 
 
+class _HFWeights:
+    """The config + state dict of a Hugging Face model captured before kernel injection (tensor
+    references, no copies), in the shape ``ragged_model_for`` accepts."""
+
+    def __init__(self, model):
+        self.config = model.config
+        self._sd = {k: v.detach() for k, v in model.state_dict().items()}
+
+    @classmethod
+    def of(cls, model):
+        cfg = getattr(model, "config", None)
+        if cfg is None or not hasattr(cfg, "to_dict") or not hasattr(cfg, "model_type"):
+            return None
+        from .v2.model_implementations.hf_decoder import spec_from_hf_config
+        try:
+            spec_from_hf_config(cfg.to_dict())
+        except Exception:  # not a ragged-decoder family: generate falls back to the module
+            return None
+        return cls(model)
+
+    def state_dict(self):
+        return self._sd
+
+    def parameters(self):
+        return (v for v in self._sd.values() if v.is_floating_point())
+
+    def eval(self):
+        return self
+
+
 class InferenceEngine(torch.nn.Module):
     def __init__(self, model, config: InferenceConfig):
         super().__init__()
@@ -79,12 +109,16 @@ class InferenceEngine(torch.nn.Module):
                 log_dist(f"kernel injection skipped ({self.injection_skipped}): fused layers need whole, dense "
                          f"weights", ranks=[0])
             else:
-                # Hugging Face layers with an injection policy -> fused gfx950 layers (replace_module.py)
+                # Hugging Face layers with an injection policy -> fused gfx950 layers (replace_module.py).
+                # The fused layers re-pack their weights, so the KV-cached ragged decoder (built on the
+                # first generate) reads the HF tensors as they were before injection.
+                self._ragged_src = _HFWeights.of(model)
                 from ..module_inject.replace_module import replace_transformer_layer
                 self.injected_layers = replace_transformer_layer(model)
         self.device = dev
         self._graphs = {}
         self._ragged = None
+        self._ragged_src = getattr(self, "_ragged_src", None)
         log_dist(f"InferenceEngine: dtype={config.dtype}, tp={config.tp_size}, hip_graph={config.enable_cuda_graph}",
                  ranks=[0])
 
@@ -128,7 +162,8 @@ class InferenceEngine(torch.nn.Module):
                 state_manager=StateManagerConfig(memory_config=MemoryConfig(fraction=self._config.kv_cache_fraction)))
             if self.device.type != "cuda":
                 cfg.num_kv_blocks = 1024
-            self._ragged = build_engine(self.module, cfg)
+            self._ragged = build_engine(self._ragged_src or self.module, cfg)
+            self._ragged_src = None  # the ragged decoder holds its own packed copy now
         return self._ragged
 
     @torch.no_grad()

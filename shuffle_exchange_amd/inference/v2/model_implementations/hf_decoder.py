@@ -36,6 +36,7 @@ from ....ops.linear import linear
 from ....ops.norm import layer_norm, rms_norm
 from ....ops.paged_attention import kv_cache_append, paged_attention
 from ....ops.rope import RopeCache, apply_rope_tokens_
+from ....ops.rows import embed, gather_last
 
 FLASH_PREFILL_MIN = 128
 
@@ -480,9 +481,9 @@ class RaggedDecoder:
     @torch.no_grad()
     def forward(self, batch, kv_cache):
         s, W = self.spec, self.w
-        x = F.embedding(batch.input_ids, W["embed"])
+        x = embed(W["embed"], batch.input_ids)
         if s.learned_pos:
-            x = x + F.embedding(batch.positions.long() + s.pos_offset, W["pos_embed"])
+            x = x + embed(W["pos_embed"], batch.positions, -s.pos_offset)
         res = None  # pending residual: the true hidden state is x + res
         for li, L in enumerate(W["layers"]):
             if s.parallel_residual:
@@ -497,7 +498,7 @@ class RaggedDecoder:
                 m, h2 = self._norm(attn, L["ln2_w"], L.get("ln2_b"), residual=h)
                 x, res = self._mlp(m, L), h2
         last = batch.last_idx
-        h = x.index_select(0, last) + res.index_select(0, last)
+        h = gather_last(x, last, res)  # one HIP gather with the residual add fused
         h = self._norm(h, W["final_w"], W.get("final_b"))
         return linear(h, W["lm_head"], W.get("lm_head_b")).float()
 

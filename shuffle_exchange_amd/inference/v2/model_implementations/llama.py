@@ -29,6 +29,7 @@ from ....ops.activation import swiglu
 from ....ops.linear import linear
 from ....ops.paged_attention import kv_cache_append, paged_attention
 from ....ops.rope import apply_rope_tokens_
+from ....ops.rows import embed, gather_rows
 
 FLASH_PREFILL_MIN = 128
 
@@ -211,7 +212,8 @@ class RaggedLlama:
         model = self.model
         rope = model.rope(self.device)
         T = batch.num_tokens
-        x = model.embed_tokens(batch.input_ids)
+        emb = getattr(model.embed_tokens, "weight", None)
+        x = embed(emb, batch.input_ids) if emb is not None else model.embed_tokens(batch.input_ids)
         res = None
         for li, layer in enumerate(model.layers):
             if res is None:
@@ -228,7 +230,7 @@ class RaggedLlama:
             m, h2 = layer.post_attention_layernorm(o, h)
             x, res = self._mlp(layer, m, li), h2
         last = batch.last_idx
-        h = model.norm(x.index_select(0, last), res.index_select(0, last))[0]
+        h = model.norm(gather_rows(x, last), gather_rows(res, last))[0]
         if self.tps is not None:  # vocab-parallel head: gather every rank's logit columns
             from .... import comm as dist
             part = linear(h, self.tps.head).float()

@@ -42,13 +42,15 @@ def token_sort_(idx):
 
 
 def gather_tokens(x, idx):
-    """x: [B, S, H], idx: [B, k] sorted token ids -> [B, k, H]."""
-    return torch.gather(x, 1, idx.unsqueeze(-1).expand(-1, -1, x.shape[-1]))
+    """x: [B, S, H], idx: [B, k] sorted token ids -> [B, k, H] (HIP row gather, ops/rows.py)."""
+    from ...ops.rows import gather_tokens as _g
+    return _g(x, idx)
 
 
 def scatter_tokens(full, part, idx):
-    """Write part [B, k, H] back into full [B, S, H] at idx (out of place)."""
-    return full.scatter(1, idx.unsqueeze(-1).expand(-1, -1, full.shape[-1]), part)
+    """Write part [B, k, H] back into full [B, S, H] at idx (out of place; HIP row scatter)."""
+    from ...ops.rows import scatter_tokens as _s
+    return _s(full, part, idx)
 
 
 class RandomLayerTokenDrop(nn.Module):
