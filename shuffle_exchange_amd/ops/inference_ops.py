@@ -27,6 +27,7 @@ import math
 import torch
 import torch.nn.functional as F
 
+from . import native
 from .activation import ACT, bias_act, gated_act
 from .linear import linear as _linear
 from .norm import layer_norm as _layer_norm
@@ -118,7 +119,20 @@ def mlp_gemm(input, residual, weight_interm, weight_out, input_bias=None, bias=N
 def softmax(attn_scores, attn_mask=None, alibi=None, triangular=False, recompute=False, local_attention=False,
             window_size=1, async_op=False, layer_scale=1.0, head_offset=0, mp_size=1):
     """scores [B, H, q, k] (already scaled) -> probabilities; additive/boolean mask, alibi bias,
-    causal (triangular) and local-window masking."""
+    causal (triangular) and local-window masking. GPU: one HIP kernel (csrc/kernels/softmax.hip)
+    reading broadcast masks / ALiBi in place."""
+    if (attn_scores.is_cuda and attn_scores.dim() == 4 and native.use_hip(attn_scores)
+            and attn_scores.dtype in (torch.float32, torch.bfloat16, torch.float16)):
+        m = attn_mask
+        if m is not None:
+            m = m if m.dtype == torch.bool else m.float()
+            while m.dim() < 4:
+                m = m.unsqueeze(0)
+        a = alibi.float() if alibi is not None else None
+        while a is not None and a.dim() < 4:
+            a = a.unsqueeze(0)
+        return torch.ops.sxe.masked_softmax(attn_scores.contiguous(), float(layer_scale), m, a, bool(triangular),
+                                            int(window_size) if local_attention else 0)
     s = attn_scores.float() * layer_scale
     if alibi is not None:
         s = s + alibi.float()
