@@ -419,13 +419,12 @@ class RaggedDecoder:
         if weight_quant:
             # weight-only FP8 (row-scaled e4m3) projections and LM head: decode GEMMs stream half
             # the bytes through the skinny MFMA kernel (reference: FP6-LLM QuantizedWf6Af16Linear)
-            assert weight_quant == "fp8", "weight_quant: 'fp8'"
-            from ....ops.fp_quantizer import FP8Weight
+            from ....ops.fp_quantizer import quantized_weight
             for L in self.w["layers"]:
                 for k in self.QUANT_KEYS:
                     if torch.is_tensor(L.get(k)) and L[k].dim() == 2:
-                        L[k] = FP8Weight(L[k])
-            self.w["lm_head"] = FP8Weight(self.w["lm_head"])
+                        L[k] = quantized_weight(L[k], weight_quant)
+            self.w["lm_head"] = quantized_weight(self.w["lm_head"], weight_quant)
         self.weight_quant = weight_quant
         self.num_layers, self.nq, self.nkv, self.head_dim = spec.n_layers, spec.nq, spec.nkv, spec.head_dim
         self.vocab_size = spec.vocab_size

@@ -84,16 +84,15 @@ class RaggedLlama:
             assert dist.get_world_size(tp_group) == self.tp, "tp_group size != tp_size"
         self.tp_rank = dist.get_rank(tp_group) if self.tp > 1 else 0
         if weight_quant:
-            assert weight_quant == "fp8", "weight_quant: 'fp8'"
-            from ....ops.fp_quantizer import FP8Weight
+            from ....ops.fp_quantizer import quantized_weight
             self.qw = []
             for layer in model.layers:
-                d = {"qkv": FP8Weight(layer.self_attn.qkv_proj.weight), "o": FP8Weight(layer.self_attn.o_proj.weight)}
+                d = {"qkv": quantized_weight(layer.self_attn.qkv_proj.weight, weight_quant), "o": quantized_weight(layer.self_attn.o_proj.weight, weight_quant)}
                 if hasattr(layer, "mlp"):
-                    d["gu"] = FP8Weight(layer.mlp.gate_up_proj.weight)
-                    d["down"] = FP8Weight(layer.mlp.down_proj.weight)
+                    d["gu"] = quantized_weight(layer.mlp.gate_up_proj.weight, weight_quant)
+                    d["down"] = quantized_weight(layer.mlp.down_proj.weight, weight_quant)
                 self.qw.append(d)
-            self.qhead = FP8Weight(model.lm_head.weight)
+            self.qhead = quantized_weight(model.lm_head.weight, weight_quant)
         self.cfg = model.cfg
         self.is_moe = hasattr(model.layers[0], "block_sparse_moe") or hasattr(model.layers[0], "moe")
         a0 = model.layers[0].self_attn

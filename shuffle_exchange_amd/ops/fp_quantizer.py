@@ -7,9 +7,14 @@ fp8_gemm_triton.py:19,67).
 
 MI355X-first:
 * FP8 uses gfx950's OCP e4m3 hardware converters (quant.hip); FP6 (e3m2) and FP4 (e2m1) are the
-  MX element formats CDNA4's ``mfma_scale`` instructions consume; here they are produced by a
-  nearest-representable rounding against the format's value table (FP4 packed 2 per byte, FP6 one
+  MX element formats CDNA4's ``mfma_scale`` instructions consume; on the GPU they are produced and
+  decoded by the HIP kernels of mxfp.hip (nearest-representable rounding, ties to the smaller
+  magnitude -- bit-identical to the value-table path used on CPU; FP4 packed 2 per byte, FP6 one
   code per byte) with one fp32 scale per group.
+* ``FPxWeight`` (FP6-LLM counterpart, reference inference/v2 'wf6af16'): per-output-row scaled
+  FP6 or FP4 weights in a bit-plane layout whose decode is byte-parallel in registers; decode-sized
+  inputs (<= 16 rows) stream 0.75 (FP6) / 0.5 (FP4) bytes per weight through the skinny MFMA
+  kernel, larger inputs decode the weight to bf16 once per call for hipBLASLt.
 * ``fp8_linear`` runs the GEMM ON the FP8 matrix cores (hipBLASLt ``_scaled_mm`` with row-wise
   scales: 2.2 PF/s measured on MI355X vs ~1.3-1.5 PF/s for bf16), quantizing activations per row
   with the HIP kernel; ``matmul_fp8`` keeps the reference's weight-only semantics (bf16 activations
@@ -75,6 +80,8 @@ class FP_Quantize:
         assert x.numel() % self.group_size == 0, "numel must be a multiple of group_size"
         if q_bits == 8:
             q, s = quantize_fp8(x, self.group_size)
+        elif x.is_cuda and native.use_hip(x):
+            q, s = torch.ops.sxe.fpx_quantize(x, q_bits, self.group_size)
         else:
             g = x.float().reshape(-1, self.group_size)
             amax = g.abs().amax(1)
@@ -94,6 +101,10 @@ class FP_Quantize:
         n = s.numel() * self.group_size
         if bits == 8:
             out = dequantize_fp8(input_q, s, self.group_size, out=fp_out, dtype=self.orig_dtype or torch.bfloat16)
+        elif input_q.is_cuda and native.use_hip(input_q):
+            v = torch.ops.sxe.fpx_dequantize(input_q.contiguous(), s.float().contiguous(), bits, self.group_size, n,
+                                             self.orig_dtype or torch.bfloat16)
+            out = fp_out.reshape(-1).copy_(v) if fp_out is not None else v
         else:
             codes = input_q
             if bits == 4:
@@ -196,3 +207,85 @@ class FP8Linear(torch.nn.Module):
     def forward(self, x):
         b = self.bias.to(x.dtype) if self.bias is not None else None
         return fp8_linear(x, self.weight_q, self.weight_scale, b, out_dtype=x.dtype)
+
+
+# ------------------------------------------------------------------------- FP6 / FP4 weights
+def _codes(w, bits):
+    """w [N, K] -> (per-element codes uint8 [N, K], per-row scales fp32 [N])."""
+    N, K = w.shape
+    fq = FP_Quantize(group_size=K)
+    q = fq.quantize(w.contiguous(), q_bits=bits, q_mantisa_bits=_FMT[bits][1])
+    if bits == 4:
+        q = torch.stack([q & 0xF, q >> 4], 1)
+    return q.reshape(N, K), fq.get_scales().float()
+
+
+def _nibble_words(c):
+    """[N, K] 4-bit values -> [N, K/2] bytes, each 32-bit word (8 values) byte b = v_b | v_{b+4} << 4."""
+    N, K = c.shape
+    v = c.reshape(N, K // 8, 2, 4)
+    return (v[:, :, 0] | (v[:, :, 1] << 4)).reshape(N, K // 2).contiguous()
+
+
+def _crumb_words(m):
+    """[N, K] 2-bit values -> [N, K/4] bytes, each 32-bit word (16 values) byte b = v_b | v_{b+4} << 2
+    | v_{b+8} << 4 | v_{b+12} << 6."""
+    N, K = m.shape
+    v = m.reshape(N, K // 16, 4, 4)
+    return (v[:, :, 0] | (v[:, :, 1] << 2) | (v[:, :, 2] << 4) | (v[:, :, 3] << 6)).reshape(N, K // 4).contiguous()
+
+
+class FPxWeight:
+    """Per-output-row scaled FP6 (e3m2) or FP4 (e2m1) weight of a linear layer, [N, K] (K a
+    multiple of 128), in the bit-plane layout of csrc/kernels/mxfp.hip: FP4 = one nibble plane,
+    FP6 = the (sign | exponent) nibble plane + a 2-bit mantissa plane."""
+
+    def __init__(self, w, bits=6):
+        assert bits in (4, 6), "FPxWeight: bits 4 or 6"
+        N, K = w.shape
+        assert K % 128 == 0, "FPxWeight: in_features must be a multiple of 128"
+        self.bits, self.shape, self.dtype = bits, (N, K), w.dtype
+        codes, self.scale = _codes(w.detach(), bits)
+        if bits == 4:
+            self.wa, self.wb = _nibble_words(codes), None
+        else:
+            self.wa, self.wb = _nibble_words(codes >> 2), _crumb_words(codes & 3)
+
+    def _codes_back(self):
+        N, K = self.shape
+        a = self.wa.reshape(N, K // 8, 4)
+        nib = torch.stack([a & 0xF, a >> 4], 2).reshape(N, K)
+        if self.bits == 4:
+            return nib
+        b = self.wb.reshape(N, K // 16, 4)
+        crumbs = torch.stack([(b >> (2 * j)) & 3 for j in range(4)], 2).reshape(N, K)
+        return (nib << 2) | crumbs
+
+    def dequantize(self, dtype=torch.bfloat16):
+        if self.wa.is_cuda and native.use_hip(self.wa):
+            return torch.ops.sxe.fpxw_unpack(self.wa, self.wb, self.scale, self.bits).to(dtype)
+        v = _decode(self._codes_back().reshape(-1), self.bits).reshape(self.shape)
+        return (v * self.scale.view(-1, 1)).to(dtype)
+
+    def linear(self, x, bias=None):
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        if (x2.is_cuda and x2.dtype == torch.bfloat16 and 0 < x2.shape[0] <= 16 and x2.stride(-1) == 1
+                and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0):
+            native.require_hip()
+            b = bias.to(torch.bfloat16).contiguous() if bias is not None else None
+            y = torch.ops.sxe.skinny_gemm_fpxw(x2, self.wa, self.wb, self.scale, b, self.bits)
+            return y.view(*x.shape[:-1], self.shape[0])
+        y = torch.nn.functional.linear(x2, self.dequantize(x2.dtype), bias.to(x2.dtype) if bias is not None else None)
+        return y.view(*x.shape[:-1], self.shape[0])
+
+
+def quantized_weight(w, kind):
+    """Inference weight-only quantization by name: 'fp8' (W8A16), 'fp6' / 'wf6af16' (FP6-LLM), 'fp4'."""
+    if kind == "fp8":
+        return FP8Weight(w)
+    if kind in ("fp6", "wf6af16"):
+        return FPxWeight(w, 6)
+    if kind in ("fp4", "wf4af16"):
+        return FPxWeight(w, 4)
+    raise ValueError(f"unknown weight quantization {kind!r} (fp8 | fp6 | fp4)")

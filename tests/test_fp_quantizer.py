@@ -58,3 +58,50 @@ def test_fp8_linear_gpu_scaled_mm():
     ref = lin(x).float()
     y = FP8Linear(lin)(x).float()
     assert ((y - ref).norm() / ref.norm()).item() < 0.06
+
+
+# ------------------------------------------------------------------ FP6 / FP4 weights (mxfp.hip)
+@pytest.mark.parametrize("bits", [4, 6])
+def test_fpx_weight_layout_roundtrip_cpu(bits):
+    """The bit-plane GEMM layout decodes back to exactly the FP_Quantize values (per-row scale)."""
+    from shuffle_exchange_amd.ops.fp_quantizer import FP_Quantize, FPxWeight
+    torch.manual_seed(0)
+    w = torch.randn(24, 256)
+    fw = FPxWeight(w, bits)
+    fq = FP_Quantize(group_size=256)
+    ref = fq.dequantize(fq.quantize(w, q_bits=bits, q_mantisa_bits=2 if bits == 6 else 1)).float()
+    torch.testing.assert_close(fw.dequantize(torch.float32), ref, rtol=0, atol=0)
+    x = torch.randn(3, 256)
+    torch.testing.assert_close(fw.linear(x), x @ ref.t(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [4, 6])
+def test_fpx_kernels_gpu(bits):
+    """HIP quantize codes == the CPU value-table codes; HIP dequantize / unpack == CPU decode; the
+    skinny FP6/FP4-weight GEMM == an fp32 GEMM on the decoded weight."""
+    from shuffle_exchange_amd.ops import native
+    from shuffle_exchange_amd.ops.fp_quantizer import FP_Quantize, FPxWeight
+    native.require_hip()
+    torch.manual_seed(0)
+    mant = 2 if bits == 6 else 1
+    x = torch.randn(64 * 1024) * 3
+    qc, qg = FP_Quantize(512), FP_Quantize(512)
+    codes_cpu = qc.quantize(x, q_bits=bits, q_mantisa_bits=mant)
+    codes_gpu = qg.quantize(x.cuda(), q_bits=bits, q_mantisa_bits=mant)
+    torch.testing.assert_close(qg.get_scales().cpu(), qc.get_scales(), rtol=0, atol=0)
+    assert torch.equal(codes_gpu.cpu(), codes_cpu)
+    torch.testing.assert_close(qg.dequantize(codes_gpu).float().cpu(), qc.dequantize(codes_cpu).float(), rtol=0, atol=0)
+    for N, K in [(16, 128), (200, 4096), (1000, 1536)]:
+        w = torch.randn(N, K) * 0.05
+        fc, fg = FPxWeight(w, bits), FPxWeight(w.cuda().bfloat16(), bits)
+        wd = FPxWeight(w.bfloat16(), bits).dequantize(torch.float32)
+        # the unpack kernel emits bf16 (hipBLASLt operand): same fp32 product, same rounding
+        torch.testing.assert_close(fg.dequantize(torch.bfloat16).cpu(), wd.bfloat16(), rtol=0, atol=0)
+        for M in (1, 5, 16):
+            xa = torch.randn(M, K).bfloat16()
+            bias = torch.randn(N).bfloat16()
+            y = fg.linear(xa.cuda(), bias.cuda()).float().cpu()
+            ref = xa.float() @ wd.t() + bias.float()
+            torch.testing.assert_close(y, ref, rtol=2e-2, atol=2e-2)
+        assert fc.bits == bits

@@ -55,7 +55,8 @@ def test_skinny_gemm_fp8_weights_matches_fp32(M, N, K):
     assert err <= 1e-2 * ref.abs().max().item() + 1e-2, err
 
 
-def test_hf_engine_fp8_weights_close_to_bf16():
+@pytest.mark.parametrize("kind,min_cos", [("fp8", 0.99), ("fp6", 0.98), ("fp4", 0.8)])
+def test_hf_engine_quantized_weights_close_to_bf16(kind, min_cos):
     transformers = pytest.importorskip("transformers")
     from shuffle_exchange_amd.inference.v2.engine_factory import build_hf_engine
     from shuffle_exchange_amd.inference.v2.engine_v2 import RaggedInferenceEngineConfig
@@ -66,10 +67,10 @@ def test_hf_engine_fp8_weights_close_to_bf16():
     cfg = RaggedInferenceEngineConfig(kv_block_size=64, num_kv_blocks=32)
     e16 = build_hf_engine(model, cfg, device="cuda")
     e8 = build_hf_engine(model, RaggedInferenceEngineConfig(kv_block_size=64, num_kv_blocks=32), device="cuda",
-                         weight_quant="fp8")
+                         weight_quant=kind)
     p = torch.randint(0, 512, (40,)).tolist()
     a, b = e16.put([0], [p]), e8.put([0], [p])
     for t in (5, 9, 11):
-        a, b = e16.put([0], [[t]]), e8.put([0], [[t]])  # decode steps: skinny FP8-weight kernel
+        a, b = e16.put([0], [[t]]), e8.put([0], [[t]])  # decode steps: skinny FP8 / FP6 / FP4-weight kernels
         cos = torch.nn.functional.cosine_similarity(a.float(), b.float()).item()
-        assert cos > 0.99, cos
+        assert cos > min_cos, (kind, cos)
