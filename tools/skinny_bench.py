@@ -54,13 +54,29 @@ def main():
             def f8():
                 i[0] = (i[0] + 1) % 4
                 torch.ops.sxe.skinny_gemm_fp8w(x, qs[i[0]][0].view(torch.uint8), qs[i[0]][1], None)
-            t_sk, t_bl, t_f8 = timeit(sk), timeit(bl), timeit(f8)
+            from shuffle_exchange_amd.ops.fp_quantizer import FPxWeight
+            f6s = [FPxWeight(wi, 6) for wi in ws]
+            f4s = [FPxWeight(wi, 4) for wi in ws]
+
+            def f6():
+                i[0] = (i[0] + 1) % 4
+                q = f6s[i[0]]
+                torch.ops.sxe.skinny_gemm_fpxw(x, q.wa, q.wb, q.scale, None, 6)
+
+            def f4():
+                i[0] = (i[0] + 1) % 4
+                q = f4s[i[0]]
+                torch.ops.sxe.skinny_gemm_fpxw(x, q.wa, None, q.scale, None, 4)
+            t_sk, t_bl, t_f8, t_f6, t_f4 = timeit(sk), timeit(bl), timeit(f8), timeit(f6), timeit(f4)
             gb = N * K * 2 / 1e9
             print(json.dumps({"shape": name, "N": N, "K": K, "M": M, "skinny_us": round(t_sk, 2),
                               "hipblaslt_us": round(t_bl, 2), "skinny_fp8w_us": round(t_f8, 2),
                               "skinny_TBps": round(gb / t_sk * 1e3, 2), "hipblaslt_TBps": round(gb / t_bl * 1e3, 2),
-                              "fp8w_weight_TBps": round(gb / 2 / t_f8 * 1e3, 2)}), flush=True)
-            del qs
+                              "fp8w_weight_TBps": round(gb / 2 / t_f8 * 1e3, 2),
+                              "skinny_fp6w_us": round(t_f6, 2), "fp6w_weight_TBps": round(gb * 0.375 / t_f6 * 1e3, 2),
+                              "skinny_fp4w_us": round(t_f4, 2), "fp4w_weight_TBps": round(gb * 0.25 / t_f4 * 1e3, 2)}),
+                  flush=True)
+            del qs, f6s, f4s
         del ws
 
 
