@@ -206,7 +206,7 @@ def multinode_commands(args, active, master_addr):
 
 def _autotune(args):
     import json
-    from ..autotuning import Autotuner, subprocess_runner
+    from ..autotuning import Autotuner, scheduled_runner
     ua = list(args.user_args)
     cfg_path = None
     for i, a in enumerate(ua):
@@ -220,12 +220,14 @@ def _autotune(args):
         base = json.load(f)
     at_cfg = base.get("autotuning", {})
     nproc = args.num_gpus if args.num_gpus > 0 else _local_gpu_count()
-    tuner = Autotuner(base, world_size=nproc, tuner_type=at_cfg.get("tuner_type", "gridsearch"),
-                      tuner_num_trials=at_cfg.get("tuner_num_trials", 50),
-                      tuner_early_stopping=at_cfg.get("tuner_early_stopping", 5),
-                      results_dir=at_cfg.get("results_dir", "autotuning_results"))
-    best = tuner.tune(subprocess_runner(args.user_script, rest, nproc=nproc))
+    tuner = Autotuner(base, world_size=nproc)
+    run = scheduled_runner(args.user_script, rest, exps_dir=tuner.exps_dir, nproc=nproc,
+                           timeout=tuner.at.exp_timeout, start_step=tuner.at.start_profile_step,
+                           end_step=tuner.at.end_profile_step, metric=tuner.metric)
+    best = tuner.tune(run, profile_model_info=not tuner.model_info.get("num_params"))
     best_cfg = tuner.best_config()
+    if best_cfg is not None:
+        tuner.write_optimal_cmd(args.user_script, rest)
     print(f"autotuning best: {best}")
     if args.autotuning == "run" and best_cfg is not None:
         best_cfg.pop("autotuning", None)

@@ -619,6 +619,9 @@ class SXEEngine(nn.Module):
         """Start the throughput timer; learn tokens per sample and model FLOPs per sample from
         the first token-id input (reference engine.py:2068 tput_timer.start)."""
         t = self.tput_timer
+        if self.global_steps == 0 and not hasattr(self, "_at_mem0") and self.device.type == "cuda":
+            self._at_mem0 = torch.cuda.memory_allocated()  # model states: the autotuner's baseline
+            torch.cuda.reset_peak_memory_stats()
         if t.seq_len is None:
             x = inputs[0] if inputs and torch.is_tensor(inputs[0]) else kwargs.get("input_ids")
             if torch.is_tensor(x) and x.dim() >= 2 and not x.is_floating_point():
@@ -659,24 +662,59 @@ class SXEEngine(nn.Module):
         mon.write_events(ev)
 
     def _autotuning_probe(self):
-        """Autotuning experiments: time steps (start, end] and write the metric file, then exit
-        (reference engine autotuning hooks)."""
+        """Autotuning experiments (reference engine autotuning hooks, autotuning/autotuner.py):
+        * ``model_info_path``: after the first optimizer step write the model info the autotuner's
+          memory model needs -- parameter counts, hidden size / layers when the module has a
+          config, and ``activation_mem_per_gpu`` = peak HBM of the step minus the HBM held before
+          it (model states) -- then exit;
+        * ``metric_path``: time steps (start, end] and write throughput (samples/s), latency
+          (s/step) and flops (model FLOP/s from 6 x params x tokens when token counts are known)."""
         at = self._config._param_dict.get("autotuning", {})
-        if not at.get("enabled") or not at.get("metric_path"):
+        if not at.get("enabled"):
+            return
+        import json
+        cuda = torch.cuda.is_available() and self.device.type == "cuda"
+        if at.get("model_info_path"):
+            if self.global_steps == 1:
+                if cuda:
+                    torch.cuda.synchronize()
+                    act = max(0, torch.cuda.max_memory_allocated() - getattr(self, "_at_mem0", 0))
+                else:
+                    act = 0
+                cfg = getattr(self.module, "config", None) or getattr(self.module, "cfg", None)
+                info = {"num_params": int(self._n_params),
+                        "trainable_num_params": int(sum(getattr(p, "ds_numel", p.numel())
+                                                        for p in self.module.parameters() if p.requires_grad)),
+                        "activation_mem_per_gpu": int(act) // max(1, self.train_micro_batch_size_per_gpu()),
+                        "micro_batch_size": self.train_micro_batch_size_per_gpu()}
+                for k in ("hidden_size", "num_hidden_layers", "num_attention_heads", "vocab_size"):
+                    if cfg is not None and hasattr(cfg, k):
+                        info[k] = int(getattr(cfg, k))
+                if self.global_rank == 0:
+                    os.makedirs(os.path.dirname(os.path.abspath(at["model_info_path"])), exist_ok=True)
+                    with open(at["model_info_path"], "w") as f:
+                        json.dump(info, f)
+                if at.get("exit_after_profile", True):
+                    dist.barrier()
+                    raise SystemExit(0)
+            return
+        if not at.get("metric_path"):
             return
         s0, s1 = at.get("start_profile_step", 3), at.get("end_profile_step", 5)
         if self.global_steps == s0:
-            if torch.cuda.is_available():
+            if cuda:
                 torch.cuda.synchronize()
             self._at_t0 = time.perf_counter()
         elif self.global_steps == s1 and hasattr(self, "_at_t0"):
-            if torch.cuda.is_available():
+            if cuda:
                 torch.cuda.synchronize()
             dt = (time.perf_counter() - self._at_t0) / max(1, s1 - s0)
+            out = {"throughput": self.train_batch_size() / dt, "latency": dt}
+            if self.tput_timer.flops_per_sample:
+                out["flops"] = self.train_batch_size() * self.tput_timer.flops_per_sample / dt
             if self.global_rank == 0:
-                import json
                 with open(at["metric_path"], "w") as f:
-                    json.dump({"throughput": self.train_batch_size() / dt, "latency": dt}, f)
+                    json.dump(out, f)
             if at.get("exit_after_profile", True):
                 dist.barrier()
                 raise SystemExit(0)
