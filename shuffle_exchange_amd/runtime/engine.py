@@ -742,6 +742,14 @@ class SXEEngine(nn.Module):
             from ..utils.fault import maybe_inject
             maybe_inject(self.global_rank, self.global_steps)
         self._autotuning_probe()
+        if getattr(self, "_compile_at_step", None) is not None and self.global_steps >= self._compile_at_step:
+            from ..compile import compile_zero3
+            self._compile_at_step = None
+            if self.optimizer.tracer is not None and self.optimizer.tracer.complete is not None:
+                self.compile_plan = compile_zero3(self.optimizer, self._compile_cfg_obj)
+                if self.compile_plan.get("offload_opt_states") and not getattr(self, "_offload_opt_states", False):
+                    self._offload_opt_states = True
+                    self.optimizer.offload_states(include=["optim_states"], non_blocking=True)
         se = self.shuffle_exchange_config
         if se.enabled and se.auto_shuffle:
             self.shuffle_exchange()
@@ -784,8 +792,14 @@ class SXEEngine(nn.Module):
           * backend ``"hipgraph"``: eval / no-grad forwards with static input shapes (ZeRO 0-2,
             parameters resident) replay a captured HIP graph per input signature.
         Training forward/backward stay eager: ZeRO collectives are launched from autograd hooks on
-        side streams, which a captured graph would freeze at capture time. ``schedule`` is accepted
-        for API parity and ignored (the prefetch schedule is the recorded trace)."""
+        side streams, which a captured graph would freeze at capture time.
+
+        With ``deepcompile`` under ZeRO-3 the schedule compiler (compile/backend.py) traces the
+        next ``profile_steps`` optimizer steps (per-group compute and all-gather times, live
+        memory), then its passes -- selective_gather (keep groups resident), prefetch (place each
+        all-gather behind enough measured compute, bounded by the bytes in flight) and
+        offload_adam_states -- rewrite the ZeRO-3 schedule under ``memory_budget``; the plan is
+        ``engine.compile_plan``. ``schedule`` is accepted for API parity and ignored."""
         if self.is_compiled:
             return
         cc = dict(self._config._param_dict.get("compile", {}) or {})
@@ -800,6 +814,12 @@ class SXEEngine(nn.Module):
             opt.prefetch_depth = max(2, opt.prefetch_depth) if cc.get("double_buffer", True) else 1
         if backend == "hipgraph" and self.device.type == "cuda" and self.zero_optimization_stage() < 3:
             self._fwd_graphs = {}
+        if cc.get("deepcompile") and self.zero_optimization_stage() == 3 and hasattr(opt, "apply_compile_plan"):
+            # schedule compiler (compile/): trace the next step(s), then run the passes
+            from ..compile import CompileConfig, install_profiler
+            self._compile_cfg_obj = CompileConfig.from_dict(cc)
+            self._compile_at_step = self.global_steps + max(1, self._compile_cfg_obj.profile_steps)
+            install_profiler(opt)
         self._is_compiled = True
         log_dist(f"compile: backend={backend} deepcompile={bool(cc.get('deepcompile'))} "
                  f"offload_opt_states={getattr(self, '_offload_opt_states', False)} "

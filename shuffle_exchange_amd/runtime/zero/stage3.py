@@ -178,6 +178,9 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         # fetch groups until this many elements are in flight (at least one group)
         self.prefetch_numel = int(prefetch_bucket_size) if prefetch_bucket_size else None
         self.persist_thr = int(param_persistence_threshold)
+        self.tracer = None          # compile/profiler.ScheduleTracer while the schedule compiler traces
+        self.prefetch_plan = None   # compiled prefetch trigger table (apply_compile_plan)
+        self.compile_plan = None
         # stage3_model_persistence_threshold: cap on the total elements kept persistent
         self.model_persist_thr = int(model_persistence_threshold)
         self._persist_total = 0
@@ -322,6 +325,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             u.flat.untyped_storage().resize_(0)
             u.state = RELEASED
         u.event = None
+        u.keep = False
         u.qshard = None
         u.sec_shard, u.sec_valid = None, False
         for p in params:
@@ -374,10 +378,14 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 self._observed.append(fg.idx)
             self._fetch(fg, wait=True)
             self._prefetch_after(fg, backward=self._in_bwd)
+            if self.tracer is not None and not self._in_bwd:
+                self.tracer.on_fwd_begin(fg)
         return pre
 
     def _make_post(self, fg):
         def post(mod, args, out):
+            if self.tracer is not None and not self._in_bwd:
+                self.tracer.on_fwd_end(fg)
             if torch.is_grad_enabled() and any(u.params[0].requires_grad for u in fg.units):
                 out = self._wrap_outputs(fg, out)
             if not self._in_bwd and not (torch.is_grad_enabled() and self._keep_for_backward(fg)):
@@ -488,6 +496,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                     ev = torch.cuda.Event()
                     ev.record(st if st is not None else cur)
                 u.swap.release(u, ev)
+            t0 = self.tracer.gather_begin(u, st) if self.tracer is not None else None
             if self.S == 1:
                 u.flat.copy_(src)
             elif self.hpz > 1 and self._in_bwd and u.sec_valid:
@@ -497,6 +506,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 self._quantized_gather(u, st)
             else:
                 dist.all_gather_into_tensor(u.flat, src, group=self.topo.slice_group)
+            if t0 is not None:
+                self.tracer.gather_end(u, st, t0)
             if st is not None:
                 u.event = torch.cuda.Event()
                 u.event.record(st)
@@ -539,7 +550,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 u.state = AVAILABLE
 
     def _release_unit(self, u):
-        if u.persistent or u.state == RELEASED or getattr(self, "_hold", False):
+        if u.persistent or u.keep or u.state == RELEASED or getattr(self, "_hold", False):
             return
         if getattr(self, "retain_params", False) and (not self._in_bwd or not self._boundary):
             return  # still valid until the optimizer step: only the boundary backward releases
@@ -560,6 +571,10 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
 
     def _prefetch_after(self, fg, backward):
         if self.prefetch_depth == 0 or (self.S == 1 and not self.offload_param):
+            return
+        if self.prefetch_plan is not None:  # compiled schedule (compile/passes.py prefetch)
+            for j in self.prefetch_plan["bwd" if backward else "fwd"].get(fg.idx, ()):
+                self._fetch(self.fgroups[j], wait=False)
             return
         order = list(reversed(self.trace)) if backward else self.trace
         if fg.idx not in order:
@@ -587,6 +602,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         self._in_bwd = True
         self._fetch(fg, wait=True)
         self._prefetch_after(fg, backward=True)
+        if self.tracer is not None:
+            self.tracer.on_bwd_begin(fg)
 
     # ------------------------------------------------------------------------------ grad reduction
     def _reduce_unit(self, u):
@@ -688,6 +705,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         self._in_bwd = False
         self._observed = []
         self._kept_numel = 0
+        if self.tracer is not None:
+            self.tracer.on_forward_start()
 
     def backward_prologue(self):
         for units in self.units:
@@ -721,6 +740,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                     order.append(i)
             self.trace = order
         self._in_bwd = False
+        if self.tracer is not None:
+            self.tracer.on_backward_end()
 
     # ------------------------------------------------------------------------------------------ step
     def step(self, closure=None, lr_kwargs=None):
@@ -753,8 +774,18 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             return
         for units in self.units:
             for u in units:
-                if u.persistent:
+                if u.persistent or (u.keep and u.state == AVAILABLE):
                     dist.all_gather_into_tensor(u.flat, u.shard, group=self.topo.slice_group)
+
+    def apply_compile_plan(self, plan):
+        """Install a schedule-compiler plan (compile/backend.py): kept groups are no longer
+        released (their next fetch is their last until the plan changes), prefetches follow the
+        compiled trigger table."""
+        for fg in self.fgroups:
+            for u in fg.units:
+                u.keep = fg.idx in plan.get("keep", ()) and not u.persistent
+        self.prefetch_plan = plan.get("prefetch")
+        self.compile_plan = plan
 
     def zero_grad(self, set_to_none=True):
         for p in self.param_unit:

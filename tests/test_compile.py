@@ -1,5 +1,9 @@
 """engine.compile (DeepCompile counterpart): optimizer-state offload between steps leaves the
-training trajectory unchanged; the HIP-graph forward (GPU) replays eval forwards exactly."""
+training trajectory unchanged; the HIP-graph forward (GPU) replays eval forwards exactly; the
+schedule compiler (shuffle_exchange_amd/compile/) turns the traced ZeRO-3 step into a
+ScheduleGraph whose passes -- selective_gather (keep groups resident within the memory budget:
+fewer all-gathers per step), prefetch (gathers placed under the budget), offload_adam_states
+(when the traced peak exceeds it) -- leave training numerics unchanged (gloo, world 2)."""
 import pytest
 import torch
 
@@ -65,3 +69,86 @@ def _graph_eval(rank, world):
 def test_compile_hipgraph_eval_forward():
     errs = run_dist(_graph_eval, 1)[0]
     assert max(errs) == 0.0, errs
+
+
+def _case(rank, world, compile_cfg, steps=4):
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd import comm as dist
+    from ._dist_cases import full_params, global_batches, tiny_llama
+    model, cfg = tiny_llama(0)
+    ds = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": 1,
+          "zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 0, "stage3_max_reuse_distance": 0},
+          "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    calls = {"n": 0}
+    orig = dist.all_gather_into_tensor
+
+    def counting(*a, **k):
+        calls["n"] += 1
+        return orig(*a, **k)
+    dist.all_gather_into_tensor = counting
+    per_step, losses = [], []
+    for i, b in enumerate(global_batches(cfg, world, 2, 16, steps)):
+        if i == 1 and compile_cfg is not None:
+            eng.compile(compile_kwargs=compile_cfg)
+        c0 = calls["n"]
+        local = b[rank * 2:(rank + 1) * 2]
+        loss = eng(local, labels=local)
+        eng.backward(loss)
+        eng.step()
+        losses.append(float(loss))
+        per_step.append(calls["n"] - c0)
+    dist.all_gather_into_tensor = orig
+    plan = getattr(eng, "compile_plan", None)
+    out = {"losses": losses, "gathers": per_step, "params": {k: v for k, v in full_params(eng).items()}}
+    if plan is not None:
+        g = plan["graph"]
+        out.update(keep=sorted(plan["keep"]), prefetch=plan["prefetch"], offload=plan["offload_opt_states"],
+                   n_groups=len(g.gather_bytes), nodes=[(n.phase, n.fg) for n in g.nodes],
+                   gather_bytes=dict(g.gather_bytes), budget=plan["budget"], peak=g.peak_bytes)
+    return out
+
+
+def test_schedule_compiler_keeps_groups_and_preserves_numerics():
+    ref = run_dist(_case, 2, None)
+    big = run_dist(_case, 2, {"deepcompile": True, "memory_budget": 1e12})
+    for a, b in zip(ref, big):
+        assert a["losses"] == b["losses"]
+        for k in a["params"]:
+            assert torch.equal(a["params"][k], b["params"][k]), k
+    r0 = big[0]
+    # a huge budget keeps every partitioned group: after compiling, a step only re-gathers the
+    # kept groups once after the optimizer update (no forward / backward gathers)
+    assert len(r0["keep"]) == r0["n_groups"] > 0
+    assert r0["gathers"][-1] < ref[0]["gathers"][-1]
+    assert ("fwd", r0["nodes"][0][1]) == r0["nodes"][0] and any(p == "bwd" for p, _ in r0["nodes"])
+    assert r0["offload"] is False
+
+
+def test_schedule_compiler_tight_budget_prefetch_and_offload():
+    # budget below the traced peak: nothing kept, gathers still scheduled (at least one trigger
+    # per remaining group), optimizer states offloaded; numerics unchanged
+    ref = run_dist(_case, 2, None)
+    tight = run_dist(_case, 2, {"deepcompile": True, "memory_budget": 1000})
+    for a, b in zip(ref, tight):
+        assert a["losses"] == b["losses"]
+    r0 = tight[0]
+    assert r0["keep"] == [] and r0["offload"] is True
+    scheduled = [j for ph in ("fwd", "bwd") for lst in r0["prefetch"][ph].values() for j in lst]
+    assert scheduled, r0["prefetch"]
+    assert r0["gathers"][-1] == ref[0]["gathers"][-1]
+
+
+def test_prefetch_pass_respects_budget_and_covers_gather_time():
+    from shuffle_exchange_amd.compile.graph import Node, ScheduleGraph
+    from shuffle_exchange_amd.compile.passes import prefetch, zero3_schedule
+    nodes = [Node("fwd", i, 1.0, 0) for i in range(6)] + [Node("bwd", i, 2.0, 0) for i in reversed(range(6))]
+    g = ScheduleGraph(nodes, {i: 100 for i in range(6)}, {i: 2.5 for i in range(6)}, peak_bytes=1000, device_bytes=0)
+    plan = prefetch(g, zero3_schedule(g, {}, 0), budget=1000 + 250, slack=1.0)
+    # forward: each gather needs 2.5 ms of cover = 3 nodes ahead, but only 2 x 100 B may be in
+    # flight (250 B of headroom) -> issued 2 nodes ahead
+    trig = {j: t for t, js in plan["prefetch"]["fwd"].items() for j in js}
+    assert trig[5] == 3 and trig[4] == 2 and trig[3] == 1
+    plan2 = prefetch(g, zero3_schedule(g, {}, 0), budget=1000 + 10_000, slack=1.0)
+    trig2 = {j: t for t, js in plan2["prefetch"]["fwd"].items() for j in js}
+    assert trig2[5] == 2 and trig2[4] == 1  # 3 nodes of 1 ms cover 2.5 ms
