@@ -61,7 +61,8 @@ class RaggedInferenceEngineConfig:
     num_kv_blocks: Optional[int] = None
     tensor_parallel: dict = field(default_factory=lambda: {"tp_size": 1})
     decode_graphs: bool = True  # replay pure-decode steps from captured HIP graphs (decode_graphs.py)
-    weight_quant: Optional[str] = None  # "fp8": row-scaled e4m3 projection / LM-head weights (W8A16 decode GEMMs)
+    weight_quant: Optional[str] = None  # "fp8" (W8A16) | "fp6" / "wf6af16" (FP6-LLM) | "fp4": weight-only decode GEMMs
+    implementations: Optional[dict] = None  # pin registry implementations by interface (modules/registry.py)
 
 
 def _tp_group(tp):
@@ -88,7 +89,7 @@ class InferenceEngineV2:
         self._tp = tp
         self._tp_group = _tp_group(tp) if tp > 1 else None
         self._model = ragged_model_for(model, weight_quant=self._config.weight_quant, tp_group=self._tp_group,
-                                       tp_size=tp)
+                                       tp_size=tp, pins=self._config.implementations)
         sm = self._config.state_manager
         dev = self._model.device
         bs = self._config.kv_block_size

@@ -10,7 +10,7 @@ from .hf_decoder import RaggedDecoder, load_hf_decoder, spec_from_hf_config  # n
 from .llama import RaggedLlama  # noqa: F401
 
 
-def ragged_model_for(model, weight_quant=None, tp_group=None, tp_size=1):
+def ragged_model_for(model, weight_quant=None, tp_group=None, tp_size=1, pins=None):
     """Pick the ragged implementation for a model object (``weight_quant='fp8'``: row-scaled e4m3
     projection / LM-head weights for the decode GEMMs; ``tp_group``: tensor-parallel sharding)."""
     if isinstance(model, (RaggedDecoder, RaggedLlama)):
@@ -23,5 +23,5 @@ def ragged_model_for(model, weight_quant=None, tp_group=None, tp_size=1):
                                        __import__("torch").float32) else None
         return load_hf_decoder(model, dtype=dtype, device=p.device, weight_quant=weight_quant)
     if hasattr(model, "layers") and hasattr(model.layers[0], "self_attn") and hasattr(model, "embed_tokens"):
-        return RaggedLlama(model, weight_quant=weight_quant, tp_group=tp_group, tp_size=tp_size)
+        return RaggedLlama(model, weight_quant=weight_quant, tp_group=tp_group, tp_size=tp_size, pins=pins)
     raise NotImplementedError(f"no ragged inference implementation for {type(model).__name__}")

@@ -74,7 +74,8 @@ class _TPShards:
 
 
 class RaggedLlama:
-    def __init__(self, model, weight_quant=None, tp_group=None, tp_size=1):
+    def __init__(self, model, weight_quant=None, tp_group=None, tp_size=1, pins=None):
+        from ..modules import heuristics as H
         self.model = model
         self.qw = None
         from .... import comm as dist
@@ -83,20 +84,41 @@ class RaggedLlama:
         if self.tp > 1:
             assert dist.get_world_size(tp_group) == self.tp, "tp_group size != tp_size"
         self.tp_rank = dist.get_rank(tp_group) if self.tp > 1 else 0
+        p0 = next(model.parameters())
+        dev = p0.device.type
         if weight_quant:
-            from ....ops.fp_quantizer import quantized_weight
+            # linear implementations from the registry (modules/heuristics.py): quantized
+            # weight-only GEMMs for decode-sized inputs, the bf16 weight on hipBLASLt otherwise
+            def lin(mod):
+                w = mod.weight
+                return H.instantiate_linear(H.LinearConfig(w.shape[1], w.shape[0], w.dtype, weight_quant, dev), w,
+                                            getattr(mod, "bias", None), pins)
             self.qw = []
             for layer in model.layers:
-                d = {"qkv": quantized_weight(layer.self_attn.qkv_proj.weight, weight_quant), "o": quantized_weight(layer.self_attn.o_proj.weight, weight_quant)}
+                d = {"qkv": lin(layer.self_attn.qkv_proj), "o": lin(layer.self_attn.o_proj)}
                 if hasattr(layer, "mlp"):
-                    d["gu"] = quantized_weight(layer.mlp.gate_up_proj.weight, weight_quant)
-                    d["down"] = quantized_weight(layer.mlp.down_proj.weight, weight_quant)
+                    d["gu"] = lin(layer.mlp.gate_up_proj)
+                    d["down"] = lin(layer.mlp.down_proj)
                 self.qw.append(d)
-            self.qhead = quantized_weight(model.lm_head.weight, weight_quant)
+            self.qhead = lin(model.lm_head)
         self.cfg = model.cfg
         self.is_moe = hasattr(model.layers[0], "block_sparse_moe") or hasattr(model.layers[0], "moe")
         a0 = model.layers[0].self_attn
         self.nq, self.nkv, self.head_dim = a0.nq, a0.nkv, a0.d
+        self.attn_impl = H.instantiate_attention(H.AttentionConfig(self.head_dim, self.nq, self.nkv, p0.dtype, 0, dev),
+                                                 pins)
+        emb = getattr(model.embed_tokens, "weight", None)
+        self.embed_impl = H.instantiate_embed(H.EmbedConfig(emb.shape[0], emb.shape[1], emb.dtype, dev), emb, pins) \
+            if emb is not None else None
+        self.moe_impl = None
+        if self.is_moe:
+            l0 = model.layers[0]
+            moe = (l0.block_sparse_moe if hasattr(l0, "block_sparse_moe") else l0.moe).deepspeed_moe
+            self.moe_impl = H.instantiate_moe(H.MoEConfig(moe.gate.wg.weight.shape[0], moe.gate.k, dev), pins)
+        self.implementations = {"attention": self.attn_impl.impl_name,
+                                "embed": self.embed_impl.impl_name if self.embed_impl else "module",
+                                "linear": self.qhead.impl_name if self.qw is not None else "module",
+                                "moe": self.moe_impl.impl_name if self.moe_impl else None}
         self.num_layers = len(model.layers)
         self.vocab_size = self.cfg.vocab_size
         self.tps = None
@@ -127,7 +149,7 @@ class RaggedLlama:
         nq, D = self.nq, self.head_dim
         scale = D ** -0.5
         q = qkv[:, :nq]
-        use_flash = native.use_hip(qkv) and D == 128 and qkv.dtype == torch.bfloat16
+        use_flash = native.use_hip(qkv) and self.attn_impl.flash_prefill and D == 128 and qkv.dtype == torch.bfloat16
         flash_ids = [i for i in range(batch.num_seqs)
                      if use_flash and batch.host_seen[i] == 0 and batch.host_q_len[i] >= FLASH_PREFILL_MIN] \
             if use_flash else []
@@ -168,8 +190,8 @@ class RaggedLlama:
             return y
         # FP8 weights pay off where the GEMM is weight-streaming bound (<= 16 rows: W8A16 skinny
         # kernel); larger batches keep the module's bf16 weight on hipBLASLt
-        if self.qw is not None and key in self.qw[li] and x.shape[0] <= 16:
-            return linear(x, self.qw[li][key], mod.bias)
+        if self.qw is not None and key in self.qw[li]:
+            return self.qw[li][key](x)
         return mod(x)
 
     def _mlp(self, layer, m, li=0):
@@ -187,8 +209,14 @@ class RaggedLlama:
         gate, ex = moe.gate, moe.experts
         assert moe.ep_size == 1, "ragged inference runs experts locally (ep_size == 1)"
         k = gate.k
-        probs = torch.softmax(F.linear(m.float(), gate.wg.weight.float()), dim=-1)
-        topw, topi = probs.topk(k, dim=-1)
+        logits = F.linear(m.float(), gate.wg.weight.float())
+        if self.moe_impl is not None and self.moe_impl.use_hip_gating and logits.is_cuda:
+            from ....ops.moe import topk_softmax  # fused softmax + top-k kernel (moe.hip)
+            probs, topi = topk_softmax(logits, k)
+            topw = probs.gather(1, topi)
+        else:
+            probs = torch.softmax(logits, dim=-1)
+            topw, topi = probs.topk(k, dim=-1)
         topw = topw / topw.sum(-1, keepdim=True)
         flat = topi.reshape(-1)
         order = torch.argsort(flat, stable=True)
@@ -211,8 +239,7 @@ class RaggedLlama:
         model = self.model
         rope = model.rope(self.device)
         T = batch.num_tokens
-        emb = getattr(model.embed_tokens, "weight", None)
-        x = embed(emb, batch.input_ids) if emb is not None else model.embed_tokens(batch.input_ids)
+        x = self.embed_impl(batch.input_ids) if self.embed_impl is not None else model.embed_tokens(batch.input_ids)
         res = None
         for li, layer in enumerate(model.layers):
             if res is None:
@@ -236,5 +263,6 @@ class RaggedLlama:
             full = torch.empty(self.tp * part.shape[0], part.shape[1], dtype=part.dtype, device=part.device)
             dist.all_gather_into_tensor(full, part, group=self.tp_group)
             return full.view(self.tp, -1, part.shape[1]).permute(1, 0, 2).reshape(part.shape[0], -1)[:, :self.tps.vocab]
-        use_q = self.qw is not None and h.shape[0] <= 16
-        return linear(h, self.qhead if use_q else model.lm_head.weight).float()
+        if self.qw is not None:
+            return self.qhead(h).float()
+        return linear(h, model.lm_head.weight).float()
