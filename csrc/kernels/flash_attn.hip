@@ -80,6 +80,13 @@ __device__ __forceinline__ bf16x8 acc_to_b(const f32x16& a, int s) {
   return r;
 }
 
+// value of the lane 32 apart (lane ^ 32) via v_permlane32_swap: a VALU op instead of a
+// ds_bpermute round trip through the LDS
+__device__ __forceinline__ float xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+}
+
 // raw v_exp_f32: exp2f() wraps it in denormal range reduction, pure VALU overhead for softmax
 // probabilities (a denormal p is 0 for every purpose here)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -104,14 +111,14 @@ struct Strides {
 
 // Stage a [rows=ROWS][D] tile of 16-byte chunks from global into registers (each of the 256
 // threads owns ROWS*16/256 chunks), then into swizzled LDS.
-template <int ROWS>
+template <int ROWS, int NWAVES = NW>
 struct Stager {
-  static constexpr int N = ROWS * (D / 8) / (NW * 64);
+  static constexpr int N = ROWS * (D / 8) / (NWAVES * 64);
   u32x4 r[N];
   __device__ __forceinline__ void load(const unsigned short* base, int64_t row_stride, int row0, int nrows_valid) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const int c = threadIdx.x + i * NW * 64;
+      const int c = threadIdx.x + i * NWAVES * 64;
       const int row = c >> 4, ch = c & 15;
       if (row0 + row < nrows_valid)
         r[i] = *reinterpret_cast<const u32x4*>(base + (int64_t)(row0 + row) * row_stride + ch * 8);
@@ -122,7 +129,7 @@ struct Stager {
   __device__ __forceinline__ void store(char* lds) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const int c = threadIdx.x + i * NW * 64;
+      const int c = threadIdx.x + i * NWAVES * 64;
       *reinterpret_cast<u32x4*>(lds + soff(c >> 4, c & 15)) = r[i];
     }
   }
@@ -178,7 +185,83 @@ __device__ __forceinline__ void map_block(int nblk, int BH, bool heavy_last_inde
 // =============================================================================================
 // Forward. Grid: nqb * B * H blocks of 256 threads. q/k/v/o: [B, S, *, D] strided; lse [B, H, S].
 // =============================================================================================
-__global__ void __launch_bounds__(256, 2) fwd_kernel(const unsigned short* __restrict__ q, Strides qs,
+// One K/V tile of a wave's online softmax. MASK = false is the interior-tile body (no causal
+// diagonal, no padded tail, dense): none of the per-score compares / selects are emitted -- on
+// the Llama-3 shape ~90 % of the tiles take it; the masked body handles the diagonal, the kv_len
+// tail and block-sparse layouts.
+template <bool MASK>
+__device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const bf16x8 (&qf)[D / 16],
+                                         f32x16 (&oacc)[D / 32], float& m, float& l, float c, int kbase, int q0,
+                                         int r, int h, int lane, bool diag, bool tail, int kvlen, const uint8_t* lrow,
+                                         int blk) {
+  f32x16 s[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    s[j] = zero16();
+#pragma unroll
+    for (int t2 = 0; t2 < D / 16; ++t2) s[j] = mfma(lds_row16(kt, 32 * j + r, 2 * t2 + h), qf[t2], s[j]);
+  }
+  // raw scores: the max is taken before scaling (c > 0) and the scale folds into the exp's FMA
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    bool b0 = true, b1 = true;  // layout bits of keys kbase+32j+[0,16) and +[16,32)
+    if (MASK && lrow) {
+      b0 = lrow[(kbase + 32 * j) / blk] != 0;
+      b1 = lrow[(kbase + 32 * j + 16) / blk] != 0;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float x = s[j][i];
+      if (MASK) {
+        if (diag && (kbase + 32 * j + acc_row(i, h) > q0 + r)) x = -INFINITY;
+        if (tail && (kbase + 32 * j + acc_row(i, h) >= kvlen)) x = -INFINITY;
+        if (!(acc_row(i, h) < 16 ? b0 : b1)) x = -INFINITY;
+        s[j][i] = x;
+      }
+      mx = fmaxf(mx, x);
+    }
+  }
+  mx = fmaxf(mx, xor32(mx)) * c;
+  // lazy rescale: the reference max only moves when the tile max exceeds it by > 2^8, so
+  // p <= 256 (harmless in fp32 / bf16) and the 64-register O rescale is skipped whenever no
+  // lane of the wave moved (most tiles after the first few)
+  const bool grow = mx > m + 8.f;
+  const float mnew = grow ? mx : m;
+  const float mref = (mnew == -INFINITY) ? 0.f : mnew;
+  const float alpha = fast_exp2(m - mref);
+  float ps = 0.f;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = fast_exp2(__builtin_fmaf(s[j][i], c, -mref));
+      s[j][i] = p;
+      ps += p;
+    }
+  l = l * alpha + ps;
+  m = mnew;
+  if (__any(grow)) {
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pb = acc_to_b(s[j], s2);
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) oacc[dt] = mfma(lds_trA(vt, 32 * j + 16 * s2, dt, lane), pb, oacc[dt]);
+    }
+}
+
+// NWF waves per workgroup, each 32 queries: NWF = 8 (256 queries, one workgroup of 2 waves per
+// SIMD per CU) shares every staged K/V tile among twice the queries of NWF = 4 (used when the
+// sequence is not a multiple of 256).
+template <bool SPARSE, int NWF>
+__global__ void __launch_bounds__(NWF * 64, 8 / NWF) fwd_kernel(const unsigned short* __restrict__ q, Strides qs,
                                                      const unsigned short* __restrict__ k, Strides ks,
                                                      const unsigned short* __restrict__ v, Strides vs,
                                                      unsigned short* __restrict__ o, Strides os,
@@ -187,13 +270,14 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const unsigned short* __res
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BUF = 2 * KT * ROWB;  // one ring slot = K tile + V tile
   int* tlist = reinterpret_cast<int*>(smem + 4 * KT * ROWB) + 1;
+  constexpr int QBF = NWF * QW;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-  const int nqb = S / QB;
+  const int nqb = S / QBF;
   int bh, qb;
   map_block(nqb, B * H, causal != 0, bh, qb);
   const int b = bh / H, head = bh - b * H;
   const int kh = head / (H / Hk);
-  const int q0 = qb * QB + w * QW;  // this wave's first query
+  const int q0 = qb * QBF + w * QW;  // this wave's first query
   const unsigned short* qp = q + b * qs.b + head * qs.h;
   const unsigned short* kp = k + b * ks.b + kh * ks.h;
   const unsigned short* vp = v + b * vs.b + kh * vs.h;
@@ -209,12 +293,12 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const unsigned short* __res
   for (int t = 0; t < D / 32; ++t) oacc[t] = zero16();
   float m = -INFINITY, l = 0.f;
 
-  const int kend = causal ? (qb + 1) * QB : S;  // keys needed by the workgroup
-  const int ntiles = sp.layout ? build_tile_list(sp, head, 0, kend / KT, KT, qb * QB, qb * QB + QB, true, tlist)
-                               : kend / KT;
-  auto tile_at = [&](int i) { return sp.layout ? tlist[i] : i; };
-  const uint8_t* lrow = sp.layout ? sp.layout + ((int64_t)head * sp.nb + (q0 + r) / sp.blk) * sp.nb : nullptr;
-  Stager<KT> sk, sv;
+  const int kend = causal ? (qb + 1) * QBF : S;  // keys needed by the workgroup
+  const int ntiles = SPARSE ? build_tile_list(sp, head, 0, kend / KT, KT, qb * QBF, qb * QBF + QBF, true, tlist)
+                            : kend / KT;
+  auto tile_at = [&](int i) { return SPARSE ? tlist[i] : i; };
+  const uint8_t* lrow = SPARSE ? sp.layout + ((int64_t)head * sp.nb + (q0 + r) / sp.blk) * sp.nb : nullptr;
+  Stager<KT, NWF> sk, sv;
   const int t0 = ntiles > 0 ? tile_at(0) : 0;
   sk.load(kp, ks.s, t0 * KT, S);
   sv.load(vp, vs.s, t0 * KT, S);
@@ -233,67 +317,13 @@ __global__ void __launch_bounds__(256, 2) fwd_kernel(const unsigned short* __res
     const bool active = !causal || kbase <= q0 + QW - 1;
     if (active) {
       const char* kt = smem + cur * BUF;
-      f32x16 s[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        s[j] = zero16();
-#pragma unroll
-        for (int t2 = 0; t2 < D / 16; ++t2) s[j] = mfma(lds_row16(kt, 32 * j + r, 2 * t2 + h), qf[t2], s[j]);
-      }
+      const char* vt = kt + KT * ROWB;
       const bool diag = causal && (kbase + KT - 1 > q0);
       const bool tail = kbase + KT > kvlen;  // keys past the valid length (sequence padded to 128)
-      float mx = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        bool b0 = true, b1 = true;  // layout bits of keys kbase+32j+[0,16) and +[16,32)
-        if (lrow) {
-          b0 = lrow[(kbase + 32 * j) / sp.blk] != 0;
-          b1 = lrow[(kbase + 32 * j + 16) / sp.blk] != 0;
-        }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float x = s[j][i] * c;
-          if (diag && (kbase + 32 * j + acc_row(i, h) > q0 + r)) x = -INFINITY;
-          if (tail && (kbase + 32 * j + acc_row(i, h) >= kvlen)) x = -INFINITY;
-          if (!(acc_row(i, h) < 16 ? b0 : b1)) x = -INFINITY;
-          s[j][i] = x;
-          mx = fmaxf(mx, x);
-        }
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      // lazy rescale: the reference max only moves when the tile max exceeds it by > 2^8, so
-      // p <= 256 (harmless in fp32 / bf16) and the 64-register O rescale is skipped whenever no
-      // lane of the wave moved (most tiles after the first few)
-      const bool grow = mx > m + 8.f;
-      const float mnew = grow ? mx : m;
-      const float mref = (mnew == -INFINITY) ? 0.f : mnew;
-      const float alpha = fast_exp2(m - mref);
-      float ps = 0.f;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = fast_exp2(s[j][i] - mref);
-          s[j][i] = p;
-          ps += p;
-        }
-      l = l * alpha + ps;
-      m = mnew;
-      if (__any(grow)) {
-#pragma unroll
-        for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
-      }
-      const char* vt = smem + cur * BUF + KT * ROWB;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 pb = acc_to_b(s[j], s2);
-#pragma unroll
-          for (int dt = 0; dt < D / 32; ++dt) oacc[dt] = mfma(lds_trA(vt, 32 * j + 16 * s2, dt, lane), pb, oacc[dt]);
-        }
+      if (SPARSE || diag || tail)
+        fwd_tile<true>(kt, vt, qf, oacc, m, l, c, kbase, q0, r, h, lane, diag, tail, kvlen, lrow, SPARSE ? sp.blk : 1);
+      else
+        fwd_tile<false>(kt, vt, qf, oacc, m, l, c, kbase, q0, r, h, lane, false, false, kvlen, nullptr, 1);
     }
     if (more) {
       sk.store(smem + (cur ^ 1) * BUF);
@@ -370,6 +400,44 @@ __device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)
 // dQ: forward-shaped. Per wave 32 queries; per K/V tile recompute S^T, P^T, dP^T = V dO^T,
 // dS^T = P^T (dP^T - delta), dQ^T += K^T dS^T.
 // =============================================================================================
+template <bool MASK>
+__device__ __forceinline__ void dq_tile(const char* kt, const char* vt, const bf16x8 (&qf)[D / 16],
+                                        const bf16x8 (&df)[D / 16], f32x16 (&dqacc)[D / 32], float c, float lse2,
+                                        float dlt, int kbase, int q0, int r, int h, int lane, bool diag, bool tail,
+                                        int kvlen, const uint8_t* lay_row, int blk) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+    for (int t2 = 0; t2 < D / 16; ++t2) {
+      s = mfma(lds_row16(kt, 32 * j + r, 2 * t2 + h), qf[t2], s);
+      dp = mfma(lds_row16(vt, 32 * j + r, 2 * t2 + h), df[t2], dp);
+    }
+    bool b0 = true, b1 = true;
+    if (MASK && lay_row) {
+      b0 = lay_row[(kbase + 32 * j) / blk] != 0;
+      b1 = lay_row[(kbase + 32 * j + 16) / blk] != 0;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float p = fast_exp2(__builtin_fmaf(s[i], c, -lse2));
+      if (MASK) {
+        if (diag && (kbase + 32 * j + acc_row(i, h) > q0 + r)) p = 0.f;
+        if (tail && (kbase + 32 * j + acc_row(i, h) >= kvlen)) p = 0.f;
+        if (!(acc_row(i, h) < 16 ? b0 : b1)) p = 0.f;
+      }
+      s[i] = p * (dp[i] - dlt);  // dS^T
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 db = acc_to_b(s, s2);
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) dqacc[dt] = mfma(lds_trA(kt, 32 * j + 16 * s2, dt, lane), db, dqacc[dt]);
+    }
+  }
+}
+
+template <bool SPARSE>
 __global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __restrict__ q, Strides qs,
                                                     const unsigned short* __restrict__ k, Strides ks,
                                                     const unsigned short* __restrict__ v, Strides vs,
@@ -394,10 +462,10 @@ __global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __rest
   const float c = scale * LOG2E;
   const int64_t lrow = ((int64_t)b * H + head) * S + q0 + r;
   const int kend = causal ? (qb + 1) * QB : S;
-  const int ntiles = sp.layout ? build_tile_list(sp, head, 0, kend / KT, KT, qb * QB, qb * QB + QB, true, tlist)
-                               : kend / KT;
-  auto tile_at = [&](int i) { return sp.layout ? tlist[i] : i; };
-  const uint8_t* lay_row = sp.layout ? sp.layout + ((int64_t)head * sp.nb + (q0 + r) / sp.blk) * sp.nb : nullptr;
+  const int ntiles = SPARSE ? build_tile_list(sp, head, 0, kend / KT, KT, qb * QB, qb * QB + QB, true, tlist)
+                            : kend / KT;
+  auto tile_at = [&](int i) { return SPARSE ? tlist[i] : i; };
+  const uint8_t* lay_row = SPARSE ? sp.layout + ((int64_t)head * sp.nb + (q0 + r) / sp.blk) * sp.nb : nullptr;
   if (ntiles > 0) {
     tile_glds<KT>(kp, ks.s, tile_at(0) * KT, smem);
     tile_glds<KT>(vp, vs.s, tile_at(0) * KT, smem + KT * ROWB);
@@ -429,34 +497,11 @@ __global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __rest
       const char* vt = smem + cur * BUF + KT * ROWB;
       const bool diag = causal && (kbase + KT - 1 > q0);
       const bool tail = kbase + KT > kvlen;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        f32x16 s = zero16(), dp = zero16();
-#pragma unroll
-        for (int t2 = 0; t2 < D / 16; ++t2) {
-          s = mfma(lds_row16(kt, 32 * j + r, 2 * t2 + h), qf[t2], s);
-          dp = mfma(lds_row16(vt, 32 * j + r, 2 * t2 + h), df[t2], dp);
-        }
-        bool b0 = true, b1 = true;
-        if (lay_row) {
-          b0 = lay_row[(kbase + 32 * j) / sp.blk] != 0;
-          b1 = lay_row[(kbase + 32 * j + 16) / sp.blk] != 0;
-        }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float p = fast_exp2(s[i] * c - lse2);
-          if (diag && (kbase + 32 * j + acc_row(i, h) > q0 + r)) p = 0.f;
-          if (tail && (kbase + 32 * j + acc_row(i, h) >= kvlen)) p = 0.f;
-          if (!(acc_row(i, h) < 16 ? b0 : b1)) p = 0.f;
-          s[i] = p * (dp[i] - dlt);  // dS^T
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 db = acc_to_b(s, s2);
-#pragma unroll
-          for (int dt = 0; dt < D / 32; ++dt) dqacc[dt] = mfma(lds_trA(kt, 32 * j + 16 * s2, dt, lane), db, dqacc[dt]);
-        }
-      }
+      if (SPARSE || diag || tail)
+        dq_tile<true>(kt, vt, qf, df, dqacc, c, lse2, dlt, kbase, q0, r, h, lane, diag, tail, kvlen, lay_row,
+                      SPARSE ? sp.blk : 1);
+      else
+        dq_tile<false>(kt, vt, qf, df, dqacc, c, lse2, dlt, kbase, q0, r, h, lane, false, false, kvlen, nullptr, 1);
     }
     vm_wait_all();
     __syncthreads();
@@ -485,6 +530,49 @@ constexpr int QT = 32;  // queries per tile in the dK/dV sweep
 constexpr int KV_TILE = QT * ROWB;                 // 8 KiB
 constexpr int KV_SLOT = 2 * KV_TILE + 2 * QT * 4;  // Q, dO, lse[32], delta[32]
 constexpr int KV_VBLK = QB * ROWB;                 // 32 KiB
+
+template <bool MASK>
+__device__ __forceinline__ void dkdv_tile(const char* slot, const char* vblk, const bf16x8 (&kf)[D / 16],
+                                          f32x16 (&dka)[D / 32], f32x16 (&dva)[D / 32], float c, int qt0, int k0,
+                                          int w, int r, int h, int lane, bool diag, const Sparse& sp, int hq0,
+                                          int kbl) {
+  const char* qt = slot;
+  const char* dt_ = slot + KV_TILE;
+  const float* l2 = reinterpret_cast<const float*>(slot + 2 * KV_TILE);
+  const float* dl = l2 + QT;
+  f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+  for (int t2 = 0; t2 < D / 16; ++t2) {
+    s = mfma(lds_row16(qt, r, 2 * t2 + h), kf[t2], s);                                       // S  [query][key]
+    dp = mfma(lds_row16(dt_, r, 2 * t2 + h), lds_row16(vblk, w * QW + r, 2 * t2 + h), dp);  // dP
+  }
+  bool b0 = true, b1 = true;  // layout bits of query rows qt0+[0,16) and qt0+[16,32) vs this key
+  if (MASK && sp.layout) {
+    b0 = sp.layout[((int64_t)hq0 * sp.nb + qt0 / sp.blk) * sp.nb + kbl] != 0;
+    b1 = sp.layout[((int64_t)hq0 * sp.nb + (qt0 + 16) / sp.blk) * sp.nb + kbl] != 0;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int qi = acc_row(i, h);
+    float p = fast_exp2(__builtin_fmaf(s[i], c, -l2[qi] * LOG2E));
+    if (MASK) {
+      if (diag && (k0 + r > qt0 + qi)) p = 0.f;
+      if (!(qi < 16 ? b0 : b1)) p = 0.f;
+    }
+    s[i] = p;                      // P
+    dp[i] = p * (dp[i] - dl[qi]);  // dS
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const bf16x8 pb = acc_to_b(s, s2);
+    const bf16x8 db = acc_to_b(dp, s2);
+#pragma unroll
+    for (int t = 0; t < D / 32; ++t) {
+      dva[t] = mfma(lds_trA(dt_, 16 * s2, t, lane), pb, dva[t]);  // dV^T += dO^T P
+      dka[t] = mfma(lds_trA(qt, 16 * s2, t, lane), db, dka[t]);   // dK^T += Q^T dS
+    }
+  }
+}
 
 // SPLIT (GQA): one workgroup per (batch, QUERY head, key block) instead of per KV head: under a
 // causal mask the KV-head form gives key block 0 G x (S/128) query tiles while the mean block has
@@ -557,41 +645,10 @@ __global__ void __launch_bounds__(256, 2) dkdv_kernel(const unsigned short* __re
     const bool active = !causal || (qt0 + QT - 1 >= k0);
     if (active) {
       const char* slot = ring + cur * KV_SLOT;
-      const char* qt = slot;
-      const char* dt_ = slot + KV_TILE;
-      const float* l2 = reinterpret_cast<const float*>(slot + 2 * KV_TILE);
-      const float* dl = l2 + QT;
-      f32x16 s = zero16(), dp = zero16();
-#pragma unroll
-      for (int t2 = 0; t2 < D / 16; ++t2) {
-        s = mfma(lds_row16(qt, r, 2 * t2 + h), kf[t2], s);                         // S  [query][key]
-        dp = mfma(lds_row16(dt_, r, 2 * t2 + h), lds_row16(vblk, w * QW + r, 2 * t2 + h), dp);  // dP
-      }
+      const int hq = sp.layout ? hq0 : hq0 + it / ntq;
+      (void)hq;
       const bool diag = causal && (qt0 < k0 + QW);
-      bool b0 = true, b1 = true;  // layout bits of query rows qt0+[0,16) and qt0+[16,32) vs this key
-      if (sp.layout) {
-        b0 = sp.layout[((int64_t)hq0 * sp.nb + qt0 / sp.blk) * sp.nb + kbl] != 0;
-        b1 = sp.layout[((int64_t)hq0 * sp.nb + (qt0 + 16) / sp.blk) * sp.nb + kbl] != 0;
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qi = acc_row(i, h);
-        float p = fast_exp2(s[i] * c - l2[qi] * LOG2E);
-        if (diag && (k0 + r > qt0 + qi)) p = 0.f;
-        if (!(qi < 16 ? b0 : b1)) p = 0.f;
-        s[i] = p;                      // P
-        dp[i] = p * (dp[i] - dl[qi]);  // dS
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pb = acc_to_b(s, s2);
-        const bf16x8 db = acc_to_b(dp, s2);
-#pragma unroll
-        for (int t = 0; t < D / 32; ++t) {
-          dva[t] = mfma(lds_trA(dt_, 16 * s2, t, lane), pb, dva[t]);  // dV^T += dO^T P
-          dka[t] = mfma(lds_trA(qt, 16 * s2, t, lane), db, dka[t]);   // dK^T += Q^T dS
-        }
-      }
+      dkdv_tile<true>(slot, vblk, kf, dka, dva, c, qt0, k0, w, r, h, lane, diag, sp, hq0, kbl);
     }
     vm_wait_all();
     __syncthreads();
@@ -694,6 +751,15 @@ static fa::Sparse sparse_of(const c10::optional<at::Tensor>& layout, int64_t blo
 
 constexpr size_t kListBytes = (1 + 2048) * sizeof(int) + 16;  // tile list + scratch flags (sparse mode)
 
+// SXE_FA_FWD_WAVES=4 forces the 4-wave forward (A/B measurements)
+static bool fwd_narrow() {
+  static const bool v = [] {
+    const char* e = std::getenv("SXE_FA_FWD_WAVES");
+    return e != nullptr && std::atoi(e) == 4;
+  }();
+  return v;
+}
+
 static std::vector<at::Tensor> fwd_impl(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, double scale,
                                         fa::Sparse sp, int64_t kv_len = -1) {
   check_qkv(q, k, v);
@@ -707,16 +773,25 @@ static std::vector<at::Tensor> fwd_impl(at::Tensor q, at::Tensor k, at::Tensor v
   const size_t lds = 4 * fa::KT * fa::ROWB + (sp.layout ? kListBytes : 0);
   static bool attr = false;
   if (!attr) {
-    SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::fwd_kernel),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * fa::KT * fa::ROWB + kListBytes)));
+    for (const void* f : {reinterpret_cast<const void*>(&fa::fwd_kernel<false, 4>),
+                          reinterpret_cast<const void*>(&fa::fwd_kernel<true, 4>),
+                          reinterpret_cast<const void*>(&fa::fwd_kernel<false, 8>),
+                          reinterpret_cast<const void*>(&fa::fwd_kernel<true, 8>)})
+      SXE_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)(4 * fa::KT * fa::ROWB + kListBytes)));
     attr = true;
   }
-  hipLaunchKernelGGL(fa::fwd_kernel, dim3(grid), dim3(256), lds, cur_stream(),
-                     reinterpret_cast<const unsigned short*>(q.data_ptr()), strides_of(q),
-                     reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
-                     reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),
-                     reinterpret_cast<unsigned short*>(o.data_ptr()), strides_of(o), lse.data_ptr<float>(), B, H, Hk,
-                     S, (float)scale, causal ? 1 : 0, sp, kvlen);
+  const bool wide = S % 256 == 0 && !fwd_narrow();
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(wide ? grid / 2 : grid), dim3(wide ? 512 : 256), lds, cur_stream(),
+                       reinterpret_cast<const unsigned short*>(q.data_ptr()), strides_of(q),
+                       reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
+                       reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),
+                       reinterpret_cast<unsigned short*>(o.data_ptr()), strides_of(o), lse.data_ptr<float>(), B, H, Hk,
+                       S, (float)scale, causal ? 1 : 0, sp, kvlen);
+  };
+  if (sp.layout) wide ? launch(fa::fwd_kernel<true, 8>) : launch(fa::fwd_kernel<true, 4>);
+  else wide ? launch(fa::fwd_kernel<false, 8>) : launch(fa::fwd_kernel<false, 4>);
   SXE_LAUNCH_CHECK();
   return {o, lse};
 }
@@ -745,7 +820,9 @@ static void bwd_impl(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, 
   const size_t lds_kv_max = fa::KV_VBLK + 2 * fa::KV_SLOT + kListBytes;
   static bool attr_set = false;
   if (!attr_set) {  // > 64 KiB of dynamic LDS must be opted into (gfx950 has 160 KiB per CU)
-    SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::dq_kernel),
+    SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::dq_kernel<false>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * fa::KT * fa::ROWB + kListBytes)));
+    SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::dq_kernel<true>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * fa::KT * fa::ROWB + kListBytes)));
     SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::dkdv_kernel<false>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv_max));
@@ -753,7 +830,7 @@ static void bwd_impl(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, 
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv_max));
     attr_set = true;
   }
-  hipLaunchKernelGGL(fa::dq_kernel, dim3((S / fa::QB) * B * H), dim3(256), lds_dq, cur_stream(),
+  hipLaunchKernelGGL(sp.layout ? fa::dq_kernel<true> : fa::dq_kernel<false>, dim3((S / fa::QB) * B * H), dim3(256), lds_dq, cur_stream(),
                      reinterpret_cast<const unsigned short*>(q.data_ptr()), strides_of(q),
                      reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
                      reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),
