@@ -505,6 +505,124 @@ class FusedDistilBertBlock(_Fused):
         return y
 
 
+def _probs_context(scores, v, mask, alibi, causal, window, scale):
+    """softmax(scale * scores + alibi + mask) @ v through the HIP masked softmax (softmax.hip):
+    scores [B, H, q, k] fp32, v [B, H, k, D]; a bool mask keeps True, a float mask is additive."""
+    from ..ops.inference_ops import softmax
+    if mask is not None and mask.dim() == 2:
+        mask = mask[:, None, None, :]
+    p = softmax(scores, attn_mask=mask, alibi=alibi, triangular=causal, local_attention=window > 0,
+                window_size=max(window, 1), layer_scale=scale)
+    return torch.matmul(p.to(v.dtype), v)
+
+
+class FusedBloomBlock(_Fused):
+    """BLOOM block (reference containers/bloom.py ``BLOOMLayerPolicy``): LN -> head-interleaved packed
+    QKV GEMM (kept in Bloom's [head][q|k|v][d] layout, so no repacking) -> scores -> ONE HIP masked
+    softmax kernel applying the ALiBi bias, the additive / causal mask and the 1/sqrt(d) scale ->
+    context GEMM -> dense + residual -> LN -> bias-GELU MLP + residual."""
+
+    def __init__(self, block, config):
+        super().__init__(block)
+        at = block.self_attention
+        self.nh, self.hd = at.num_heads, at.head_dim
+        self.layer_idx = at.layer_idx
+        self.inv_norm = float(at.inv_norm_factor)
+        self.post_ln_residual = bool(block.apply_residual_connection_post_layernorm)
+        self.w_qkv, self.b_qkv = self._p(at.query_key_value.weight), self._p(at.query_key_value.bias)
+        self.w_o, self.b_o = self._p(at.dense.weight), self._p(at.dense.bias)
+        l1, l2 = block.input_layernorm, block.post_attention_layernorm
+        self.ln1_w, self.ln1_b, self.eps1 = self._p(l1.weight), self._p(l1.bias), l1.eps
+        self.ln2_w, self.ln2_b, self.eps2 = self._p(l2.weight), self._p(l2.bias), l2.eps
+        mlp = block.mlp
+        self.w_fc, self.b_fc = self._p(mlp.dense_h_to_4h.weight), self._p(mlp.dense_h_to_4h.bias)
+        self.w_out, self.b_out = self._p(mlp.dense_4h_to_h.weight), self._p(mlp.dense_4h_to_h.bias)
+        self._link()
+
+    def _links(self):
+        b = self.orig
+        at, mlp = b.self_attention, b.mlp
+        return [(at.query_key_value.weight, self.w_qkv), (at.query_key_value.bias, self.b_qkv),
+                (at.dense.weight, self.w_o), (at.dense.bias, self.b_o),
+                (b.input_layernorm.weight, self.ln1_w), (b.input_layernorm.bias, self.ln1_b),
+                (b.post_attention_layernorm.weight, self.ln2_w), (b.post_attention_layernorm.bias, self.ln2_b),
+                (mlp.dense_h_to_4h.weight, self.w_fc), (mlp.dense_h_to_4h.bias, self.b_fc),
+                (mlp.dense_4h_to_h.weight, self.w_out), (mlp.dense_4h_to_h.bias, self.b_out)]
+
+    def forward(self, hidden_states, alibi=None, attention_mask=None, layer_past=None, use_cache=False,
+                output_attentions=False, **kwargs):
+        if output_attentions or alibi is None:
+            return self._delegate(hidden_states, alibi, attention_mask, layer_past=layer_past, use_cache=use_cache,
+                                  output_attentions=output_attentions, **kwargs)
+        x = hidden_states
+        B, S, H = x.shape
+        y = layer_norm(x, self.ln1_w, self.ln1_b, self.eps1)
+        qkv = linear(y, self.w_qkv, self.b_qkv).view(B, S, self.nh, 3, self.hd)
+        q, k, v = (qkv[..., i, :].transpose(1, 2) for i in range(3))  # [B, nh, S, hd]
+        if layer_past is not None:
+            k, v = layer_past.update(k, v, self.layer_idx)
+        scores = torch.matmul(q, k.transpose(-1, -2)).float()
+        ab = alibi.view(B, self.nh, 1, -1).float()  # HF builds [B*nh, 1, kv]
+        o = _probs_context(scores, v, attention_mask, ab, attention_mask is None, 0, self.inv_norm)
+        res = y if self.post_ln_residual else x
+        a = linear(o.transpose(1, 2).reshape(B, S, H), self.w_o, self.b_o)
+        h2, h = layer_norm(a, self.ln2_w, self.ln2_b, self.eps2, residual=res)
+        res2 = h2 if self.post_ln_residual else h
+        m = linear(bias_act(linear(h2, self.w_fc), self.b_fc, "gelu"), self.w_out, self.b_out)
+        return res2 + m, None
+
+
+class FusedGPTNeoBlock(_Fused):
+    """GPT-Neo block (reference containers/gptneo.py ``HFGPTNEOLayerPolicy``): LN -> q|k|v packed
+    into one GEMM -> unscaled fp32 scores (GPT-Neo applies no 1/sqrt(d)) -> ONE HIP masked softmax
+    with the causal and, on "local" layers, the sliding-window mask -> out-proj + residual folded
+    into LN2 -> bias-GELU MLP + residual."""
+
+    def __init__(self, block, config):
+        super().__init__(block)
+        at = block.attn.attention
+        self.nh, self.hd = at.num_heads, at.head_dim
+        self.layer_idx = at.layer_id
+        self.window = int(config.window_size) if at.attention_type == "local" else 0
+        self.w_qkv = self._p(torch.cat([at.q_proj.weight, at.k_proj.weight, at.v_proj.weight]))
+        self.w_o, self.b_o = self._p(at.out_proj.weight), self._p(at.out_proj.bias)
+        self.ln1_w, self.ln1_b, self.eps1 = self._p(block.ln_1.weight), self._p(block.ln_1.bias), block.ln_1.eps
+        self.ln2_w, self.ln2_b, self.eps2 = self._p(block.ln_2.weight), self._p(block.ln_2.bias), block.ln_2.eps
+        self.w_fc, self.b_fc = self._p(block.mlp.c_fc.weight), self._p(block.mlp.c_fc.bias)
+        self.w_out, self.b_out = self._p(block.mlp.c_proj.weight), self._p(block.mlp.c_proj.bias)
+        self.act = _act_name(getattr(config, "activation_function", "gelu_new"))
+        self._link()
+
+    def _links(self):
+        b = self.orig
+        at = b.attn.attention
+        H = self.nh * self.hd
+        return [(at.q_proj.weight, self.w_qkv[:H]), (at.k_proj.weight, self.w_qkv[H:2 * H]),
+                (at.v_proj.weight, self.w_qkv[2 * H:]), (at.out_proj.weight, self.w_o), (at.out_proj.bias, self.b_o),
+                (b.ln_1.weight, self.ln1_w), (b.ln_1.bias, self.ln1_b), (b.ln_2.weight, self.ln2_w),
+                (b.ln_2.bias, self.ln2_b), (b.mlp.c_fc.weight, self.w_fc), (b.mlp.c_fc.bias, self.b_fc),
+                (b.mlp.c_proj.weight, self.w_out), (b.mlp.c_proj.bias, self.b_out)]
+
+    def forward(self, hidden_states, layer_past=None, attention_mask=None, use_cache=False, output_attentions=False,
+                **kwargs):
+        if output_attentions:
+            return self._delegate(hidden_states, layer_past=layer_past, attention_mask=attention_mask,
+                                  use_cache=use_cache, output_attentions=output_attentions, **kwargs)
+        x = hidden_states
+        B, S, H = x.shape
+        y = layer_norm(x, self.ln1_w, self.ln1_b, self.eps1)
+        qkv = linear(y, self.w_qkv).view(B, S, 3, self.nh, self.hd)
+        q, k, v = (qkv[:, :, i].transpose(1, 2) for i in range(3))
+        if layer_past is not None:
+            k, v = layer_past.update(k, v, self.layer_idx)
+        scores = torch.matmul(q.float(), k.float().transpose(-1, -2))
+        o = _probs_context(scores, v, attention_mask, None, True, self.window, 1.0)
+        a = linear(o.transpose(1, 2).reshape(B, S, H), self.w_o, self.b_o)
+        h2, h = layer_norm(a, self.ln2_w, self.ln2_b, self.eps2, residual=x)
+        m = linear(bias_act(linear(h2, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
+        return h + m, None
+
+
 # layer class name -> fused layer constructor (reference containers/__init__.py policy list)
 POLICIES = {
     "BertLayer": FusedEncoderLayer,
@@ -517,6 +635,8 @@ POLICIES = {
     "OPTDecoderLayer": FusedOPTLayer,
     "GPTJBlock": FusedGPTJBlock,
     "TransformerBlock": FusedDistilBertBlock,  # DistilBERT
+    "BloomBlock": FusedBloomBlock,
+    "GPTNeoBlock": FusedGPTNeoBlock,
 }
 
 

@@ -236,14 +236,24 @@ def _decoder(arch, max_pos=64):
     if arch == "gptj":
         cfg = transformers.GPTJConfig(vocab_size=300, n_embd=64, n_layer=2, n_head=4, rotary_dim=8, n_positions=max_pos)
         return transformers.GPTJForCausalLM(cfg).eval()
+    if arch == "bloom":
+        cfg = transformers.BloomConfig(vocab_size=300, hidden_size=64, n_layer=2, n_head=4)
+        return transformers.BloomForCausalLM(cfg).eval()
+    if arch == "gptneo":
+        cfg = transformers.GPTNeoConfig(vocab_size=300, hidden_size=64, num_layers=2, num_heads=4,
+                                        attention_types=[[["global", "local"], 1]], window_size=4,
+                                        max_position_embeddings=max_pos)
+        return transformers.GPTNeoForCausalLM(cfg).eval()
     raise ValueError(arch)
 
 
-@pytest.mark.parametrize("arch", ["llama", "qwen2", "mistral", "opt", "gptj"])
+@pytest.mark.parametrize("arch", ["llama", "qwen2", "mistral", "opt", "gptj", "bloom", "gptneo"])
 def test_decoder_injection_logits_and_generate(arch):
-    """Llama / Qwen2 / Mistral (GQA, RoPE, SwiGLU), OPT (biased QKV, pre-LN, ReLU) and GPT-J (parallel
-    residual, interleaved partial rotary) injection: logits and greedy generation through the HF
-    cache match the original modules (reference module_inject/containers/{llama,llama2,opt,gptj}.py)."""
+    """Llama / Qwen2 / Mistral (GQA, RoPE, SwiGLU), OPT (biased QKV, pre-LN, ReLU), GPT-J (parallel
+    residual, interleaved partial rotary), BLOOM (ALiBi, head-interleaved QKV) and GPT-Neo (unscaled
+    scores, alternating global / local-window layers) injection: logits and greedy generation through
+    the HF cache match the original modules (reference module_inject/containers/{llama,llama2,opt,
+    gptj,bloom,gptneo}.py)."""
     model = _decoder(arch)
     ids = torch.randint(3, 300, (2, 10))
     with torch.no_grad():
@@ -275,7 +285,7 @@ def test_distilbert_injection_matches_hf():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("arch", ["llama", "opt", "gptj"])
+@pytest.mark.parametrize("arch", ["llama", "opt", "gptj", "bloom", "gptneo"])
 def test_decoder_injection_gpu_bf16(arch):
     """The new decoder policies on the MI355X in bf16 (HIP norm / GEMM / activation / flash kernels):
     logits close to the HF modules, greedy generation runs through the HF cache."""
