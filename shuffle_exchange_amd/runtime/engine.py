@@ -891,6 +891,17 @@ class SXEEngine(nn.Module):
         optim = os.path.join(d, f"{prefix}zero_pp_rank_{dp}_mp_rank_{mp:02d}_optim_states.pt")
         return d, model, optim
 
+    def _tp_partitions(self):
+        """AutoTP layers: {module name: split_dim / layout / full shape} (reference universal
+        checkpoint 'cat_dim' metadata, checkpoint/ds_to_universal.py)."""
+        from ..module_inject.layers import TensorParallelLinearBase
+        out = {}
+        for name, m in self.module.named_modules():
+            if isinstance(m, TensorParallelLinearBase) and m.tp_world_size > 1:
+                out[name] = {"split_dim": int(m.split_dim), "layout": m.layout, "full_shape": list(m.full_shape),
+                             "bias_split": bool(m.split_dim == 0 and m.bias is not None)}
+        return out
+
     def module_state_dict(self, exclude_frozen_parameters=False):
         if hasattr(self.optimizer, "wait_params"):
             self.optimizer.wait_params()
@@ -950,6 +961,9 @@ class SXEEngine(nn.Module):
                 ds_config=self._config._param_dict,
                 ds_version="sxe-0.1",
             )
+            tp_parts = self._tp_partitions()
+            if tp_parts:
+                state["tp_partitions"] = tp_parts  # checkpoint/reshape.py re-splits to another TP degree
             state.update(client_state)
             self.checkpoint_engine.save(state, model_path)
         if self.optimizer is not None:

@@ -96,3 +96,40 @@ def test_autotp_zero3_trains():
     ref = run_dist(_case_tp, 2, "llama", 2, 1, 3)
     for a, b in zip(res[0]["losses"], ref[0]["losses"]):
         assert a == pytest.approx(b, rel=1e-4)
+
+
+def _case_tp_save(rank, world, path):
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd.module_inject.auto_tp import gather_tp_state_dict
+    model, V = _model("llama")
+    ds = {"train_micro_batch_size_per_gpu": 2, "tensor_parallel": {"autotp_size": 2},
+          "zero_optimization": {"stage": 1}, "optimizer": {"type": "SGD", "params": {"lr": 0.2}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    b = torch.randint(0, V, (2, 16), generator=torch.Generator().manual_seed(3))
+    loss = eng(b, labels=b)
+    eng.backward(loss)
+    eng.step()
+    eng.save_checkpoint(path, tag="t")
+    return {k: v.cpu() for k, v in gather_tp_state_dict(eng.module).items()}
+
+
+def test_tp_checkpoint_reshape(tmp_path):
+    """AutoTP TP=2 checkpoint -> TP=1 (full weights equal the gathered TP model, incl. the packed
+    GQA q|k|v and gate|up layouts) -> TP=2 again (shards equal the original files)."""
+    from shuffle_exchange_amd.checkpoint.reshape import inspect_checkpoint, reshape_checkpoint, tp_full_state_dict
+    full = run_dist(_case_tp_save, 2, str(tmp_path / "tp2"))[0]
+    info = inspect_checkpoint(str(tmp_path / "tp2"))
+    assert info.tp_degree == 2 and len(info.model_files) == 2
+    sd1 = tp_full_state_dict(str(tmp_path / "tp2"))
+    for k, v in full.items():
+        assert torch.equal(sd1[k], v), k
+    model, _ = _model("llama")
+    model.load_state_dict(sd1)  # a plain single-GPU model loads the reshaped weights
+    reshape_checkpoint(str(tmp_path / "tp2"), str(tmp_path / "tp1"), new_tp=1)
+    reshape_checkpoint(str(tmp_path / "tp1"), str(tmp_path / "tp2b"), new_tp=2)
+    for r in range(2):
+        a = torch.load(tmp_path / "tp2" / "t" / f"mp_rank_{r:02d}_model_states.pt", weights_only=True)["module"]
+        b = torch.load(tmp_path / "tp2b" / "t" / f"mp_rank_{r:02d}_model_states.pt", weights_only=True)["module"]
+        assert a.keys() == b.keys()
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
