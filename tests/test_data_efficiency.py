@@ -1,5 +1,7 @@
 """data_efficiency engine wiring (reference runtime/engine.py:384-388, 698-741, 1954-1962, 2064-2065):
 curriculum data sampling from a per-sample difficulty metric and random layerwise token drop."""
+import os
+
 import numpy as np
 import torch
 
@@ -81,3 +83,70 @@ def test_curriculum_sampler_engine_wiring(tmp_path):
         thr = max(10 + int((step + 1) / 8 * 53), 4)
         assert max(both) <= max(thr, 3), (step, both, thr)
     assert max(res[0]["batches"][0] + res[1]["batches"][0]) <= 16
+
+
+class _Toks(torch.utils.data.Dataset):
+    def __init__(self, n=97):
+        g = torch.Generator().manual_seed(0)
+        self.items = [torch.randint(0, 16, (int(torch.randint(2, 20, (1,), generator=g)),), generator=g)
+                      for _ in range(n)]
+
+    def __len__(self):
+        return len(self.items)
+
+    def __getitem__(self, i):
+        return self.items[i]
+
+
+def _seqlen(x):
+    return len(x)
+
+
+def _vocab(x):
+    return np.bincount(x.numpy(), minlength=16)
+
+
+def _check_outputs(path, ds):
+    from shuffle_exchange_amd.runtime.data_pipeline.indexed_dataset import MMapIndexedDataset
+    lens = np.array([len(x) for x in ds.items])
+    s2m = MMapIndexedDataset(os.path.join(path, "seqlen", "seqlen_sample_to_metric"))[0]
+    assert np.array_equal(s2m, lens)
+    i2m = MMapIndexedDataset(os.path.join(path, "seqlen", "seqlen_index_to_metric"))[0]
+    assert np.array_equal(i2m, np.unique(lens))
+    i2s = MMapIndexedDataset(os.path.join(path, "seqlen", "seqlen_index_to_sample"))
+    for k, v in enumerate(i2m):
+        assert np.array_equal(np.sort(i2s[k]), np.nonzero(lens == v)[0])
+    pct = MMapIndexedDataset(os.path.join(path, "seqlen", "seqlen_index_to_sample_percentile_merged"))
+    assert sum(len(pct[k]) for k in range(len(pct))) == len(lens)
+    vocab = np.load(os.path.join(path, "vocab", "vocab_metric_value.npy"))
+    assert np.array_equal(vocab, np.bincount(torch.cat(ds.items).numpy(), minlength=16))
+
+
+def test_data_analyzer_map_reduce(tmp_path):
+    """Threaded map over 3 workers' shards + file reduce == brute force; outputs are indexed datasets."""
+    from shuffle_exchange_amd.runtime.data_pipeline import DataAnalyzer
+    ds = _Toks()
+    kw = dict(metric_functions=[_seqlen, _vocab], metric_names=["seqlen", "vocab"], save_path=str(tmp_path),
+              batch_size=8, num_workers=3, num_threads=2,
+              metric_types=["single_value_per_sample", "accumulate_value_over_samples"],
+              metric_dtypes=[np.int64, np.int64])
+    for w in range(3):
+        DataAnalyzer(ds, worker_id=w, **kw).run_map()
+    DataAnalyzer(ds, worker_id=0, **kw).run_reduce()
+    _check_outputs(str(tmp_path), ds)
+
+
+def _case_dist_analyzer(rank, world, path):
+    from shuffle_exchange_amd.runtime.data_pipeline import DistributedDataAnalyzer
+    ds = _Toks()
+    DistributedDataAnalyzer(ds, [_seqlen, _vocab], ["seqlen", "vocab"], path, batch_size=5,
+                            metric_types=["single_value_per_sample", "accumulate_value_over_samples"],
+                            metric_dtypes=[np.int64, np.int64]).run_map_reduce()
+    return True
+
+
+def test_distributed_data_analyzer(tmp_path):
+    """Collective map-reduce over 3 gloo ranks (distributed sample sort) == brute force."""
+    from .dist_utils import run_dist
+    run_dist(_case_dist_analyzer, 3, str(tmp_path))
+    _check_outputs(str(tmp_path), _Toks())
