@@ -7,7 +7,10 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from shuffle_exchange_amd.ops import native  # noqa: E402
 from shuffle_exchange_amd.ops.deepspeed4science import evoformer_attn as ea  # noqa: E402
+
+native.require_hip()
 
 
 def t(fn, n=5):
