@@ -412,9 +412,9 @@ class SXEConfig:
         for k, why in self.IGNORED_ZERO_KNOBS.items():
             if k in set_:
                 out.append((f"zero_optimization.{k}", why))
-        if self.model.sparse_gradients:
-            out.append(("sparse_gradients", "embedding gradients are reduced densely inside the flat units "
-                                            "(same numerics; one large collective instead of a sparse all-gather)"))
+        if self.model.sparse_gradients and zc.stage > 0:
+            out.append(("sparse_gradients", "under ZeRO stages 1-3 embedding gradients are reduced densely inside "
+                                            "the flat units (same numerics); the sparse all-gather runs at stage 0"))
         for k, why in out:
             logger.warning(f"config: '{k}' is accepted but has no effect: {why}")
         return out

@@ -489,6 +489,10 @@ class SXEEngine(nn.Module):
                 self.optimizer.attach_module(self.module)
         else:
             from .zero.stage0 import DataParallelOptimizer
+            if cfg.sparse_gradients:  # sparse embedding gradients: sparse all-gather (reference engine.py:2752)
+                for m in self.module.modules():
+                    if isinstance(m, torch.nn.Embedding) and m.sparse:
+                        m.weight._sxe_sparse = True
             self.optimizer = DataParallelOptimizer(
                 basic, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks, dp_group=dp_group,
                 bucket_size=zc.reduce_bucket_size, mp_group=mp_group, shuffle_exchange_cfg=se)

@@ -113,6 +113,8 @@ class FlatUnit:
         self.filled = [False] * len(self.params)
 
     def stage_grad(self, p, grad):
+        if grad.is_sparse:  # nn.Embedding(sparse=True) under ZeRO: reduced densely with its unit
+            grad = grad.to_dense()
         i = self.param_index[id(p)]
         if self.staging is None:
             self.staging = torch.empty(self.padded, dtype=self.staging_dtype or self.dtype, device=self.device)

@@ -6,6 +6,13 @@ Parameters are grouped into flat units of ``bucket_size`` elements (replicated, 
 gradient accumulator of a unit is all-reduced (``ReduceOp.AVG`` on RCCL) on a side HIP stream as
 soon as its last gradient arrives on the accumulation-boundary micro-step, then the fused optimizer
 updates fp32 masters and writes the bit16 weights in one pass.
+
+Sparse gradients (``sparse_gradients``: nn.Embedding(sparse=True) weights, marked by the engine;
+reference engine.py:2752-2823 ``sparse_allreduce``): each such weight is its own unit; its
+gradient stays a sparse (row index, row) tensor through the accumulation micro-steps, and at the
+boundary every rank all-gathers the touched rows (sizes first, then padded indices / rows) and
+scatter-adds them into the dense fp32 accumulator -- the dense all-reduce result at a fraction of
+the bytes when a step touches few rows of a large table.
 """
 import torch
 
@@ -39,13 +46,17 @@ class DataParallelOptimizer(ZeroOptimizerBase):
                 groups.create_expert_and_data_parallel(int(name.rsplit("_", 1)[-1]), name)
                 rgroup = groups.get_expert_data_parallel_group(name)
                 rsize = groups.get_expert_data_parallel_world_size(name)
-            if params:
-                for i, plist in enumerate(split_into_units(params, max(1, int(bucket_size)))):
-                    u = FlatUnit(plist, 1, 0, params[0].dtype, device, name=f"g{g}u{i}", index=i)
-                    u.rgroup, u.rsize = rgroup, rsize
-                    units.append(u)
-                    for p in plist:
-                        self.param_unit[p] = u
+            sparse = [p for p in params if getattr(p, "_sxe_sparse", False)]
+            dense = [p for p in params if not getattr(p, "_sxe_sparse", False)]
+            plists = (list(split_into_units(dense, max(1, int(bucket_size)))) if dense else []) + [[p] for p in sparse]
+            for i, plist in enumerate(plists):
+                u = FlatUnit(plist, 1, 0, plist[0].dtype, device, name=f"g{g}u{i}", index=i)
+                u.rgroup, u.rsize = rgroup, rsize
+                u.sparse = getattr(plist[0], "_sxe_sparse", False)
+                u.sparse_parts = []
+                units.append(u)
+                for p in plist:
+                    self.param_unit[p] = u
             self.units.append(units)
         self._init_master()
         # MoE: expert gradients differ across the expert-parallel group (each rank holds other
@@ -75,14 +86,21 @@ class DataParallelOptimizer(ZeroOptimizerBase):
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(u)))
         log_dist(f"DP (ZeRO-0): {sum(len(u) for u in self.units)} buckets over {self.dp_size} ranks", ranks=[0])
 
+    def _take_grad(self, u, i, p):
+        if u.sparse and p.grad.is_sparse:
+            u.sparse_parts.append(p.grad.coalesce())
+        else:
+            o, n = u.offsets[i], u.numels[i]
+            g = p.grad.to_dense() if p.grad.is_sparse else p.grad
+            u.grad[o:o + n].add_(g.reshape(-1))
+        p.grad = None
+
     def _make_hook(self, u):
         def hook(p):
             if p.grad is None or not self.boundary:
                 return
             i = u.param_index[id(p)]
-            o, n = u.offsets[i], u.numels[i]
-            u.grad[o:o + n].add_(p.grad.reshape(-1))
-            p.grad = None
+            self._take_grad(u, i, p)
             if not u.filled[i]:
                 u.filled[i] = True
                 u.pending -= 1
@@ -90,7 +108,44 @@ class DataParallelOptimizer(ZeroOptimizerBase):
                     self._allreduce_unit(u)
         return hook
 
+    def _sparse_allreduce_unit(self, u):
+        """All-gather the touched rows of a sparse-gradient unit and scatter-add them densely."""
+        p = u.params[0]
+        rows, width = p.shape[0], p.numel() // p.shape[0]
+        dense = u.grad[:u.numel].view(rows, width)
+        if u.sparse_parts:
+            g = torch.sparse_coo_tensor(torch.cat([t.indices() for t in u.sparse_parts], 1),
+                                        torch.cat([t.values() for t in u.sparse_parts], 0), p.shape).coalesce()
+            idx, val = g.indices()[0], g.values().reshape(-1, width).to(dense.dtype)
+        else:
+            idx = torch.zeros(0, dtype=torch.long, device=dense.device)
+            val = torch.zeros(0, width, dtype=dense.dtype, device=dense.device)
+        u.sparse_parts = []
+        if u.rsize == 1:
+            dense.index_add_(0, idx, val)
+            return
+        n = torch.tensor([idx.numel()], dtype=torch.long, device=dense.device)
+        ns = [torch.zeros_like(n) for _ in range(u.rsize)]
+        dist.all_gather(ns, n, group=u.rgroup)
+        ns = [int(x) for x in ns]
+        m = max(ns)
+        pi = torch.zeros(m, dtype=torch.long, device=dense.device)
+        pv = torch.zeros(m, width, dtype=dense.dtype, device=dense.device)
+        pi[:idx.numel()].copy_(idx)
+        pv[:idx.numel()].copy_(val)
+        ai = torch.empty(u.rsize * m, dtype=torch.long, device=dense.device)
+        av = torch.empty(u.rsize * m, width, dtype=dense.dtype, device=dense.device)
+        dist.all_gather_into_tensor(ai, pi, group=u.rgroup)
+        dist.all_gather_into_tensor(av.view(-1), pv.view(-1), group=u.rgroup)
+        keep = torch.cat([torch.arange(r * m, r * m + ns[r], device=dense.device) for r in range(u.rsize)])
+        dense.index_add_(0, ai[keep], av[keep])
+        dense.mul_(self.sp_scale / u.rsize)
+
     def _allreduce_unit(self, u):
+        if u.sparse and not u.reduced:
+            u.reduced = True
+            self._sparse_allreduce_unit(u)
+            return
         # 1-bit optimizers past their warm-up synchronise compressed momentum themselves
         if u.rsize == 1 or u.reduced or getattr(self.optimizer, "comm_active", False):
             u.reduced = True
@@ -122,9 +177,7 @@ class DataParallelOptimizer(ZeroOptimizerBase):
             for u in units:
                 for i, p in enumerate(u.params):
                     if p.grad is not None:
-                        o, n = u.offsets[i], u.numels[i]
-                        u.grad[o:o + n].add_(p.grad.reshape(-1))
-                        p.grad = None
+                        self._take_grad(u, i, p)
                 self._allreduce_unit(u)
 
     def step(self, closure=None):

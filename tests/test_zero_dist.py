@@ -277,3 +277,50 @@ def test_moe_zero0_clipping_keeps_dense_weights_in_sync():
     a, b = run_dist(C.case_mixtral_dense_sync, 2)
     for k in a:
         assert torch.allclose(a[k], b[k], atol=1e-6), k
+
+
+class _EmbNet(torch.nn.Module):
+    def __init__(self, sparse):
+        super().__init__()
+        torch.manual_seed(0)
+        self.emb = torch.nn.Embedding(1000, 16, sparse=sparse)
+        self.out = torch.nn.Linear(16, 4)
+
+    def forward(self, ids):
+        return self.out(self.emb(ids)).pow(2).mean()
+
+
+def _case_sparse(rank, world, sparse):
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd import comm as dist
+    model = _EmbNet(sparse)
+    ds = {"train_micro_batch_size_per_gpu": 4, "gradient_accumulation_steps": 2, "sparse_gradients": sparse,
+          "zero_optimization": {"stage": 0}, "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    calls = {"ag": 0}
+    orig = dist.all_gather_into_tensor
+
+    def ag(*a, **k):
+        calls["ag"] += 1
+        return orig(*a, **k)
+    dist.all_gather_into_tensor = ag
+    g = torch.Generator().manual_seed(5)
+    for _ in range(6):
+        ids = torch.randint(0, 50, (world * 4, 7), generator=g)[rank * 4:(rank + 1) * 4]  # few rows touched
+        loss = eng(ids)
+        eng.backward(loss)
+        eng.step()
+    dist.all_gather_into_tensor = orig
+    return {"params": [p.detach().clone() for p in eng.module.parameters()], "ag": calls["ag"]}
+
+
+def test_sparse_embedding_gradients_stage0():
+    """sparse_gradients with nn.Embedding(sparse=True): the touched rows are all-gathered (reference
+    engine.py sparse_allreduce) and training equals the dense-gradient run."""
+    sp = run_dist(_case_sparse, 2, True)
+    dn = run_dist(_case_sparse, 2, False)
+    assert sp[0]["ag"] > 0 and dn[0]["ag"] == 0
+    for a, b in zip(sp[0]["params"], dn[0]["params"]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    for a, b in zip(sp[0]["params"], sp[1]["params"]):
+        assert torch.equal(a, b)
