@@ -22,7 +22,7 @@ class CompileConfig:
     keep_int_input_tensors: bool = True
     keep_all_input_tensors: bool = False
     # schedule compiler (this framework)
-    passes: tuple = ("selective_gather", "prefetch", "offload_adam_states")
+    passes: tuple = ("selective_gather", "prefetch", "offload_adam_states", "offload_activation")
     memory_budget: Optional[float] = None   # bytes (> 1) or a fraction of device memory (<= 1); default 0.9
     profile_steps: int = 1                  # optimizer steps traced before the passes run
     prefetch_slack: float = 1.25            # gather-time safety factor when placing prefetches

@@ -1,5 +1,5 @@
 """Schedule passes over a traced ZeRO-3 micro-step (reference compile/passes/: zero3_compile.py,
-selective_gather.py, prefetch.py, offload_adam_states.py).
+selective_gather.py, prefetch.py, offload_adam_states.py, offload_activation.py).
 
 Each pass takes the ScheduleGraph, the plan built so far and the memory budget, and returns the
 plan. A plan is what stage3.ZeroStage3Optimizer.apply_compile_plan installs:
@@ -7,7 +7,8 @@ plan. A plan is what stage3.ZeroStage3Optimizer.apply_compile_plan installs:
              updated shards after each optimizer step) -- no per-micro-step all-gather;
   prefetch   {"fwd"|"bwd": {trigger fg: [fgs to start gathering there]}} -- each gather is issued
              far enough ahead to hide behind measured compute, as long as the bytes in flight fit;
-  offload_opt_states   park optimizer states on the host during forward/backward.
+  offload_opt_states   park optimizer states on the host during forward/backward;
+  offload_activation   keep saved activations in pinned host memory (autograd save_on_cpu).
 """
 
 
@@ -16,6 +17,7 @@ def zero3_schedule(g, plan, budget):
     plan.setdefault("keep", set())
     plan.setdefault("prefetch", {"fwd": {}, "bwd": {}})
     plan.setdefault("offload_opt_states", False)
+    plan.setdefault("offload_activation", False)
     plan.setdefault("log", [])
     return plan
 
@@ -83,5 +85,17 @@ def offload_adam_states(g, plan, budget):
     return plan
 
 
+def offload_activation(g, plan, budget):
+    """Keep activations saved for backward in pinned host memory when, even after the optimizer
+    states leave HBM (their traced bytes credited back), the traced peak exceeds the budget
+    (reference offload_activation.py)."""
+    over = -_headroom(g, plan, budget)
+    if plan.get("offload_opt_states"):
+        over -= g.meta.get("optimizer_bytes", 0)
+    plan["offload_activation"] = over > 0
+    plan["log"].append(f"offload_activation: {plan['offload_activation']}")
+    return plan
+
+
 PASSES = {"zero3_compile": zero3_schedule, "selective_gather": selective_gather, "prefetch": prefetch,
-          "offload_adam_states": offload_adam_states}
+          "offload_adam_states": offload_adam_states, "offload_activation": offload_activation}

@@ -108,4 +108,6 @@ class ScheduleTracer:
                 gm[fg.idx] = t
         persistent = sum(u.padded * u.flat.element_size() for fg in opt.fgroups for u in fg.units if u.persistent)
         dev = torch.cuda.get_device_properties(torch.cuda.current_device()).total_memory if self.cuda else 0
-        return ScheduleGraph(nodes, gb, gm, peak, dev, persistent, meta={"world": opt.S})
+        opt_bytes = sum(t.numel() * t.element_size() for st in getattr(getattr(opt, "optimizer", None), "state", {}).values()
+                        for t in st.values() if torch.is_tensor(t) and t.is_cuda)
+        return ScheduleGraph(nodes, gb, gm, peak, dev, persistent, meta={"world": opt.S, "optimizer_bytes": opt_bytes})

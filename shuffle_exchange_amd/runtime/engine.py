@@ -561,6 +561,11 @@ class SXEEngine(nn.Module):
         if self.fp16_enabled() and self._config.model.fp16.auto_cast:
             with torch.autocast(device_type=self.device.type, dtype=torch.float16):
                 out = self.module(*inputs, **kwargs)
+        elif getattr(self, "_offload_activations", False) and self.module.training and torch.is_grad_enabled():
+            # schedule-compiler plan (compile/passes.py offload_activation): tensors saved for
+            # backward go to pinned host memory during the forward and come back for the backward
+            with torch.autograd.graph.save_on_cpu(pin_memory=self.device.type == "cuda"):
+                out = self.module(*inputs, **kwargs)
         else:
             out = self.module(*inputs, **kwargs)
         if prof is not None:
@@ -754,6 +759,7 @@ class SXEEngine(nn.Module):
                 if self.compile_plan.get("offload_opt_states") and not getattr(self, "_offload_opt_states", False):
                     self._offload_opt_states = True
                     self.optimizer.offload_states(include=["optim_states"], non_blocking=True)
+                self._offload_activations = bool(self.compile_plan.get("offload_activation"))
         se = self.shuffle_exchange_config
         if se.enabled and se.auto_shuffle:
             self.shuffle_exchange()

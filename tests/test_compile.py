@@ -104,6 +104,7 @@ def _case(rank, world, compile_cfg, steps=4):
     if plan is not None:
         g = plan["graph"]
         out.update(keep=sorted(plan["keep"]), prefetch=plan["prefetch"], offload=plan["offload_opt_states"],
+                   offload_act=plan["offload_activation"],
                    n_groups=len(g.gather_bytes), nodes=[(n.phase, n.fg) for n in g.nodes],
                    gather_bytes=dict(g.gather_bytes), budget=plan["budget"], peak=g.peak_bytes)
     return out
@@ -122,7 +123,7 @@ def test_schedule_compiler_keeps_groups_and_preserves_numerics():
     assert len(r0["keep"]) == r0["n_groups"] > 0
     assert r0["gathers"][-1] < ref[0]["gathers"][-1]
     assert ("fwd", r0["nodes"][0][1]) == r0["nodes"][0] and any(p == "bwd" for p, _ in r0["nodes"])
-    assert r0["offload"] is False
+    assert r0["offload"] is False and r0["offload_act"] is False
 
 
 def test_schedule_compiler_tight_budget_prefetch_and_offload():
@@ -133,7 +134,7 @@ def test_schedule_compiler_tight_budget_prefetch_and_offload():
     for a, b in zip(ref, tight):
         assert a["losses"] == b["losses"]
     r0 = tight[0]
-    assert r0["keep"] == [] and r0["offload"] is True
+    assert r0["keep"] == [] and r0["offload"] is True and r0["offload_act"] is True
     scheduled = [j for ph in ("fwd", "bwd") for lst in r0["prefetch"][ph].values() for j in lst]
     assert scheduled, r0["prefetch"]
     assert r0["gathers"][-1] == ref[0]["gathers"][-1]
