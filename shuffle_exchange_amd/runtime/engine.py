@@ -478,7 +478,8 @@ class SXEEngine(nn.Module):
                 defer_reduce=zc.defer_reduce, retain_params=zc.retain_params, loco_param=zc.zeropp_loco_param,
                 prefetch_bucket_size=(zc.prefetch_bucket_size if "prefetch_bucket_size" in zc.model_fields_set
                                       and "prefetch_depth" not in zc.model_fields_set else None),
-                model_persistence_threshold=zc.model_persistence_threshold, param_swap=param_swap)
+                model_persistence_threshold=zc.model_persistence_threshold, param_swap=param_swap,
+                overlap_step=zc.overlap_step)
         elif stage in (1, 2):
             self.optimizer = ZeroStage12Optimizer(
                 basic, stage=stage, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks,

@@ -298,6 +298,8 @@ class ZeroOptimizerBase:
     def offload_states(self, include=None, device="cpu", pin_memory=True, non_blocking=False):
         """Move optimizer states / fp32 masters / grad accumulators (and ZeRO-3 bit16 shards) to the
         host to free HBM between phases (reference runtime/zero/offload_states.py:17-71)."""
+        if hasattr(self, "wait_params"):
+            self.wait_params()
         inc = set(include or ["optim_states", "hp_params", "lp_grads", "lp_params"])
         pin = pin_memory and torch.cuda.is_available()
 
@@ -344,6 +346,8 @@ class ZeroOptimizerBase:
             torch.cuda.synchronize()
 
     def reload_states(self, non_blocking=False):
+        if hasattr(self, "wait_params"):
+            self.wait_params()
         dev = self.device
         inc = getattr(self, "_offloaded", {}).get("include", set())
 

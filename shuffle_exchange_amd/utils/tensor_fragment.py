@@ -20,6 +20,8 @@ def _loc(param):
     loc = getattr(param, "_sxe_zero", None)
     if loc is None:
         raise ValueError("parameter is not managed by a ZeRO optimizer of this framework")
+    if hasattr(loc[0], "wait_params"):  # overlapped optimizer updates still in flight
+        loc[0].wait_params()
     return loc  # (optimizer, group index, unit, param index in unit)
 
 
