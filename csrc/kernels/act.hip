@@ -12,7 +12,7 @@
 
 namespace sxe {
 
-enum Act : int { ACT_IDENTITY = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_SILU = 3, ACT_GELU_ERF = 4 };
+enum Act : int { ACT_IDENTITY = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_SILU = 3, ACT_GELU_ERF = 4, ACT_QUICK_GELU = 5 };
 
 __device__ __forceinline__ float act_f(float x, int act) {
   switch (act) {
@@ -24,6 +24,7 @@ __device__ __forceinline__ float act_f(float x, int act) {
     }
     case ACT_SILU: return x / (1.f + __expf(-x));
     case ACT_GELU_ERF: return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+    case ACT_QUICK_GELU: return x / (1.f + __expf(-1.702f * x));  // CLIP
     default: return x;
   }
 }
@@ -44,6 +45,10 @@ __device__ __forceinline__ float act_df(float x, int act) {
     case ACT_GELU_ERF: {
       const float cdf = 0.5f * (1.f + erff(x * 0.7071067811865476f));
       return cdf + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+    }
+    case ACT_QUICK_GELU: {
+      const float sg = 1.f / (1.f + __expf(-1.702f * x));
+      return sg + 1.702f * x * sg * (1.f - sg);
     }
     default: return 1.f;
   }

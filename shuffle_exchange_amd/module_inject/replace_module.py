@@ -623,6 +623,54 @@ class FusedGPTNeoBlock(_Fused):
         return h + m, None
 
 
+class FusedCLIPEncoderLayer(_Fused):
+    """CLIP text / vision encoder layer (reference containers/clip.py ``HFCLIPLayerPolicy``): pre-LN,
+    packed biased QKV GEMM, flash attention (causal for the text tower, through ``is_causal`` or
+    its 4-D mask), out-proj + residual folded into LN2, bias + quick-GELU MLP (HIP kernel)."""
+
+    def __init__(self, layer, config):
+        super().__init__(layer)
+        at = layer.self_attn
+        self.nh, self.hd = at.num_heads, at.head_dim
+        self.scale = float(at.scale)
+        self.w_qkv = self._p(torch.cat([at.q_proj.weight, at.k_proj.weight, at.v_proj.weight]))
+        self.b_qkv = self._p(torch.cat([at.q_proj.bias, at.k_proj.bias, at.v_proj.bias]))
+        self.w_o, self.b_o = self._p(at.out_proj.weight), self._p(at.out_proj.bias)
+        l1, l2 = layer.layer_norm1, layer.layer_norm2
+        self.ln1_w, self.ln1_b, self.eps1 = self._p(l1.weight), self._p(l1.bias), l1.eps
+        self.ln2_w, self.ln2_b, self.eps2 = self._p(l2.weight), self._p(l2.bias), l2.eps
+        self.w_fc, self.b_fc = self._p(layer.mlp.fc1.weight), self._p(layer.mlp.fc1.bias)
+        self.w_out, self.b_out = self._p(layer.mlp.fc2.weight), self._p(layer.mlp.fc2.bias)
+        self.act = _act_name(getattr(getattr(layer.mlp, "config", config), "hidden_act", "quick_gelu"))
+        self._link()
+
+    def _links(self):
+        L = self.orig
+        at, H = L.self_attn, self.nh * self.hd
+        out = []
+        for i, lin in enumerate((at.q_proj, at.k_proj, at.v_proj)):
+            out += [(lin.weight, self.w_qkv[i * H:(i + 1) * H]), (lin.bias, self.b_qkv[i * H:(i + 1) * H])]
+        return out + [(at.out_proj.weight, self.w_o), (at.out_proj.bias, self.b_o),
+                      (L.layer_norm1.weight, self.ln1_w), (L.layer_norm1.bias, self.ln1_b),
+                      (L.layer_norm2.weight, self.ln2_w), (L.layer_norm2.bias, self.ln2_b),
+                      (L.mlp.fc1.weight, self.w_fc), (L.mlp.fc1.bias, self.b_fc),
+                      (L.mlp.fc2.weight, self.w_out), (L.mlp.fc2.bias, self.b_out)]
+
+    def forward(self, hidden_states, attention_mask=None, *args, **kwargs):
+        if kwargs.get("output_attentions") or args:
+            return self._delegate(hidden_states, attention_mask, *args, **kwargs)
+        x = hidden_states
+        B, S, H = x.shape
+        y = layer_norm(x, self.ln1_w, self.ln1_b, self.eps1)
+        qkv = linear(y, self.w_qkv, self.b_qkv).view(B, S, 3, self.nh, self.hd)
+        causal = bool(kwargs.get("is_causal", False)) and attention_mask is None
+        o = _attend(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], attention_mask, causal, self.scale)
+        a = linear(o.reshape(B, S, H), self.w_o, self.b_o)
+        h2, h = layer_norm(a, self.ln2_w, self.ln2_b, self.eps2, residual=x)
+        m = linear(bias_act(linear(h2, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
+        return h + m
+
+
 # layer class name -> fused layer constructor (reference containers/__init__.py policy list)
 POLICIES = {
     "BertLayer": FusedEncoderLayer,
@@ -637,6 +685,7 @@ POLICIES = {
     "TransformerBlock": FusedDistilBertBlock,  # DistilBERT
     "BloomBlock": FusedBloomBlock,
     "GPTNeoBlock": FusedGPTNeoBlock,
+    "CLIPEncoderLayer": FusedCLIPEncoderLayer,
 }
 
 

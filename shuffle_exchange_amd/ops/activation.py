@@ -8,7 +8,7 @@ import torch.nn.functional as F
 
 from . import native
 
-ACT = {"identity": 0, "relu": 1, "gelu": 2, "silu": 3, "gelu_exact": 4,
+ACT = {"identity": 0, "relu": 1, "gelu": 2, "silu": 3, "gelu_exact": 4, "quick_gelu": 5,
        # HF activation names
        "gelu_new": 2, "gelu_pytorch_tanh": 2, "gelu_fast": 2, "swish": 3}
 
@@ -22,6 +22,8 @@ def _act_ref(x, act):
         return F.silu(x)
     if act == 4:
         return F.gelu(x)
+    if act == 5:
+        return x * torch.sigmoid(1.702 * x)
     return x
 
 

@@ -302,3 +302,46 @@ def test_decoder_injection_gpu_bf16(arch):
     rel = ((got - ref).norm() / ref.norm()).item()
     assert rel < 3e-2, rel
     assert gen.shape == (2, 20)
+
+
+def _clip(kind, dev="cpu", dtype=torch.float32):
+    torch.manual_seed(0)
+    if kind == "text":
+        cfg = transformers.CLIPTextConfig(vocab_size=300, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                                          num_attention_heads=2, max_position_embeddings=64)
+        return transformers.CLIPTextModel(cfg).eval().to(dev, dtype), cfg
+    cfg = transformers.CLIPVisionConfig(hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                                        num_attention_heads=2, image_size=32, patch_size=8)
+    return transformers.CLIPVisionModel(cfg).eval().to(dev, dtype), cfg
+
+
+@pytest.mark.parametrize("kind", ["text", "vision"])
+def test_clip_injection_matches_hf(kind):
+    """CLIP text (causal) and vision towers (reference containers/clip.py): quick-GELU MLP, packed QKV."""
+    model, cfg = _clip(kind)
+    if kind == "text":
+        inp = {"input_ids": torch.randint(3, 300, (2, 12))}
+    else:
+        inp = {"pixel_values": torch.randn(2, 3, 32, 32)}
+    with torch.no_grad():
+        ref = model(**inp).last_hidden_state
+        n = replace_transformer_layer(model)
+        got = model(**inp).last_hidden_state
+    assert n == 2
+    torch.testing.assert_close(got, ref, atol=5e-5, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["text", "vision"])
+def test_clip_injection_gpu_bf16(kind):
+    from shuffle_exchange_amd.ops import native
+    native.require_hip()
+    model, cfg = _clip(kind, "cuda", torch.bfloat16)
+    inp = ({"input_ids": torch.randint(3, 300, (2, 40), device="cuda")} if kind == "text"
+           else {"pixel_values": torch.randn(2, 3, 32, 32, device="cuda", dtype=torch.bfloat16)})
+    with torch.no_grad():
+        ref = model(**inp).last_hidden_state.float()
+        assert replace_transformer_layer(model) == 2
+        got = model(**inp).last_hidden_state.float()
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel < 3e-2, rel
