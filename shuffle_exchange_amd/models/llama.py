@@ -7,7 +7,8 @@ hipBLASLt calls):
   rope_(qkv[:, :, :Hq+Hkv])            in place, no transposes               (ops/rope.py)
   o      = attention(q, k, v)          [B, S, H, D] strided views, GQA       (ops/attention.py)
   m, h2  = rmsnorm(o @ Wo^T + h)
-  out    = swiglu(m @ Wgu^T) @ Wd^T    ONE GEMM for gate|up                  (ops/activation.py)
+  out    = swiglu(m @ Wgu^T) @ Wd^T    ONE GEMM for gate|up; weight grads on  (ops/mlp.py)
+                                       token-minor copies the gated kernels write
   loss   = fused_linear_cross_entropy(final_norm(...), Wlm)                  (ops/cross_entropy.py)
 
 Reference counterparts: the inference-v2 Llama implementation
@@ -21,7 +22,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.activation import swiglu
+from ..ops.mlp import swiglu_mlp
 from ..runtime.activation_checkpointing.checkpointing import checkpoint
 from ..runtime.zero.partition_parameters import local_shard
 from ..ops.attention import attention_qkv_rope
@@ -141,7 +142,9 @@ class LlamaMLP(nn.Module):
         self.down_proj._tp_row_parallel = True
 
     def forward(self, x):
-        return self.down_proj(swiglu(self.gate_up_proj(x)))
+        # GPU training: one autograd node whose weight-gradient GEMMs run on token-minor operands
+        # written by the dual-layout gated kernels (ops/mlp.py); otherwise the module path
+        return swiglu_mlp(x, self.gate_up_proj, self.down_proj)
 
 
 class LlamaDecoderLayer(nn.Module):
