@@ -144,12 +144,13 @@ at::Tensor gated_act_bwd(at::Tensor dout, at::Tensor gu, int64_t act) {
 // written from LDS while the token-major tile is still in registers).
 //   fwd: out[t, j] = act(gu[t, j]) * gu[t, I + j]; outT[j, t] = out[t, j]
 //   bwd: dgu[t, j] = d * u * act'(g), dgu[t, I + j] = d * act(g); dguT = dgu^T   (d = dout[t, j])
-// Geometry: one 256-thread workgroup per 64-token x 64-column tile (transpose16's layout): thread
-// t loads row t/4, columns (t%4)*16 .. +16 as two 16-byte vectors per operand, and stores 16 tokens
-// of one output column as two 16-byte vectors of the transposed row. LDS rows are padded to 66
-// elements so the four row groups a wave reads together sit on distinct banks.
-constexpr int GT = 64, GLD = GT + 2;
-
+// Geometry (template TR tokens x TC columns per workgroup, TR*TC/16 threads): thread t loads
+// row t/(TC/16), 16 columns from (t%(TC/16))*16 as two 16-byte vectors per operand (TC*2-byte row
+// segments), and stores 16 tokens of one output column as two 16-byte vectors of the transposed
+// row (TR*2-byte segments). LDS rows are padded by 2 elements (an odd dword stride) so the
+// column-wise reads of a wave spread over the banks. The variant is
+// chosen per intermediate size by ops/mlp.py (64 x 256 where it divides: 5.0-5.2 TB/s vs 4.1 for
+// 64 x 64 at 16k tokens x 14336, profiles/act_layout_exp.log); the others remain for A/B.
 __device__ __forceinline__ void ld16(const unsigned short* p, float (&v)[16]) {
   const u16x8 a = *reinterpret_cast<const u16x8*>(p), b = *reinterpret_cast<const u16x8*>(p + 8);
 #pragma unroll
@@ -159,6 +160,7 @@ __device__ __forceinline__ void ld16(const unsigned short* p, float (&v)[16]) {
   }
 }
 
+// token-major store of 16 values + their copy into the LDS tile row (as 8 dword writes)
 __device__ __forceinline__ void st16(unsigned short* p, unsigned short* lds_row, const float (&v)[16]) {
   u16x8 a, b;
 #pragma unroll
@@ -168,50 +170,54 @@ __device__ __forceinline__ void st16(unsigned short* p, unsigned short* lds_row,
   }
   *reinterpret_cast<u16x8*>(p) = a;
   *reinterpret_cast<u16x8*>(p + 8) = b;
+  unsigned* l = reinterpret_cast<unsigned*>(lds_row);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    lds_row[j] = a[j];
-    lds_row[8 + j] = b[j];
+  for (int j = 0; j < 4; ++j) {
+    l[j] = (unsigned)a[2 * j] | ((unsigned)a[2 * j + 1] << 16);
+    l[4 + j] = (unsigned)b[2 * j] | ((unsigned)b[2 * j + 1] << 16);
   }
 }
 
-// transposed store of one LDS tile: output row = tile column t/4, 16 tokens from (t%4)*16
+// transposed store of one LDS tile: output row = tile column t/(TR/16), 16 tokens from
+// (t%(TR/16))*16
+template <int TR, int LD>
 __device__ __forceinline__ void st_t(const unsigned short* tile, unsigned short* dstT, int64_t T) {
-  const int t = threadIdx.x, oc = t >> 2, r0 = (t & 3) * 16;
+  const int t = threadIdx.x, oc = t / (TR / 16), r0 = (t % (TR / 16)) * 16;
   u16x8 o0, o1;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    o0[j] = tile[(r0 + j) * GLD + oc];
-    o1[j] = tile[(r0 + 8 + j) * GLD + oc];
+    o0[j] = tile[(r0 + j) * LD + oc];
+    o1[j] = tile[(r0 + 8 + j) * LD + oc];
   }
   unsigned short* d = dstT + (int64_t)oc * T + r0;
   *reinterpret_cast<u16x8*>(d) = o0;
   *reinterpret_cast<u16x8*>(d + 8) = o1;
 }
 
-template <bool BWD>
-__global__ void __launch_bounds__(256) gated_dual_kernel(const unsigned short* __restrict__ gu,
-                                                         const unsigned short* __restrict__ dout,
-                                                         unsigned short* __restrict__ out,
-                                                         unsigned short* __restrict__ outT, int64_t T, int I,
-                                                         int act) {
-  __shared__ unsigned short tile[2][GT * GLD];
-  const int tiles_c = I / GT;
+template <bool BWD, int TR, int TC>
+__global__ void __launch_bounds__(TR * TC / 16) gated_dual_kernel(const unsigned short* __restrict__ gu,
+                                                                  const unsigned short* __restrict__ dout,
+                                                                  unsigned short* __restrict__ out,
+                                                                  unsigned short* __restrict__ outT, int64_t T,
+                                                                  int I, int act) {
+  constexpr int LD = TC + 2;
+  __shared__ __attribute__((aligned(16))) unsigned short tile[BWD ? 2 : 1][TR * LD];
+  const int tiles_c = I / TC;
   const int64_t tr = blockIdx.x / tiles_c;
   const int tc = (int)(blockIdx.x - tr * tiles_c);
-  const int t = threadIdx.x, r = t >> 2, c0 = (t & 3) * 16;
-  const int64_t row = tr * GT + r;
-  const int col = tc * GT + c0;
+  const int t = threadIdx.x, r = t / (TC / 16), c0 = (t % (TC / 16)) * 16;
+  const int64_t row = tr * TR + r;
+  const int col = tc * TC + c0;
   float g[16], u[16];
   ld16(gu + row * 2 * I + col, g);
   ld16(gu + row * 2 * I + I + col, u);
-  if (!BWD) {
+  if constexpr (!BWD) {
     float o[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) o[j] = act_f(g[j], act) * u[j];
-    st16(out + row * I + col, &tile[0][r * GLD + c0], o);
+    st16(out + row * I + col, &tile[0][r * LD + c0], o);
     __syncthreads();
-    st_t(tile[0], outT + (int64_t)(tc * GT) * T + tr * GT, T);
+    st_t<TR, LD>(tile[0], outT + (int64_t)(tc * TC) * T + tr * TR, T);
   } else {
     float d[16], dg[16], du[16];
     ld16(dout + row * I + col, d);
@@ -220,60 +226,84 @@ __global__ void __launch_bounds__(256) gated_dual_kernel(const unsigned short* _
       du[j] = d[j] * act_f(g[j], act);
       dg[j] = d[j] * u[j] * act_df(g[j], act);
     }
-    st16(out + row * 2 * I + col, &tile[0][r * GLD + c0], dg);
-    st16(out + row * 2 * I + I + col, &tile[1][r * GLD + c0], du);
+    st16(out + row * 2 * I + col, &tile[0][r * LD + c0], dg);
+    st16(out + row * 2 * I + I + col, &tile[1][r * LD + c0], du);
     __syncthreads();
-    st_t(tile[0], outT + (int64_t)(tc * GT) * T + tr * GT, T);
-    st_t(tile[1], outT + (int64_t)(I + tc * GT) * T + tr * GT, T);
+    st_t<TR, LD>(tile[0], outT + (int64_t)(tc * TC) * T + tr * TR, T);
+    st_t<TR, LD>(tile[1], outT + (int64_t)(I + tc * TC) * T + tr * TR, T);
   }
 }
 
-static void check_dual(const at::Tensor& gu, int64_t& T, int& I) {
+// variant -> (TR, TC): 0 = 64 x 64, 1 = 64 x 128, 2 = 128 x 64, 3 = 128 x 128, 4 = 64 x 256
+static void dual_tile(int64_t variant, int& TR, int& TC) {
+  SXE_CHECK(variant >= 0 && variant <= 4, "gated dual: variant must be 0..4");
+  TR = (variant == 2 || variant == 3) ? 128 : 64;
+  TC = variant == 4 ? 256 : (variant & 1) ? 128 : 64;
+}
+
+static void check_dual(const at::Tensor& gu, int TR, int TC, int64_t& T, int& I) {
   SXE_CHECK_CUDA(gu);
   SXE_CHECK(gu.is_contiguous() && gu.scalar_type() == at::kBFloat16, "gated dual: contiguous bf16 gate|up");
   const int64_t two_i = gu.size(-1);
   I = (int)(two_i / 2);
   T = gu.numel() / two_i;
-  SXE_CHECK(T % GT == 0 && I % GT == 0, "gated dual: tokens and intermediate size must be multiples of 64");
-  SXE_CHECK((T / GT) * (I / GT) < (1ll << 31), "gated dual: too many tiles");
+  SXE_CHECK(T % TR == 0 && I % TC == 0, "gated dual: tokens / intermediate size must be multiples of the tile (",
+            TR, " x ", TC, ")");
+  SXE_CHECK((T / TR) * (I / TC) < (1ll << 31), "gated dual: too many tiles");
+}
+
+template <bool BWD>
+static void launch_dual(int TR, int TC, const unsigned short* gu, const unsigned short* dout, unsigned short* out,
+                        unsigned short* outT, int64_t T, int I, int act) {
+  const dim3 grid((unsigned)((T / TR) * (I / TC)));
+  hipStream_t s = cur_stream();
+  if (TR == 64 && TC == 64)
+    hipLaunchKernelGGL((gated_dual_kernel<BWD, 64, 64>), grid, dim3(256), 0, s, gu, dout, out, outT, T, I, act);
+  else if (TR == 64 && TC == 256)
+    hipLaunchKernelGGL((gated_dual_kernel<BWD, 64, 256>), grid, dim3(1024), 0, s, gu, dout, out, outT, T, I, act);
+  else if (TR == 64)
+    hipLaunchKernelGGL((gated_dual_kernel<BWD, 64, 128>), grid, dim3(512), 0, s, gu, dout, out, outT, T, I, act);
+  else if (TC == 64)
+    hipLaunchKernelGGL((gated_dual_kernel<BWD, 128, 64>), grid, dim3(512), 0, s, gu, dout, out, outT, T, I, act);
+  else
+    hipLaunchKernelGGL((gated_dual_kernel<BWD, 128, 128>), grid, dim3(1024), 0, s, gu, dout, out, outT, T, I, act);
+  SXE_LAUNCH_CHECK();
 }
 
 // -> (out [..., I], outT [I, T])
-std::tuple<at::Tensor, at::Tensor> gated_act_fwd_dual(at::Tensor gu, int64_t act) {
+std::tuple<at::Tensor, at::Tensor> gated_act_fwd_dual(at::Tensor gu, int64_t act, int64_t variant) {
+  int TR, TC, I;
   int64_t T;
-  int I;
-  check_dual(gu, T, I);
+  dual_tile(variant, TR, TC);
+  check_dual(gu, TR, TC, T, I);
   c10::DeviceGuard guard(gu.device());
   auto sizes = gu.sizes().vec();
   sizes.back() = I;
   auto out = at::empty(sizes, gu.options());
   auto outT = at::empty({I, T}, gu.options());
   if (T == 0) return {out, outT};
-  hipLaunchKernelGGL(gated_dual_kernel<false>, dim3((unsigned)((T / GT) * (I / GT))), dim3(256), 0, cur_stream(),
-                     reinterpret_cast<const unsigned short*>(gu.data_ptr()), nullptr,
+  launch_dual<false>(TR, TC, reinterpret_cast<const unsigned short*>(gu.data_ptr()), nullptr,
                      reinterpret_cast<unsigned short*>(out.data_ptr()), reinterpret_cast<unsigned short*>(outT.data_ptr()),
                      T, I, (int)act);
-  SXE_LAUNCH_CHECK();
   return {out, outT};
 }
 
 // -> (dgu [..., 2I], dguT [2I, T])
-std::tuple<at::Tensor, at::Tensor> gated_act_bwd_dual(at::Tensor dout, at::Tensor gu, int64_t act) {
+std::tuple<at::Tensor, at::Tensor> gated_act_bwd_dual(at::Tensor dout, at::Tensor gu, int64_t act, int64_t variant) {
+  int TR, TC, I;
   int64_t T;
-  int I;
-  check_dual(gu, T, I);
+  dual_tile(variant, TR, TC);
+  check_dual(gu, TR, TC, T, I);
   SXE_CHECK(dout.is_contiguous() && dout.scalar_type() == at::kBFloat16 && dout.numel() == T * I,
             "gated dual bwd: dout shape");
   c10::DeviceGuard guard(gu.device());
   auto dgu = at::empty_like(gu);
   auto dguT = at::empty({2 * (int64_t)I, T}, gu.options());
   if (T == 0) return {dgu, dguT};
-  hipLaunchKernelGGL(gated_dual_kernel<true>, dim3((unsigned)((T / GT) * (I / GT))), dim3(256), 0, cur_stream(),
-                     reinterpret_cast<const unsigned short*>(gu.data_ptr()),
-                     reinterpret_cast<const unsigned short*>(dout.data_ptr()),
-                     reinterpret_cast<unsigned short*>(dgu.data_ptr()), reinterpret_cast<unsigned short*>(dguT.data_ptr()),
-                     T, I, (int)act);
-  SXE_LAUNCH_CHECK();
+  launch_dual<true>(TR, TC, reinterpret_cast<const unsigned short*>(gu.data_ptr()),
+                    reinterpret_cast<const unsigned short*>(dout.data_ptr()),
+                    reinterpret_cast<unsigned short*>(dgu.data_ptr()), reinterpret_cast<unsigned short*>(dguT.data_ptr()),
+                    T, I, (int)act);
   return {dgu, dguT};
 }
 
@@ -370,8 +400,8 @@ TORCH_LIBRARY_FRAGMENT(sxe, m) {
   m.def("gated_act_bwd(Tensor dout, Tensor gu, int act) -> Tensor");
   m.def("bias_act_fwd(Tensor x, Tensor? bias, int act) -> Tensor");
   m.def("bias_act_bwd(Tensor dy, Tensor x, Tensor? bias, int act) -> Tensor");
-  m.def("gated_act_fwd_dual(Tensor gu, int act) -> (Tensor, Tensor)");
-  m.def("gated_act_bwd_dual(Tensor dout, Tensor gu, int act) -> (Tensor, Tensor)");
+  m.def("gated_act_fwd_dual(Tensor gu, int act, int variant=0) -> (Tensor, Tensor)");
+  m.def("gated_act_bwd_dual(Tensor dout, Tensor gu, int act, int variant=0) -> (Tensor, Tensor)");
 }
 TORCH_LIBRARY_IMPL(sxe, CUDA, m) {
   m.impl("gated_act_fwd_dual", &sxe::gated_act_fwd_dual);

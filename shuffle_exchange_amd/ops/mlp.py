@@ -34,6 +34,13 @@ ACT_SILU = 3
 ENABLED = os.environ.get("SXE_MLP_TN", "1") == "1"
 
 
+def dual_variant(inter):
+    """Tile of the dual-layout gated kernels: 64 tokens x 256 columns where the intermediate size
+    allows (5.0-5.2 TB/s at 16k tokens x 14336 vs 4.1 TB/s for 64 x 64 tiles, profiles/act_layout_exp.log),
+    else 64 x 128, else 64 x 64."""
+    return 4 if inter % 256 == 0 else 1 if inter % 128 == 0 else 0
+
+
 def weight_grad_tn(w, gyT, xT):
     """dW = gyT @ xT^T (gyT [N, T], xT [K, T], both token-minor): written into the optimizer's
     target for ``w`` when it has one (returns None), else returned."""
@@ -56,12 +63,13 @@ class _SwiGLUMLP(torch.autograd.Function):
     def forward(ctx, x, wgu, wd):
         x2 = x.reshape(-1, x.shape[-1])
         gu = F.linear(x2, wgu)
-        h, hT = torch.ops.sxe.gated_act_fwd_dual(gu, ACT_SILU)
+        v = dual_variant(wd.shape[1])
+        h, hT = torch.ops.sxe.gated_act_fwd_dual(gu, ACT_SILU, v)
         out = F.linear(h, wd)
         del h
         xT = torch.ops.sxe.transpose16(x2) if ctx.needs_input_grad[1] else None
         ctx.save_for_backward(xT, gu, hT, wgu, wd)
-        ctx.x_shape = x.shape
+        ctx.x_shape, ctx.variant = x.shape, v
         return out.view(*x.shape[:-1], wd.shape[0])
 
     @staticmethod
@@ -73,7 +81,7 @@ class _SwiGLUMLP(torch.autograd.Function):
         if ctx.needs_input_grad[2]:
             dwd = weight_grad_tn(wd, torch.ops.sxe.transpose16(d2), hT)
         del hT
-        dgu, dguT = torch.ops.sxe.gated_act_bwd_dual(dh, gu, ACT_SILU)
+        dgu, dguT = torch.ops.sxe.gated_act_bwd_dual(dh, gu, ACT_SILU, ctx.variant)
         del dh
         if ctx.needs_input_grad[0]:
             dx = data_grad(dgu, wgu).view(ctx.x_shape)

@@ -26,19 +26,20 @@ def test_cpu_falls_back_to_module_path():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("T,I", [(128, 256), (2048, 1408)])
-def test_dual_gated_kernels_vs_fp32(T, I):
+@pytest.mark.parametrize("T,I", [(128, 256), (2048, 1536)])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+def test_dual_gated_kernels_vs_fp32(T, I, variant):
     from shuffle_exchange_amd.ops import native
     native.require_hip()
     torch.manual_seed(0)
     gu = torch.randn(T, 2 * I, device="cuda", dtype=torch.bfloat16)
     d = torch.randn(T, I, device="cuda", dtype=torch.bfloat16)
-    h, hT = torch.ops.sxe.gated_act_fwd_dual(gu, 3)
+    h, hT = torch.ops.sxe.gated_act_fwd_dual(gu, 3, variant)
     g, u = gu.float().chunk(2, -1)
     ref = F.silu(g) * u
     assert _rel(h, ref) < 5e-3
     assert torch.equal(hT, h.t())
-    dgu, dguT = torch.ops.sxe.gated_act_bwd_dual(d, gu, 3)
+    dgu, dguT = torch.ops.sxe.gated_act_bwd_dual(d, gu, 3, variant)
     s = torch.sigmoid(g)
     ref_dg = d.float() * u * s * (1 + g * (1 - s))
     ref_du = d.float() * F.silu(g)

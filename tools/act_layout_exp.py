@@ -60,6 +60,13 @@ gu, d = bf(T, 28672), bf(T, 14336)
 g1 = t(lambda: torch.ops.sxe.gated_act_fwd(gu, 3))
 g2 = t(lambda: torch.ops.sxe.gated_act_bwd(d, gu, 3))
 tr = t(lambda: torch.ops.sxe.transpose16(gu))
-print(f"[gated] fwd {g1:.3f} ms ({3 * T * 14336 * 2 / g1 / 1e9:.0f} GB/s) | bwd {g2:.3f} ms "
-      f"({5 * T * 14336 * 2 / g2 / 1e9:.0f} GB/s) | transpose16 of gu {tr:.3f} ms "
-      f"({2 * T * 28672 * 2 / tr / 1e9:.0f} GB/s)", flush=True)
+print(f"[gated] fwd {g1:.3f} ms ({3 * T * 14336 * 2 / g1 / 1e9:.2f} TB/s) | bwd {g2:.3f} ms "
+      f"({5 * T * 14336 * 2 / g2 / 1e9:.2f} TB/s) | transpose16 of gu {tr:.3f} ms "
+      f"({2 * T * 28672 * 2 / tr / 1e9:.2f} TB/s)", flush=True)
+
+# dual-layout kernels (token-major + token-minor outputs), per tile variant
+for v, name in enumerate(["64x64", "64x128", "128x64", "128x128", "64x256"]):
+    f = t(lambda: torch.ops.sxe.gated_act_fwd_dual(gu, 3, v))
+    b = t(lambda: torch.ops.sxe.gated_act_bwd_dual(d, gu, 3, v))
+    print(f"[gated dual {name}] fwd {f:.3f} ms ({4 * T * 14336 * 2 / f / 1e9:.2f} TB/s) | bwd {b:.3f} ms "
+          f"({7 * T * 14336 * 2 / b / 1e9:.2f} TB/s)", flush=True)
