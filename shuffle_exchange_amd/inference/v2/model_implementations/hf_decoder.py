@@ -376,6 +376,13 @@ def ragged_attention(qkv, kv_layer, batch, nq, nkv, D, scale, window=None):
     return out
 
 
+# Measured on MI355X (tools/grouped_gemm_bench.py, profiles/grouped_gemm_bench.log): the grouped
+# kernel wins with many experts / few rows each (Qwen-MoE 60 experts x 273 rows: 0.47 vs 1.33 ms;
+# Mixtral decode 16 rows/expert: 0.39 vs 0.50 ms) and loses to per-expert hipBLASLt at 1024 rows
+# per expert (Mixtral prefill gate_up: 3.99 vs 1.77 ms).
+GROUPED_MAX_ROWS_PER_EXPERT = 512
+
+
 def dropless_moe(x, router_w, e_gu, e_down, top_k, norm_topk, act="silu"):
     """Exact top-k routing (no capacity): group rows by expert with one argsort, one GEMM pair per
     expert that received rows, weighted scatter-add back (reference ragged_ops top_k_gating +
@@ -387,6 +394,18 @@ def dropless_moe(x, router_w, e_gu, e_down, top_k, norm_topk, act="silu"):
     flat = topi.reshape(-1)
     order = torch.argsort(flat, stable=True)
     tok = order // top_k
+    from ....ops.moe import expert_offsets, grouped_gemm, grouped_gemm_ok
+    E = e_gu.shape[0]
+    if (grouped_gemm_ok(x, e_gu) and grouped_gemm_ok(x, e_down.transpose(1, 2))
+            and flat.numel() <= GROUPED_MAX_ROWS_PER_EXPERT * E):
+        # one ragged grouped-GEMM launch per projection (grouped_gemm.hip), routing weight fused
+        # into the down projection's epilogue, offsets kept on the device: no host sync. Large
+        # per-expert row counts keep hipBLASLt's per-expert GEMMs (faster there; see below).
+        offs = expert_offsets(flat, E)
+        xs = x.index_select(0, tok)
+        ws = topw.reshape(-1).index_select(0, order).float()
+        h = gated_act(grouped_gemm(xs, e_gu, offs), act)
+        return torch.zeros_like(x).index_add_(0, tok, grouped_gemm(h, e_down, offs, ws))
     counts = torch.bincount(flat, minlength=e_gu.shape[0]).tolist()
     xs = x.index_select(0, tok)
     ws = topw.reshape(-1).index_select(0, order).to(x.dtype).unsqueeze(1)

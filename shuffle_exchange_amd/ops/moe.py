@@ -104,3 +104,40 @@ def combine(expert_out, slots, slot_src, w):
     rows = expert_out.index_select(0, idx).view(S, k, -1)
     ww = (w.float() * (slots >= 0)).to(rows.dtype).unsqueeze(-1)
     return (rows * ww).sum(1)
+
+
+# ------------------------------------------------------------------------------ grouped expert GEMM
+def expert_offsets(flat_expert, num_experts):
+    """int32 [E + 1] cumulative row offsets of expert-sorted rows, computed on the device without a
+    host synchronisation (torch.bincount on the GPU reads the max back to the host)."""
+    counts = torch.zeros(num_experts, dtype=torch.int32, device=flat_expert.device)
+    counts.index_add_(0, flat_expert, torch.ones_like(flat_expert, dtype=torch.int32))
+    offs = torch.zeros(num_experts + 1, dtype=torch.int32, device=flat_expert.device)
+    torch.cumsum(counts, 0, out=offs[1:])
+    return offs
+
+
+def grouped_gemm_ok(x, w):
+    return (_hip(x) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 2 and w.dim() == 3
+            and w.is_cuda and w.shape[2] == x.shape[1] and x.shape[1] % 128 == 0 and w.shape[1] % 128 == 0)
+
+
+def grouped_gemm(x, w, offsets, row_scale=None):
+    """y[r] = row_scale[r] * x[r] @ w[e]^T for expert-sorted rows x [R, K], per-expert weights
+    w [E, N, K] (nn.Linear layout) and device offsets [E + 1] (``expert_offsets``): ONE launch of
+    the ragged MFMA kernel (csrc/kernels/grouped_gemm.hip; reference cutlass_ops/moe_gemm), no host
+    sync. CPU / unsupported shapes: a per-expert loop (reads the offsets on the host)."""
+    if grouped_gemm_ok(x, w):
+        rs = None if row_scale is None else row_scale.reshape(-1).contiguous()
+        if rs is not None and rs.dtype not in (torch.float32, torch.bfloat16):
+            rs = rs.float()
+        return torch.ops.sxe.grouped_gemm(x.contiguous(), w.contiguous(), offsets.to(torch.int32).contiguous(), rs)
+    y = x.new_empty(x.shape[0], w.shape[1])
+    off = offsets.tolist()
+    for e in range(w.shape[0]):
+        a, b = off[e], off[e + 1]
+        if b > a:
+            y[a:b] = F.linear(x[a:b], w[e])
+    if row_scale is not None:
+        y = (y.float() * row_scale.reshape(-1, 1).float()).to(x.dtype)
+    return y
