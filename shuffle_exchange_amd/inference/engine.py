@@ -114,7 +114,11 @@ class InferenceEngine(torch.nn.Module):
                 # first generate) reads the HF tensors as they were before injection.
                 self._ragged_src = _HFWeights.of(model)
                 from ..module_inject.replace_module import replace_transformer_layer
+                from ..module_inject.diffusers import generic_injection
                 self.injected_layers = replace_transformer_layer(model)
+                # diffusers-style attention (UNet / VAE / transformer blocks; reference
+                # generic_injection): fused packed-projection attention modules
+                self.injected_layers += generic_injection(model)
         self.device = dev
         self._graphs = {}
         self._ragged = None
