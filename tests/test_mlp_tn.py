@@ -167,3 +167,31 @@ def test_transposed_weight_cache_bitwise(monkeypatch):
     p0, _ = run(False)
     assert max(hits) >= 2 and lin.WT_CACHE["entries"] == {}
     assert all(torch.equal(a, b) for a, b in zip(p0, p1))
+
+
+@pytest.mark.gpu
+def test_grouped_swiglu_experts_fused_vs_grouped_mm(monkeypatch):
+    """MoE experts (moe/experts.py GroupedSwiGLUExperts): the fused path with token-minor
+    weight-gradient operands equals the per-expert grouped_mm + SwiGLU path in output and grads."""
+    from shuffle_exchange_amd.moe.experts import GroupedSwiGLUExperts
+    from shuffle_exchange_amd.ops import native
+    native.require_hip()
+    torch.manual_seed(0)
+    E, C, H, I = 4, 320, 256, 512
+    ex = GroupedSwiGLUExperts(H, I, E).cuda().bfloat16()
+    x = torch.randn(E, C, H, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    dy = torch.randn(E, C, H, device="cuda", dtype=torch.bfloat16)
+
+    from shuffle_exchange_amd.moe import experts as experts_mod
+
+    def run(enabled):
+        monkeypatch.setattr(experts_mod, "MOE_TN", enabled)
+        for t in (x, ex.w_gate_up, ex.w_down):
+            t.grad = None
+        y = ex(x)
+        y.backward(dy)
+        return y.detach().float(), x.grad.float(), ex.w_gate_up.grad.float(), ex.w_down.grad.float()
+
+    fused, ref = run(True), run(False)
+    for a, b in zip(fused, ref):
+        assert _rel(a, b) < 1e-2, _rel(a, b)
