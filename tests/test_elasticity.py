@@ -1,27 +1,75 @@
-"""Elastic batch-size selection: every reported GPU count divides the batch with a listed micro
-batch; incompatible world sizes are rejected; micro batch returned for a given world size."""
+"""Elastic batch-size selection (elasticity/elasticity.py) pinned to hand-derived results of the
+reference algorithm (deepspeed/elasticity/elasticity.py): highly-composite-number candidates per
+micro batch and per lcm, most valid GPU counts wins, v0.2 node-level search."""
 import pytest
 
+from shuffle_exchange_amd.elasticity import (ElasticityConfigError, ElasticityIncompatibleWorldSize,
+                                             compute_elastic_config)
+from shuffle_exchange_amd.elasticity.elasticity import candidate_batch_sizes, valid_gpus
 
-def test_compute_elastic_config():
-    from shuffle_exchange_amd.elasticity import ElasticityIncompatibleWorldSize, compute_elastic_config
-    cfg = {"elasticity": {"enabled": True, "max_train_batch_size": 2000, "micro_batch_sizes": [2, 4, 6],
-                          "min_gpus": 1, "max_gpus": 64, "version": 0.1}}
-    batch, gpus = compute_elastic_config(cfg)
-    assert batch <= 2000 and len(gpus) > 10
+
+def _cfg(**kw):
+    el = {"enabled": True, "max_train_batch_size": 2000, "micro_batch_sizes": [2, 4, 6], "min_gpus": 1,
+          "max_gpus": 10000, "version": 0.1}
+    el.update(kw)
+    return {"elasticity": el}
+
+
+def _divisors(n):
+    return [d for d in range(1, n + 1) if n % d == 0]
+
+
+def test_v01_candidates_and_choice():
+    # bases 2, 4, 6 and lcm 12 scaled by the largest HCN <= 2000 // base: 840*2, 360*4, 240*6, 120*12
+    assert candidate_batch_sizes([2, 4, 6], 2000) == [1440, 1680]
+    # 1440 is valid for the 30 divisors of 720, 1680 for the 32 divisors of 840
+    assert valid_gpus(1440, [2, 4, 6], 1, 10000) == _divisors(720)
+    batch, gpus = compute_elastic_config(_cfg())
+    assert batch == 1680 and gpus == _divisors(840)
     for g in gpus:
         assert batch % g == 0 and any((batch // g) % m == 0 for m in (2, 4, 6))
-    b2, g2, mb = compute_elastic_config(cfg, world_size=gpus[-1], return_microbatch=True)
-    assert b2 == batch and (batch // gpus[-1]) % mb == 0
-    bad = next(g for g in range(1, 65) if g not in gpus)
+
+
+def test_v01_world_size_micro_batch_and_rejection():
+    b, gpus, mb = compute_elastic_config(_cfg(), world_size=7)
+    assert (b, mb) == (1680, 6)  # 1680 // 7 = 240: the largest listed micro batch dividing it
+    b, gpus, mb = compute_elastic_config(_cfg(), world_size=42)
+    assert mb == 4  # 1680 // 42 = 40
     with pytest.raises(ElasticityIncompatibleWorldSize):
-        compute_elastic_config(cfg, world_size=bad)
+        compute_elastic_config(_cfg(), world_size=9)
 
 
-def test_elastic_model_parallel():
-    from shuffle_exchange_amd.elasticity import compute_elastic_config
-    cfg = {"elasticity": {"enabled": True, "max_train_batch_size": 1024, "micro_batch_sizes": [1, 2, 4],
-                          "min_gpus": 8, "max_gpus": 64, "model_parallel_size": 8, "num_gpus_per_node": 8,
-                          "version": 0.2}}
-    batch, gpus = compute_elastic_config(cfg)
-    assert all(g % 8 == 0 for g in gpus)
+def test_v01_gpu_range_and_cap():
+    # in [100, 500]: 1440 has 5 valid counts (divisors of 720), 1680 has 7 (divisors of 840)
+    b, gpus = compute_elastic_config(_cfg(min_gpus=100, max_gpus=500))
+    assert b == 1680 and gpus == [105, 120, 140, 168, 210, 280, 420]
+    # a micro batch at the cap is its own candidate
+    assert candidate_batch_sizes([64], 64) == [64]
+    with pytest.raises(ElasticityConfigError):
+        compute_elastic_config(_cfg(micro_batch_sizes=[4096]))
+    with pytest.raises(ElasticityConfigError):
+        compute_elastic_config(_cfg(model_parallel_size=2))  # model parallel needs v0.2
+    with pytest.raises(ElasticityConfigError):
+        compute_elastic_config(_cfg(enabled=False))
+
+
+def test_v02_node_level_search():
+    cfg = _cfg(max_train_batch_size=1024, micro_batch_sizes=[2, 4], min_gpus=8, max_gpus=64,
+               model_parallel_size=2, num_gpus_per_node=8, version=0.2)
+    # per node: 4 data-parallel ranks, batch cap 1024 / 4 = 256 -> candidates 120*2 = 60*4 = 240,
+    # valid for 1..8 nodes dividing 120 -> data-parallel sizes 4 * {1, 2, 3, 4, 5, 6, 8}
+    b, valid, mb = compute_elastic_config(cfg, world_size=16)
+    assert b == 960 and valid == [4, 8, 12, 16, 20, 24, 32] and mb == 4
+    with pytest.raises(ElasticityConfigError):
+        compute_elastic_config(dict(elasticity=dict(cfg["elasticity"], num_gpus_per_node=5)), world_size=16)
+
+
+def test_v02_world_size_from_env(monkeypatch):
+    cfg = _cfg(max_train_batch_size=1024, micro_batch_sizes=[2, 4], min_gpus=8, max_gpus=64,
+               model_parallel_size=2, num_gpus_per_node=8, version=0.2)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    with pytest.raises(ElasticityConfigError):
+        compute_elastic_config(cfg)
+    monkeypatch.setenv("WORLD_SIZE", "16")
+    b, valid, mb = compute_elastic_config(cfg, return_microbatch=True)
+    assert (b, mb) == (960, 4)
