@@ -25,6 +25,13 @@ def _register_sxe_formulas():
     if _REGISTERED["done"]:
         return
     _REGISTERED["done"] = True
+    try:  # PyTorch has formulas for its GPU SDPA kernels, not for the CPU flash kernel
+        @register_flop_formula(torch.ops.aten._scaled_dot_product_flash_attention_for_cpu)
+        def _sdpa_cpu(q, k, v, *a, out_shape=None, **kw):
+            B, H, S, D = q
+            return 2 * (2 * B * H * S * k[2] * D)  # Q K^T and P V, as torch counts its GPU SDPA
+    except Exception:
+        pass
     try:
         from ...ops import native
         if not native.hip_available():
@@ -45,6 +52,23 @@ def _register_sxe_formulas():
         def _fa_bwd(dout, q, k, v, *a, out_shape=None, **kw):
             causal = a[3] if len(a) > 3 else True
             return int(2.5 * attn_flops(q, k, causal))
+
+        # hand-written GEMMs: 2 * rows * out * in
+        @register_flop_formula(ops.skinny_gemm)
+        def _skinny(x, w, *a, out_shape=None, **kw):
+            return 2 * x[0] * w[0] * w[1]
+
+        @register_flop_formula(ops.skinny_gemm_fp8w)
+        def _skinny8(x, wq, *a, out_shape=None, **kw):
+            return 2 * x[0] * wq[0] * wq[1]
+
+        @register_flop_formula(ops.grouped_gemm)
+        def _grouped(x, w, *a, out_shape=None, **kw):  # every row meets exactly one expert
+            return 2 * x[0] * w[1] * w[2]
+
+        @register_flop_formula(ops.wgrad_gemm_)
+        def _wgrad(a, b, *rest, out_shape=None, **kw):  # c (+)= a^T b, a [K, M], b [K, N]
+            return 2 * a[0] * a[1] * b[1]
     except Exception:  # formulas are optional; generic ops are still counted
         pass
 
