@@ -56,7 +56,8 @@ class LlamaConfig:
     activation_checkpointing: bool = False
     loss_chunk_tokens: Optional[int] = None
     sequence_parallel: bool = False  # Ulysses: inputs are [B, S/sp] chunks of the SP group
-    sp_mode: str = "ulysses"         # "ring": ring attention (context parallelism) over the SP group
+    sp_mode: str = "ulysses"         # "ring" / "ring_zigzag": ring attention (context parallelism) over
+                                     # the SP group, contiguous or zig-zag (sequence.ring_attention) shards
     fpdt_chunk_size: int = 0         # >0: FPDT chunked attention (global chunk length); inputs laid
                                      # out by sequence.fpdt_layer.FPDT_InputConstruct
     fpdt_offload: bool = False       # FPDT: keep the saved q/k/v/o chunks in pinned host memory
@@ -122,8 +123,9 @@ class LlamaAttention(nn.Module):
             p = dist.get_world_size(spg) if spg is not None else 1
             n = max(1, S * p // self.cfg.fpdt_chunk_size)
             o = fpdt_attention(qkv, self.nq, self.nkv, rope, spg, n, offload=self.cfg.fpdt_offload)
-        elif spg is not None and self.cfg.sp_mode == "ring":
-            o = ring_qkv_attention(qkv, self.nq, self.nkv, rope, spg, position_ids, causal=True)
+        elif spg is not None and self.cfg.sp_mode in ("ring", "ring_zigzag"):
+            o = ring_qkv_attention(qkv, self.nq, self.nkv, rope, spg, position_ids, causal=True,
+                                   layout="zigzag" if self.cfg.sp_mode == "ring_zigzag" else "contiguous")
         elif spg is not None:
             o = ulysses_qkv_attention(qkv, self.nq, self.nkv, rope, spg, position_ids, causal=True)
         else:

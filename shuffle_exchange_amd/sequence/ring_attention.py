@@ -14,8 +14,12 @@ Backward runs the ring again: each pair's dQ/dK/dV come from the flash backward 
 GLOBAL output and LSE (so P and delta are the merged softmax's), dQ accumulates locally and the
 dK/dV partials travel with their k/v chunk, arriving home after the p-th hop. Unlike Ulysses the
 head count need not be divisible by p and no all-to-all of the activations is needed; compared
-with FPDT nothing is offloaded. Without load balancing, causal ring attention idles the first ranks
-for the later steps (ranks hold contiguous chunks; a zig-zag chunk order would balance it).
+with FPDT nothing is offloaded.
+
+Load balance: with contiguous chunks (``layout="contiguous"``) a causal mask gives rank i only i+1
+non-empty pairs, so the last rank's work sets the step time. ``layout="zigzag"`` cuts the sequence
+into 2p chunks and gives rank r chunks r and 2p-1-r (``zigzag_shard`` lays out the batch and the
+position ids): every rank then computes the same number of (half-chunk) pairs at every step.
 
 Shapes the flash kernel does not take (CPU / gloo tests, head dims other than 128, chunks not a
 multiple of 128) run the same algorithm through an fp32 math path.
@@ -114,25 +118,48 @@ def _merge(o_acc, lse_acc, o, lse):
     return o_acc * a + o * b, new
 
 
+def _halves(layout, r, p):
+    """Global chunk ids of a rank's local sequence pieces (in local order)."""
+    return (r,) if layout == "contiguous" else (r, 2 * p - 1 - r)
+
+
+def _split(t, n):
+    return t.chunk(n, dim=1) if n > 1 else (t,)
+
+
+def _mode(iq, ik, causal):
+    """(run, causal flag) of the pair (query piece iq, key piece ik) under the global causal mask."""
+    if not causal:
+        return True, False
+    return ik <= iq, ik == iq
+
+
 class _RingAttention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, group, causal, scale):
+    def forward(ctx, q, k, v, group, causal, scale, layout):
         ring = _Ring(group)
         Hk = k.shape[2]
+        mine = _halves(layout, ring.r, ring.p)
+        n = len(mine)
+        qs = _split(q, n)
         kv = torch.cat([k, v], dim=2).contiguous()
-        o_acc = lse_acc = None
+        acc = [(None, None)] * n
         for step in range(ring.p):
             j = (ring.r - step) % ring.p
             pending = ring.start(kv) if step + 1 < ring.p else None
-            if not causal or j <= ring.r:
-                o, lse = _pair_fwd(q, kv[:, :, :Hk], kv[:, :, Hk:], causal and j == ring.r, scale)
-                o_acc, lse_acc = _merge(o_acc, lse_acc, o, lse)
+            for a, (iq, qa) in enumerate(zip(mine, qs)):
+                for ik, kva in zip(_halves(layout, j, ring.p), _split(kv, n)):
+                    run, cflag = _mode(iq, ik, causal)
+                    if run:
+                        o, lse = _pair_fwd(qa, kva[:, :, :Hk], kva[:, :, Hk:], cflag, scale)
+                        acc[a] = _merge(acc[a][0], acc[a][1], o, lse)
             if pending is not None:
                 ring.finish(pending[1])
                 kv = pending[0]
-        out = o_acc.to(q.dtype)
-        ctx.save_for_backward(q, k, v, out, lse_acc)
-        ctx.group, ctx.causal, ctx.scale = group, causal, scale
+        out = torch.cat([o for o, _ in acc], 1).to(q.dtype)
+        lse = torch.cat([l for _, l in acc], 2)
+        ctx.save_for_backward(q, k, v, out, lse)
+        ctx.group, ctx.causal, ctx.scale, ctx.layout = group, causal, scale, layout
         return out
 
     @staticmethod
@@ -140,38 +167,70 @@ class _RingAttention(torch.autograd.Function):
         q, k, v, o, lse = ctx.saved_tensors
         ring = _Ring(ctx.group)
         Hk = k.shape[2]
+        mine = _halves(ctx.layout, ring.r, ring.p)
+        n = len(mine)
+        qs, os_, dos = _split(q, n), _split(o, n), _split(do.contiguous(), n)
+        lses = lse.chunk(n, dim=2) if n > 1 else (lse,)
         kv = torch.cat([k, v], dim=2).contiguous()
         dkv = torch.zeros(kv.shape, dtype=torch.float32, device=kv.device)
         dq = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
+        dqs = _split(dq, n)
         for step in range(ring.p):
             j = (ring.r - step) % ring.p
             pending = ring.start(kv) if step + 1 < ring.p else None
-            if not ctx.causal or j <= ring.r:
-                dqp, dkp, dvp = _pair_bwd(do, q, kv[:, :, :Hk], kv[:, :, Hk:], o, lse, ctx.causal and j == ring.r,
-                                          ctx.scale)
-                dq += dqp
-                dkv[:, :, :Hk] += dkp
-                dkv[:, :, Hk:] += dvp
+            for a, iq in enumerate(mine):
+                for b, (ik, kvb) in enumerate(zip(_halves(ctx.layout, j, ring.p), _split(kv, n))):
+                    run, cflag = _mode(iq, ik, ctx.causal)
+                    if not run:
+                        continue
+                    dqp, dkp, dvp = _pair_bwd(dos[a], qs[a], kvb[:, :, :Hk], kvb[:, :, Hk:], os_[a],
+                                              lses[a].contiguous(), cflag, ctx.scale)
+                    dqs[a].add_(dqp)
+                    dkb = _split(dkv, n)[b]
+                    dkb[:, :, :Hk] += dkp
+                    dkb[:, :, Hk:] += dvp
             # the partial dK/dV of chunk j travel with it; after the p-th hop they are home
             dkv, reqs = ring.start(dkv)
             ring.finish(reqs)
             if pending is not None:
                 ring.finish(pending[1])
                 kv = pending[0]
-        return dq.to(q.dtype), dkv[:, :, :Hk].to(k.dtype), dkv[:, :, Hk:].to(v.dtype), None, None, None
+        return dq.to(q.dtype), dkv[:, :, :Hk].to(k.dtype), dkv[:, :, Hk:].to(v.dtype), None, None, None, None
 
 
-def ring_attention(q, k, v, group, causal=True, softmax_scale=None):
-    """q [B, S/p, H, D], k/v [B, S/p, Hk, D]: this rank's contiguous sequence chunk (rank order =
-    sequence order) -> [B, S/p, H, D] attention over the whole sequence."""
+def zigzag_indices(seq_len, rank, p, device=None):
+    """Token positions of ``rank``'s zig-zag shard: chunks rank and 2p-1-rank of 2p equal chunks."""
+    assert seq_len % (2 * p) == 0, f"sequence length {seq_len} must be divisible by 2 * {p}"
+    c = seq_len // (2 * p)
+    idx = torch.arange(seq_len, device=device).view(2 * p, c)
+    return torch.cat([idx[rank], idx[2 * p - 1 - rank]])
+
+
+def zigzag_shard(input_ids, rank, p, labels=None, ignore_index=-100):
+    """``shard_batch_for_sp`` for the zig-zag layout: input ids, next-token labels and position ids
+    of this rank's two chunks."""
+    B, S = input_ids.shape
+    labels = input_ids if labels is None else labels
+    shifted = torch.cat([labels[:, 1:], torch.full_like(labels[:, :1], ignore_index)], dim=1)
+    idx = zigzag_indices(S, rank, p, input_ids.device)
+    return {"input_ids": input_ids[:, idx].contiguous(), "labels": shifted[:, idx].contiguous(),
+            "position_ids": idx.unsqueeze(0).expand(B, -1).contiguous(), "shift_labels": False}
+
+
+def ring_attention(q, k, v, group, causal=True, softmax_scale=None, layout="contiguous"):
+    """q [B, S/p, H, D], k/v [B, S/p, Hk, D]: this rank's share of the sequence -- its contiguous
+    chunk (rank order = sequence order) or, with ``layout="zigzag"``, chunks r and 2p-1-r
+    concatenated -- -> [B, S/p, H, D] attention over the whole sequence."""
+    assert layout in ("contiguous", "zigzag"), layout
     scale = softmax_scale if softmax_scale is not None else q.shape[-1] ** -0.5
     if group is None or dist.get_world_size(group) == 1:
         from ..ops.attention import attention
         return attention(q, k, v, causal=causal, softmax_scale=scale)
-    return _RingAttention.apply(q, k, v, group, causal, scale)
+    return _RingAttention.apply(q, k, v, group, causal, scale, layout)
 
 
-def ring_qkv_attention(qkv, nq, nkv, rope, group, position_ids=None, causal=True, softmax_scale=None):
+def ring_qkv_attention(qkv, nq, nkv, rope, group, position_ids=None, causal=True, softmax_scale=None,
+                       layout="contiguous"):
     """Ring attention on a packed QKV chunk [B, S/p, nq + 2nkv, D] (the Llama layout) -> [B, S/p, nq, D]:
     RoPE at the chunk's global positions, then ``ring_attention`` on strided q/k/v views."""
     from ..ops.rope import apply_rope_qkv_
@@ -180,7 +239,11 @@ def ring_qkv_attention(qkv, nq, nkv, rope, group, position_ids=None, causal=True
         pos = position_ids
         if pos is None:
             r = dist.get_rank(group) if group is not None else 0
-            pos = (torch.arange(Sl, device=qkv.device) + r * Sl).unsqueeze(0).expand(B, Sl)
+            if layout == "zigzag" and group is not None:
+                p = dist.get_world_size(group)
+                pos = zigzag_indices(Sl * p, r, p, qkv.device).unsqueeze(0).expand(B, Sl)
+            else:
+                pos = (torch.arange(Sl, device=qkv.device) + r * Sl).unsqueeze(0).expand(B, Sl)
         qkv = apply_rope_qkv_(qkv, rope, nq + nkv, pos)
     q, k, v = qkv[:, :, :nq], qkv[:, :, nq:nq + nkv], qkv[:, :, nq + nkv:]
-    return ring_attention(q, k, v, group, causal=causal, softmax_scale=softmax_scale)
+    return ring_attention(q, k, v, group, causal=causal, softmax_scale=softmax_scale, layout=layout)

@@ -13,9 +13,9 @@ def _full(q, k, v, causal):
     return torch.nn.functional.scaled_dot_product_attention(qt, kt, vt, is_causal=causal).transpose(1, 2)
 
 
-def _case_ring(rank, world, causal):
+def _case_ring(rank, world, causal, layout):
     from shuffle_exchange_amd.parallel import groups
-    from shuffle_exchange_amd.sequence.ring_attention import ring_attention
+    from shuffle_exchange_amd.sequence.ring_attention import ring_attention, zigzag_indices
     groups.initialize(sequence_parallel_size=world)
     g = groups.get_sequence_parallel_group()
     torch.manual_seed(0)
@@ -26,9 +26,9 @@ def _case_ring(rank, world, causal):
     qr, kr, vr = (t.clone().requires_grad_() for t in (q, k, v))
     ref = _full(qr, kr, vr, causal)
     ref.backward(dy)
-    sl = slice(rank * 6, (rank + 1) * 6)
+    sl = zigzag_indices(S, rank, world) if layout == "zigzag" else torch.arange(rank * 6, (rank + 1) * 6)
     ql, kl, vl = (t[:, sl].clone().requires_grad_() for t in (q, k, v))
-    out = ring_attention(ql, kl, vl, g, causal=causal)
+    out = ring_attention(ql, kl, vl, g, causal=causal, layout=layout)
     out.backward(dy[:, sl])
     err = lambda a, b: float((a - b).abs().max())  # noqa: E731
     return {"o": err(out, ref[:, sl]), "dq": err(ql.grad, qr.grad[:, sl]), "dk": err(kl.grad, kr.grad[:, sl]),
@@ -37,19 +37,22 @@ def _case_ring(rank, world, causal):
 
 @pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("causal", [True, False])
-def test_ring_attention_equals_full(world, causal):
-    for r in run_dist(_case_ring, world, causal):
+@pytest.mark.parametrize("layout", ["contiguous", "zigzag"])
+def test_ring_attention_equals_full(world, causal, layout):
+    for r in run_dist(_case_ring, world, causal, layout):
         assert max(r.values()) < 1e-5, r
 
 
-def _case_ring_llama(rank, world):
+def _case_ring_llama(rank, world, mode):
     import shuffle_exchange_amd as sxe
     from shuffle_exchange_amd import comm
     from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
     from shuffle_exchange_amd.parallel import groups
     from shuffle_exchange_amd.sequence.data import shard_batch_for_sp
+    from shuffle_exchange_amd.sequence.ring_attention import zigzag_shard
+    shard = zigzag_shard if mode == "ring_zigzag" else shard_batch_for_sp
     torch.manual_seed(0)
-    cfg = llama_config("llama-tiny", sequence_parallel=True, sp_mode="ring")
+    cfg = llama_config("llama-tiny", sequence_parallel=True, sp_mode=mode)
     model = LlamaForCausalLM(cfg)
     ds = {"train_micro_batch_size_per_gpu": 2, "sequence_parallel_size": world,
           "zero_optimization": {"stage": 1}, "optimizer": {"type": "SGD", "params": {"lr": 0.1}}}
@@ -58,7 +61,7 @@ def _case_ring_llama(rank, world):
     losses = []
     for _ in range(2):
         ids = torch.randint(0, cfg.vocab_size, (2, 32), generator=g)
-        b = shard_batch_for_sp(ids, groups.get_sequence_parallel_rank(), world)
+        b = shard(ids, groups.get_sequence_parallel_rank(), world)
         loss = eng(b["input_ids"], labels=b["labels"], position_ids=b["position_ids"], shift_labels=False)
         tot = loss.detach().clone()
         comm.all_reduce(tot, group=groups.get_sequence_parallel_group())
@@ -68,7 +71,8 @@ def _case_ring_llama(rank, world):
     return {"losses": losses}
 
 
-def test_ring_context_parallel_llama_step():
+@pytest.mark.parametrize("mode", ["ring", "ring_zigzag"])
+def test_ring_context_parallel_llama_step(mode):
     from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
     torch.manual_seed(0)
     model = LlamaForCausalLM(llama_config("llama-tiny"))
@@ -82,7 +86,7 @@ def test_ring_context_parallel_llama_step():
         loss.backward()
         opt.step()
         ref.append(float(loss))
-    for r in run_dist(_case_ring_llama, 2):
+    for r in run_dist(_case_ring_llama, 2, mode):
         for a, b in zip(r["losses"], ref):
             assert abs(a - b) < 1e-4 * max(1.0, abs(b)), (r["losses"], ref)
 
