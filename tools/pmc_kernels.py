@@ -1,7 +1,8 @@
 """Workload for rocprofv3 --pmc passes over the hand-written gfx950 kernels (a few dispatches each):
 flash attention fwd/bwd (B4 S2048 H32/8 D128 causal), skinny decode GEMM (bf16 and FP8 weights,
 4096x14336 at M=1), paged decode attention (B32 ctx 1024), RMSNorm fwd (8192x4096), fused AdamW on
-64M params. Run under:  rocprofv3 --pmc <counters> --output-format csv -d DIR -o pmc -- python3 tools/pmc_kernels.py"""
+64M params, k-major wgrad GEMM, dual-layout gated kernels (16k x 14336), grouped expert GEMM
+(60 experts). Run under:  rocprofv3 --pmc <counters> --output-format csv -d DIR -o pmc -- python3 tools/pmc_kernels.py"""
 import os
 import sys
 
@@ -58,6 +59,22 @@ def main():
     for _ in range(3):
         torch.ops.sxe.wgrad_gemm_variant_(gy, xw, accw, 1.0, True, 0)
         torch.mm(gyt, xwt.t())
+    del gy, xw, accw, gyt, xwt
+    # dual-layout gated kernels of the fused MLP (16k tokens x 14336) and the grouped expert GEMM
+    gu = torch.randn(16384, 28672, device=dev, dtype=bf)
+    dh = torch.randn(16384, 14336, device=dev, dtype=bf)
+    for _ in range(3):
+        torch.ops.sxe.gated_act_fwd_dual(gu, 3, 4)
+        torch.ops.sxe.gated_act_bwd_dual(dh, gu, 3, 4)
+    del gu, dh
+    E, N, K, R = 60, 2816, 2048, 16384
+    xs = torch.randn(R, K, device=dev, dtype=bf)
+    we = torch.randn(E, N, K, device=dev, dtype=bf)
+    flat = torch.randint(0, E, (R,), device=dev).sort().values
+    from shuffle_exchange_amd.ops.moe import expert_offsets
+    offs = expert_offsets(flat, E)
+    for _ in range(3):
+        torch.ops.sxe.grouped_gemm(xs, we, offs, None)
     torch.cuda.synchronize()
     print("pmc workload done", flush=True)
 
