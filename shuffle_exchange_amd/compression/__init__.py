@@ -1,2 +1,3 @@
 """Compression (reference compression/)."""
-from .compress import LinearLayer_Compress, compression_scheduler, init_compression, redundancy_clean  # noqa: F401
+from .compress import (BNLayer_Compress, Conv2dLayer_Compress, Embedding_Compress, LinearLayer_Compress,  # noqa: F401
+                       compression_scheduler, init_compression, redundancy_clean)
