@@ -59,10 +59,13 @@ template <DT T>
 __global__ void __launch_bounds__(256) gated_fwd_kernel(const typename dt_traits<T>::storage* __restrict__ gu,
                                                         typename dt_traits<T>::storage* __restrict__ out, int64_t rows,
                                                         int I, int act) {
+  // flat over (row, 8-column chunk): a single decode row spreads over I/8/256 blocks instead of
+  // one block looping over the whole row
   const int per_row = I / 8;
-  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x)
-  for (int cc = threadIdx.x; cc < per_row; cc += blockDim.x) {
-    const int c = cc * 8;
+  const int64_t n = rows * per_row;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / per_row;
+    const int c = (int)(i - r * per_row) * 8;
     float g[8], u[8], o[8];
     load8<T>(gu + r * 2 * I + c, g);
     load8<T>(gu + r * 2 * I + I + c, u);
@@ -78,9 +81,10 @@ __global__ void __launch_bounds__(256) gated_bwd_kernel(const typename dt_traits
                                                         typename dt_traits<T>::storage* __restrict__ dgu, int64_t rows,
                                                         int I, int act) {
   const int per_row = I / 8;
-  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x)
-  for (int cc = threadIdx.x; cc < per_row; cc += blockDim.x) {
-    const int c = cc * 8;
+  const int64_t n = rows * per_row;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / per_row;
+    const int c = (int)(i - r * per_row) * 8;
     float g[8], u[8], d[8], dg[8], du[8];
     load8<T>(gu + r * 2 * I + c, g);
     load8<T>(gu + r * 2 * I + I + c, u);
@@ -109,7 +113,7 @@ at::Tensor gated_act_fwd(at::Tensor gu, int64_t act) {
   DT d = dtype_of(gu);
   SXE_DISPATCH_DT(d, TT, {
     using S = typename dt_traits<TT>::storage;
-    hipLaunchKernelGGL((gated_fwd_kernel<TT>), dim3((int)std::min<int64_t>(rows, 4096)), dim3(256), 0, cur_stream(),
+    hipLaunchKernelGGL((gated_fwd_kernel<TT>), dim3(stream_grid(rows * (I / 8), 256)), dim3(256), 0, cur_stream(),
                        reinterpret_cast<const S*>(gu.data_ptr()), reinterpret_cast<S*>(out.data_ptr()), rows, I, (int)act);
   });
   SXE_LAUNCH_CHECK();
@@ -128,7 +132,7 @@ at::Tensor gated_act_bwd(at::Tensor dout, at::Tensor gu, int64_t act) {
   DT d = dtype_of(gu);
   SXE_DISPATCH_DT(d, TT, {
     using S = typename dt_traits<TT>::storage;
-    hipLaunchKernelGGL((gated_bwd_kernel<TT>), dim3((int)std::min<int64_t>(rows, 4096)), dim3(256), 0, cur_stream(),
+    hipLaunchKernelGGL((gated_bwd_kernel<TT>), dim3(stream_grid(rows * (I / 8), 256)), dim3(256), 0, cur_stream(),
                        reinterpret_cast<const S*>(dout.data_ptr()), reinterpret_cast<const S*>(gu.data_ptr()),
                        reinterpret_cast<S*>(dgu.data_ptr()), rows, I, (int)act);
   });

@@ -28,7 +28,10 @@ __device__ __forceinline__ void load_w8(const typename WType<T, WF32>::type* w, 
 }
 
 // ---------------------------------------------------------------------------------------------
-template <DT T, bool WF32, bool LN, bool RES, int NCH>
+// WPR = waves per row: 1 (the default: one wave per row, no barrier) or 4 (the whole 256-thread
+// block on one row, block-level reductions) for launches with few rows -- decode's single-token
+// RMSNorm took 9 us as one wave sweeping 4096 elements in 8 dependent-latency chunks.
+template <DT T, bool WF32, bool LN, bool RES, int NCH, int WPR = 1>
 __global__ void __launch_bounds__(256) norm_fwd_kernel(const typename dt_traits<T>::storage* __restrict__ x,
                                                        const typename dt_traits<T>::storage* __restrict__ res,
                                                        const typename WType<T, WF32>::type* __restrict__ w,
@@ -38,16 +41,19 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const typename dt_traits<
                                                        float* __restrict__ rstd_out, float* __restrict__ mean_out,
                                                        int64_t rows, int H, float eps) {
   using S = typename dt_traits<T>::storage;
-  const int lane = threadIdx.x & 63;
-  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  constexpr int LPR = 64 * WPR;  // lanes per row
+  __shared__ float red[4];
+  const int lane = WPR == 1 ? (threadIdx.x & 63) : threadIdx.x;
+  const int64_t wid = WPR == 1 ? ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6 : blockIdx.x;
+  const int64_t nw = WPR == 1 ? ((int64_t)gridDim.x * blockDim.x) >> 6 : gridDim.x;
+  auto row_sum = [&](float v) { return WPR == 1 ? wave_sum(v) : block_sum<4>(v, red); };
   for (int64_t r = wid; r < rows; r += nw) {
     const S* xr = x + r * H;
     float v[NCH][8];
     float s = 0.f;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      const int col = (c * 64 + lane) * 8;
+      const int col = (c * LPR + lane) * 8;
       if (col < H) {
         load8<T>(xr + col, v[c]);
         if constexpr (RES) {
@@ -66,11 +72,11 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const typename dt_traits<
     }
     float mean = 0.f;
     if constexpr (LN) {
-      mean = wave_sum(s) / (float)H;
+      mean = row_sum(s) / (float)H;
       s = 0.f;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
-        const int col = (c * 64 + lane) * 8;
+        const int col = (c * LPR + lane) * 8;
         if (col < H) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) { float d = v[c][j] - mean; s += d * d; }
@@ -80,17 +86,17 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const typename dt_traits<
       s = 0.f;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
-        const int col = (c * 64 + lane) * 8;
+        const int col = (c * LPR + lane) * 8;
         if (col < H) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) s += v[c][j] * v[c][j];
         }
       }
     }
-    const float rstd = rsqrtf(wave_sum(s) / (float)H + eps);
+    const float rstd = rsqrtf(row_sum(s) / (float)H + eps);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      const int col = (c * 64 + lane) * 8;
+      const int col = (c * LPR + lane) * 8;
       if (col < H) {
         float wv[8], o[8];
         load_w8<T, WF32>(w + col, wv);
@@ -255,13 +261,16 @@ std::vector<at::Tensor> norm_fwd(at::Tensor x, c10::optional<at::Tensor> residua
   SXE_CHECK(wf32 || weight.scalar_type() == x.scalar_type(), "norm_fwd: weight dtype must be fp32 or match x");
   if (has_b) SXE_CHECK(bias->scalar_type() == weight.scalar_type() && bias->numel() == H, "norm_fwd: bias");
   if (rows == 0) return {y, rstd, mean, h};
-  const int grid = (int)std::min<int64_t>((rows + 3) / 4, 2048);
+  // few rows (decode, small batches): a whole block per row; otherwise one wave per row
+  const bool block_rows = rows <= 256 && H >= 1024;
+  const int grid = block_rows ? (int)rows : (int)std::min<int64_t>((rows + 3) / 4, 2048);
   DT d = dtype_of(x);
-  const int nch = pick_nch(H);
+  const int nch = block_rows ? pick_nch((H + 3) / 4) : pick_nch(H);
   SXE_DISPATCH_DT(d, TT, SXE_DISPATCH_BOOL(wf32, WF, SXE_DISPATCH_BOOL(layernorm, LNB, SXE_DISPATCH_BOOL(has_res, RB, SXE_DISPATCH_NCH(nch, NC, {
     using S = typename dt_traits<TT>::storage;
     using W = typename WType<TT, WF>::type;
-    hipLaunchKernelGGL((norm_fwd_kernel<TT, WF, LNB, RB, NC>), dim3(grid), dim3(256), 0, cur_stream(),
+    auto kern = block_rows ? norm_fwd_kernel<TT, WF, LNB, RB, NC, 4> : norm_fwd_kernel<TT, WF, LNB, RB, NC, 1>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, cur_stream(),
                        reinterpret_cast<const S*>(x.data_ptr()), has_res ? reinterpret_cast<const S*>(residual->data_ptr()) : nullptr,
                        reinterpret_cast<const W*>(weight.data_ptr()), has_b ? reinterpret_cast<const W*>(bias->data_ptr()) : nullptr,
                        reinterpret_cast<S*>(y.data_ptr()), has_res ? reinterpret_cast<S*>(h.data_ptr()) : nullptr,

@@ -7,6 +7,7 @@ tokens of each sequence over all of its cached keys. Both have PyTorch reference
 (CPU processes / numerics oracles).
 """
 import math
+import os
 
 import torch
 
@@ -65,11 +66,16 @@ def paged_attention_reference(q, cache, block_table, q_start, q_len, kv_len, sca
     return out
 
 
+# keys per split floor (A/B knob; see choose_splits)
+PA_MIN_KEYS = int(os.environ.get("SXE_PA_MIN_KEYS", 256))
+
+
 def choose_splits(num_seqs, nkv, max_kv_len, target_wgs=512):
-    """KV splits so (seqs x kv heads x splits) fills the 256 CUs, never below 256 keys per split."""
+    """KV splits so (seqs x kv heads x splits) fills the 256 CUs, never below PA_MIN_KEYS keys
+    per split."""
     base = max(1, num_seqs * nkv)
     want = max(1, math.ceil(target_wgs / base))
-    return max(1, min(want, math.ceil(max(max_kv_len, 1) / 256)))
+    return max(1, min(want, math.ceil(max(max_kv_len, 1) / PA_MIN_KEYS)))
 
 
 def paged_attention(q, cache, block_table, q_start, q_len, kv_len, scale, max_kv_len, splits=None, window=None):

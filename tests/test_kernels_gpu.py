@@ -75,10 +75,11 @@ def test_multi_tensor_adam_matches_flat():
 
 @pytest.mark.parametrize("H", [128, 1000, 4096, 8192])
 @pytest.mark.parametrize("residual", [False, True])
-def test_rmsnorm(H, residual):
+@pytest.mark.parametrize("rows", [1, 185, 300])  # <= 256 rows and H >= 1024: block-per-row forward
+def test_rmsnorm(H, residual, rows):
     from shuffle_exchange_amd.ops.norm import rms_norm
     H = H - H % 8
-    x = torch.randn(37, 5, H, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    x = torch.randn(rows, 1, H, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     r = torch.randn_like(x, requires_grad=True) if residual else None
     w = (torch.rand(H, device="cuda") + 0.5).to(torch.bfloat16).requires_grad_()
     out = rms_norm(x, w, 1e-5, residual=r)
@@ -138,9 +139,10 @@ def test_rope_qkv_roundtrip():
     assert _rel(x.grad[:, :, :Hq + Hk].reshape(B * S, Hq + Hk, D), gi) < 1e-2
 
 
-def test_swiglu():
+@pytest.mark.parametrize("rows", [1, 33])
+def test_swiglu(rows):
     from shuffle_exchange_amd.ops.activation import swiglu
-    gu = torch.randn(33, 2 * 1024, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    gu = torch.randn(rows, 2 * 1024, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     y = swiglu(gu)
     gu2 = gu.detach().float().requires_grad_()
     g, u = gu2.chunk(2, -1)
