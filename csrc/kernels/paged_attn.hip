@@ -47,6 +47,54 @@ __global__ __launch_bounds__(256) void kv_append_kernel(const unsigned short* __
   }
 }
 
+// Decode/prefill prologue in ONE launch: rotate the q and k heads of each token in place
+// (rotate-half RoPE, fp32 cos/sin table [max_pos, D/2] at the token's absolute position) and write
+// the rotated k plus v into the paged cache -- the separate rope_ + kv_append launches were ~7 us
+// of latency per layer at batch 1. One workgroup per token; a thread handles 8 rotation pairs.
+template <int D>
+__global__ __launch_bounds__(256) void rope_kv_append_kernel(unsigned short* __restrict qkv, int64_t tok_stride,
+                                                             int nq, int nkv, const int64_t* __restrict pos,
+                                                             const float* __restrict cos_t,
+                                                             const float* __restrict sin_t,
+                                                             const int64_t* __restrict slots,
+                                                             unsigned short* __restrict cache, int bs) {
+  constexpr int HALF = D / 2, VR = HALF / 8, VV = D / 8;
+  const int t = blockIdx.x;
+  const int64_t slot = slots[t];
+  const int64_t blk = slot / bs, off = slot % bs;
+  const int64_t p = pos[t];
+  unsigned short* row = qkv + (int64_t)t * tok_stride;
+  const int nrot = (nq + nkv) * VR;
+  for (int i = threadIdx.x; i < nrot + nkv * VV; i += blockDim.x) {
+    if (i < nrot) {
+      const int h = i / VR, c = (i - h * VR) * 8;
+      unsigned short* base = row + (int64_t)h * D;
+      float a[8], b[8], cs[8], sn[8], oa[8], ob[8];
+      load8<DT::BF16>(base + c, a);
+      load8<DT::BF16>(base + HALF + c, b);
+      load8<DT::F32>(cos_t + p * HALF + c, cs);
+      load8<DT::F32>(sin_t + p * HALF + c, sn);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        oa[j] = a[j] * cs[j] - b[j] * sn[j];
+        ob[j] = b[j] * cs[j] + a[j] * sn[j];
+      }
+      store8<DT::BF16>(base + c, oa);
+      store8<DT::BF16>(base + HALF + c, ob);
+      if (h >= nq && slot >= 0) {  // rotated k -> cache
+        unsigned short* dst = cache + (((blk * 2 + 0) * nkv + (h - nq)) * bs + off) * D;
+        store8<DT::BF16>(dst + c, oa);
+        store8<DT::BF16>(dst + HALF + c, ob);
+      }
+    } else if (slot >= 0) {  // v -> cache
+      const int j = i - nrot, h = j / VV, v = j - h * VV;
+      const unsigned short* src = row + (int64_t)(nq + nkv + h) * D + v * 8;
+      unsigned short* dst = cache + (((blk * 2 + 1) * nkv + h) * bs + off) * D + v * 8;
+      *reinterpret_cast<u16x8*>(dst) = *reinterpret_cast<const u16x8*>(src);
+    }
+  }
+}
+
 struct Args {
   const unsigned short* q;
   int64_t q_tok_stride;  // elements between consecutive tokens (heads are D apart)
@@ -277,6 +325,38 @@ __global__ __launch_bounds__(D) void merge_kernel(const float* __restrict part_o
 }  // namespace pa
 
 // qkv: [T, nq + 2 nkv, D] bf16 (token stride may exceed the row); slots: [T] int64 (-1 = skip)
+void rope_kv_cache_append(at::Tensor qkv, const at::Tensor& cos_t, const at::Tensor& sin_t, const at::Tensor& pos,
+                          at::Tensor cache, const at::Tensor& slots, int64_t nq, int64_t nkv) {
+  SXE_CHECK_CUDA(qkv);
+  SXE_CHECK(qkv.scalar_type() == at::kBFloat16 && cache.scalar_type() == at::kBFloat16, "bf16 only");
+  SXE_CHECK(qkv.dim() == 3 && qkv.stride(2) == 1 && qkv.stride(1) == qkv.size(2), "qkv must be [T, H, D] row-major");
+  SXE_CHECK(qkv.size(1) == nq + 2 * nkv, "qkv heads != nq + 2 nkv");
+  SXE_CHECK(cache.dim() == 5 && cache.is_contiguous() && cache.size(2) == nkv && cache.size(4) == qkv.size(2),
+            "cache must be [blocks, 2, nkv, bs, D]");
+  SXE_CHECK(slots.scalar_type() == at::kLong && slots.numel() == qkv.size(0), "slots: int64 [T]");
+  SXE_CHECK(pos.scalar_type() == at::kLong && pos.numel() == qkv.size(0) && pos.is_contiguous(), "pos: int64 [T]");
+  const int D = qkv.size(2);
+  SXE_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat && cos_t.is_contiguous() &&
+                sin_t.is_contiguous() && cos_t.dim() == 2 && cos_t.size(1) == D / 2 && sin_t.sizes() == cos_t.sizes(),
+            "cos/sin: fp32 [max_pos, D/2]");
+  const int T = qkv.size(0);
+  if (T == 0) return;
+  c10::DeviceGuard g(qkv.device());
+  auto* q = reinterpret_cast<unsigned short*>(qkv.data_ptr());
+  auto* c = reinterpret_cast<unsigned short*>(cache.data_ptr());
+  const int bs = cache.size(3);
+#define SXE_RKA(DD)                                                                                              \
+  hipLaunchKernelGGL(pa::rope_kv_append_kernel<DD>, dim3(T), dim3(256), 0, cur_stream(), q, qkv.stride(0), (int)nq, \
+                     (int)nkv, pos.data_ptr<int64_t>(), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(),       \
+                     slots.data_ptr<int64_t>(), c, bs)
+  if (D == 128) SXE_RKA(128);
+  else if (D == 64) SXE_RKA(64);
+  else if (D == 256) SXE_RKA(256);
+  else SXE_CHECK(false, "rope_kv_cache_append: head_dim must be 64, 128 or 256");
+#undef SXE_RKA
+  SXE_LAUNCH_CHECK();
+}
+
 void kv_cache_append(const at::Tensor& qkv, at::Tensor cache, const at::Tensor& slots, int64_t nq, int64_t nkv) {
   SXE_CHECK_CUDA(qkv);
   SXE_CHECK(qkv.scalar_type() == at::kBFloat16 && cache.scalar_type() == at::kBFloat16, "bf16 only");
@@ -393,10 +473,13 @@ at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const a
 
 TORCH_LIBRARY_FRAGMENT(sxe, m) {
   m.def("kv_cache_append(Tensor qkv, Tensor(a!) cache, Tensor slots, int nq, int nkv) -> ()");
+  m.def("rope_kv_cache_append(Tensor(a!) qkv, Tensor cos, Tensor sin, Tensor pos, Tensor(b!) cache, Tensor slots, "
+        "int nq, int nkv) -> ()");
   m.def("paged_attention(Tensor q, Tensor cache, Tensor block_table, Tensor q_start, Tensor q_len, Tensor kv_len, "
         "float scale, int max_kv_len, int splits, int window=0) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(sxe, CUDA, m) {
   m.impl("kv_cache_append", &sxe::kv_cache_append);
+  m.impl("rope_kv_cache_append", &sxe::rope_kv_cache_append);
   m.impl("paged_attention", &sxe::paged_attention);
 }

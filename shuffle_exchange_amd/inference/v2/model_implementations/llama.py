@@ -27,8 +27,7 @@ import torch.nn.functional as F
 from ....ops import native
 from ....ops.activation import swiglu
 from ....ops.linear import linear
-from ....ops.paged_attention import kv_cache_append, paged_attention
-from ....ops.rope import apply_rope_tokens_
+from ....ops.paged_attention import paged_attention, rope_kv_cache_append
 from ....ops.rows import embed, gather_rows
 
 FLASH_PREFILL_MIN = 128
@@ -248,9 +247,9 @@ class RaggedLlama:
                 a, h = layer.input_layernorm(x, res)
             attn = layer.self_attn
             qkv = self._proj(attn.qkv_proj, a, li, "qkv").view(T, self.nq + 2 * self.nkv, self.head_dim)
-            apply_rope_tokens_(qkv, rope, self.nq + self.nkv, batch.positions)
             kv_layer = kv_cache.layer(li)
-            kv_cache_append(qkv, kv_layer, batch.slots, self.nq, self.nkv)
+            # RoPE on q/k + append of k/v to the paged cache: one launch (paged_attn.hip)
+            rope_kv_cache_append(qkv, rope, batch.positions, kv_layer, batch.slots, self.nq, self.nkv)
             o = self._attention(qkv, kv_layer, batch)
             o = self._proj(attn.o_proj, o.reshape(T, self.nq * self.head_dim), li, "o")
             m, h2 = layer.post_attention_layernorm(o, h)

@@ -14,6 +14,21 @@ import torch
 from . import native
 
 
+def rope_kv_cache_append(qkv, rope, positions, cache, slots, nq, nkv):
+    """RoPE on the q and k heads of ``qkv`` [T, nq + 2 nkv, D] (in place, absolute ``positions``)
+    and the rotated k + v appended to the paged ``cache`` -- one HIP launch
+    (paged_attn.hip ``rope_kv_append_kernel``) instead of rope_ + kv_cache_append."""
+    from .rope import apply_rope_tokens_
+    if (native.use_hip(qkv) and qkv.dtype == torch.bfloat16 and qkv.shape[-1] in (64, 128, 256)
+            and qkv.is_contiguous() and rope.cos.shape[-1] * 2 == qkv.shape[-1]):
+        torch.ops.sxe.rope_kv_cache_append(qkv, rope.cos, rope.sin, positions.reshape(-1).contiguous().long(), cache,
+                                           slots, int(nq), int(nkv))
+        return qkv
+    apply_rope_tokens_(qkv, rope, nq + nkv, positions)
+    kv_cache_append(qkv, cache, slots, nq, nkv)
+    return qkv
+
+
 def kv_cache_append(qkv, cache, slots, nq, nkv):
     """qkv: [T, nq + 2 nkv, D]; cache: [blocks, 2, nkv, bs, D]; slots: int64 [T] (-1 = skip)."""
     if native.use_hip(qkv) and qkv.shape[-1] in (64, 128) and qkv.is_contiguous():

@@ -77,3 +77,30 @@ def test_paged_attention_window_and_d256(seqs, nq, nkv, D, bs, window, splits):
     ref = paged_attention_reference(q.float(), cache.float(), bt, qs, ql, kl, scale, w)
     err = ((out.float() - ref).norm() / ref.norm()).item()
     assert err < 1e-2, err
+
+
+def test_fused_rope_kv_cache_append_matches_separate_ops():
+    """rope_kv_cache_append (one launch) == apply_rope_tokens_ + kv_cache_append (same math; bf16
+    rounding may differ by FMA contraction), including skipped (-1) slots that stay untouched."""
+    import torch
+    from shuffle_exchange_amd.ops import native
+    from shuffle_exchange_amd.ops.paged_attention import kv_cache_append, rope_kv_cache_append
+    from shuffle_exchange_amd.ops.rope import RopeCache, apply_rope_tokens_
+    native.require_hip()
+    torch.manual_seed(0)
+    for D in (64, 128):
+        T, nq, nkv, bs, nblk = 37, 8, 2, 16, 8
+        rope = RopeCache(D, 512, 10000.0, device="cuda")
+        qkv = torch.randn(T, nq + 2 * nkv, D, device="cuda", dtype=torch.bfloat16)
+        pos = torch.randint(0, 512, (T,), device="cuda")
+        slots = torch.randperm(nblk * bs, device="cuda")[:T].long()
+        slots[::7] = -1
+        c1 = torch.zeros(nblk, 2, nkv, bs, D, device="cuda", dtype=torch.bfloat16)
+        c2 = torch.zeros_like(c1)
+        a, b = qkv.clone(), qkv.clone()
+        apply_rope_tokens_(a, rope, nq + nkv, pos)
+        kv_cache_append(a, c1, slots, nq, nkv)
+        rope_kv_cache_append(b, rope, pos, c2, slots, nq, nkv)
+        torch.testing.assert_close(b, a, rtol=1e-2, atol=1e-2)
+        torch.testing.assert_close(c2, c1, rtol=1e-2, atol=1e-2)
+        assert torch.equal(c2 == 0, c1 == 0)
