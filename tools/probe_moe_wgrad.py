@@ -1,3 +1,5 @@
+"""Probe: are the Mixtral-arch expert weight-gradient shapes (capacity 1280 tokens) eligible for the
+hand-written k-major wgrad kernel (ops/linear._sxe_wgrad_ok)? usage: python tools/probe_moe_wgrad.py"""
 import torch, sys
 sys.path.insert(0, ".")
 from shuffle_exchange_amd.ops.linear import _sxe_wgrad_ok
