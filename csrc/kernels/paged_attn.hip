@@ -111,6 +111,7 @@ struct Args {
   int64_t out_tok_stride;
   float* part_o;   // [splits, T, nq, D]
   float* part_ml;  // [splits, T, nq, 2]
+  int* counters;   // [S * nkv] self-resetting split counters (nullptr: separate merge kernel)
   int T;
   int window;      // sliding window (Mistral / Qwen2): keys older than `window` positions are masked; 0 = off
 };
@@ -299,6 +300,38 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(Args a) {
     }
     __syncthreads();
   }
+  // split-KV merge fused in: the LAST workgroup of (seq, kv head) to finish (device-scope counter,
+  // release fence before / acquire fence after the vector atomic) combines every split's partial
+  // o / (max, sum) for this sequence's rows and resets the counter for the next launch. No
+  // workgroup waits on another, so there is nothing to deadlock on.
+  if (a.splits > 1 && a.counters != nullptr) {
+    __shared__ int is_last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) is_last = atomicAdd(&a.counters[blockIdx.x], 1) == a.splits - 1;
+    __syncthreads();
+    if (is_last) {
+      __threadfence();
+      for (int i = threadIdx.x; i < nrows_total * D; i += 256) {
+        const int row = i / D, d = i - row * D, tok = row / G, g = row - tok * G;
+        const int64_t th = (int64_t)(qs + tok) * a.nq + kvh * G + g;
+        float M = -INFINITY;
+        for (int s = 0; s < a.splits; ++s) M = fmaxf(M, __builtin_nontemporal_load(&a.part_ml[((int64_t)s * a.T * a.nq + th) * 2]));
+        float acc = 0.f, L = 0.f;
+        for (int s = 0; s < a.splits; ++s) {
+          const int64_t idx = (int64_t)s * a.T * a.nq + th;
+          const float ms = __builtin_nontemporal_load(&a.part_ml[idx * 2]);
+          if (ms == -INFINITY) continue;
+          const float f = exp2f(ms - M);
+          acc += f * __builtin_nontemporal_load(&a.part_o[idx * D + d]);
+          L += f * __builtin_nontemporal_load(&a.part_ml[idx * 2 + 1]);
+        }
+        a.out[(int64_t)(qs + tok) * a.out_tok_stride + (int64_t)(kvh * G + g) * D + d] =
+            f32_to_bf16(L > 0.f ? acc / L : 0.f);
+      }
+      if (threadIdx.x == 0) atomicExch(&a.counters[blockIdx.x], 0);
+    }
+  }
 }
 
 template <int D>
@@ -385,6 +418,25 @@ void kv_cache_append(const at::Tensor& qkv, at::Tensor cache, const at::Tensor& 
 }
 
 // q: [T, nq, D] (token stride free); returns out [T, nq, D] bf16
+// Persistent, self-resetting per-(seq, kv head) split counters for the fused merge: allocated zeroed
+// once per device OUTSIDE any stream capture (a buffer first allocated inside a HIP-graph capture
+// would belong to the graph's pool); while capturing with too small a buffer, or without
+// SXE_PA_FUSED_MERGE=1, the separate merge kernel runs instead.
+static int* split_counters(const c10::Device& dev, int64_t need) {
+  static at::Tensor buf[64];
+  static const bool enabled = [] {  // opt-in until measured on the decode benchmark
+    const char* e = std::getenv("SXE_PA_FUSED_MERGE");
+    return e && e[0] == '1';
+  }();
+  if (!enabled || dev.index() < 0 || dev.index() >= 64) return nullptr;
+  at::Tensor& b = buf[dev.index()];
+  if (b.defined() && b.numel() >= need) return b.data_ptr<int>();
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(cur_stream(), &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+  b = at::zeros({std::max<int64_t>(need, 1 << 16)}, at::TensorOptions().device(dev).dtype(at::kInt));
+  return b.data_ptr<int>();
+}
+
 at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const at::Tensor& block_table,
                            const at::Tensor& q_start, const at::Tensor& q_len, const at::Tensor& kv_len, double scale,
                            int64_t max_kv_len, int64_t splits, int64_t window) {
@@ -429,12 +481,14 @@ at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const a
   a.T = T;
   a.part_o = nullptr;
   a.part_ml = nullptr;
+  a.counters = nullptr;
   a.window = (int)std::max<int64_t>(0, window);
   if (splits > 1) {
     part_o = at::empty({splits, T, nq, D}, q.options().dtype(at::kFloat));
     part_ml = at::empty({splits, T, nq, 2}, q.options().dtype(at::kFloat));
     a.part_o = part_o.data_ptr<float>();
     a.part_ml = part_ml.data_ptr<float>();
+    a.counters = split_counters(q.device(), S * nkv);
   }
   dim3 grid(S * nkv, splits);
   const int G = nq / nkv;
@@ -454,7 +508,7 @@ at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const a
   }
 #undef SXE_PA_LAUNCH
   SXE_LAUNCH_CHECK();
-  if (splits > 1) {
+  if (splits > 1 && a.counters == nullptr) {
     if (D == 128)
       hipLaunchKernelGGL(pa::merge_kernel<128>, dim3(T * nq), dim3(128), 0, cur_stream(), a.part_o, a.part_ml,
                          (int)splits, T, nq, a.out, a.out_tok_stride);
