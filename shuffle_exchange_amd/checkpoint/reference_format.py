@@ -92,7 +92,11 @@ def _tag_dir(checkpoint_dir, tag=None):
 
 
 def _rank_files(d, suffix):
+    """Per-rank files; the reference's BF16_Optimizer writes them with a ``bf16_`` prefix
+    (runtime/engine.py:2927)."""
     files = glob.glob(os.path.join(d, f"zero_pp_rank_*_mp_rank_00{suffix}"))
+    if not files and suffix == "_optim_states.pt":
+        files = glob.glob(os.path.join(d, f"bf16_zero_pp_rank_*_mp_rank_00{suffix}"))
     return sorted(files, key=lambda f: int(re.search(r"zero_pp_rank_(\d+)_", os.path.basename(f)).group(1)))
 
 
@@ -158,6 +162,10 @@ def read_reference_checkpoint(checkpoint_dir, tag=None):
         raise FileNotFoundError(f"no zero_pp_rank_*_optim_states.pt under {d}")
     osds = [load_file(f)["optimizer_state_dict"] for f in optim_files]
     stage = _stage(osds[0])
+    if os.path.basename(optim_files[0]).startswith("bf16_") and "zero_stage" not in osds[0]:
+        # BF16_Optimizer (reference runtime/bf16_optimizer.py:467-477): ZeRO-1 layout -- fp32
+        # partitions + param_slice_mappings, base-optimizer state keyed by group index
+        stage = 1
     world = len(osds)
     model_file = os.path.join(d, "mp_rank_00_model_states.pt")
     if not os.path.exists(model_file):

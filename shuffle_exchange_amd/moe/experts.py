@@ -9,7 +9,6 @@ Every expert parameter is tagged ``allreduce = False`` and ``group_name`` (refer
 so the ZeRO optimizers reduce its gradient over the expert-data-parallel group only.
 """
 import copy
-import os
 
 import torch
 import torch.nn as nn
@@ -51,113 +50,9 @@ class GroupedSwiGLUExperts(nn.Module):
 
     def forward(self, x):
         # x: [E_local, C, H] -> [E_local, C, 2I] -> SwiGLU (one HIP launch for all experts) -> [E_local, C, H]
-        if _fused_ok(x, self.w_gate_up, self.w_down):
-            return _GroupedSwiGLU.apply(x, self.w_gate_up, self.w_down)
+        # (the dense MLP's token-minor weight-gradient scheme, ops/mlp.py, measured no faster here: the
+        # experts reduce over only C capacity tokens -- Mixtral-arch 8 layers 311.8 vs 309.9 ms/step)
         return grouped_mm(swiglu(grouped_mm(x, self.w_gate_up)), self.w_down)
-
-
-# Opt-in (SXE_MOE_TN=1): unlike the dense MLP (16k tokens of reduction) the experts' weight
-# gradients reduce over only C capacity tokens, and the token-minor TN GEMMs measured no faster
-# than the k-major wgrad kernel there (Mixtral-arch 8 layers: 311.8 vs 309.9 ms per step with
-# fp32-out accumulating GEMMs, 332.6 ms with bf16 GEMMs + fp32 add passes).
-MOE_TN = os.environ.get("SXE_MOE_TN", "0") == "1"
-
-
-def _fused_ok(x, w_gu, w_down):
-    from ..ops import native
-    if not (MOE_TN and x.is_cuda and x.dtype == torch.bfloat16 and torch.is_grad_enabled()
-            and w_gu.dtype == torch.bfloat16 and w_down.dtype == torch.bfloat16 and x.dim() == 3):
-        return False
-    E, C, H = x.shape
-    I2 = w_gu.shape[2]
-    return ((E * C) % 64 == 0 and C > 0 and H % 64 == 0 and I2 % 128 == 0 and w_down.shape[1:] == (I2 // 2, H)
-            and native.use_hip(x))
-
-
-def _expert_wgrad_tn(w, e, aT, bT, buf_acc):
-    """dW[e] = aT @ bT^T (both token-minor slices of one expert): into the optimizer target when
-    there is one (``buf_acc`` = (buf, accumulate)), else returned."""
-    if buf_acc is None:
-        return torch.mm(aT, bT.t())
-    buf, acc = buf_acc
-    if buf.dtype == torch.float32:
-        # fp32-out GEMM accumulating in its epilogue: with only C tokens of reduction a separate
-        # fp32 add pass over the expert's weight gradient would cost as much as the GEMM itself
-        torch.ops.aten.addmm.dtype_out(buf[e], aT, bT.t(), torch.float32, beta=1 if acc else 0, alpha=1,
-                                       out=buf[e])
-    else:
-        dw = torch.mm(aT, bT.t())
-        buf[e].add_(dw) if acc else buf[e].copy_(dw)
-    return None
-
-
-class _GroupedSwiGLU(torch.autograd.Function):
-    """The experts' SwiGLU MLP with the dense MLP's token-minor weight-gradient scheme (ops/mlp.py):
-    the dual-layout gated kernels write h^T / dgu^T over all E*C rows next to the token-major
-    outputs, so each expert's weight gradients are hipBLASLt "TN" GEMMs on column slices of them
-    (1.3-1.5 PF vs 1.0-1.2 PF for the k-major product at these shapes) instead of k-strided ones."""
-
-    @staticmethod
-    def forward(ctx, x, w_gu, w_down):
-        from ..ops import mlp as mlp_ops
-        E, C, H = x.shape
-        x = x.contiguous()
-        gu = x.new_empty(E, C, w_gu.shape[2])
-        for e in range(E):
-            torch.mm(x[e], w_gu[e], out=gu[e])
-        v = mlp_ops.dual_variant(w_down.shape[1])
-        h, hT = torch.ops.sxe.gated_act_fwd_dual(gu.view(E * C, -1), mlp_ops.ACT_SILU, v)
-        h = h.view(E, C, -1)
-        out = x.new_empty(E, C, H)
-        for e in range(E):
-            torch.mm(h[e], w_down[e], out=out[e])
-        del h
-        xT = torch.ops.sxe.transpose16(x.view(E * C, H)) if ctx.needs_input_grad[1] else None
-        ctx.save_for_backward(xT, gu, hT, w_gu, w_down)
-        ctx.variant = v
-        return out
-
-    @staticmethod
-    def backward(ctx, dout):
-        from ..ops import mlp as mlp_ops
-        xT, gu, hT, w_gu, w_down = ctx.saved_tensors
-        E, C, I2 = gu.shape
-        H = w_down.shape[2]
-        dout = dout.contiguous()
-        dx = dwgu = dwd = None
-        dh = dout.new_empty(E, C, I2 // 2)
-        for e in range(E):
-            torch.mm(dout[e], w_down[e].t(), out=dh[e])
-        sl = [slice(e * C, (e + 1) * C) for e in range(E)]
-        if ctx.needs_input_grad[2]:
-            doutT = torch.ops.sxe.transpose16(dout.view(E * C, H))
-            tgt = getattr(w_down, "_sxe_grad_target", None)
-            ba = tgt(w_down) if tgt is not None else None
-            parts = [_expert_wgrad_tn(w_down, e, hT[:, sl[e]], doutT[:, sl[e]], ba) for e in range(E)]
-            if ba is None:
-                dwd = torch.stack(parts)
-            else:
-                w_down._sxe_grad_done(w_down)
-            del doutT
-        del hT
-        dgu, dguT = torch.ops.sxe.gated_act_bwd_dual(dh.view(E * C, -1), gu.view(E * C, -1), mlp_ops.ACT_SILU,
-                                                     ctx.variant)
-        del dh
-        dgu = dgu.view(E, C, I2)
-        if ctx.needs_input_grad[0]:
-            dx = dout.new_empty(E, C, H)
-            for e in range(E):
-                torch.mm(dgu[e], w_gu[e].t(), out=dx[e])
-        del dgu
-        if ctx.needs_input_grad[1]:
-            tgt = getattr(w_gu, "_sxe_grad_target", None)
-            ba = tgt(w_gu) if tgt is not None else None
-            parts = [_expert_wgrad_tn(w_gu, e, xT[:, sl[e]], dguT[:, sl[e]], ba) for e in range(E)]
-            if ba is None:
-                dwgu = torch.stack(parts)
-            else:
-                w_gu._sxe_grad_done(w_gu)
-        return dx, dwgu, dwd
 
 
 class _GroupedMM(torch.autograd.Function):

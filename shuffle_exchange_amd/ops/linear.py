@@ -12,7 +12,6 @@ Megatron-style ``gradient_accumulation_fusion``; DeepSpeed's ZeRO copies each ``
 IPG bucket instead, stage_1_and_2.py:1137-1139.)
 """
 import os
-import weakref
 
 import torch
 import torch.nn.functional as F
@@ -81,41 +80,8 @@ def _tn_ok(gy2, x2):
 DGRAD_WT_MIN_ELEMS = int(os.environ.get("SXE_DGRAD_WT_MIN_ELEMS", 16 * 2**20))
 
 
-# W^T of a weight is the same for every micro-step of one optimizer step: with gradient
-# accumulation and SXE_WT_CACHE=1 the engine enables a per-step cache of the transposed weights (bounded by
-# SXE_WT_CACHE_GB; 14 GB for Llama-3-8B's projections), invalidated at every optimizer step and at
-# the first forward of each accumulation window, so only the first micro-step pays the transposes.
-# Keyed by (tensor identity, storage pointer, version counter): a weight re-gathered into another
-# buffer or modified in place through autograd-visible ops misses.
-WT_CACHE = {"enabled": False, "epoch": 0, "bytes": 0,
-            "budget": int(float(os.environ.get("SXE_WT_CACHE_GB", 16)) * 2**30), "entries": {}}
-
-
-def wt_cache_configure(enabled):
-    WT_CACHE["enabled"] = bool(enabled)
-    wt_cache_invalidate()
-
-
-def wt_cache_invalidate():
-    WT_CACHE["epoch"] += 1
-    WT_CACHE["entries"].clear()
-    WT_CACHE["bytes"] = 0
-
-
 def _transposed_weight(w):
-    c = WT_CACHE
-    if not c["enabled"]:
-        return torch.ops.sxe.transpose16(w)
-    key = id(w)
-    ent = c["entries"].get(key)
-    if ent is not None and ent[0]() is w and ent[1] == w.data_ptr() and ent[2] == w._version:
-        return ent[3]
-    wt = torch.ops.sxe.transpose16(w)
-    nbytes = wt.numel() * wt.element_size()
-    if ent is None and c["bytes"] + nbytes <= c["budget"]:
-        c["entries"][key] = (weakref.ref(w), w.data_ptr(), w._version, wt)  # weakref: ids are reused
-        c["bytes"] += nbytes
-    return wt
+    return torch.ops.sxe.transpose16(w)
 
 
 def data_grad(gy, w):

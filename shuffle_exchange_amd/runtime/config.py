@@ -18,17 +18,12 @@ from ..utils.logging import logger
 
 
 class ConfigModel(BaseModel):
-    """Base: unknown keys are kept (and warned about) so reference configs never fail to load;
-    deprecated aliases map to their new field."""
+    """Base: deprecated aliases map to their new field. Unknown keys are collected by
+    ``SXEConfig._check_unknown_keys`` after parsing: a warning naming the key (with the closest
+    known field) by default, a ``ValueError`` with ``"strict_config": true`` or SXE_STRICT_CONFIG=1
+    (the reference forbids extras in every block, runtime/config_utils.py:110 ``extra="forbid"``)."""
     model_config = ConfigDict(extra="allow", populate_by_name=True, validate_assignment=True,
                               arbitrary_types_allowed=True, protected_namespaces=())
-
-    @model_validator(mode="after")
-    def _warn_extra(self):
-        extra = getattr(self, "__pydantic_extra__", None) or {}
-        for k in extra:
-            logger.debug(f"config: unrecognized key '{k}' in {type(self).__name__} (kept, ignored)")
-        return self
 
 
 # ---------------------------------------------------------------------------------------------- ZeRO
@@ -95,11 +90,6 @@ class ZeroConfig(ConfigModel):
     defer_reduce: bool = Field(False, alias="stage3_defer_reduce")
     # ... and keeps gathered parameters resident across those micro-steps (one all-gather per step)
     retain_params: bool = Field(False, alias="stage3_retain_params_in_step")
-    # MI355X option: run each fetch group's optimizer update on a side stream in forward order so
-    # the next forward starts on the first updated group while later groups are still being stepped.
-    # Off by default: on one MI355X the overlap is real (47 of 51 ms covered) but the HBM-bound Adam
-    # and the forward slow each other by as much (Llama-3-8B bench: 24,457 vs 24,586 tok/s)
-    overlap_step: bool = Field(False, alias="stage3_overlap_step")
 
     @model_validator(mode="after")
     def _compat(self):
@@ -152,7 +142,16 @@ class BF16Config(ConfigModel):
 
 
 class DataTypesConfig(ConfigModel):
+    # None: the reference default (fp32 for bf16 without ZeRO, else the model dtype,
+    # reference runtime/engine.py:1074-1089); "fp32" with bf16 ZeRO-1 = BF16_Optimizer semantics
     grad_accum_dtype: Optional[str] = None
+
+    @model_validator(mode="after")
+    def _check(self):
+        if self.grad_accum_dtype is not None and self.grad_accum_dtype not in ("fp32", "fp16", "bf16", "float32",
+                                                                                 "float16", "bfloat16"):
+            raise ValueError(f"data_types.grad_accum_dtype must be fp32|fp16|bf16, got {self.grad_accum_dtype}")
+        return self
 
 
 class OptimizerConfig(ConfigModel):
@@ -328,6 +327,17 @@ class SXEConfigModel(ConfigModel):
     moe: MoEConfig = Field(default_factory=MoEConfig)
     amp: Dict[str, Any] = Field(default_factory=dict)
     compile: Dict[str, Any] = Field(default_factory=dict)
+    strict_config: bool = False  # new: unknown keys raise instead of warning
+
+
+# Root blocks consumed from the raw dict by their own subsystems (engine / data pipeline / compression
+# / autotuning / sparse attention ...), plus reference root keys accepted for compatibility.
+RAW_ROOT_KEYS = {
+    "data_efficiency", "curriculum_learning", "progressive_layer_drop", "quantize_training", "autotuning",
+    "compression_training", "sparse_attention", "eigenvalue", "weight_quantization", "dataloader_drop_last",
+    "bfloat16", "torch_autocast", "nebula", "monitor_config", "data_sampling", "zero_enabled", "deepcompile",
+    "timers", "use_node_local_storage", "pipeline_stage", "inference", "mesh_param",
+}
 
 
 def _load_raw(config):
@@ -392,7 +402,50 @@ class SXEConfig:
         self.scheduler_params = dict(m.scheduler.params) if m.scheduler else {}
         self.comms_logger = m.comms_logger
         self.seed = m.seed
+        if "bfloat16" in raw and "bf16" not in raw:  # reference alias (runtime/constants.py BFLOAT16_OLD)
+            self.model.bf16 = BF16Config(**raw["bfloat16"])
+        self.bfloat16_enabled = m.bf16.enabled
+        self.unknown_keys = self._check_unknown_keys()
+        self.grad_accum_dtype = self._grad_accum_dtype()
         self.ignored_knobs = self._check_ignored_knobs()
+
+    def _check_unknown_keys(self):
+        """Every key no block defines, as dotted paths. Warns (naming the closest known field) or,
+        with ``strict_config`` / SXE_STRICT_CONFIG=1, raises."""
+        import difflib
+        out = []
+
+        def walk(model, path):
+            for k in (getattr(model, "__pydantic_extra__", None) or {}):
+                if not path and k in RAW_ROOT_KEYS:
+                    continue
+                known = list(type(model).model_fields) + [f.alias for f in type(model).model_fields.values()
+                                                          if f.alias]
+                near = difflib.get_close_matches(k, known, n=1)
+                out.append((".".join(path + [k]), near[0] if near else None))
+            for name in type(model).model_fields:
+                v = getattr(model, name, None)
+                if isinstance(v, BaseModel):
+                    walk(v, path + [name])
+        walk(self.model, [])
+        if not out:
+            return []
+        msg = "; ".join(f"'{k}'" + (f" (did you mean '{n}'?)" if n else "") for k, n in out)
+        if self.model.strict_config or os.environ.get("SXE_STRICT_CONFIG", "0") == "1":
+            raise ValueError(f"config: unknown keys: {msg}")
+        logger.warning(f"config: unknown keys are ignored: {msg}")
+        return [k for k, _ in out]
+
+    def _grad_accum_dtype(self):
+        """Reference runtime/engine.py:1074-1089 get_data_types: explicit data_types.grad_accum_dtype,
+        else fp32 for bf16 without ZeRO, else the model dtype."""
+        name = self.model.data_types.grad_accum_dtype
+        if name is not None:
+            return {"fp32": "fp32", "float32": "fp32", "fp16": "fp16", "float16": "fp16", "bf16": "bf16",
+                    "bfloat16": "bf16"}[name]
+        if self.bfloat16_enabled and not self.zero_enabled:
+            return "fp32"
+        return "fp16" if self.fp16_enabled else ("bf16" if self.bfloat16_enabled else "fp32")
 
     # Reference knobs that are accepted for config compatibility but have no effect here, with the
     # reason. Setting one explicitly logs a warning (never silent); ``ignored_knobs`` lists them.

@@ -212,16 +212,21 @@ class DistributedDataAnalyzer:
 
 class CurriculumDataSampler(torch.utils.data.Sampler):
     """Yields this rank's sample indices for each global batch; difficulty threshold from a
-    ``CurriculumScheduler`` updated every batch."""
+    ``CurriculumScheduler`` updated once per global batch = once per optimizer step (reference
+    data_sampling/data_sampler.py:60,266: global_batch_size = micro x dp x gas). The global batch is
+    laid out [gas, dp, micro]: this rank's indices come out as ``gas`` consecutive micro-batches."""
 
     def __init__(self, metric_values, scheduler, global_batch_size, dp_rank=0, dp_size=1, seed=1234,
-                 total_steps=None):
+                 total_steps=None, gradient_accumulation_steps=1):
         self.metric = np.asarray(metric_values)
         self.order = np.argsort(self.metric, kind="stable")
         self.sorted_vals = self.metric[self.order]
         self.sched = scheduler
         self.gbs = global_batch_size
+        self.gas = max(1, int(gradient_accumulation_steps))
         self.rank, self.size = dp_rank, dp_size
+        if self.gbs % (self.size * self.gas):
+            raise ValueError(f"global batch {self.gbs} not divisible by dp {self.size} x gas {self.gas}")
         self.seed = seed
         self.step = 0
         self.total_steps = total_steps
@@ -243,8 +248,8 @@ class CurriculumDataSampler(torch.utils.data.Sampler):
         n_ok = max(n_ok, self.gbs)
         rng = np.random.default_rng(self.seed + self.step)
         picks = self.order[rng.choice(n_ok, size=self.gbs, replace=n_ok < self.gbs)]
-        per = self.gbs // self.size
-        return picks[self.rank * per:(self.rank + 1) * per].tolist()
+        micro = self.gbs // (self.size * self.gas)
+        return picks.reshape(self.gas, self.size, micro)[:, self.rank, :].reshape(-1).tolist()
 
     def __iter__(self):
         steps = self.total_steps or (len(self.metric) // self.gbs)

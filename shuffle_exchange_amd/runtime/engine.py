@@ -23,7 +23,6 @@ import torch.nn as nn
 
 from .. import comm as dist
 from ..accelerator import get_accelerator
-from ..ops import linear as _linear_ops
 from ..ops import optim as fused
 from ..parallel import groups
 from ..utils.logging import log_dist, logger
@@ -121,7 +120,6 @@ class SXEEngine(nn.Module):
         self.global_steps = 0
         self.global_samples = 0
         self.micro_steps = 0
-        self._wt_cache = None  # per-step transposed-weight cache (ops/linear.py), set on first forward
         self.skipped_steps = 0
         self.gradient_average = True
         self._in_no_sync = False
@@ -266,10 +264,9 @@ class SXEEngine(nn.Module):
         if len(vals) != len(dataset):
             raise ValueError(f"curriculum metric {name}: {len(vals)} values for {len(dataset)} samples")
         sched = CurriculumScheduler(mc)
-        return CurriculumDataSampler(vals, sched, self.train_batch_size() // self.gradient_accumulation_steps(),
-                                     dp_rank=groups.get_data_parallel_rank(),
-                                     dp_size=groups.get_data_parallel_world_size(),
-                                     seed=self._de.get("seed", 1234))
+        return CurriculumDataSampler(vals, sched, self.train_batch_size(), dp_rank=groups.get_data_parallel_rank(),
+                                     dp_size=groups.get_data_parallel_world_size(), seed=self._de.get("seed", 1234),
+                                     gradient_accumulation_steps=self.gradient_accumulation_steps())
 
     def curriculum_enabled_legacy(self):
         return self.curriculum_scheduler_legacy is not None
@@ -480,14 +477,24 @@ class SXEEngine(nn.Module):
                 defer_reduce=zc.defer_reduce, retain_params=zc.retain_params, loco_param=zc.zeropp_loco_param,
                 prefetch_bucket_size=(zc.prefetch_bucket_size if "prefetch_bucket_size" in zc.model_fields_set
                                       and "prefetch_depth" not in zc.model_fields_set else None),
-                model_persistence_threshold=zc.model_persistence_threshold, param_swap=param_swap,
-                overlap_step=zc.overlap_step)
+                model_persistence_threshold=zc.model_persistence_threshold, param_swap=param_swap)
+        elif stage == 1 and dtype == torch.bfloat16 and cfg.grad_accum_dtype == "fp32" and host_step is None:
+            # reference engine.py:1384-1386: bf16 + ZeRO-1 + fp32 gradient accumulation -> BF16_Optimizer
+            from .bf16_optimizer import BF16_Optimizer
+            self.optimizer = BF16_Optimizer(
+                basic, clip_grad=cfg.gradient_clipping, allgather_bucket_size=zc.reduce_bucket_size,
+                dp_process_group=dp_group, dp_ranks=dp_ranks, timers=self.timers, grad_acc_dtype=torch.float32,
+                communication_data_type=self.communication_data_type, overlap_comm=zc.overlap_comm,
+                mp_group=mp_group, loss_scaler=scaler, shuffle_exchange_cfg=se)
+            if zc.overlap_comm:
+                self.optimizer.attach_module(self.module)
         elif stage in (1, 2):
             self.optimizer = ZeroStage12Optimizer(
                 basic, stage=stage, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks,
                 dp_group=dp_group, reduce_bucket_size=zc.reduce_bucket_size,
                 communication_data_type=self.communication_data_type, overlap_comm=zc.overlap_comm,
-                shuffle_exchange_cfg=se, mp_group=mp_group, timers=self.timers, host_step=host_step)
+                shuffle_exchange_cfg=se, mp_group=mp_group, timers=self.timers, host_step=host_step,
+                fp32_accum=(stage == 1 and dtype != torch.float32 and cfg.grad_accum_dtype == "fp32"))
             if zc.overlap_comm:
                 self.optimizer.attach_module(self.module)
         else:
@@ -498,7 +505,8 @@ class SXEEngine(nn.Module):
                         m.weight._sxe_sparse = True
             self.optimizer = DataParallelOptimizer(
                 basic, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks, dp_group=dp_group,
-                bucket_size=zc.reduce_bucket_size, mp_group=mp_group, shuffle_exchange_cfg=se)
+                bucket_size=zc.reduce_bucket_size, mp_group=mp_group, shuffle_exchange_cfg=se,
+                fp32_accum=(dtype != torch.float32 and cfg.grad_accum_dtype == "fp32"))
 
         self.optimizer.sp_scale = float(cfg.sequence_parallel_size)
 
@@ -548,15 +556,6 @@ class SXEEngine(nn.Module):
             self._tput_start(inputs, kwargs)
         if self.optimizer is not None and hasattr(self.optimizer, "forward_prologue"):
             self.optimizer.forward_prologue()
-        if self._wt_cache is None:
-            # opt-in (SXE_WT_CACHE=1), and only when several micro-steps share one set of weights:
-            # measured neutral on the 8B bench (24,932 vs 24,940 tok/s, +14 GB peak HBM)
-            self._wt_cache = (self.device.type == "cuda" and self.gradient_accumulation_steps() > 1
-                              and os.environ.get("SXE_WT_CACHE", "0") == "1")
-            if self._wt_cache:
-                _linear_ops.wt_cache_configure(True)
-        if self._wt_cache and self.micro_steps % self.gradient_accumulation_steps() == 0:
-            _linear_ops.wt_cache_invalidate()  # a new accumulation window: weights may have changed
         if self.progressive_layer_drop is not None:
             kwargs.update(self.progressive_layer_drop.get_state())
         if self.curriculum_scheduler_legacy is not None:
@@ -627,8 +626,6 @@ class SXEEngine(nn.Module):
         boundary = self.is_gradient_accumulation_boundary() if boundary is None else boundary
         if boundary:
             self._take_model_step(lr_kwargs)
-            if self._wt_cache:
-                _linear_ops.wt_cache_invalidate()  # updated weights: drop the transposed copies
         self.micro_steps += 1
         self._boundary_override = None
         self.timers(STEP_MICRO_TIMER).stop()
@@ -742,7 +739,44 @@ class SXEEngine(nn.Module):
                 dist.barrier()
                 raise SystemExit(0)
 
+    def _defer_skip(self, skip_t, lr_kwargs):
+        host = getattr(self, "_skip_host", None)
+        if host is None:
+            host = self._skip_host = torch.zeros(1, dtype=torch.float32, pin_memory=skip_t.is_cuda)
+        host.copy_(skip_t.reshape(-1)[:1], non_blocking=skip_t.is_cuda)
+        ev = None
+        if skip_t.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+        self._pending_skip = (ev, dict(lr_kwargs or {}))
+
+    def _resolve_skip(self):
+        """Apply the previous step's deferred non-finite verdict: count it, or advance the LR."""
+        pend = self.__dict__.get("_pending_skip")
+        if pend is None:
+            return
+        self._pending_skip = None
+        ev, kw = pend
+        if ev is not None:
+            ev.synchronize()
+        if float(self._skip_host[0]) != 0.0:
+            self._skipped_steps += 1
+            log_dist(f"step {self.global_steps}: non-finite gradients, update skipped", ranks=[0])
+        elif self.lr_scheduler is not None:
+            self.lr_scheduler.step(**kw)
+
+    @property
+    def skipped_steps(self):
+        self._resolve_skip()
+        return self._skipped_steps
+
+    @skipped_steps.setter
+    def skipped_steps(self, v):
+        self.__dict__["_pending_skip"] = None
+        self._skipped_steps = v
+
     def _take_model_step(self, lr_kwargs=None):
+        self._resolve_skip()
         off = getattr(self, "_offload_opt_states", False)
         if off:
             self.optimizer.reload_states()
@@ -755,8 +789,16 @@ class SXEEngine(nn.Module):
         if self.quantizer is not None and self.zero_optimization_stage() < 3:
             self.quantizer.quantize([[p for p in self.module.parameters() if p.requires_grad]], overflow)
         self.optimizer.zero_grad()
+        skip_t = getattr(self.optimizer, "_skip_t", None)
         if overflow:
             self.skipped_steps += 1
+        elif skip_t is not None and not getattr(self.optimizer.loss_scaler, "dynamic", False):
+            # bf16 / static-scale step: the non-finite check stayed on the device (the fused kernel
+            # skipped the update itself). Its verdict is read one step later, when it is long
+            # computed -- the scheduler advances (or the skip is counted) before the next update
+            # reads the LR, so the schedule matches the reference's per-step host check
+            # (engine.py:2376-2390) without a host sync in step()
+            self._defer_skip(skip_t, lr_kwargs)
         elif self.lr_scheduler is not None:
             self.lr_scheduler.step(**(lr_kwargs or {}))
         self.global_steps += 1
@@ -876,6 +918,7 @@ class SXEEngine(nn.Module):
         return static_out
 
     def get_lr(self):
+        self._resolve_skip()
         return [g["lr"] for g in self.optimizer.param_groups] if self.optimizer is not None else []
 
     def get_global_grad_norm(self):
@@ -911,7 +954,10 @@ class SXEEngine(nn.Module):
             model = os.path.join(d, f"zero_pp_rank_{dp}_mp_rank_{mp:02d}_model_states.pt")
         else:
             model = os.path.join(d, f"mp_rank_{mp:02d}_model_states.pt")
-        prefix = "bf16_" if (self.bfloat16_enabled() and stage == 0) else ""
+        from .bf16_optimizer import BF16_Optimizer
+        # reference engine.py:2927: BF16_Optimizer (bf16 at stage 0, or stage 1 + fp32 accumulation)
+        prefix = "bf16_" if (self.bfloat16_enabled() and stage == 0) or isinstance(self.optimizer,
+                                                                                     BF16_Optimizer) else ""
         optim = os.path.join(d, f"{prefix}zero_pp_rank_{dp}_mp_rank_{mp:02d}_optim_states.pt")
         return d, model, optim
 
@@ -956,6 +1002,7 @@ class SXEEngine(nn.Module):
     def save_checkpoint(self, save_dir, tag=None, client_state=None, save_latest=True,
                         exclude_frozen_parameters=False):
         client_state = client_state or {}
+        self._resolve_skip()
         if tag is None:
             tag = f"global_step{self.global_steps}"
         tag = str(tag)

@@ -25,12 +25,16 @@ from .flat import FlatUnit, split_into_units
 
 class DataParallelOptimizer(ZeroOptimizerBase):
     def __init__(self, init_optimizer, *, loss_scaler, clip_grad=0.0, dp_ranks=None, dp_group=None,
-                 bucket_size=500_000_000, mp_group=None, shuffle_exchange_cfg=None):
+                 bucket_size=500_000_000, mp_group=None, shuffle_exchange_cfg=None, fp32_accum=False):
         acc = get_accelerator()
         device = torch.device(acc.current_device_name())
         super().__init__(init_optimizer, loss_scaler, clip_grad, None, overflow_group=None, mp_group=mp_group,
                          device=device)
         self.dp_group = dp_group
+        # bf16 without ZeRO accumulates micro-step gradients in fp32 (reference default grad_accum_dtype,
+        # engine.py:1081-1085 -> BF16_Optimizer): every micro-step's .grad is added to the unit's fp32
+        # accumulator right away instead of accumulating in the bit16 .grad until the boundary
+        self.fp32_accum = bool(fp32_accum)
         self.dp_size = len(dp_ranks) if dp_ranks is not None else dist.get_world_size()
         self.comm_stream = acc.named_stream("dp_reduce") if acc.gpu else None
         self.boundary = True
@@ -54,6 +58,7 @@ class DataParallelOptimizer(ZeroOptimizerBase):
                 u.rgroup, u.rsize = rgroup, rsize
                 u.sparse = getattr(plist[0], "_sxe_sparse", False)
                 u.sparse_parts = []
+                u.dense_seen = False
                 units.append(u)
                 for p in plist:
                     self.param_unit[p] = u
@@ -90,6 +95,10 @@ class DataParallelOptimizer(ZeroOptimizerBase):
         if u.sparse and p.grad.is_sparse:
             u.sparse_parts.append(p.grad.coalesce())
         else:
+            if u.sparse:
+                # a sparse-marked weight that received a dense gradient (e.g. an embedding tied to
+                # the LM head: sparse + dense = dense): this window's reduce must be the dense one
+                u.dense_seen = True
             o, n = u.offsets[i], u.numels[i]
             g = p.grad.to_dense() if p.grad.is_sparse else p.grad
             u.grad[o:o + n].add_(g.reshape(-1))
@@ -97,7 +106,11 @@ class DataParallelOptimizer(ZeroOptimizerBase):
 
     def _make_hook(self, u):
         def hook(p):
-            if p.grad is None or not self.boundary:
+            if p.grad is None:
+                return
+            if not self.boundary:
+                if self.fp32_accum:
+                    self._take_grad(u, u.param_index[id(p)], p)
                 return
             i = u.param_index[id(p)]
             self._take_grad(u, i, p)
@@ -123,6 +136,8 @@ class DataParallelOptimizer(ZeroOptimizerBase):
         u.sparse_parts = []
         if u.rsize == 1:
             dense.index_add_(0, idx, val)
+            if self.sp_scale != 1.0:
+                dense.mul_(self.sp_scale)
             return
         n = torch.tensor([idx.numel()], dtype=torch.long, device=dense.device)
         ns = [torch.zeros_like(n) for _ in range(u.rsize)]
@@ -142,7 +157,16 @@ class DataParallelOptimizer(ZeroOptimizerBase):
         dense.mul_(self.sp_scale / u.rsize)
 
     def _allreduce_unit(self, u):
-        if u.sparse and not u.reduced:
+        if u.sparse and u.dense_seen and u.sparse_parts:
+            # mixed window: fold the sparse rows into the dense accumulator, reduce densely
+            p = u.params[0]
+            g = torch.sparse_coo_tensor(torch.cat([t.indices() for t in u.sparse_parts], 1),
+                                        torch.cat([t.values() for t in u.sparse_parts], 0), p.shape).coalesce()
+            width = p.numel() // p.shape[0]
+            u.grad[:u.numel].view(p.shape[0], width).index_add_(0, g.indices()[0],
+                                                                 g.values().reshape(-1, width).to(u.grad.dtype))
+            u.sparse_parts = []
+        if u.sparse and not u.dense_seen and not u.reduced:
             u.reduced = True
             self._sparse_allreduce_unit(u)
             return
@@ -190,6 +214,12 @@ class DataParallelOptimizer(ZeroOptimizerBase):
         self._fused_update(coef, skip)
         self.zero_grad_buffers()
         self.global_step += 1
+
+    def zero_grad_buffers(self):
+        super().zero_grad_buffers()
+        for units in self.units:
+            for u in units:
+                u.dense_seen = False
 
     def zero_grad(self, set_to_none=True):
         for p in self.param_unit:

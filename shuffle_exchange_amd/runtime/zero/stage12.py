@@ -31,7 +31,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
     def __init__(self, init_optimizer, *, stage=2, loss_scaler, clip_grad=0.0, dp_ranks=None, dp_group=None,
                  reduce_bucket_size=500_000_000, communication_data_type=None, overlap_comm=True,
                  shuffle_exchange_cfg=None, method=None, slice_count=None, rings=None, shuffle_step=None,
-                 mp_group=None, timers=None, average_master=False, host_step=None):
+                 mp_group=None, timers=None, average_master=False, host_step=None, fp32_accum=False):
         acc = get_accelerator()
         device = torch.device(acc.current_device_name())
         self.stage = stage
@@ -57,6 +57,11 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         super().__init__(init_optimizer, loss_scaler, clip_grad, slice_group, overflow_group=world_group,
                          mp_group=mp_group, device=device)
         self.host_step = host_step
+        # data_types.grad_accum_dtype == fp32 at stage 1 (reference BF16_Optimizer semantics,
+        # runtime/bf16_optimizer.py:35, engine.py:1384-1386): micro-step gradients are summed in a
+        # full-size fp32 buffer per unit instead of the bit16 .grad, and reduced (in fp32 unless
+        # communication_data_type says otherwise) once at the accumulation boundary
+        self.fp32_accum = bool(fp32_accum) and stage == 1
         self.comm_dtype = communication_data_type
         self.overlap_comm = overlap_comm
         self.comm_stream = acc.named_stream("zero_reduce") if (overlap_comm and acc.gpu) else None
@@ -78,6 +83,8 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                 gt = self._group_topo(pg)
                 u = FlatUnit(plist, gt.S, gt.offset, dtype, device, name=f"g{g}u{i}", index=i)
                 u.topo = gt
+                if self.fp32_accum:
+                    u.staging_dtype = torch.float32
                 units.append(u)
                 for p in plist:
                     self.param_unit[p] = u
@@ -141,9 +148,13 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
 
     def _make_hook(self, unit):
         def hook(p):
-            if not self.micro_step_boundary and self.stage == 1:
-                return  # ZeRO-1 keeps accumulating full grads until the boundary
             if p.grad is None:
+                return
+            if not self.micro_step_boundary and self.stage == 1:
+                # ZeRO-1 keeps accumulating full grads until the boundary: in the bit16 .grad
+                # (autograd's own accumulation), or with fp32_accum in the unit's fp32 buffer
+                if self.fp32_accum:
+                    self._accumulate_fp32(unit, p)
                 return
             if unit.topo.S == 1:
                 i = unit.param_index[id(p)]
@@ -158,6 +169,15 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                 self._reduce_unit(unit)
         return hook
 
+    def _accumulate_fp32(self, unit, p):
+        if unit.topo.S == 1:
+            i = unit.param_index[id(p)]
+            o, n = unit.offsets[i], unit.numels[i]
+            unit.grad[o:o + n].add_(p.grad.reshape(-1))
+        else:
+            unit.stage_grad(p, p.grad)  # fp32 staging (staging_dtype), no reduce before the boundary
+        p.grad = None
+
     def set_gradient_accumulation_boundary(self, flag):
         self.micro_step_boundary = bool(flag)
 
@@ -169,6 +189,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
     def _reduce_unit(self, u):
         st = u.staging
         u.staging = None
+        u.carry = False
         cur = torch.cuda.current_stream() if st.is_cuda else None
         stream = self.comm_stream
         if stream is not None:
@@ -187,6 +208,14 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         """Backward epilogue: reduce units whose params did not all produce grads (unused params)
         and, for ZeRO-1 at the boundary, everything still pending."""
         if self.stage == 1 and not self.micro_step_boundary:
+            if self.fp32_accum:  # the fp32 staging sums carry into the next micro-step
+                for units in self.units:
+                    for u in units:
+                        for i, p in enumerate(u.params):
+                            if p.grad is not None:  # no hook fired (e.g. grads set outside autograd)
+                                self._accumulate_fp32(u, p)
+                        if u.staging is not None:
+                            u.carry = True
             return
         for units in self.units:
             for u in units:

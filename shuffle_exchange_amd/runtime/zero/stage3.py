@@ -111,7 +111,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                  quantized_gradients=False, hpz_partition_size=1, quant_group_size=128, grad_quant_bits=8,
                  max_reuse_distance=1_000_000_000, max_live_parameters=1_000_000_000, defer_reduce=False,
                  retain_params=False, loco_param=None, prefetch_bucket_size=None,
-                 model_persistence_threshold=2**63 - 1, param_swap=None, overlap_step=False):
+                 model_persistence_threshold=2**63 - 1, param_swap=None):
         acc = get_accelerator()
         device = torch.device(acc.current_device_name())
         self.module = module
@@ -197,8 +197,6 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         self.rs_stream = acc.named_stream("zero3_reduce") if acc.gpu and comm else None
         # the optimizer-step stream is created high-priority: HIP serves high-priority streams from
         # their own queue pool, so it never lands on the compute stream's queue
-        self.opt_stream = acc.named_stream("zero3_step", priority=-1) if acc.gpu and overlap_step else None
-        self._opt_events = {}  # fetch group idx -> event of its overlapped optimizer update
         self._in_bwd = False
         self._hooks = []
         self.fgroups = []
@@ -545,10 +543,6 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             sa.record_stream(st)
 
     def _fetch(self, fg, wait=True):
-        if self._opt_events:
-            ev = self._opt_events.pop(fg.idx, None)
-            if ev is not None:  # the group's overlapped optimizer update (step) must land first
-                torch.cuda.current_stream().wait_event(ev)
         for u in fg.units:
             if u.persistent:
                 continue
@@ -757,63 +751,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
 
     # ------------------------------------------------------------------------------------------ step
     def wait_params(self):
-        """Make the current stream wait for every in-flight overlapped optimizer update."""
-        if self._opt_events:
-            cur = torch.cuda.current_stream()
-            for ev in self._opt_events.values():
-                cur.wait_event(ev)
-            self._opt_events.clear()
-
-    def _overlap_ok(self):
-        return (self.opt_stream is not None and self.kind == "adam" and self.host_step is None and self.se is None
-                and not self.qwz and self.pswap is None and not self.offload_param and self.hpz == 1
-                and all(m.is_cuda for m in self.master))
-
-    def _overlapped_update(self, coef, skip):
-        """The fused Adam of ``_fused_update``, one launch per fetch group in forward order on the
-        step stream; each group's event is waited for by its next fetch (``_fetch``), so the next
-        forward runs on the updated first groups while the later ones are still being stepped.
-        Persistent units of a multi-rank group re-gather their full weight on the all-gather
-        stream behind the group's update (one collective stream, host issue order)."""
-        st = self.opt_stream
-        st.wait_stream(torch.cuda.current_stream())
-        offs, steps = {}, []
-        for g, units in enumerate(self.units):
-            pg = self.optimizer.param_groups[g]
-            state = self.optimizer.state[self.master[g]]
-            state["step"] = int(state.get("step", 0)) + 1
-            steps.append((pg, state))
-            for u, o in zip(units, self._unit_offsets(g)):
-                offs[u] = (g, o)
-        order = list(self.trace) + [fg.idx for fg in self.fgroups if fg.idx not in set(self.trace)]
-        for fi in order:
-            fg = self.fgroups[fi]
-            with get_accelerator().stream(st):
-                byg = {}
-                for u in fg.units:
-                    byg.setdefault(offs[u][0], []).append(u)
-                for g, us in byg.items():
-                    pg, state = steps[g]
-                    b1, b2 = pg["betas"]
-                    torch.ops.sxe.multi_tensor_adam_(
-                        [u.master for u in us], [u.grad for u in us],
-                        [state["exp_avg"][offs[u][1]:offs[u][1] + u.chunk] for u in us],
-                        [state["exp_avg_sq"][offs[u][1]:offs[u][1] + u.chunk] for u in us],
-                        [u.shard for u in us], coef, skip, float(pg["lr"]), float(b1), float(b2), float(pg["eps"]),
-                        float(pg["weight_decay"]), int(state["step"]), bool(self.adamw),
-                        bool(pg.get("bias_correction", True)), 1.0)
-                ev = torch.cuda.Event()
-                ev.record(st)
-            if self.S > 1 and any(u.persistent for u in fg.units):
-                ag = self.ag_stream
-                ag.wait_event(ev)
-                with get_accelerator().stream(ag):
-                    for u in fg.units:
-                        if u.persistent:
-                            dist.all_gather_into_tensor(u.flat, u.shard, group=self.topo.slice_group)
-                    ev = torch.cuda.Event()
-                    ev.record(ag)
-            self._opt_events[fi] = ev
+        """Nothing in flight across steps: the update runs on the compute stream."""
 
     def step(self, closure=None, lr_kwargs=None):
         self.wait_params()
@@ -825,13 +763,6 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         coef, skip = self._grad_norm_and_flags()
         if getattr(self.loss_scaler, "dynamic", False) and self._handle_overflow_host():
             self.zero_grad_buffers()
-            return
-        if self._overlap_ok():
-            self._overlapped_update(coef, skip)
-            self.zero_grad_buffers()
-            self.global_step += 1
-            for j in self.trace[:self.prefetch_depth]:
-                self._fetch(self.fgroups[j], wait=False)
             return
         self._fused_update(coef, skip)
         self.zero_grad_buffers()

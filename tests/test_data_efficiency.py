@@ -85,6 +85,27 @@ def test_curriculum_sampler_engine_wiring(tmp_path):
     assert max(res[0]["batches"][0] + res[1]["batches"][0]) <= 16
 
 
+def test_curriculum_difficulty_advances_per_optimizer_step():
+    """gas > 1: the difficulty schedule advances once per GLOBAL batch (micro x dp x gas), and the
+    rank's share of one global batch comes out as gas micro-batches (reference data_sampler.py:60,266;
+    ADVICE r02). Before the fix it advanced once per micro-batch, gas times too fast."""
+    from shuffle_exchange_amd.runtime.data_pipeline import CurriculumDataSampler, CurriculumScheduler
+    metric = np.arange(256, dtype=np.float64)
+    cfg = {"curriculum_type": "seqlen", "min_difficulty": 16, "max_difficulty": 255, "schedule_type": "fixed_linear",
+           "schedule_config": {"total_curriculum_step": 10, "difficulty_step": 1}}
+    micro, dp, gas = 2, 2, 4
+    samplers = [CurriculumDataSampler(metric, CurriculumScheduler(dict(cfg)), micro * dp * gas, dp_rank=r, dp_size=dp,
+                                      gradient_accumulation_steps=gas, total_steps=6) for r in range(dp)]
+    streams = [list(iter(s)) for s in samplers]
+    per_step = micro * gas
+    for step in range(6):
+        thr = CurriculumScheduler(dict(cfg)).update_difficulty(step + 1)
+        both = sum((st[step * per_step:(step + 1) * per_step] for st in streams), [])
+        assert len(set(both)) == len(both) == micro * dp * gas  # one global batch, no overlap
+        assert max(both) <= max(thr, micro * dp * gas - 1), (step, max(both), thr)
+    assert samplers[0].step == 6  # one scheduler step per optimizer step, not per micro-batch
+
+
 class _Toks(torch.utils.data.Dataset):
     def __init__(self, n=97):
         g = torch.Generator().manual_seed(0)

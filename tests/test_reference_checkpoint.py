@@ -68,7 +68,9 @@ def _synthetic_state():
     return [n for n, _ in named], fp32, m, v
 
 
-def write_reference_checkpoint(d, stage, dp, step=7):
+def write_reference_checkpoint(d, stage, dp, step=7, bf16_optimizer=False):
+    """``bf16_optimizer``: the reference BF16_Optimizer's files (runtime/bf16_optimizer.py:467-477:
+    no zero_stage / loss scaler keys, ``bf16_zero_pp_rank_*`` names, engine.py:2927)."""
     mods, DLS, ZSE, FA = _fake_reference_modules()
     names, fp32, m, v = _synthetic_state()
     saved = {k: sys.modules.get(k) for k in mods}
@@ -109,8 +111,13 @@ def write_reference_checkpoint(d, stage, dp, step=7):
                        "single_partition_of_fp32_groups": [pad(flat["p"])[:max(0, min(hi, total) - lo)]],
                        "zero_stage": ZSE(stage), "group_paddings": [padded - total if r == dp - 1 else 0],
                        "partition_count": [dp], "ds_version": "0.16.0", "param_slice_mappings": [mapping]}
+                prefix = ""
+                if bf16_optimizer:
+                    for k in ("loss_scaler", "dynamic_loss_scale", "overflow", "zero_stage"):
+                        osd.pop(k)
+                    prefix = "bf16_"
                 torch.save({"optimizer_state_dict": osd, "ds_config": {}, "ds_version": "0.16.0"},
-                           os.path.join(tag_dir, f"zero_pp_rank_{r}_mp_rank_00_optim_states.pt"))
+                           os.path.join(tag_dir, f"{prefix}zero_pp_rank_{r}_mp_rank_00_optim_states.pt"))
         else:
             for r in range(dp):
                 torch.save(dict(model_states, module={}),
@@ -171,6 +178,19 @@ def test_resume_from_reference_layout_checkpoint(tmp_path, saved_stage, saved_dp
             assert torch.allclose(r["fp32"][n], fp32[n], atol=1e-7), n
             assert torch.allclose(r["m"][n], m[n], atol=1e-9), n
             assert torch.allclose(r["v"][n], v[n], atol=1e-9), n
+
+
+def test_resume_from_reference_bf16_optimizer_checkpoint(tmp_path):
+    """Files of the reference's BF16_Optimizer (bf16_ prefix, ZeRO-1 schema without zero_stage) are
+    detected as reference format and resume exactly."""
+    from shuffle_exchange_amd.checkpoint.reference_format import is_reference_checkpoint
+    fp32, m, v = write_reference_checkpoint(str(tmp_path), 1, 2, bf16_optimizer=True)
+    assert is_reference_checkpoint(str(tmp_path))
+    for r in run_dist(_case_resume, 2, str(tmp_path), 1):
+        assert r["steps"] == 7
+        for n in fp32:
+            assert torch.allclose(r["fp32"][n], fp32[n], atol=1e-7), n
+            assert torch.allclose(r["m"][n], m[n], atol=1e-9), n
 
 
 def test_zero_to_fp32_reads_reference_layout(tmp_path):

@@ -97,42 +97,3 @@ def test_zero_init_gpu_memory_two_ranks():
         assert r["held"] <= r["full"] / 2 + (4 << 20), r
         assert r["peak"] <= r["full"] / 2 + 2 * max(r["layer"], 8192 * 1024 * 2) + (16 << 20), r
         assert r["peak"] < 0.75 * r["full"], r
-
-
-def _case_overlap(rank, world, overlap):
-    os.environ["LOCAL_RANK"] = "0"
-    import shuffle_exchange_amd as sxe
-    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
-    torch.cuda.set_device(0)
-    torch.manual_seed(0)
-    cfg = llama_config("llama-tiny", hidden_size=256, intermediate_size=512, num_attention_heads=2,
-                       num_key_value_heads=1, vocab_size=1024, num_hidden_layers=2)
-    model = LlamaForCausalLM(cfg)
-    ds = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": 2, "bf16": {"enabled": True},
-          "gradient_clipping": 1.0,
-          "zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 1000,
-                                "stage3_overlap_step": overlap},
-          "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}}}
-    eng, _, _, _ = sxe.initialize(model=model, config=ds)
-    g = torch.Generator().manual_seed(7)
-    for _ in range(3):
-        for _ in range(2):
-            ids = torch.randint(0, cfg.vocab_size, (2 * world, 128), generator=g)
-            local = ids[rank * 2:(rank + 1) * 2].cuda()
-            loss = eng(local, labels=local)
-            eng.backward(loss)
-            eng.step()
-    used = eng.optimizer._overlap_ok()
-    torch.cuda.synchronize()
-    return {"params": C.full_params(eng), "used": used}
-
-
-@pytest.mark.parametrize("world", [1, 2])
-def test_zero3_overlapped_step_matches(world):
-    """stage3_overlap_step (per-group Adam on a side stream, waited for by each group's next fetch;
-    persistent units re-gathered on the all-gather stream) gives bitwise the same parameters."""
-    a = run_dist(_case_overlap, world, True)
-    b = run_dist(_case_overlap, world, False)
-    assert a[0]["used"] and not b[0]["used"]
-    for k in a[0]["params"]:
-        assert torch.equal(a[0]["params"][k], b[0]["params"][k]), k

@@ -324,3 +324,42 @@ def test_sparse_embedding_gradients_stage0():
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
     for a, b in zip(sp[0]["params"], sp[1]["params"]):
         assert torch.equal(a, b)
+
+
+class _TiedEmbNet(torch.nn.Module):
+    """Sparse embedding tied to the output projection: its gradient is sparse + dense = dense."""
+
+    def __init__(self, sparse):
+        super().__init__()
+        torch.manual_seed(0)
+        self.emb = torch.nn.Embedding(64, 16, sparse=sparse)
+
+    def forward(self, ids):
+        h = self.emb(ids)
+        return (h @ self.emb.weight.t()).pow(2).mean()
+
+
+def _case_tied_sparse(rank, world, sparse):
+    import shuffle_exchange_amd as sxe
+    model = _TiedEmbNet(sparse)
+    ds = {"train_micro_batch_size_per_gpu": 4, "gradient_accumulation_steps": 2, "sparse_gradients": sparse,
+          "zero_optimization": {"stage": 0}, "optimizer": {"type": "AdamW", "params": {"lr": 1e-2}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    g = torch.Generator().manual_seed(5)
+    for _ in range(4):
+        ids = torch.randint(0, 64, (world * 4, 7), generator=g)[rank * 4:(rank + 1) * 4]
+        loss = eng(ids)
+        eng.backward(loss)
+        eng.step()
+    return [p.detach().clone() for p in eng.module.parameters()]
+
+
+def test_sparse_marked_weight_with_dense_gradient_stays_in_sync():
+    """A sparse-marked weight that receives a dense gradient is reduced densely: replicas stay
+    identical and equal the dense run (the dense part was never reduced before)."""
+    sp = run_dist(_case_tied_sparse, 2, True)
+    dn = run_dist(_case_tied_sparse, 2, False)
+    for a, b in zip(sp[0], sp[1]):
+        assert torch.equal(a, b)
+    for a, b in zip(sp[0], dn[0]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
