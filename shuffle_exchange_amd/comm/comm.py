@@ -14,7 +14,15 @@ logger via ``timed_op`` :102-135) and deepspeed/comm/torch.py (``TorchBackend`` 
   the race/ordering detector SURVEY §5.2 asks for (it catches e.g. ranks whose shuffle RNG
   diverged, which deadlocks or silently mis-averages in the reference).
 * a comms logger reporting per-op latency, algbw and busbw (busbw uses the ring factors of each
-  collective, so it is directly comparable to the per-link xGMI bandwidth).
+  collective, so it is directly comparable to the per-link xGMI bandwidth), and always-on per-op
+  byte counters (``get_comm_volume``, no device sync) that bench.py reports per step.
+* a test-only **deferred-completion mode** (``set_deferred_completion`` / SXE_COMM_DEFER=1): every
+  collective's output reads as NaN until the consumer has synchronised with it -- for device
+  tensors, the true result lands on the issuing stream only after a spin delay, so a consumer on
+  another stream that skipped its ``wait_event``/``wait_stream`` reads NaN; for async host ops the
+  result appears at ``Work.wait()``. The gloo parity suites run under it to prove every consumer of
+  an overlapped collective synchronises before RCCL ever runs the code (RCCL completes
+  asynchronously on its own stream; gloo and world-size-1 shortcuts complete immediately).
 """
 import datetime
 import hashlib
@@ -46,6 +54,9 @@ class _State:
     logger_prof_ops = []
     comms = defaultdict(lambda: defaultdict(list))  # op -> msg_size -> [latency_ms...]
     op_counts = defaultdict(int)  # log_name -> collectives issued (always counted, no sync)
+    volume = defaultdict(lambda: [0, 0])  # op -> [calls, payload bytes] (always counted, no sync)
+    defer = os.environ.get("SXE_COMM_DEFER", "0") == "1"
+    defer_cycles = int(os.environ.get("SXE_COMM_DEFER_CYCLES", 2_000_000))
 
 
 # ------------------------------------------------------------------------------------------------
@@ -220,8 +231,87 @@ def _bus_factor(op, n):
     return 1.0
 
 
-def _timed(op, fn, tensor, group, async_op):
+def _payload(op, tensor, group):
+    size = (tensor.numel() * tensor.element_size()) if isinstance(tensor, torch.Tensor) else \
+        sum(x.numel() * x.element_size() for x in tensor)
+    if op in ("all_gather_into_tensor", "all_gather"):
+        size *= get_world_size(group)
+    return size
+
+
+def get_comm_volume():
+    """{op: (calls, payload bytes)} since the last ``reset_comms_stats()``. Payload as in
+    rccl-tests: the gathered output for all-gathers, the input for reduce-scatter / all-reduce /
+    all-to-all / broadcast, the message for point-to-point."""
+    return {op: (v[0], v[1]) for op, v in _State.volume.items()}
+
+
+def set_deferred_completion(on=True, cycles=None):
+    _State.defer = bool(on)
+    if cycles is not None:
+        _State.defer_cycles = int(cycles)
+
+
+class _DeferredWork:
+    """Async handle whose result becomes visible at ``wait()`` (deferred-completion mode)."""
+
+    def __init__(self, work, finish):
+        self._work, self._finish = work, finish
+
+    def wait(self, timeout=None):
+        if self._work is not None:
+            self._work.wait()
+            self._work = None
+        if self._finish is not None:
+            self._finish()
+            self._finish = None
+        return True
+
+    def is_completed(self):
+        return self._finish is None
+
+
+def _deferred(fn, outs, async_op):
+    """Run ``fn`` (synchronously), then hide the result of every tensor in ``outs`` until the
+    consumer has synchronised: device tensors get NaN now and the result after a spin delay on the
+    issuing stream; host tensors of async ops get NaN until ``wait()``."""
+    r = fn()
+    if r is not None and hasattr(r, "wait"):
+        r.wait()
+    outs = [t for t in outs if isinstance(t, torch.Tensor) and t.is_floating_point() and t.numel()]
+    if not outs:
+        return _DeferredWork(None, None) if async_op else None
+    stash = [t.clone() for t in outs]
+    for t in outs:
+        t.fill_(float("nan"))
+    if outs[0].is_cuda:
+        stream = torch.cuda.current_stream(outs[0].device)
+        torch.cuda._sleep(_State.defer_cycles)
+        for t, s in zip(outs, stash):
+            t.copy_(s)
+        if not async_op:
+            return None
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        return _DeferredWork(None, lambda: torch.cuda.current_stream(outs[0].device).wait_event(ev))
+    if not async_op:  # a blocking host collective has completed when it returns
+        for t, s in zip(outs, stash):
+            t.copy_(s)
+        return None
+
+    def finish():
+        for t, s in zip(outs, stash):
+            t.copy_(s)
+    return _DeferredWork(None, finish)
+
+
+def _timed(op, fn, tensor, group, async_op, outs=None):
     _fp(op, group, tensor)
+    v = _State.volume[op]
+    v[0] += 1
+    v[1] += _payload(op, tensor, group)
+    if _State.defer and outs is not None:
+        return _deferred(fn, outs, async_op)
     if not _State.logger_enabled or async_op or (not _State.logger_prof_all and op not in _State.logger_prof_ops):
         return fn()
     from ..accelerator import get_accelerator
@@ -231,10 +321,7 @@ def _timed(op, fn, tensor, group, async_op):
     r = fn()
     acc.synchronize()
     ms = (time.perf_counter() - t0) * 1000.0
-    size = (tensor.numel() * tensor.element_size()) if isinstance(tensor, torch.Tensor) else \
-        sum(x.numel() * x.element_size() for x in tensor)
-    if op in ("all_gather_into_tensor", "all_gather"):
-        size *= get_world_size(group)
+    size = _payload(op, tensor, group)
     _State.comms[op][size].append(ms)
     if _State.logger_verbose:
         n = get_world_size(group)
@@ -266,6 +353,7 @@ def get_comms_stats():
 def reset_comms_stats():
     _State.comms.clear()
     _State.op_counts.clear()
+    _State.volume.clear()
 
 
 def get_op_counts():
@@ -284,7 +372,7 @@ def all_reduce(tensor, op=ReduceOp.SUM, group=None, async_op=False, prof=False, 
         return None
     _State.op_counts[log_name] += 1
     return _timed("all_reduce", lambda: tdist.all_reduce(tensor, op=op, group=group, async_op=async_op), tensor,
-                  group, async_op)
+                  group, async_op, outs=[tensor])
 
 
 def inference_all_reduce(tensor, op=ReduceOp.SUM, group=None):
@@ -296,14 +384,14 @@ def all_reduce_coalesced(tensors, op=ReduceOp.SUM, group=None, async_op=False):
         return None
     return _timed("all_reduce_coalesced",
                   lambda: tdist.all_reduce_coalesced(tensors, op=op, group=group, async_op=async_op), tensors, group,
-                  async_op)
+                  async_op, outs=list(tensors))
 
 
 def reduce(tensor, dst, op=ReduceOp.SUM, group=None, async_op=False):
     if _skip("REDUCE") or get_world_size(group) == 1:
         return None
     return _timed("reduce", lambda: tdist.reduce(tensor, dst, op=op, group=group, async_op=async_op), tensor, group,
-                  async_op)
+                  async_op, outs=[tensor])
 
 
 def reduce_scatter_tensor(output, input, op=ReduceOp.SUM, group=None, async_op=False):
@@ -320,10 +408,10 @@ def reduce_scatter_tensor(output, input, op=ReduceOp.SUM, group=None, async_op=F
             tdist.all_reduce(buf, op=op, group=group)
             r = get_rank(group)
             output.copy_(buf.view(get_world_size(group), -1)[r].view_as(output))
-        return _timed("reduce_scatter_tensor", fn, input, group, False)
+        return _timed("reduce_scatter_tensor", fn, input, group, False, outs=[output])
     return _timed("reduce_scatter_tensor",
                   lambda: tdist.reduce_scatter_tensor(output, input, op=op, group=group, async_op=async_op), input,
-                  group, async_op)
+                  group, async_op, outs=[output])
 
 
 reduce_scatter_fn = reduce_scatter_tensor
@@ -340,10 +428,10 @@ def all_gather_into_tensor(output, input, group=None, async_op=False):
         def fn():
             parts = list(output.view(get_world_size(group), -1).unbind(0))
             tdist.all_gather(parts, input.reshape(-1), group=group)
-        return _timed("all_gather_into_tensor", fn, input, group, False)
+        return _timed("all_gather_into_tensor", fn, input, group, False, outs=[output])
     return _timed("all_gather_into_tensor",
                   lambda: tdist.all_gather_into_tensor(output, input, group=group, async_op=async_op), input, group,
-                  async_op)
+                  async_op, outs=[output])
 
 
 allgather_fn = all_gather_into_tensor
@@ -353,7 +441,7 @@ def all_gather(tensor_list, tensor, group=None, async_op=False):
     if _skip("ALL_GATHER"):
         return None
     return _timed("all_gather", lambda: tdist.all_gather(tensor_list, tensor, group=group, async_op=async_op), tensor,
-                  group, async_op)
+                  group, async_op, outs=list(tensor_list))
 
 
 def all_gather_object(obj_list, obj, group=None):
@@ -364,7 +452,7 @@ def broadcast(tensor, src, group=None, async_op=False):
     if _skip("BROADCAST") or get_world_size(group) == 1:
         return None
     return _timed("broadcast", lambda: tdist.broadcast(tensor, src, group=group, async_op=async_op), tensor, group,
-                  async_op)
+                  async_op, outs=[tensor])
 
 
 def broadcast_object_list(objs, src, group=None):
@@ -381,15 +469,22 @@ def all_to_all_single(output, input, output_split_sizes=None, input_split_sizes=
         return None
     return _timed("all_to_all_single",
                   lambda: tdist.all_to_all_single(output, input, output_split_sizes, input_split_sizes, group=group,
-                                                  async_op=async_op), input, group, async_op)
+                                                  async_op=async_op), input, group, async_op, outs=[output])
 
 
 def all_to_all(output_tensor_list, input_tensor_list, group=None, async_op=False):
     return tdist.all_to_all(output_tensor_list, input_tensor_list, group=group, async_op=async_op)
 
 
+def _count_p2p(op, tensor):
+    v = _State.volume[op]
+    v[0] += 1
+    v[1] += tensor.numel() * tensor.element_size()
+
+
 def send(tensor, dst, group=None, tag=0):
     _fp("send", None, tensor)
+    _count_p2p("send", tensor)
     return tdist.send(tensor, dst, group=group, tag=tag)
 
 
@@ -400,16 +495,42 @@ def recv(tensor, src=None, group=None, tag=0):
 
 def isend(tensor, dst, group=None, tag=0):
     _fp("isend", None, tensor)
+    _count_p2p("send", tensor)
     return tdist.isend(tensor, dst, group=group, tag=tag)
 
 
 def irecv(tensor, src=None, group=None, tag=0):
     _fp("irecv", None, tensor)
+    if _State.defer and tensor.is_floating_point():
+        priv = torch.empty_like(tensor)
+        return _DeferredRecv(tdist.irecv(priv, src, group=group, tag=tag), tensor, priv)
     return tdist.irecv(tensor, src, group=group, tag=tag)
 
 
+class _DeferredRecv(_DeferredWork):
+    """irecv under deferred completion: the message lands in a private buffer and the user's
+    tensor reads NaN until ``wait()`` copies it over."""
+
+    def __init__(self, work, tensor, priv):
+        tensor.fill_(float("nan"))
+        super().__init__(work, lambda: tensor.copy_(priv))
+
+
 def batch_isend_irecv(p2p_op_list):
-    return tdist.batch_isend_irecv(p2p_op_list)
+    ops, wrap = [], []
+    for o in p2p_op_list:
+        is_recv = o.op in (tdist.irecv, irecv)
+        if not is_recv:
+            _count_p2p("send", o.tensor)
+        if _State.defer and is_recv and o.tensor.is_floating_point():
+            priv = torch.empty_like(o.tensor)
+            ops.append(tdist.P2POp(tdist.irecv, priv, o.peer, o.group, o.tag))
+            wrap.append((o.tensor, priv))
+        else:
+            ops.append(o)
+            wrap.append(None)
+    works = tdist.batch_isend_irecv(ops)
+    return [w if x is None else _DeferredRecv(w, x[0], x[1]) for w, x in zip(works, wrap)]
 
 
 P2POp = tdist.P2POp

@@ -22,7 +22,9 @@ MI355X-first differences, each a fix or a cost the reference pays per step:
 * all rank-shared randomness (shuffle permutation, Gossip senders/destinations) comes from a
   dedicated ``torch.Generator`` seeded identically on every rank, so it cannot diverge with
   model-side RNG use (the reference relies on the global torch RNG being in lock-step);
-* ``RR``/``shuffle`` use ``ReduceOp.AVG`` on RCCL (one pass, no bf16 pre-division rounding);
+* means are exact-divided: with a power-of-two member count the pre-division of a bit16 chunk is an
+  exponent shift (no rounding) and only the summation rounds -- pinned against the fp32 mean in
+  tests/test_shuffle_exchange_w8.py; other counts average in fp32 (upcast, sum, divide, round once);
 * Gossip sends exactly-sized buffers with ``batch_isend_irecv`` (the reference receives into an
   8 GB 4e9-element buffer regardless of the tensor size, stage_1_and_2.py:2190-2194) and keeps
   ``alpha`` in fp32 so the push-sum mass is conserved to fp32 precision;
@@ -134,17 +136,15 @@ class ShuffleExchange:
             raise ValueError(f"shuffle_exchange: rings={rings} must divide the number of slices {n}")
         return rings
 
-    def _avg_op(self):
-        be = dist.get_backend()
-        return dist.ReduceOp.AVG if be == "nccl" else None
-
-    def _mean_allreduce(self, t, group, n):
-        op = self._avg_op()
-        if op is not None:
-            dist.all_reduce(t, op=op, group=group)
-        else:
-            t.div_(n)
+    @staticmethod
+    def _mean_allreduce(t, group, n):
+        if n & (n - 1) == 0 or t.dtype == torch.float32:
+            t.div_(n)  # exact for a power-of-two n
             dist.all_reduce(t, group=group)
+        else:
+            f = t.float().div_(n)
+            dist.all_reduce(f, group=group)
+            t.copy_(f)
 
     # -------------------------------------------------------------------------------------------
     def shuffle_exchange(self):
