@@ -1,13 +1,33 @@
 #!/usr/bin/env python3
-"""Headline benchmark: Llama-3-8B, ZeRO-3, bf16, tokens/s on N MI355X GPUs (one process per GPU).
+"""Training benchmarks on N MI355X GPUs (one process per GPU, RCCL over xGMI), one per BASELINE.json config.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched by
-``torch.distributed.run`` (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from env, RCCL backend). W untimed
-steps, then EXACTLY K timed optimizer steps bracketed by barrier + device sync; the time is the MAX
-over ranks; rank 0 prints one JSON line. Every timed step is a full training step: forward, backward,
-gradient reduce-scatter, fused AdamW on fp32 masters (all 8.03B parameters), no skipped work.
-Data: synthetic token ids (uniform over the 128256-token vocabulary); weights: random init of the
-exact Llama-3-8B architecture (no network access for checkpoints/datasets).
+``torch.distributed.run`` (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from env). W untimed steps, then
+EXACTLY K timed optimizer steps bracketed by barrier + device sync; the time is the MAX over ranks;
+rank 0 prints one JSON line. Every timed step is a full training step: forward, backward, gradient
+reduction, optimizer step on fp32 masters for every parameter -- no skipped work.
+Data: synthetic token ids (uniform over the vocabulary); weights: random init of the named
+architecture (no network access for checkpoints/datasets).
+
+``--config`` (default ``llama8b-z3``, the headline):
+  llama8b-z3          Llama-3-8B, ZeRO-3, bf16, seq 2048, 16 sequences per GPU (8 x 2 micro-steps),
+                      MI355X-tuned residency (288 GB HBM: gathered weights kept for the step,
+                      gradient sums reduce-scattered once per step) -- BASELINE.json metric
+  llama8b-z3-default  the same model/batch with the REFERENCE's default ZeRO-3 knobs (a gather per
+                      micro-step forward, backward re-gathers beyond reuse distance 1e9 / max_live
+                      1e9, a reduce-scatter every micro-step, prefetch bucket 5e7)
+  mixtral-ep          Mixtral-8x7B, expert parallel over all N GPUs (ep = N, one all-to-all pair per
+                      MoE layer), ZeRO-2 (the reference asserts MoE off at stage 3, engine.py:1760),
+                      seq 2048; min(32, 8N) layers so the experts per GPU stay fixed (full 32 at N >= 4)
+  llama70b-infinity   Llama-3-70B, ZeRO-3 + ZeRO-Infinity optimizer offload to pinned host DRAM
+                      (C++ AVX-512 Adam), activation checkpointing, seq 2048; 10N layers up to the
+                      full 80 (host DRAM of one node bounds the fp32 state: 12 B/param)
+  llama8b-sp32k       Llama-3-8B, Ulysses sequence parallel over all N GPUs, seq 32768, ZeRO-3,
+                      activation checkpointing; one 32k sequence per SP group (strong scaling)
+Every JSON line carries the full ZeRO/SP/EP configuration, the measured per-step communication
+volume per collective (``comm_measured``: calls and bytes per rank per step, from the comm facade's
+counters) and an analytic model of it (``comm_model``), so a scaling curve can be checked against the
+bytes that crossed xGMI.
 """
 import argparse
 import json
@@ -19,27 +39,114 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+CONFIGS = {
+    "llama8b-z3": dict(family="llama", model="llama3-8b", seq=2048, mbs=8, gas=2, stage=3, knobs="tuned",
+                       metric="tokens/sec Llama-3-8B ZeRO-3 bf16 (training, whole job)"),
+    "llama8b-z3-default": dict(family="llama", model="llama3-8b", seq=2048, mbs=8, gas=2, stage=3, knobs="reference",
+                               metric="tokens/sec Llama-3-8B ZeRO-3 bf16 (training, whole job)"),
+    "mixtral-ep": dict(family="mixtral", model="mixtral-8x7b", seq=2048, mbs=2, gas=2, stage=2, knobs="tuned",
+                       ep=True, metric="tokens/sec Mixtral-8x7B expert-parallel bf16 (training, whole job)"),
+    "llama70b-infinity": dict(family="llama", model="llama3-70b", seq=2048, mbs=2, gas=2, stage=3, knobs="reference",
+                              offload=True, ac=True,
+                              metric="tokens/sec Llama-3-70B ZeRO-3 + ZeRO-Infinity host offload bf16 "
+                                     "(training, whole job)"),
+    "llama8b-sp32k": dict(family="llama", model="llama3-8b", seq=32768, mbs=1, gas=1, stage=3, knobs="tuned", sp=True,
+                          ac=True, metric="tokens/sec Llama-3-8B Ulysses SP seq 32k bf16 (training, whole job)"),
+}
+
+
+def default_layers(name, world):
+    """Layer count of the model for a config at `world` GPUs (None = the full architecture)."""
+    if name == "mixtral-ep":
+        return None if world >= 4 else 8 * world
+    if name == "llama70b-infinity":
+        return None if world >= 8 else 10 * world
+    return None
+
+
+def zero_knobs(c, cfg, stage):
+    z = {"stage": stage, "overlap_comm": True, "reduce_bucket_size": 500_000_000}
+    if stage == 3:
+        z.update({"stage3_param_persistence_threshold": 100_000})
+        if c["knobs"] == "tuned":
+            z.update({"prefetch_depth": 2,
+                      # 288 GB HBM: the whole bf16 model (16 GB for 8B) may stay gathered from its
+                      # forward use to its backward re-use -> no backward all-gather
+                      "stage3_max_reuse_distance": 2 * cfg.num_params(),
+                      "stage3_max_live_parameters": cfg.num_params(),
+                      # fp32 gradient sums stay local across the micro-steps: one reduce-scatter per step
+                      "stage3_defer_reduce": True,
+                      # gathered weights stay valid until the optimizer step: gather once per step
+                      "stage3_retain_params_in_step": True})
+        else:  # the reference's defaults (runtime/zero/config.py)
+            z.update({"stage3_prefetch_bucket_size": 50_000_000, "stage3_max_live_parameters": 1_000_000_000,
+                      "stage3_max_reuse_distance": 1_000_000_000})
+    if c.get("offload"):
+        z["offload_optimizer"] = {"device": "cpu", "pin_memory": True}
+    return z
+
+
+def comm_model(opt, world, stage, knobs, gas, elem_bytes=2):
+    """Analytic per-rank payload bytes per optimizer step of the ZeRO collectives (rccl-tests payload
+    convention: gathered size for all-gather, input size for reduce-scatter / all-reduce)."""
+    if world == 1 or opt is None:
+        return {}
+    out = {}
+    if stage == 3 and hasattr(opt, "fgroups"):
+        S = opt.S
+        if S == 1:
+            return {}
+        # the gather policy of runtime/zero/stage3.py replayed on the recorded forward trace
+        size = {fg.idx: sum(u.padded for u in fg.units if not u.persistent) for fg in opt.fgroups}
+        persistent = sum(u.padded for fg in opt.fgroups for u in fg.units if u.persistent)
+        trace = list(opt.trace)
+        if getattr(opt, "retain_params", False):
+            gathered = sum(size[i] for i in trace)  # once per step: retained until the boundary backward
+        else:
+            dist_, kept, live = opt._reuse_distances(), set(), 0
+            for i in trace:  # _keep_for_backward, in forward order
+                if i == trace[-1]:
+                    kept.add(i)
+                elif (opt.max_reuse_distance > 0 and dist_.get(i, 1 << 62) < opt.max_reuse_distance
+                      and live + size[i] <= opt.max_live_parameters):
+                    kept.add(i)
+                    live += size[i]
+            gathered = gas * (sum(size[i] for i in trace) + sum(size[i] for i in trace if i not in kept))
+        n_rs = 1 if getattr(opt, "defer_reduce", False) else gas
+        out["all_gather_into_tensor"] = (gathered + persistent) * elem_bytes  # persistent: refreshed after the step
+        out["reduce_scatter_tensor"] = n_rs * (sum(size.values()) + persistent) * elem_bytes
+    elif stage in (1, 2) and hasattr(opt, "units"):
+        total = sum(u.padded for units in opt.units for u in units if u.topo.S > 1) * elem_bytes
+        out["reduce_scatter_tensor"] = total * (gas if stage == 2 else 1)
+        out["all_gather_into_tensor"] = total
+    return out
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--model", default="llama3-8b")
-    ap.add_argument("--seq", type=int, default=int(os.environ.get("SXE_BENCH_SEQ", 2048)))
-    # global batch 16 per GPU as 8 x 2 micro-steps: 288 GB HBM holds the activations of 8 x 2048
-    # tokens (peak 211 GB); half the weight-gradient accumulation passes of 4 x 4 and larger GEMM M
-    # (measured 24,254 vs 23,799 tok/s, profiles/bench_1gpu_r02.log)
-    ap.add_argument("--mbs", type=int, default=int(os.environ.get("SXE_BENCH_MBS", 8)))
-    ap.add_argument("--gas", type=int, default=int(os.environ.get("SXE_BENCH_GAS", 2)))
-    ap.add_argument("--stage", type=int, default=3)
+    ap.add_argument("--config", default=os.environ.get("SXE_BENCH_CONFIG", "llama8b-z3"), choices=sorted(CONFIGS))
+    ap.add_argument("--model", default=None, help="override the architecture preset (tests: llama-tiny / mixtral-tiny)")
+    ap.add_argument("--seq", type=int, default=None)
+    ap.add_argument("--mbs", type=int, default=None)
+    ap.add_argument("--gas", type=int, default=None)
+    ap.add_argument("--stage", type=int, default=None)
     ap.add_argument("--ac", action="store_true", help="activation checkpointing")
-    ap.add_argument("--layers", type=int, default=None, help="override layer count (debug only; invalid for the metric)")
-    ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--layers", type=int, default=None, help="override layer count (a cut model: not the metric)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = plumbing dry-run over gloo (tests only; invalid for the metric)")
     args = ap.parse_args()
+    c = CONFIGS[args.config]
     on_gpu = args.device == "cuda"
+    seq = args.seq or int(os.environ.get("SXE_BENCH_SEQ", c["seq"]))
+    # llama8b-z3: 16 sequences per GPU as 8 x 2 micro-steps -- 288 GB HBM holds the activations of
+    # 8 x 2048 tokens (peak 211 GB); half the weight-gradient accumulation passes of 4 x 4
+    mbs = args.mbs or int(os.environ.get("SXE_BENCH_MBS", c["mbs"]))
+    gas = args.gas or int(os.environ.get("SXE_BENCH_GAS", c["gas"]))
+    stage = c["stage"] if args.stage is None else args.stage
+    model_name = args.model or c["model"]
 
     def sync():
         if on_gpu:
@@ -47,51 +154,72 @@ def main():
 
     import shuffle_exchange_amd as sxe
     from shuffle_exchange_amd import comm as dist
-    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
 
     dist.init_distributed(verbose=False)
     world = dist.get_world_size()
     rank = dist.get_rank()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    sp = world if c.get("sp") else 1
+    ep = world if c.get("ep") else 1
+    dp = world // sp
+    layers = args.layers if args.layers is not None else default_layers(args.config, world)
+    ac = args.ac or bool(c.get("ac"))
     torch.manual_seed(1234)
-    over = {"activation_checkpointing": args.ac, "max_position_embeddings": max(8192, args.seq)}
-    if args.layers:
-        over["num_hidden_layers"] = args.layers
-    cfg = llama_config(args.model, **over)
+    over = {"activation_checkpointing": ac, "max_position_embeddings": max(8192, seq)}
+    if layers:
+        over["num_hidden_layers"] = layers
+    if sp > 1:
+        over["sequence_parallel"] = True
+    if c["family"] == "mixtral":
+        from shuffle_exchange_amd.models.mixtral import MixtralForCausalLM, mixtral_config
+        if ep > 1:
+            over["ep_size"] = ep
+        cfg = mixtral_config(model_name, **over)
+        ctor = MixtralForCausalLM
+    else:
+        from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+        cfg = llama_config(model_name, **over)
+        ctor = LlamaForCausalLM
     dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
-    with sxe.zero.Init(dtype=torch.bfloat16):
-        model = LlamaForCausalLM(cfg)
+    if stage == 3:
+        with sxe.zero.Init(dtype=torch.bfloat16):
+            model = ctor(cfg)
+    else:
+        model = ctor(cfg)
+    zero = zero_knobs(c, cfg, stage)
     ds_config = {
-        "train_micro_batch_size_per_gpu": args.mbs,
-        "gradient_accumulation_steps": args.gas,
+        "train_micro_batch_size_per_gpu": mbs,
+        "gradient_accumulation_steps": gas,
         "bf16": {"enabled": True},
         "gradient_clipping": 1.0,
-        "zero_optimization": {"stage": args.stage, "overlap_comm": True, "reduce_bucket_size": 500_000_000,
-                              "stage3_param_persistence_threshold": 100_000, "prefetch_depth": 2,
-                              # 288 GB HBM: the whole bf16 model (16 GB for 8B) may stay gathered from
-                              # its forward use to its backward re-use -> no backward all-gather
-                              "stage3_max_reuse_distance": 2 * cfg.num_params(),
-                              "stage3_max_live_parameters": cfg.num_params(),
-                              # and keep fp32 gradient sums local across the grad-accumulation
-                              # micro-steps: one reduce-scatter per step instead of one per micro-step
-                              "stage3_defer_reduce": True,
-                              # gathered weights stay valid until the optimizer step: gather once per step
-                              "stage3_retain_params_in_step": True},
+        "zero_optimization": zero,
         "optimizer": {"type": "AdamW", "params": {"lr": 3e-4, "betas": [0.9, 0.95], "eps": 1e-8,
                                                    "weight_decay": 0.1}},
         "steps_per_print": 1000000,
     }
+    if sp > 1:
+        ds_config["sequence_parallel_size"] = sp
     engine, _, _, _ = sxe.initialize(model=model, config=ds_config)
-    n_params = sum(p.numel() for p in model.parameters())
+    n_params = sum(getattr(p, "ds_numel", p.numel()) for p in model.parameters())
+    if c.get("ep"):
+        n_params = cfg.num_params()  # every expert of the architecture (each rank holds 1/ep of them)
     gen = torch.Generator(device=dev)
-    gen.manual_seed(1000 + rank)
+    # one data stream per data-parallel replica; the ranks of an SP group shard the same sequences
+    gen.manual_seed(1000 + rank // sp)
+    from shuffle_exchange_amd.parallel import groups
+    sp_rank = groups.get_sequence_parallel_rank() if sp > 1 else 0
 
     def train_step():
-        for i in range(args.gas):
+        for _ in range(gas):
             # a fresh synthetic batch every micro-step (generated on the device: no H2D in the loop)
-            batch = torch.randint(0, cfg.vocab_size, (args.mbs, args.seq), generator=gen, device=dev)
-            loss = engine(batch, labels=batch)
+            batch = torch.randint(0, cfg.vocab_size, (mbs, seq), generator=gen, device=dev)
+            if sp > 1:
+                from shuffle_exchange_amd.sequence.data import shard_batch_for_sp
+                b = shard_batch_for_sp(batch, sp_rank, sp)
+                loss = engine(b["input_ids"], labels=b["labels"], position_ids=b["position_ids"], shift_labels=False)
+            else:
+                loss = engine(batch, labels=batch)
             engine.backward(loss)
             engine.step()
         return loss
@@ -101,6 +229,7 @@ def main():
     sync()
     dist.barrier()
     sync()
+    dist.reset_comms_stats()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = train_step()
@@ -108,18 +237,32 @@ def main():
     dist.barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    vol = dist.get_comm_volume()
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    tokens = args.gpus * args.mbs * args.gas * args.seq * args.steps
+    tokens = dp * mbs * gas * seq * args.steps
     tps = tokens / elapsed
-    flops_tok = cfg.flops_per_token(args.seq)
-    mfu_tflops = tps * flops_tok / args.gpus / 1e12
-    valid = (args.layers is None and args.model == "llama3-8b" and args.stage == 3 and on_gpu and args.seq == 2048
-             and args.mbs * args.gas == 16)
+    if c["family"] == "mixtral":
+        d = cfg.hidden_size // cfg.num_attention_heads
+        flops_tok = 6 * cfg.active_params_per_token() + 6 * cfg.num_hidden_layers * seq * cfg.num_attention_heads * d
+    else:
+        flops_tok = cfg.flops_per_token(seq)
+    tflops = tps * flops_tok / world / 1e12
+    full_model = layers is None
+    valid = (full_model and model_name == c["model"] and stage == c["stage"] and on_gpu and seq == c["seq"]
+             and mbs * gas == c["mbs"] * c["gas"])
     if rank == 0:
+        model_tag = model_name + (f" ({layers} of {c['model']}'s layers)" if layers else "")
+        par = [f"zero{stage}", f"dp{dp}"]
+        if sp > 1:
+            par.append(f"sp{sp}")
+        if ep > 1:
+            par.append(f"ep{ep}")
+        if c.get("offload"):
+            par.append("offload-optimizer-cpu")
         out = {
-            "metric": "tokens/sec Llama-3-8B ZeRO-3 bf16 (training, whole job)",
+            "metric": c["metric"],
             "value": round(tps, 2),
             "unit": "tokens/s",
             "n_gpus": args.gpus,
@@ -127,17 +270,23 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1000.0, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sp > 1 else "weak",
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic",
-            "config": {"model": args.model, "global_batch": args.gpus * args.mbs * args.gas, "seq_len": args.seq,
-                       "micro_batch_per_gpu": args.mbs, "grad_accum": args.gas,
-                       "parallelism": f"zero{args.stage}-dp{args.gpus}", "params": n_params,
-                       "activation_checkpointing": args.ac, "optimizer": "AdamW(fp32 master, fused HIP)"},
-            "tflops_per_gpu": round(mfu_tflops, 1),
+            "config": {"name": args.config, "model": model_tag, "global_batch": dp * mbs * gas, "seq_len": seq,
+                       "micro_batch_per_gpu": mbs, "grad_accum": gas, "parallelism": "-".join(par),
+                       "params": n_params, "activation_checkpointing": ac,
+                       "optimizer": "AdamW(fp32 master, " + ("C++ CPU Adam on host" if c.get("offload") else
+                                                             "fused HIP") + ")",
+                       "zero_knobs": c["knobs"], "zero_optimization": zero, "sequence_parallel_size": sp,
+                       "expert_parallel_size": ep},
+            "tflops_per_gpu": round(tflops, 1),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if on_gpu else None,
             "final_loss": round(float(loss.detach()), 4),
+            "comm_measured": {op: {"calls_per_step": round(n / args.steps, 2), "bytes_per_step": b // args.steps}
+                              for op, (n, b) in sorted(vol.items())},
+            "comm_model": comm_model(engine.optimizer, world, stage, c["knobs"], gas),
             "valid_for_metric": valid,
         }
         print(json.dumps(out), flush=True)

@@ -465,6 +465,12 @@ class SXEEngine(nn.Module):
             param_swap = dict(nvme_path=zc.offload_param.nvme_path, rank=dist.get_rank(), dtype=dtype,
                               aio_config=cfg.model.aio, buffer_count=zc.offload_param.buffer_count)
         if stage == 3:
+            moe_ep = [pg for pg in basic.param_groups if pg.get("moe", False)
+                      and str(pg.get("name", "")).startswith("ep_size_") and int(pg["name"].rsplit("_", 1)[-1]) > 1]
+            if moe_ep:
+                # expert weights differ across the EP group: ZeRO-3 would partition/gather them as one
+                # tensor (the reference asserts "MoE not supported with Stage 3", engine.py:1760)
+                raise NotImplementedError("expert parallelism (ep_size > 1) needs ZeRO stage 0, 1 or 2")
             self.optimizer = ZeroStage3Optimizer(
                 self.module, basic, loss_scaler=scaler, clip_grad=cfg.gradient_clipping, dp_ranks=dp_ranks,
                 dp_group=dp_group, prefetch_depth=zc.prefetch_depth,

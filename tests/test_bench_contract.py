@@ -27,3 +27,67 @@ def test_bench_two_ranks_cpu(tmp_path):
     tokens = 2 * 2 * 2 * 64 * 2
     assert abs(out["value"] - tokens / (out["ms_per_step"] * 2 / 1000.0)) / out["value"] < 0.01
     assert out["valid_for_metric"] is False  # tiny model on CPU is never a metric number
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("config,model,extra", [
+    ("llama8b-z3-default", "llama-tiny", []),
+    ("mixtral-ep", "mixtral-tiny", []),
+    ("llama70b-infinity", "llama-tiny", ["--layers", "2"]),
+    ("llama8b-sp32k", "llama-tiny", ["--seq", "128"]),
+])
+def test_bench_configs_two_ranks_cpu(tmp_path, config, model, extra):
+    """Every BASELINE config's harness under torch.distributed.run with 2 gloo ranks: one JSON line,
+    the config's parallelism (ep2 / sp2 / offload), its ZeRO knobs, the measured comm volume next to
+    the analytic model."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    port = {"llama8b-z3-default": 29641, "mixtral-ep": 29643, "llama70b-infinity": 29645, "llama8b-sp32k": 29647}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port[config]), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--config", config, "--model", model, "--device", "cpu",
+           "--mbs", "1", "--gas", "2"] + extra
+    if "--seq" not in extra:
+        cmd += ["--seq", "64"]
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=900)
+    assert r.returncode == 0, r.stdout[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-4000:]
+    out = json.loads(lines[0])
+    cfg = out["config"]
+    assert cfg["name"] == config and out["n_gpus"] == 2 and out["valid_for_metric"] is False
+    assert "zero_optimization" in cfg and cfg["zero_optimization"]["stage"] in (2, 3)
+    meas, model_ = out["comm_measured"], out["comm_model"]
+    if config == "mixtral-ep":
+        assert cfg["expert_parallel_size"] == 2 and "ep2" in cfg["parallelism"]
+        assert meas["all_to_all_single"]["calls_per_step"] > 0
+    if config == "llama8b-sp32k":
+        assert cfg["sequence_parallel_size"] == 2 and out["scaling"] == "strong"
+        assert cfg["global_batch"] == 2  # one sequence per SP group per micro-step x gas 2
+        assert meas["all_to_all_single"]["calls_per_step"] > 0
+    if config == "llama70b-infinity":
+        assert cfg["zero_optimization"]["offload_optimizer"]["device"] == "cpu"
+    if config == "llama8b-z3-default":
+        assert cfg["zero_knobs"] == "reference"
+        # 2 gathers (fwd + bwd) and 1 reduce-scatter per micro-step: the analytic model agrees with the
+        # bytes the facade counted
+        for op in ("all_gather_into_tensor", "reduce_scatter_tensor"):
+            assert meas[op]["bytes_per_step"] == model_[op], (op, meas[op], model_[op])
+
+
+def test_bench_tuned_zero3_comm_model_matches_measured(tmp_path):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29649", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--model", "llama-tiny", "--device", "cpu", "--seq", "64", "--mbs", "1", "--gas", "2"]
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-4000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    meas, model_ = out["comm_measured"], out["comm_model"]
+    assert out["config"]["zero_knobs"] == "tuned"
+    # tuned: ONE gather of the model per step and ONE deferred reduce-scatter per step
+    for op in ("all_gather_into_tensor", "reduce_scatter_tensor"):
+        assert meas[op]["bytes_per_step"] == model_[op], (op, meas[op], model_[op])
