@@ -1,6 +1,8 @@
-// Flash attention forward + backward for gfx950 (MI355X), bf16 in / fp32 accumulate, head dim 128,
-// causal or full, GQA, arbitrary [B, S, H, D] strides (so the fused QKV projection output is read in
-// place and dq/dk/dv are written straight into one dqkv buffer).
+// Flash attention forward + backward for gfx950 (MI355X), bf16 in / fp32 accumulate, head dims 64,
+// 128 and 256 (templated: no zero-padding of the head dim), causal or full, GQA, query length !=
+// key length (cross / prefix / chunked-prefill attention: the causal mask is bottom-right aligned by
+// `qoff`, query i sees keys <= i + qoff), arbitrary [B, S, H, D] strides (so the fused QKV projection
+// output is read in place and dq/dk/dv are written straight into one dqkv buffer).
 //
 // Reference users: FPDT's chunked attention with LSE merging (deepspeed/sequence/fpdt_layer.py:134-460),
 // Ulysses local attention (sequence/layer.py:434), the Triton flash kernels of the inference path
@@ -28,12 +30,10 @@
 namespace sxe {
 namespace fa {
 
-constexpr int D = 128;          // head dim
 constexpr int NW = 4;           // waves per workgroup
 constexpr int QW = 32;          // rows per wave
 constexpr int QB = NW * QW;     // 128 rows per workgroup
 constexpr int KT = 64;          // keys per K/V tile (forward / dQ)
-constexpr int ROWB = D * 2;     // 256 bytes per LDS row
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
@@ -43,13 +43,20 @@ typedef short i16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-// Byte offset of 16-byte chunk `ch` (0..15) of row `row` in a swizzled [rows][128 bf16] tile.
+// Byte offset of 16-byte chunk `ch` (0..D/8-1) of row `row` in a swizzled [rows][D bf16] tile: the
+// chunk index is XORed with a 4-bit function of the row (3 bits when a row has only 8 chunks) so
+// both the row reads (ds_read_b128) and the transposed 4-row reads (ds_read_b64_tr_b16) spread over
+// the banks (guide T10, image (b)); the XOR is an involution, which the direct-to-LDS loader uses.
+template <int D>
 __device__ __forceinline__ int soff(int row, int ch) {
-  return row * ROWB + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+  constexpr int CH = D / 8;
+  const int f = (((row & 3) << 2) | ((row >> 2) & 3)) & (CH >= 16 ? 15 : CH - 1);
+  return row * (2 * D) + 16 * (ch ^ f);
 }
 
+template <int D>
 __device__ __forceinline__ bf16x8 lds_row16(const char* base, int row, int ch) {
-  return *reinterpret_cast<const bf16x8*>(base + soff(row, ch));
+  return *reinterpret_cast<const bf16x8*>(base + soff<D>(row, ch));
 }
 
 // Transposed read: 4 consecutive rows x one column per lane (ds_read_b64_tr_b16).
@@ -61,12 +68,13 @@ __device__ __forceinline__ i16x4 lds_tr(const char* base, int byte_off) {
 // A operand of a 32x32x16 MFMA taken from a row-major [rows][d] LDS tile, transposed:
 // A[m = d][k] with d = 32*dt + (lane&31), k permuted to match an accumulator used as B operand:
 // element j of lane half h <- tile row (row0 + 8*(j>>2) + 4h + (j&3)), column d.
+template <int D>
 __device__ __forceinline__ bf16x8 lds_trA(const char* base, int row0, int dt, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, h = g >> 1;
   const int ch = 4 * dt + 2 * (g & 1) + (p >> 1);
   const int row = row0 + 4 * h + q;
-  i16x4 lo = lds_tr(base, soff(row, ch) + 8 * (p & 1));
-  i16x4 hi = lds_tr(base, soff(row + 8, ch) + 8 * (p & 1));
+  i16x4 lo = lds_tr(base, soff<D>(row, ch) + 8 * (p & 1));
+  i16x4 hi = lds_tr(base, soff<D>(row + 8, ch) + 8 * (p & 1));
   // whole-vector bitcast: element-wise bf16 inserts from the tr-read result miscompile (hipcc 7.2)
   const i16x8 c = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8, c);
@@ -109,17 +117,18 @@ struct Strides {
   int64_t b, s, h;  // element strides; d is unit stride
 };
 
-// Stage a [rows=ROWS][D] tile of 16-byte chunks from global into registers (each of the 256
-// threads owns ROWS*16/256 chunks), then into swizzled LDS.
-template <int ROWS, int NWAVES = NW>
+// Stage a [rows=ROWS][D] tile of 16-byte chunks from global into registers (each thread owns
+// ROWS*(D/8)/threads chunks), then into swizzled LDS. Rows at or beyond `nrows_valid` read as zeros.
+template <int ROWS, int NWAVES, int D>
 struct Stager {
-  static constexpr int N = ROWS * (D / 8) / (NWAVES * 64);
+  static constexpr int CH = D / 8;
+  static constexpr int N = ROWS * CH / (NWAVES * 64);
   u32x4 r[N];
   __device__ __forceinline__ void load(const unsigned short* base, int64_t row_stride, int row0, int nrows_valid) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       const int c = threadIdx.x + i * NWAVES * 64;
-      const int row = c >> 4, ch = c & 15;
+      const int row = c / CH, ch = c % CH;
       if (row0 + row < nrows_valid)
         r[i] = *reinterpret_cast<const u32x4*>(base + (int64_t)(row0 + row) * row_stride + ch * 8);
       else
@@ -130,7 +139,7 @@ struct Stager {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       const int c = threadIdx.x + i * NWAVES * 64;
-      *reinterpret_cast<u32x4*>(lds + soff(c >> 4, c & 15)) = r[i];
+      *reinterpret_cast<u32x4*>(lds + soff<D>(c / CH, c % CH)) = r[i];
     }
   }
 };
@@ -183,15 +192,44 @@ __device__ __forceinline__ void map_block(int nblk, int BH, bool heavy_last_inde
 }
 
 // =============================================================================================
-// Forward. Grid: nqb * B * H blocks of 256 threads. q/k/v/o: [B, S, *, D] strided; lse [B, H, S].
+// Direct-to-LDS tile loads (global_load_lds_dwordx4): no staging registers. A wave-instruction
+// writes 1 KiB = 1024 / (2 D) rows linearly, so the XOR swizzle goes on the per-lane SOURCE chunk
+// (the swizzle is an involution: position c' of row `row` holds logical chunk c' ^ f(row)).
+// =============================================================================================
+__device__ __forceinline__ void glds16(const void* gsrc, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* gsrc, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 4, 0, 0);
+}
+template <int ROWS, int D>
+__device__ __forceinline__ void tile_glds(const unsigned short* base, int64_t row_stride, int row0, char* lds) {
+  constexpr int CH = D / 8, RPK = 64 / CH;  // rows per 1 KiB wave-instruction
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < ROWS / RPK / NW; ++i) {
+    const int n = i * NW + w;
+    const int row = RPK * n + lane / CH;
+    const int cpos = lane % CH;
+    const int ch = cpos ^ ((((row & 3) << 2) | ((row >> 2) & 3)) & (CH >= 16 ? 15 : CH - 1));
+    glds16(base + (int64_t)(row0 + row) * row_stride + ch * 8, lds + n * 1024);
+  }
+}
+__device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// =============================================================================================
+// Forward. Grid: (Sq / rows per workgroup) * B * H blocks. q: [B, Sq, *, D], k/v/o: [B, Sk, *, D]
+// strided; lse [B, H, Sq]. Causal: query i sees keys <= i + qoff (qoff = Sk - Sq unless padded).
 // =============================================================================================
 // One K/V tile of a wave's online softmax. MASK = false is the interior-tile body (no causal
 // diagonal, no padded tail, dense): none of the per-score compares / selects are emitted -- on
 // the Llama-3 shape ~90 % of the tiles take it; the masked body handles the diagonal, the kv_len
 // tail and block-sparse layouts.
-template <bool MASK>
+template <bool MASK, int D>
 __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const bf16x8 (&qf)[D / 16],
-                                         f32x16 (&oacc)[D / 32], float& m, float& l, float c, int kbase, int q0,
+                                         f32x16 (&oacc)[D / 32], float& m, float& l, float c, int kbase, int qpos,
                                          int r, int h, int lane, bool diag, bool tail, int kvlen, const uint8_t* lrow,
                                          int blk) {
   f32x16 s[2];
@@ -199,7 +237,7 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const b
   for (int j = 0; j < 2; ++j) {
     s[j] = zero16();
 #pragma unroll
-    for (int t2 = 0; t2 < D / 16; ++t2) s[j] = mfma(lds_row16(kt, 32 * j + r, 2 * t2 + h), qf[t2], s[j]);
+    for (int t2 = 0; t2 < D / 16; ++t2) s[j] = mfma(lds_row16<D>(kt, 32 * j + r, 2 * t2 + h), qf[t2], s[j]);
   }
   // raw scores: the max is taken before scaling (c > 0) and the scale folds into the exp's FMA
   float mx = -INFINITY;
@@ -214,7 +252,7 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const b
     for (int i = 0; i < 16; ++i) {
       float x = s[j][i];
       if (MASK) {
-        if (diag && (kbase + 32 * j + acc_row(i, h) > q0 + r)) x = -INFINITY;
+        if (diag && (kbase + 32 * j + acc_row(i, h) > qpos + r)) x = -INFINITY;
         if (tail && (kbase + 32 * j + acc_row(i, h) >= kvlen)) x = -INFINITY;
         if (!(acc_row(i, h) < 16 ? b0 : b1)) x = -INFINITY;
         s[j][i] = x;
@@ -224,8 +262,8 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const b
   }
   mx = fmaxf(mx, xor32(mx)) * c;
   // lazy rescale: the reference max only moves when the tile max exceeds it by > 2^8, so
-  // p <= 256 (harmless in fp32 / bf16) and the 64-register O rescale is skipped whenever no
-  // lane of the wave moved (most tiles after the first few)
+  // p <= 256 (harmless in fp32 / bf16) and the O rescale is skipped whenever no lane of the wave
+  // moved (most tiles after the first few)
   const bool grow = mx > m + 8.f;
   const float mnew = grow ? mx : m;
   const float mref = (mnew == -INFINITY) ? 0.f : mnew;
@@ -253,31 +291,36 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const b
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 pb = acc_to_b(s[j], s2);
 #pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt) oacc[dt] = mfma(lds_trA(vt, 32 * j + 16 * s2, dt, lane), pb, oacc[dt]);
+      for (int dt = 0; dt < D / 32; ++dt) oacc[dt] = mfma(lds_trA<D>(vt, 32 * j + 16 * s2, dt, lane), pb, oacc[dt]);
     }
 }
 
-// NWF waves per workgroup, each 32 queries: NWF = 8 (256 queries, one workgroup of 2 waves per
-// SIMD per CU) shares every staged K/V tile among twice the queries of NWF = 4 (used when the
-// sequence is not a multiple of 256).
-template <bool SPARSE, int NWF>
-__global__ void __launch_bounds__(NWF * 64, 8 / NWF) fwd_kernel(const unsigned short* __restrict__ q, Strides qs,
-                                                     const unsigned short* __restrict__ k, Strides ks,
-                                                     const unsigned short* __restrict__ v, Strides vs,
-                                                     unsigned short* __restrict__ o, Strides os,
-                                                     float* __restrict__ lse, int B, int H, int Hk, int S,
-                                                     float scale, int causal, Sparse sp, int kvlen) {
+// Waves per workgroup (each 32 queries): NWF = 8 (256 queries; one workgroup of 2 waves per SIMD
+// per CU) shares every staged K/V tile among twice the queries of NWF = 4, which serves sequences
+// that are not a multiple of 256 and head dim 256 (whose accumulators need a whole SIMD's
+// register file: 1 wave per SIMD).
+template <int D, int NWF>
+constexpr int fwd_min_waves() { return D >= 256 ? 1 : 8 / NWF; }
+
+template <bool SPARSE, int NWF, int D>
+__global__ void __launch_bounds__(NWF * 64, (fwd_min_waves<D, NWF>())) fwd_kernel(
+    const unsigned short* __restrict__ q, Strides qs, const unsigned short* __restrict__ k, Strides ks,
+    const unsigned short* __restrict__ v, Strides vs, unsigned short* __restrict__ o, Strides os,
+    float* __restrict__ lse, int B, int H, int Hk, int Sq, int Sk, float scale, int causal, Sparse sp, int kvlen,
+    int qoff) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int ROWB = 2 * D;
   constexpr int BUF = 2 * KT * ROWB;  // one ring slot = K tile + V tile
   int* tlist = reinterpret_cast<int*>(smem + 4 * KT * ROWB) + 1;
   constexpr int QBF = NWF * QW;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-  const int nqb = S / QBF;
+  const int nqb = Sq / QBF;
   int bh, qb;
   map_block(nqb, B * H, causal != 0, bh, qb);
   const int b = bh / H, head = bh - b * H;
   const int kh = head / (H / Hk);
   const int q0 = qb * QBF + w * QW;  // this wave's first query
+  const int qpos = q0 + qoff;        // its position on the key axis (causal diagonal)
   const unsigned short* qp = q + b * qs.b + head * qs.h;
   const unsigned short* kp = k + b * ks.b + kh * ks.h;
   const unsigned short* vp = v + b * vs.b + kh * vs.h;
@@ -293,39 +336,59 @@ __global__ void __launch_bounds__(NWF * 64, 8 / NWF) fwd_kernel(const unsigned s
   for (int t = 0; t < D / 32; ++t) oacc[t] = zero16();
   float m = -INFINITY, l = 0.f;
 
-  const int kend = causal ? (qb + 1) * QBF : S;  // keys needed by the workgroup
-  const int ntiles = SPARSE ? build_tile_list(sp, head, 0, kend / KT, KT, qb * QBF, qb * QBF + QBF, true, tlist)
-                            : kend / KT;
+  // keys needed by the workgroup (causal: up to its last query's diagonal)
+  const int kend = causal ? min(Sk, (qb + 1) * QBF + qoff) : Sk;
+  const int nkt = (max(kend, 0) + KT - 1) / KT;
+  const int ntiles = SPARSE ? build_tile_list(sp, head, 0, nkt, KT, qb * QBF, qb * QBF + QBF, true, tlist) : nkt;
   auto tile_at = [&](int i) { return SPARSE ? tlist[i] : i; };
   const uint8_t* lrow = SPARSE ? sp.layout + ((int64_t)head * sp.nb + (q0 + r) / sp.blk) * sp.nb : nullptr;
-  Stager<KT, NWF> sk, sv;
+  // head dim 256: K/V tiles go straight to LDS (global_load_lds): register staging would not fit
+  // next to the 128 accumulator + 64 Q-fragment registers of a wave
+  constexpr bool DMA = D >= 256;
+  Stager<KT, NWF, D> sk, sv;
   const int t0 = ntiles > 0 ? tile_at(0) : 0;
-  sk.load(kp, ks.s, t0 * KT, S);
-  sv.load(vp, vs.s, t0 * KT, S);
-  sk.store(smem);
-  sv.store(smem + KT * ROWB);
+  if constexpr (DMA) {
+    if (ntiles > 0) {
+      tile_glds<KT, D>(kp, ks.s, t0 * KT, smem);
+      tile_glds<KT, D>(vp, vs.s, t0 * KT, smem + KT * ROWB);
+    }
+    vm_wait_all();
+  } else {
+    sk.load(kp, ks.s, t0 * KT, Sk);
+    sv.load(vp, vs.s, t0 * KT, Sk);
+    sk.store(smem);
+    sv.store(smem + KT * ROWB);
+  }
   __syncthreads();
   int cur = 0;
   for (int t = 0; t < ntiles; ++t) {
     const bool more = (t + 1) < ntiles;
     if (more) {
-      sk.load(kp, ks.s, tile_at(t + 1) * KT, S);
-      sv.load(vp, vs.s, tile_at(t + 1) * KT, S);
+      if constexpr (DMA) {
+        tile_glds<KT, D>(kp, ks.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF);
+        tile_glds<KT, D>(vp, vs.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF + KT * ROWB);
+      } else {
+        sk.load(kp, ks.s, tile_at(t + 1) * KT, Sk);
+        sv.load(vp, vs.s, tile_at(t + 1) * KT, Sk);
+      }
     }
     const int kbase = tile_at(t) * KT;
     // a wave whose queries all precede this tile has nothing to add (causal)
-    const bool active = !causal || kbase <= q0 + QW - 1;
+    const bool active = !causal || kbase <= qpos + QW - 1;
     if (active) {
       const char* kt = smem + cur * BUF;
       const char* vt = kt + KT * ROWB;
-      const bool diag = causal && (kbase + KT - 1 > q0);
-      const bool tail = kbase + KT > kvlen;  // keys past the valid length (sequence padded to 128)
+      const bool diag = causal && (kbase + KT - 1 > qpos);
+      const bool tail = kbase + KT > kvlen;  // keys past the valid length (padded key axis)
       if (SPARSE || diag || tail)
-        fwd_tile<true>(kt, vt, qf, oacc, m, l, c, kbase, q0, r, h, lane, diag, tail, kvlen, lrow, SPARSE ? sp.blk : 1);
+        fwd_tile<true, D>(kt, vt, qf, oacc, m, l, c, kbase, qpos, r, h, lane, diag, tail, kvlen, lrow,
+                          SPARSE ? sp.blk : 1);
       else
-        fwd_tile<false>(kt, vt, qf, oacc, m, l, c, kbase, q0, r, h, lane, false, false, kvlen, nullptr, 1);
+        fwd_tile<false, D>(kt, vt, qf, oacc, m, l, c, kbase, qpos, r, h, lane, false, false, kvlen, nullptr, 1);
     }
-    if (more) {
+    if constexpr (DMA) {
+      vm_wait_all();
+    } else if (more) {
       sk.store(smem + (cur ^ 1) * BUF);
       sv.store(smem + (cur ^ 1) * BUF + KT * ROWB);
     }
@@ -333,7 +396,7 @@ __global__ void __launch_bounds__(NWF * 64, 8 / NWF) fwd_kernel(const unsigned s
     cur ^= 1;
   }
   const float lt = l + __shfl_xor(l, 32, 64);
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;  // a fully masked (sparse) row outputs zeros
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;  // a fully masked row outputs zeros
   unsigned short* op = o + b * os.b + head * os.h + (int64_t)(q0 + r) * os.s;
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt)
@@ -344,17 +407,19 @@ __global__ void __launch_bounds__(NWF * 64, 8 / NWF) fwd_kernel(const unsigned s
       for (int e = 0; e < 4; ++e) pk[e] = f32_to_bf16(oacc[dt][4 * rg + e] * inv);
       *reinterpret_cast<u16x4*>(op + 32 * dt + 8 * rg + 4 * h) = pk;
     }
-  if (h == 0) lse[((int64_t)b * H + head) * S + q0 + r] = lt > 0.f ? (m + log2f(lt)) * LN2 : INFINITY;
+  if (h == 0) lse[((int64_t)b * H + head) * Sq + q0 + r] = lt > 0.f ? (m + log2f(lt)) * LN2 : INFINITY;
 }
 
 // =============================================================================================
-// Backward pre-pass: delta[b, h, s] = sum_d dO * O  (fp32)
+// Backward pre-pass: delta[b, h, s] = sum_d dO * O  (fp32); D/8 threads per row
 // =============================================================================================
+template <int D>
 __global__ void __launch_bounds__(256) delta_kernel(const unsigned short* __restrict__ dout, Strides ds,
                                                     const unsigned short* __restrict__ o, Strides os,
                                                     float* __restrict__ delta, int B, int H, int S) {
-  const int64_t row = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
-  const int part = threadIdx.x & 15;
+  constexpr int TPR = D / 8, RPB = 256 / TPR;
+  const int64_t row = (int64_t)blockIdx.x * RPB + (threadIdx.x / TPR);
+  const int part = threadIdx.x % TPR;
   if (row >= (int64_t)B * H * S) return;
   const int s = (int)(row % S);
   const int64_t bh = row / S;
@@ -366,52 +431,29 @@ __global__ void __launch_bounds__(256) delta_kernel(const unsigned short* __rest
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc += x[e] * y[e];
 #pragma unroll
-  for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
+  for (int off = TPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, TPR);
   if (part == 0) delta[row] = acc;
 }
 
-// =============================================================================================
-// Direct-to-LDS tile loads (global_load_lds_dwordx4): no staging registers. A wave-instruction
-// writes 1 KiB = 4 rows linearly, so the XOR swizzle goes on the per-lane SOURCE chunk (the
-// swizzle is an involution: position c' of row `row` holds logical chunk c' ^ f(row)).
-// =============================================================================================
-__device__ __forceinline__ void glds16(const void* gsrc, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
-}
-__device__ __forceinline__ void glds4(const void* gsrc, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 4, 0, 0);
-}
-template <int ROWS>
-__device__ __forceinline__ void tile_glds(const unsigned short* base, int64_t row_stride, int row0, char* lds) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int i = 0; i < ROWS / 4 / NW; ++i) {
-    const int n = i * NW + w;
-    const int row = 4 * n + (lane >> 4);
-    const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
-    glds16(base + (int64_t)(row0 + row) * row_stride + ch * 8, lds + n * 1024);
-  }
-}
-__device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+template <int D>
+constexpr int bwd_min_waves() { return D >= 256 ? 1 : 2; }
 
 // =============================================================================================
 // dQ: forward-shaped. Per wave 32 queries; per K/V tile recompute S^T, P^T, dP^T = V dO^T,
 // dS^T = P^T (dP^T - delta), dQ^T += K^T dS^T.
 // =============================================================================================
-template <bool MASK>
+template <bool MASK, int D>
 __device__ __forceinline__ void dq_tile(const char* kt, const char* vt, const bf16x8 (&qf)[D / 16],
                                         const bf16x8 (&df)[D / 16], f32x16 (&dqacc)[D / 32], float c, float lse2,
-                                        float dlt, int kbase, int q0, int r, int h, int lane, bool diag, bool tail,
+                                        float dlt, int kbase, int qpos, int r, int h, int lane, bool diag, bool tail,
                                         int kvlen, const uint8_t* lay_row, int blk) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     f32x16 s = zero16(), dp = zero16();
 #pragma unroll
     for (int t2 = 0; t2 < D / 16; ++t2) {
-      s = mfma(lds_row16(kt, 32 * j + r, 2 * t2 + h), qf[t2], s);
-      dp = mfma(lds_row16(vt, 32 * j + r, 2 * t2 + h), df[t2], dp);
+      s = mfma(lds_row16<D>(kt, 32 * j + r, 2 * t2 + h), qf[t2], s);
+      dp = mfma(lds_row16<D>(vt, 32 * j + r, 2 * t2 + h), df[t2], dp);
     }
     bool b0 = true, b1 = true;
     if (MASK && lay_row) {
@@ -422,7 +464,7 @@ __device__ __forceinline__ void dq_tile(const char* kt, const char* vt, const bf
     for (int i = 0; i < 16; ++i) {
       float p = fast_exp2(__builtin_fmaf(s[i], c, -lse2));
       if (MASK) {
-        if (diag && (kbase + 32 * j + acc_row(i, h) > q0 + r)) p = 0.f;
+        if (diag && (kbase + 32 * j + acc_row(i, h) > qpos + r)) p = 0.f;
         if (tail && (kbase + 32 * j + acc_row(i, h) >= kvlen)) p = 0.f;
         if (!(acc_row(i, h) < 16 ? b0 : b1)) p = 0.f;
       }
@@ -432,43 +474,44 @@ __device__ __forceinline__ void dq_tile(const char* kt, const char* vt, const bf
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 db = acc_to_b(s, s2);
 #pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt) dqacc[dt] = mfma(lds_trA(kt, 32 * j + 16 * s2, dt, lane), db, dqacc[dt]);
+      for (int dt = 0; dt < D / 32; ++dt)
+        dqacc[dt] = mfma(lds_trA<D>(kt, 32 * j + 16 * s2, dt, lane), db, dqacc[dt]);
     }
   }
 }
 
-template <bool SPARSE>
-__global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __restrict__ q, Strides qs,
-                                                    const unsigned short* __restrict__ k, Strides ks,
-                                                    const unsigned short* __restrict__ v, Strides vs,
-                                                    const unsigned short* __restrict__ dout, Strides dos,
-                                                    const float* __restrict__ lse, const float* __restrict__ delta,
-                                                    unsigned short* __restrict__ dq, Strides dqs, int B, int H,
-                                                    int Hk, int S, float scale, int causal, Sparse sp, int kvlen) {
+template <bool SPARSE, int D>
+__global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dq_kernel(
+    const unsigned short* __restrict__ q, Strides qs, const unsigned short* __restrict__ k, Strides ks,
+    const unsigned short* __restrict__ v, Strides vs, const unsigned short* __restrict__ dout, Strides dos,
+    const float* __restrict__ lse, const float* __restrict__ delta, unsigned short* __restrict__ dq, Strides dqs,
+    int B, int H, int Hk, int Sq, int Sk, float scale, int causal, Sparse sp, int kvlen, int qoff) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int ROWB = 2 * D;
   constexpr int BUF = 2 * KT * ROWB;
   int* tlist = reinterpret_cast<int*>(smem + 4 * KT * ROWB) + 1;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-  const int nqb = S / QB;
+  const int nqb = Sq / QB;
   int bh, qb;
   map_block(nqb, B * H, causal != 0, bh, qb);
   const int b = bh / H, head = bh - b * H;
   const int kh = head / (H / Hk);
   const int q0 = qb * QB + w * QW;
+  const int qpos = q0 + qoff;
   const unsigned short* qp = q + b * qs.b + head * qs.h;
   const unsigned short* dop = dout + b * dos.b + head * dos.h;
   const unsigned short* kp = k + b * ks.b + kh * ks.h;
   const unsigned short* vp = v + b * vs.b + kh * vs.h;
   const float c = scale * LOG2E;
-  const int64_t lrow = ((int64_t)b * H + head) * S + q0 + r;
-  const int kend = causal ? (qb + 1) * QB : S;
-  const int ntiles = SPARSE ? build_tile_list(sp, head, 0, kend / KT, KT, qb * QB, qb * QB + QB, true, tlist)
-                            : kend / KT;
+  const int64_t lrow = ((int64_t)b * H + head) * Sq + q0 + r;
+  const int kend = causal ? min(Sk, (qb + 1) * QB + qoff) : Sk;
+  const int nkt = (max(kend, 0) + KT - 1) / KT;
+  const int ntiles = SPARSE ? build_tile_list(sp, head, 0, nkt, KT, qb * QB, qb * QB + QB, true, tlist) : nkt;
   auto tile_at = [&](int i) { return SPARSE ? tlist[i] : i; };
   const uint8_t* lay_row = SPARSE ? sp.layout + ((int64_t)head * sp.nb + (q0 + r) / sp.blk) * sp.nb : nullptr;
   if (ntiles > 0) {
-    tile_glds<KT>(kp, ks.s, tile_at(0) * KT, smem);
-    tile_glds<KT>(vp, vs.s, tile_at(0) * KT, smem + KT * ROWB);
+    tile_glds<KT, D>(kp, ks.s, tile_at(0) * KT, smem);
+    tile_glds<KT, D>(vp, vs.s, tile_at(0) * KT, smem + KT * ROWB);
   }
 
   const float lse2 = lse[lrow] * LOG2E;
@@ -487,21 +530,22 @@ __global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __rest
   int cur = 0;
   for (int t = 0; t < ntiles; ++t) {
     if (t + 1 < ntiles) {
-      tile_glds<KT>(kp, ks.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF);
-      tile_glds<KT>(vp, vs.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF + KT * ROWB);
+      tile_glds<KT, D>(kp, ks.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF);
+      tile_glds<KT, D>(vp, vs.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF + KT * ROWB);
     }
     const int kbase = tile_at(t) * KT;
-    const bool active = !causal || kbase <= q0 + QW - 1;
+    const bool active = !causal || kbase <= qpos + QW - 1;
     if (active) {
       const char* kt = smem + cur * BUF;
       const char* vt = smem + cur * BUF + KT * ROWB;
-      const bool diag = causal && (kbase + KT - 1 > q0);
+      const bool diag = causal && (kbase + KT - 1 > qpos);
       const bool tail = kbase + KT > kvlen;
       if (SPARSE || diag || tail)
-        dq_tile<true>(kt, vt, qf, df, dqacc, c, lse2, dlt, kbase, q0, r, h, lane, diag, tail, kvlen, lay_row,
-                      SPARSE ? sp.blk : 1);
+        dq_tile<true, D>(kt, vt, qf, df, dqacc, c, lse2, dlt, kbase, qpos, r, h, lane, diag, tail, kvlen, lay_row,
+                         SPARSE ? sp.blk : 1);
       else
-        dq_tile<false>(kt, vt, qf, df, dqacc, c, lse2, dlt, kbase, q0, r, h, lane, false, false, kvlen, nullptr, 1);
+        dq_tile<false, D>(kt, vt, qf, df, dqacc, c, lse2, dlt, kbase, qpos, r, h, lane, false, false, kvlen,
+                          nullptr, 1);
     }
     vm_wait_all();
     __syncthreads();
@@ -523,28 +567,30 @@ __global__ void __launch_bounds__(256, 2) dq_kernel(const unsigned short* __rest
 // dK, dV: per wave 32 keys held on the lanes; sweep every query head of the GQA group and every
 // 32-query tile at or after the keys (causal). Q/dO tiles + LSE/delta arrive by LDS-DMA into a
 // 2-slot ring; the workgroup's V block (128 keys) sits in LDS for the whole kernel (V fragments in
-// registers too would exceed the 256-VGPR budget of 2 waves/SIMD and spill); K fragments,
-// dK^T and dV^T live in registers.
+// registers too would exceed the VGPR budget and spill); K fragments, dK^T and dV^T live in
+// registers.
 // =============================================================================================
 constexpr int QT = 32;  // queries per tile in the dK/dV sweep
-constexpr int KV_TILE = QT * ROWB;                 // 8 KiB
-constexpr int KV_SLOT = 2 * KV_TILE + 2 * QT * 4;  // Q, dO, lse[32], delta[32]
-constexpr int KV_VBLK = QB * ROWB;                 // 32 KiB
+template <int D> struct KVL {
+  static constexpr int TILE = QT * 2 * D;              // one Q (or dO) tile
+  static constexpr int SLOT = 2 * TILE + 2 * QT * 4;   // Q, dO, lse[32], delta[32]
+  static constexpr int VBLK = QB * 2 * D;              // the V block
+};
 
-template <bool MASK>
+template <bool MASK, int D>
 __device__ __forceinline__ void dkdv_tile(const char* slot, const char* vblk, const bf16x8 (&kf)[D / 16],
                                           f32x16 (&dka)[D / 32], f32x16 (&dva)[D / 32], float c, int qt0, int k0,
                                           int w, int r, int h, int lane, bool diag, const Sparse& sp, int hq0,
-                                          int kbl) {
+                                          int kbl, int qoff) {
   const char* qt = slot;
-  const char* dt_ = slot + KV_TILE;
-  const float* l2 = reinterpret_cast<const float*>(slot + 2 * KV_TILE);
+  const char* dt_ = slot + KVL<D>::TILE;
+  const float* l2 = reinterpret_cast<const float*>(slot + 2 * KVL<D>::TILE);
   const float* dl = l2 + QT;
   f32x16 s = zero16(), dp = zero16();
 #pragma unroll
   for (int t2 = 0; t2 < D / 16; ++t2) {
-    s = mfma(lds_row16(qt, r, 2 * t2 + h), kf[t2], s);                                       // S  [query][key]
-    dp = mfma(lds_row16(dt_, r, 2 * t2 + h), lds_row16(vblk, w * QW + r, 2 * t2 + h), dp);  // dP
+    s = mfma(lds_row16<D>(qt, r, 2 * t2 + h), kf[t2], s);                                        // S  [query][key]
+    dp = mfma(lds_row16<D>(dt_, r, 2 * t2 + h), lds_row16<D>(vblk, w * QW + r, 2 * t2 + h), dp);  // dP
   }
   bool b0 = true, b1 = true;  // layout bits of query rows qt0+[0,16) and qt0+[16,32) vs this key
   if (MASK && sp.layout) {
@@ -556,7 +602,7 @@ __device__ __forceinline__ void dkdv_tile(const char* slot, const char* vblk, co
     const int qi = acc_row(i, h);
     float p = fast_exp2(__builtin_fmaf(s[i], c, -l2[qi] * LOG2E));
     if (MASK) {
-      if (diag && (k0 + r > qt0 + qi)) p = 0.f;
+      if (diag && (k0 + r > qt0 + qi + qoff)) p = 0.f;
       if (!(qi < 16 ? b0 : b1)) p = 0.f;
     }
     s[i] = p;                      // P
@@ -568,33 +614,31 @@ __device__ __forceinline__ void dkdv_tile(const char* slot, const char* vblk, co
     const bf16x8 db = acc_to_b(dp, s2);
 #pragma unroll
     for (int t = 0; t < D / 32; ++t) {
-      dva[t] = mfma(lds_trA(dt_, 16 * s2, t, lane), pb, dva[t]);  // dV^T += dO^T P
-      dka[t] = mfma(lds_trA(qt, 16 * s2, t, lane), db, dka[t]);   // dK^T += Q^T dS
+      dva[t] = mfma(lds_trA<D>(dt_, 16 * s2, t, lane), pb, dva[t]);  // dV^T += dO^T P
+      dka[t] = mfma(lds_trA<D>(qt, 16 * s2, t, lane), db, dka[t]);   // dK^T += Q^T dS
     }
   }
 }
 
 // SPLIT (GQA): one workgroup per (batch, QUERY head, key block) instead of per KV head: under a
-// causal mask the KV-head form gives key block 0 G x (S/128) query tiles while the mean block has
-// half of that, and with B*Hk*S/128 ~ 2 workgroups per CU the whole launch waits for block 0
+// causal mask the KV-head form gives key block 0 G x (Sq/128) query tiles while the mean block has
+// half of that, and with B*Hk*Sk/128 ~ 2 workgroups per CU the whole launch waits for block 0
 // (measured 650 us at B4 S2048 H32/8). Splitting the G query heads cuts the longest job by G; the
-// per-head fp32 dK/dV partials [B, S, H, D] are summed over G by dkdv_reduce_kernel.
-template <bool SPLIT>
-__global__ void __launch_bounds__(256, 2) dkdv_kernel(const unsigned short* __restrict__ q, Strides qs,
-                                                      const unsigned short* __restrict__ k, Strides ks,
-                                                      const unsigned short* __restrict__ v, Strides vs,
-                                                      const unsigned short* __restrict__ dout, Strides dos,
-                                                      const float* __restrict__ lse, const float* __restrict__ delta,
-                                                      unsigned short* __restrict__ dk, Strides dks,
-                                                      unsigned short* __restrict__ dv, Strides dvs,
-                                                      float* __restrict__ pk, float* __restrict__ pv, int B, int H,
-                                                      int Hk, int S, float scale, int causal, Sparse sp) {
+// per-head fp32 dK/dV partials [B, Sk, H, D] are summed over G by dkdv_reduce_kernel.
+template <bool SPLIT, int D>
+__global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
+    const unsigned short* __restrict__ q, Strides qs, const unsigned short* __restrict__ k, Strides ks,
+    const unsigned short* __restrict__ v, Strides vs, const unsigned short* __restrict__ dout, Strides dos,
+    const float* __restrict__ lse, const float* __restrict__ delta, unsigned short* __restrict__ dk, Strides dks,
+    unsigned short* __restrict__ dv, Strides dvs, float* __restrict__ pk, float* __restrict__ pv, int B, int H,
+    int Hk, int Sq, int Sk, float scale, int causal, Sparse sp, int qoff) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  using G_ = KVL<D>;
   char* vblk = smem;
-  char* ring = smem + KV_VBLK;
-  int* tlist = reinterpret_cast<int*>(ring + 2 * KV_SLOT) + 1;
+  char* ring = smem + G_::VBLK;
+  int* tlist = reinterpret_cast<int*>(ring + 2 * G_::SLOT) + 1;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-  const int nkb = S / QB;
+  const int nkb = Sk / QB;
   int bh, kb;
   const int HB = SPLIT ? H : Hk;
   map_block(nkb, B * HB, false, bh, kb);  // key block 0 is the heaviest under causality
@@ -606,10 +650,11 @@ __global__ void __launch_bounds__(256, 2) dkdv_kernel(const unsigned short* __re
   const unsigned short* kp = k + b * ks.b + kh * ks.h;
   const unsigned short* vp = v + b * vs.b + kh * vs.h;
   const float c = scale * LOG2E;
-  const int qstart = causal ? kb * QB : 0;
-  const int ntq = (S - qstart) / QT;
+  // causal: the first query that sees key block kb (query i sees keys <= i + qoff)
+  const int qstart = causal ? min(Sq, max(0, kb * QB - qoff) / QT * QT) : 0;
+  const int ntq = (Sq - qstart) / QT;
   // sparse: SPLIT mode (G == 1), list of the active 32-query tiles of this key block
-  const int total = sp.layout ? build_tile_list(sp, hq0, qstart / QT, S / QT, QT, kb * QB, kb * QB + QB, false, tlist)
+  const int total = sp.layout ? build_tile_list(sp, hq0, qstart / QT, Sq / QT, QT, kb * QB, kb * QB + QB, false, tlist)
                               : ntq * G;
   auto qtile_at = [&](int it) { return sp.layout ? tlist[it] * QT : qstart + (it % ntq) * QT; };
   const int kbl = sp.layout ? (k0 + r) / sp.blk : 0;
@@ -617,14 +662,14 @@ __global__ void __launch_bounds__(256, 2) dkdv_kernel(const unsigned short* __re
   auto issue = [&](int it, char* slot) {
     const int hq = sp.layout ? hq0 : hq0 + it / ntq;
     const int qt0 = qtile_at(it);
-    tile_glds<QT>(q + b * qs.b + hq * qs.h, qs.s, qt0, slot);
-    tile_glds<QT>(dout + b * dos.b + hq * dos.h, dos.s, qt0, slot + KV_TILE);
+    tile_glds<QT, D>(q + b * qs.b + hq * qs.h, qs.s, qt0, slot);
+    tile_glds<QT, D>(dout + b * dos.b + hq * dos.h, dos.s, qt0, slot + G_::TILE);
     if (w == 0) {  // 64 lanes x 4 B: lse[32] then delta[32]
-      const int64_t lr = ((int64_t)b * H + hq) * S + qt0 + (lane & 31);
-      glds4(lane < 32 ? (const void*)(lse + lr) : (const void*)(delta + lr), slot + 2 * KV_TILE);
+      const int64_t lr = ((int64_t)b * H + hq) * Sq + qt0 + (lane & 31);
+      glds4(lane < 32 ? (const void*)(lse + lr) : (const void*)(delta + lr), slot + 2 * G_::TILE);
     }
   };
-  tile_glds<QB>(vp, vs.s, kb * QB, vblk);
+  tile_glds<QB, D>(vp, vs.s, kb * QB, vblk);
   if (total > 0) issue(0, ring);
   bf16x8 kf[D / 16];
 #pragma unroll
@@ -640,35 +685,33 @@ __global__ void __launch_bounds__(256, 2) dkdv_kernel(const unsigned short* __re
   __syncthreads();
   int cur = 0;
   for (int it = 0; it < total; ++it) {
-    if (it + 1 < total) issue(it + 1, ring + (cur ^ 1) * KV_SLOT);
+    if (it + 1 < total) issue(it + 1, ring + (cur ^ 1) * G_::SLOT);
     const int qt0 = qtile_at(it);
-    const bool active = !causal || (qt0 + QT - 1 >= k0);
+    const bool active = !causal || (qt0 + QT - 1 + qoff >= k0);
     if (active) {
-      const char* slot = ring + cur * KV_SLOT;
-      const int hq = sp.layout ? hq0 : hq0 + it / ntq;
-      (void)hq;
-      const bool diag = causal && (qt0 < k0 + QW);
-      dkdv_tile<true>(slot, vblk, kf, dka, dva, c, qt0, k0, w, r, h, lane, diag, sp, hq0, kbl);
+      const char* slot = ring + cur * G_::SLOT;
+      const bool diag = causal && (qt0 + qoff < k0 + QW);
+      dkdv_tile<true, D>(slot, vblk, kf, dka, dva, c, qt0, k0, w, r, h, lane, diag, sp, hq0, kbl, qoff);
     }
     vm_wait_all();
     __syncthreads();
     cur ^= 1;
   }
-  if (SPLIT && pk != nullptr) {  // fp32 partials, layout [B, S, H, D] contiguous
-    float* kp32 = pk + (((int64_t)b * S + k0 + r) * H + hq0) * D;
-    float* vp32 = pv + (((int64_t)b * S + k0 + r) * H + hq0) * D;
+  if (SPLIT && pk != nullptr) {  // fp32 partials, layout [B, Sk, H, D] contiguous
+    float* kp32 = pk + (((int64_t)b * Sk + k0 + r) * H + hq0) * D;
+    float* vp32 = pv + (((int64_t)b * Sk + k0 + r) * H + hq0) * D;
 #pragma unroll
     for (int t = 0; t < D / 32; ++t)
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
-        f32x4 a, c;
+        f32x4 a, cc;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           a[e] = dka[t][4 * rg + e] * scale;
-          c[e] = dva[t][4 * rg + e];
+          cc[e] = dva[t][4 * rg + e];
         }
         *reinterpret_cast<f32x4*>(kp32 + 32 * t + 8 * rg + 4 * h) = a;
-        *reinterpret_cast<f32x4*>(vp32 + 32 * t + 8 * rg + 4 * h) = c;
+        *reinterpret_cast<f32x4*>(vp32 + 32 * t + 8 * rg + 4 * h) = cc;
       }
     return;
   }
@@ -678,19 +721,20 @@ __global__ void __launch_bounds__(256, 2) dkdv_kernel(const unsigned short* __re
   for (int t = 0; t < D / 32; ++t)
 #pragma unroll
     for (int rg = 0; rg < 4; ++rg) {
-      u16x4 pk, pv;
+      u16x4 pk4, pv4;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        pk[e] = f32_to_bf16(dka[t][4 * rg + e] * scale);
-        pv[e] = f32_to_bf16(dva[t][4 * rg + e]);
+        pk4[e] = f32_to_bf16(dka[t][4 * rg + e] * scale);
+        pv4[e] = f32_to_bf16(dva[t][4 * rg + e]);
       }
-      *reinterpret_cast<u16x4*>(kop + 32 * t + 8 * rg + 4 * h) = pk;
-      *reinterpret_cast<u16x4*>(vop + 32 * t + 8 * rg + 4 * h) = pv;
+      *reinterpret_cast<u16x4*>(kop + 32 * t + 8 * rg + 4 * h) = pk4;
+      *reinterpret_cast<u16x4*>(vop + 32 * t + 8 * rg + 4 * h) = pv4;
     }
 }
 
 
 // dk[b, s, kh, :] = sum_g pk[b, s, kh*G + g, :] (dv likewise); one thread per 8 output elements.
+template <int D>
 __global__ void __launch_bounds__(256) dkdv_reduce_kernel(const float* __restrict__ pk, const float* __restrict__ pv,
                                                           unsigned short* __restrict__ dk, Strides dks,
                                                           unsigned short* __restrict__ dv, Strides dvs, int B, int S,
@@ -724,15 +768,18 @@ static fa::Strides strides_of(const at::Tensor& t) {
   return fa::Strides{t.stride(0), t.stride(1), t.stride(2)};
 }
 
+// q: [B, Sq, Hq, D]; k, v: [B, Sk, Hk, D]; D in {64, 128, 256}; Sq, Sk multiples of 128
 static void check_qkv(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v) {
   SXE_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "flash_attn: tensors must be [B, S, H, D]");
   SXE_CHECK(q.scalar_type() == at::kBFloat16 && k.scalar_type() == at::kBFloat16 && v.scalar_type() == at::kBFloat16,
             "flash_attn: bf16 only");
-  SXE_CHECK(q.size(3) == fa::D && k.size(3) == fa::D && v.size(3) == fa::D, "flash_attn: head dim must be 128");
+  const int64_t D = q.size(3);
+  SXE_CHECK(D == 64 || D == 128 || D == 256, "flash_attn: head dim must be 64, 128 or 256");
+  SXE_CHECK(k.size(3) == D && v.size(3) == D, "flash_attn: q/k/v head dims differ");
   SXE_CHECK(q.stride(3) == 1 && k.stride(3) == 1 && v.stride(3) == 1, "flash_attn: unit stride on D");
-  SXE_CHECK(k.sizes() == v.sizes() && q.size(0) == k.size(0) && q.size(1) == k.size(1), "flash_attn: q/k/v shapes");
+  SXE_CHECK(k.sizes() == v.sizes() && q.size(0) == k.size(0), "flash_attn: q/k/v shapes");
   SXE_CHECK(q.size(2) % k.size(2) == 0, "flash_attn: Hq must be a multiple of Hkv");
-  SXE_CHECK(q.size(1) % fa::QB == 0, "flash_attn: seq_len must be a multiple of 128");
+  SXE_CHECK(q.size(1) % fa::QB == 0 && k.size(1) % fa::QB == 0, "flash_attn: seq lengths must be multiples of 128");
   for (const at::Tensor* t : {&q, &k, &v})
     SXE_CHECK((t->stride(1) % 8) == 0 && (t->stride(2) % 8) == 0 && (t->stride(0) % 8) == 0 &&
                   (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "flash_attn: 16-byte aligned rows required");
@@ -760,97 +807,120 @@ static bool fwd_narrow() {
   return v;
 }
 
-static std::vector<at::Tensor> fwd_impl(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, double scale,
-                                        fa::Sparse sp, int64_t kv_len = -1) {
-  check_qkv(q, k, v);
-  const int B = q.size(0), S = q.size(1), H = q.size(2), Hk = k.size(2);
-  const int kvlen = kv_len < 0 ? S : (int)kv_len;
-  SXE_CHECK(kvlen >= 1 && kvlen <= S, "flash_attn: kv_len must be in [1, seq_len]");
-  c10::DeviceGuard guard(q.device());
-  auto o = at::empty({B, S, H, fa::D}, q.options());
-  auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
-  const int grid = (S / fa::QB) * B * H;
-  const size_t lds = 4 * fa::KT * fa::ROWB + (sp.layout ? kListBytes : 0);
+template <typename F>
+static void set_lds_limit(F* f, size_t bytes) {
+  SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)bytes));
+}
+
+// kv_len: valid keys (the rest of the padded key axis is masked); qoff: causal offset (query i sees
+// keys <= i + qoff), default Sk - Sq (bottom-right aligned)
+template <int D>
+static std::vector<at::Tensor> fwd_impl_d(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, double scale,
+                                          fa::Sparse sp, int kvlen, int qoff) {
+  const int B = q.size(0), Sq = q.size(1), H = q.size(2), Sk = k.size(1), Hk = k.size(2);
+  auto o = at::empty({B, Sq, H, D}, q.options());
+  auto lse = at::empty({B, H, Sq}, q.options().dtype(at::kFloat));
+  constexpr int ROWB = 2 * D;
+  const size_t lds = 4 * fa::KT * ROWB + (sp.layout ? kListBytes : 0);
   static bool attr = false;
   if (!attr) {
-    for (const void* f : {reinterpret_cast<const void*>(&fa::fwd_kernel<false, 4>),
-                          reinterpret_cast<const void*>(&fa::fwd_kernel<true, 4>),
-                          reinterpret_cast<const void*>(&fa::fwd_kernel<false, 8>),
-                          reinterpret_cast<const void*>(&fa::fwd_kernel<true, 8>)})
-      SXE_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)(4 * fa::KT * fa::ROWB + kListBytes)));
+    const size_t mx = 4 * fa::KT * ROWB + kListBytes;
+    set_lds_limit(&fa::fwd_kernel<false, 4, D>, mx);
+    set_lds_limit(&fa::fwd_kernel<true, 4, D>, mx);
+    if constexpr (D < 256) {
+      set_lds_limit(&fa::fwd_kernel<false, 8, D>, mx);
+      set_lds_limit(&fa::fwd_kernel<true, 8, D>, mx);
+    }
     attr = true;
   }
-  const bool wide = S % 256 == 0 && !fwd_narrow();
-  auto launch = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(wide ? grid / 2 : grid), dim3(wide ? 512 : 256), lds, cur_stream(),
+  // 8 waves share each staged K/V tile when the query axis allows; head dim 256 runs 4 (register budget)
+  const bool wide = D < 256 && Sq % 256 == 0 && !fwd_narrow();
+  const int grid = (Sq / fa::QB) * B * H;
+  auto launch = [&](auto kern, int nwf) {
+    hipLaunchKernelGGL(kern, dim3(nwf == 8 ? grid / 2 : grid), dim3(nwf * 64), lds, cur_stream(),
                        reinterpret_cast<const unsigned short*>(q.data_ptr()), strides_of(q),
                        reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
                        reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),
                        reinterpret_cast<unsigned short*>(o.data_ptr()), strides_of(o), lse.data_ptr<float>(), B, H, Hk,
-                       S, (float)scale, causal ? 1 : 0, sp, kvlen);
+                       Sq, Sk, (float)scale, causal ? 1 : 0, sp, kvlen, qoff);
   };
-  if (sp.layout) wide ? launch(fa::fwd_kernel<true, 8>) : launch(fa::fwd_kernel<true, 4>);
-  else wide ? launch(fa::fwd_kernel<false, 8>) : launch(fa::fwd_kernel<false, 4>);
+  if constexpr (D < 256) {
+    if (wide) {
+      sp.layout ? launch(fa::fwd_kernel<true, 8, D>, 8) : launch(fa::fwd_kernel<false, 8, D>, 8);
+      SXE_LAUNCH_CHECK();
+      return {o, lse};
+    }
+  }
+  sp.layout ? launch(fa::fwd_kernel<true, 4, D>, 4) : launch(fa::fwd_kernel<false, 4, D>, 4);
   SXE_LAUNCH_CHECK();
   return {o, lse};
 }
 
-// dq/dk/dv are caller-provided (possibly strided views of one dqkv buffer).
-static void bwd_impl(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
-                     at::Tensor dq, at::Tensor dk, at::Tensor dv, bool causal, double scale, fa::Sparse sp,
-                     int64_t kv_len = -1) {
+static std::vector<at::Tensor> fwd_impl(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, double scale,
+                                        fa::Sparse sp, int64_t kv_len = -1, int64_t causal_offset = INT64_MIN) {
   check_qkv(q, k, v);
-  check_qkv(dq, dk, dv);
-  const int kvlen = kv_len < 0 ? (int)q.size(1) : (int)kv_len;
-  SXE_CHECK(kvlen >= 1 && kvlen <= q.size(1), "flash_attn_bwd: kv_len must be in [1, seq_len]");
-  SXE_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && dout.stride(3) == 1 && o.stride(3) == 1,
-            "flash_attn_bwd: dout/o shapes");
-  SXE_CHECK(dq.sizes() == q.sizes() && dk.sizes() == k.sizes() && dv.sizes() == v.sizes(), "flash_attn_bwd: grad shapes");
-  const int B = q.size(0), S = q.size(1), H = q.size(2), Hk = k.size(2);
+  const int Sq = q.size(1), Sk = k.size(1);
+  const int kvlen = kv_len < 0 ? Sk : (int)kv_len;
+  SXE_CHECK(kvlen >= 1 && kvlen <= Sk, "flash_attn: kv_len must be in [1, Sk]");
+  const int qoff = causal_offset == INT64_MIN ? Sk - Sq : (int)causal_offset;
+  SXE_CHECK(!sp.layout || (Sq == Sk && qoff == 0), "block-sparse attention needs Sq == Sk");
   c10::DeviceGuard guard(q.device());
-  auto delta = at::empty({B, H, S}, q.options().dtype(at::kFloat));
-  const int64_t rows = (int64_t)B * H * S;
-  hipLaunchKernelGGL(fa::delta_kernel, dim3((rows + 15) / 16), dim3(256), 0, cur_stream(),
+  switch (q.size(3)) {
+    case 64: return fwd_impl_d<64>(q, k, v, causal, scale, sp, kvlen, qoff);
+    case 256: return fwd_impl_d<256>(q, k, v, causal, scale, sp, kvlen, qoff);
+    default: return fwd_impl_d<128>(q, k, v, causal, scale, sp, kvlen, qoff);
+  }
+}
+
+template <int D>
+static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
+                       at::Tensor dq, at::Tensor dk, at::Tensor dv, bool causal, double scale, fa::Sparse sp,
+                       int kvlen, int qoff) {
+  const int B = q.size(0), Sq = q.size(1), H = q.size(2), Sk = k.size(1), Hk = k.size(2);
+  constexpr int ROWB = 2 * D;
+  using G_ = fa::KVL<D>;
+  auto delta = at::empty({B, H, Sq}, q.options().dtype(at::kFloat));
+  const int64_t rows = (int64_t)B * H * Sq;
+  constexpr int RPB = 256 / (D / 8);
+  hipLaunchKernelGGL(fa::delta_kernel<D>, dim3((rows + RPB - 1) / RPB), dim3(256), 0, cur_stream(),
                      reinterpret_cast<const unsigned short*>(dout.data_ptr()), strides_of(dout),
                      reinterpret_cast<const unsigned short*>(o.data_ptr()), strides_of(o), delta.data_ptr<float>(), B,
-                     H, S);
+                     H, Sq);
   SXE_LAUNCH_CHECK();
-  const size_t lds_dq = 4 * fa::KT * fa::ROWB + (sp.layout ? kListBytes : 0);
-  const size_t lds_kv_max = fa::KV_VBLK + 2 * fa::KV_SLOT + kListBytes;
+  const size_t lds_dq = 4 * fa::KT * ROWB + (sp.layout ? kListBytes : 0);
+  const size_t lds_kv_max = G_::VBLK + 2 * G_::SLOT + kListBytes;
   static bool attr_set = false;
   if (!attr_set) {  // > 64 KiB of dynamic LDS must be opted into (gfx950 has 160 KiB per CU)
-    SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::dq_kernel<false>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * fa::KT * fa::ROWB + kListBytes)));
-    SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::dq_kernel<true>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4 * fa::KT * fa::ROWB + kListBytes)));
-    SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::dkdv_kernel<false>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv_max));
-    SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&fa::dkdv_kernel<true>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv_max));
+    set_lds_limit(&fa::dq_kernel<false, D>, 4 * fa::KT * ROWB + kListBytes);
+    set_lds_limit(&fa::dq_kernel<true, D>, 4 * fa::KT * ROWB + kListBytes);
+    set_lds_limit(&fa::dkdv_kernel<false, D>, lds_kv_max);
+    set_lds_limit(&fa::dkdv_kernel<true, D>, lds_kv_max);
     attr_set = true;
   }
-  hipLaunchKernelGGL(sp.layout ? fa::dq_kernel<true> : fa::dq_kernel<false>, dim3((S / fa::QB) * B * H), dim3(256), lds_dq, cur_stream(),
+  auto* dqk = sp.layout ? fa::dq_kernel<true, D> : fa::dq_kernel<false, D>;
+  hipLaunchKernelGGL(dqk, dim3((Sq / fa::QB) * B * H),
+                     dim3(256), lds_dq, cur_stream(),
                      reinterpret_cast<const unsigned short*>(q.data_ptr()), strides_of(q),
                      reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
                      reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),
                      reinterpret_cast<const unsigned short*>(dout.data_ptr()), strides_of(dout),
                      lse.data_ptr<float>(), delta.data_ptr<float>(),
-                     reinterpret_cast<unsigned short*>(dq.data_ptr()), strides_of(dq), B, H, Hk, S, (float)scale,
-                     causal ? 1 : 0, sp, kvlen);
+                     reinterpret_cast<unsigned short*>(dq.data_ptr()), strides_of(dq), B, H, Hk, Sq, Sk, (float)scale,
+                     causal ? 1 : 0, sp, kvlen, qoff);
   SXE_LAUNCH_CHECK();
   // sparse: always one workgroup per query head (per-head tile lists); with GQA the per-head fp32
   // partials are reduced; causal GQA: split to remove the key-block-0 tail (see dkdv_kernel)
   const bool split = sp.layout != nullptr || (causal && H > Hk);
   const bool partials = split && H > Hk;
-  const size_t lds_kv = fa::KV_VBLK + 2 * fa::KV_SLOT + (sp.layout ? kListBytes : 0);
+  const size_t lds_kv = G_::VBLK + 2 * G_::SLOT + (sp.layout ? kListBytes : 0);
   at::Tensor pk, pv;
   if (partials) {
-    pk = at::empty({B, S, H, fa::D}, q.options().dtype(at::kFloat));
-    pv = at::empty({B, S, H, fa::D}, q.options().dtype(at::kFloat));
+    pk = at::empty({B, Sk, H, D}, q.options().dtype(at::kFloat));
+    pv = at::empty({B, Sk, H, D}, q.options().dtype(at::kFloat));
   }
   auto launch = [&](auto kern, int heads) {
-    hipLaunchKernelGGL(kern, dim3((S / fa::QB) * B * heads), dim3(256), lds_kv, cur_stream(),
+    hipLaunchKernelGGL(kern, dim3((Sk / fa::QB) * B * heads), dim3(256), lds_kv, cur_stream(),
                        reinterpret_cast<const unsigned short*>(q.data_ptr()), strides_of(q),
                        reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
                        reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),
@@ -859,31 +929,58 @@ static void bwd_impl(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, 
                        reinterpret_cast<unsigned short*>(dk.data_ptr()), strides_of(dk),
                        reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv),
                        partials ? pk.data_ptr<float>() : nullptr, partials ? pv.data_ptr<float>() : nullptr, B, H, Hk,
-                       S, (float)scale, causal ? 1 : 0, sp);
+                       Sq, Sk, (float)scale, causal ? 1 : 0, sp, qoff);
   };
   if (split) {
-    launch(fa::dkdv_kernel<true>, H);
+    launch(fa::dkdv_kernel<true, D>, H);
     SXE_LAUNCH_CHECK();
     if (partials) {
-      const int64_t n8 = (int64_t)B * S * Hk * (fa::D / 8);
-      hipLaunchKernelGGL(fa::dkdv_reduce_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, cur_stream(),
+      const int64_t n8 = (int64_t)B * Sk * Hk * (D / 8);
+      hipLaunchKernelGGL(fa::dkdv_reduce_kernel<D>, dim3(stream_grid(n8, 256)), dim3(256), 0, cur_stream(),
                          pk.data_ptr<float>(), pv.data_ptr<float>(), reinterpret_cast<unsigned short*>(dk.data_ptr()),
-                         strides_of(dk), reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv), B, S, H, Hk);
+                         strides_of(dk), reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv), B, Sk, H,
+                         Hk);
     }
   } else {
-    launch(fa::dkdv_kernel<false>, Hk);
+    launch(fa::dkdv_kernel<false, D>, Hk);
   }
   SXE_LAUNCH_CHECK();
 }
 
+// dq/dk/dv are caller-provided (possibly strided views of one dqkv buffer).
+static void bwd_impl(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
+                     at::Tensor dq, at::Tensor dk, at::Tensor dv, bool causal, double scale, fa::Sparse sp,
+                     int64_t kv_len = -1, int64_t causal_offset = INT64_MIN) {
+  check_qkv(q, k, v);
+  check_qkv(dq, dk, dv);
+  const int Sq = q.size(1), Sk = k.size(1);
+  const int kvlen = kv_len < 0 ? Sk : (int)kv_len;
+  SXE_CHECK(kvlen >= 1 && kvlen <= Sk, "flash_attn_bwd: kv_len must be in [1, Sk]");
+  const int qoff = causal_offset == INT64_MIN ? Sk - Sq : (int)causal_offset;
+  SXE_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && dout.stride(3) == 1 && o.stride(3) == 1,
+            "flash_attn_bwd: dout/o shapes");
+  SXE_CHECK(dq.sizes() == q.sizes() && dk.sizes() == k.sizes() && dv.sizes() == v.sizes(), "flash_attn_bwd: grad shapes");
+  SXE_CHECK(lse.is_contiguous() && lse.size(2) == Sq, "flash_attn_bwd: lse [B, H, Sq]");
+  c10::DeviceGuard guard(q.device());
+  switch (q.size(3)) {
+    case 64: return bwd_impl_d<64>(dout, q, k, v, o, lse, dq, dk, dv, causal, scale, sp, kvlen, qoff);
+    case 256: return bwd_impl_d<256>(dout, q, k, v, o, lse, dq, dk, dv, causal, scale, sp, kvlen, qoff);
+    default: return bwd_impl_d<128>(dout, q, k, v, o, lse, dq, dk, dv, causal, scale, sp, kvlen, qoff);
+  }
+}
+
+static int64_t offset_arg(int64_t causal_offset) { return causal_offset == -(int64_t(1) << 40) ? INT64_MIN : causal_offset; }
+
 std::vector<at::Tensor> flash_attn_fwd(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, double scale,
-                                       int64_t kv_len) {
-  return fwd_impl(q, k, v, causal, scale, fa::Sparse{nullptr, 0, 0}, kv_len);
+                                       int64_t kv_len, int64_t causal_offset) {
+  return fwd_impl(q, k, v, causal, scale, fa::Sparse{nullptr, 0, 0}, kv_len, offset_arg(causal_offset));
 }
 
 void flash_attn_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
-                    at::Tensor dq, at::Tensor dk, at::Tensor dv, bool causal, double scale, int64_t kv_len) {
-  bwd_impl(dout, q, k, v, o, lse, dq, dk, dv, causal, scale, fa::Sparse{nullptr, 0, 0}, kv_len);
+                    at::Tensor dq, at::Tensor dk, at::Tensor dv, bool causal, double scale, int64_t kv_len,
+                    int64_t causal_offset) {
+  bwd_impl(dout, q, k, v, o, lse, dq, dk, dv, causal, scale, fa::Sparse{nullptr, 0, 0}, kv_len,
+           offset_arg(causal_offset));
 }
 
 std::vector<at::Tensor> flash_attn_fwd_sparse(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor layout,
@@ -900,9 +997,11 @@ void flash_attn_bwd_sparse(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tens
 }  // namespace sxe
 
 TORCH_LIBRARY_FRAGMENT(sxe, m) {
-  m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, int kv_len=-1) -> Tensor[]");
+  // causal_offset: query i sees keys <= i + causal_offset; the default sentinel means Sk - Sq
+  m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, int kv_len=-1, "
+        "int causal_offset=-1099511627776) -> Tensor[]");
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, "
-        "Tensor(c!) dv, bool causal, float scale, int kv_len=-1) -> ()");
+        "Tensor(c!) dv, bool causal, float scale, int kv_len=-1, int causal_offset=-1099511627776) -> ()");
   m.def("flash_attn_fwd_sparse(Tensor q, Tensor k, Tensor v, Tensor layout, int block, bool causal, float scale) -> Tensor[]");
   m.def("flash_attn_bwd_sparse(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, "
         "Tensor(b!) dk, Tensor(c!) dv, Tensor layout, int block, bool causal, float scale) -> ()");

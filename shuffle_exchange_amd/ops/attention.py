@@ -3,16 +3,18 @@ QKV / output projections).
 
 Backends:
 * ``hip``  -- this repo's gfx950 flash-attention kernels (csrc/kernels/flash_attn.hip): MFMA bf16,
-  online softmax, LSE output; deterministic backward (dK/dV kernel + dQ kernel, no atomics);
-* ``sdpa`` -- ``torch.nn.functional.scaled_dot_product_attention``: used on CPU (plumbing tests) and
-  for head dims above 128 on GPU (logged once so a silent fallback cannot hide in a benchmark).
+  online softmax, LSE output; deterministic backward (dK/dV kernel + dQ kernel, no atomics); head
+  dims 64 / 128 / 256 natively, query length != key length (cross / prefix attention, causal mask
+  bottom-right aligned as in flash-attn: query i sees keys <= i + Sk - Sq);
+* ``sdpa`` -- ``torch.nn.functional.scaled_dot_product_attention``: CPU (plumbing tests) and head
+  dims above 256 on GPU (logged once so a silent fallback cannot hide in a benchmark).
 
-Shapes outside the kernel's native tile (head dim 128, sequence a multiple of 128) run the same
-kernels on padded copies: the sequence is zero-padded to the next multiple of 128 (padded keys
-are masked with the kernels' ``kv_len``; padded query rows are dropped) and head dims below 128
-(64, 80, 96, ...) are zero-padded to 128 (zero q/k columns leave the scores unchanged, zero v
-columns produce zero output columns that are dropped). The softmax scale is the true head dim's.
-``SXE_ATTN_BACKEND=sdpa`` forces the stopgap for A/B comparisons.
+Shapes outside the kernels' native tiles run the same kernels on padded copies: each sequence axis
+is zero-padded to the next multiple of 128 (padded keys are masked with the kernels' ``kv_len``,
+padded query rows are dropped, the causal offset is the one of the true lengths) and other head
+dims (80, 96, 160, ...) are zero-padded to the next native one (zero q/k columns leave the scores
+unchanged, zero v columns produce zero output columns that are dropped). The softmax scale is the
+true head dim's. ``SXE_ATTN_BACKEND=sdpa`` forces the stopgap for A/B comparisons.
 
 ``attention_qkv_rope`` is the training entry point of the Llama family: it takes the fused QKV
 projection output [B, S, Hq + 2*Hkv, D], applies RoPE in place, runs attention reading q/k/v as
@@ -41,7 +43,12 @@ def _sdpa(q, k, v, causal, scale):
     return o.transpose(1, 2)
 
 
-TILE, HEAD_DIM = 128, 128
+TILE = 128
+HEAD_DIMS = (64, 128, 256)
+
+
+def _native_dim(D):
+    return next((d for d in HEAD_DIMS if d >= D), None)
 
 
 def _aligned(t):
@@ -53,16 +60,18 @@ def hip_supported(q, k, v):
     """The kernels run these tensors in place (no padding copies)."""
     if os.environ.get("SXE_ATTN_BACKEND") == "sdpa":
         return False
-    return (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] == HEAD_DIM and q.shape[1] % TILE == 0
-            and q.shape[1] == k.shape[1] and q.shape[2] % k.shape[2] == 0 and all(_aligned(t) for t in (q, k, v)))
+    return (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in HEAD_DIMS and q.shape[1] % TILE == 0
+            and k.shape[1] % TILE == 0 and k.shape[-1] == q.shape[-1] and v.shape[-1] == q.shape[-1]
+            and q.shape[2] % k.shape[2] == 0 and all(_aligned(t) for t in (q, k, v)))
 
 
 def hip_paddable(q, k, v):
-    """The kernels run these tensors on padded copies (sequence and/or head dim)."""
+    """The kernels run these tensors on padded copies (sequence axes and/or head dim)."""
     if os.environ.get("SXE_ATTN_BACKEND") == "sdpa":
         return False
-    return (q.is_cuda and q.dtype in (torch.bfloat16, torch.float16, torch.float32) and q.shape[-1] <= HEAD_DIM
-            and q.shape[-1] % 8 == 0 and q.shape[1] == k.shape[1] and q.shape[2] % k.shape[2] == 0)
+    return (q.is_cuda and q.dtype in (torch.bfloat16, torch.float16, torch.float32)
+            and _native_dim(q.shape[-1]) is not None and q.shape[-1] % 8 == 0 and k.shape[-1] == q.shape[-1]
+            and v.shape[-1] == q.shape[-1] and q.shape[2] % k.shape[2] == 0)
 
 
 def _pad(t, S_pad, D_pad):
@@ -74,28 +83,36 @@ def _pad(t, S_pad, D_pad):
     return out
 
 
+def _padded_fwd(q, k, v, causal, scale):
+    Sq, Sk, D = q.shape[1], k.shape[1], q.shape[-1]
+    Dp = _native_dim(D)
+    Sqp, Skp = -(-Sq // TILE) * TILE, -(-Sk // TILE) * TILE
+    qp, kp, vp = _pad(q, Sqp, Dp), _pad(k, Skp, Dp), _pad(v, Skp, Dp)
+    o, lse = torch.ops.sxe.flash_attn_fwd(qp, kp, vp, bool(causal), float(scale), Sk, Sk - Sq)
+    return qp, kp, vp, o, lse
+
+
 class _FlashAttnPadded(torch.autograd.Function):
     """Flash attention on padded copies (see the module docstring)."""
 
     @staticmethod
     def forward(ctx, q, k, v, causal, scale):
-        S, D = q.shape[1], q.shape[-1]
-        Sp = -(-S // TILE) * TILE
-        qp, kp, vp = _pad(q, Sp, HEAD_DIM), _pad(k, Sp, HEAD_DIM), _pad(v, Sp, HEAD_DIM)
-        o, lse = torch.ops.sxe.flash_attn_fwd(qp, kp, vp, bool(causal), float(scale), S)
+        Sq, Sk, D = q.shape[1], k.shape[1], q.shape[-1]
+        qp, kp, vp, o, lse = _padded_fwd(q, k, v, causal, scale)
         ctx.save_for_backward(qp, kp, vp, o, lse)
-        ctx.meta = (causal, scale, S, D, q.dtype)
-        return o[:, :S, :, :D].to(q.dtype)
+        ctx.meta = (causal, scale, Sq, Sk, D, q.dtype)
+        return o[:, :Sq, :, :D].to(q.dtype)
 
     @staticmethod
     def backward(ctx, do):
         qp, kp, vp, o, lse = ctx.saved_tensors
-        causal, scale, S, D, dtype = ctx.meta
-        dop = _pad(do, qp.shape[1], HEAD_DIM)
+        causal, scale, Sq, Sk, D, dtype = ctx.meta
+        dop = _pad(do, qp.shape[1], qp.shape[-1])
         dq, dk, dv = torch.empty_like(qp), torch.empty_like(kp), torch.empty_like(vp)
-        torch.ops.sxe.flash_attn_bwd(dop, qp, kp, vp, o, lse, dq, dk, dv, bool(causal), float(scale), S)
-        sl = (slice(None), slice(0, S), slice(None), slice(0, D))
-        return dq[sl].to(dtype), dk[sl].to(dtype), dv[sl].to(dtype), None, None
+        torch.ops.sxe.flash_attn_bwd(dop, qp, kp, vp, o, lse, dq, dk, dv, bool(causal), float(scale), Sk, Sk - Sq)
+        sq = (slice(None), slice(0, Sq), slice(None), slice(0, D))
+        sk = (slice(None), slice(0, Sk), slice(None), slice(0, D))
+        return dq[sq].to(dtype), dk[sk].to(dtype), dv[sk].to(dtype), None, None
 
 
 class _FlashAttn(torch.autograd.Function):
@@ -116,7 +133,8 @@ class _FlashAttn(torch.autograd.Function):
 
 
 def attention(q, k, v, causal=True, softmax_scale=None):
-    """q: [B, S, Hq, D], k/v: [B, S, Hkv, D] (strided views allowed) -> [B, S, Hq, D]."""
+    """q: [B, Sq, Hq, D], k/v: [B, Sk, Hkv, D] (strided views allowed) -> [B, Sq, Hq, D]. With Sq != Sk
+    and ``causal`` the mask is bottom-right aligned (query i sees keys <= i + Sk - Sq)."""
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if q.is_cuda:
         native.require_hip()
@@ -179,14 +197,12 @@ def attention_qkv_rope(qkv, nq, nkv, rope=None, position_ids=None, causal=True, 
 def attention_with_lse(q, k, v, causal=True, softmax_scale=None):
     """Forward-only attention returning (out [B,S,H,D], lse [B,H,S]) for chunk merging (FPDT)."""
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1])
-    if q.is_cuda and hip_supported(q, k, v) and q.shape[1] == k.shape[1]:
+    if q.is_cuda and hip_supported(q, k, v):
         return torch.ops.sxe.flash_attn_fwd(q, k, v, bool(causal), float(scale))
     if q.is_cuda and hip_paddable(q, k, v):
-        S, D = q.shape[1], q.shape[-1]
-        Sp = -(-S // TILE) * TILE
-        o, lse = torch.ops.sxe.flash_attn_fwd(_pad(q, Sp, HEAD_DIM), _pad(k, Sp, HEAD_DIM), _pad(v, Sp, HEAD_DIM),
-                                              bool(causal), float(scale), S)
-        return o[:, :S, :, :D].to(q.dtype), lse[:, :, :S].contiguous()
+        Sq, D = q.shape[1], q.shape[-1]
+        _, _, _, o, lse = _padded_fwd(q, k, v, causal, scale)
+        return o[:, :Sq, :, :D].to(q.dtype), lse[:, :, :Sq].contiguous()
     return reference_attention(q, k, v, causal, scale, return_lse=True)
 
 

@@ -137,3 +137,62 @@ def test_smoke_shape_llama_d64_uses_hip():
     o = A.attention_qkv_rope(qkv * 1.0, nq, nkv, cache)
     o.float().square().mean().backward()
     assert o.shape == (B, S, nq, D) and torch.isfinite(qkv.grad).all()
+
+
+def _no_sdpa(monkeypatch):
+    from shuffle_exchange_amd.ops import attention as A
+
+    def boom(*a, **k):
+        raise AssertionError("SDPA ran")
+    monkeypatch.setattr(A, "_sdpa", boom)
+    return A
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("D", [64, 256])
+@pytest.mark.parametrize("B,S,H,Hk", [(2, 256, 4, 2), (1, 384, 4, 4)])
+def test_flash_native_head_dims(causal, D, B, S, H, Hk, monkeypatch):
+    """Head dims 64 and 256 run their own kernel instantiations in place (no padding copy, no SDPA)."""
+    A = _no_sdpa(monkeypatch)
+    torch.manual_seed(0)
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    assert A.hip_supported(q, k, v)
+    o = A.attention(q, k, v, causal=causal)
+    q2, k2, v2 = (t.detach().float().requires_grad_() for t in (q, k, v))
+    o2 = A.reference_attention(q2, k2, v2, causal=causal)
+    assert _rel(o, o2) < 1e-2
+    do = torch.randn_like(o2)
+    (o.float() * do).sum().backward()
+    (o2 * do).sum().backward()
+    for a, b in ((q.grad, q2.grad), (k.grad, k2.grad), (v.grad, v2.grad)):
+        assert _rel(a, b) < 2e-2
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("Sq,Sk,D", [(128, 384, 128), (256, 1024, 64), (100, 300, 96), (1, 517, 128),
+                                     (384, 128, 128), (200, 200, 256)])
+def test_flash_cross_and_prefix_lengths(causal, Sq, Sk, D, monkeypatch):
+    """q_len != kv_len (prefix / chunked-prefill / cross attention): bottom-right aligned causal mask
+    like flash-attn, on the HIP kernels (padded where the lengths are not multiples of 128)."""
+    if causal and Sq > Sk:
+        pytest.skip("causal with more queries than keys leaves fully masked rows (not a real use)")
+    A = _no_sdpa(monkeypatch)
+    torch.manual_seed(1)
+    B, H, Hk = 2, 4, 2
+    q = torch.randn(B, Sq, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, Sk, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, Sk, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    o = A.attention(q, k, v, causal=causal)
+    q2, k2, v2 = (t.detach().float().requires_grad_() for t in (q, k, v))
+    o2 = A.reference_attention(q2, k2, v2, causal=causal)
+    assert o.shape == o2.shape and _rel(o, o2) < 1e-2
+    do = torch.randn_like(o2)
+    (o.float() * do).sum().backward()
+    (o2 * do).sum().backward()
+    for a, b in ((q.grad, q2.grad), (k.grad, k2.grad), (v.grad, v2.grad)):
+        assert a.shape == b.shape and _rel(a, b) < 2e-2
+    ol, lse = A.attention_with_lse(q.detach(), k.detach(), v.detach(), causal=causal)
+    _, lse2 = A.reference_attention(q2.detach(), k2.detach(), v2.detach(), causal=causal, return_lse=True)
+    assert (lse - lse2).abs().max().item() < 2e-2
