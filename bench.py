@@ -270,7 +270,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1000.0, 3),
             "higher_is_better": True,
-            "scaling": "strong" if sp > 1 else "weak",
+            "scaling": "strong" if c.get("sp") else "weak",
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic",

@@ -577,7 +577,9 @@ template <int D> struct KVL {
   static constexpr int VBLK = QB * 2 * D;              // the V block
 };
 
-template <bool MASK, int D>
+// PART: 3 = dK and dV in one sweep; 1 = dV only; 2 = dK only (head dim 256: the two 128-register
+// accumulators of one sweep would spill, so two sweeps each recompute S = Q K^T)
+template <bool MASK, int D, int PART>
 __device__ __forceinline__ void dkdv_tile(const char* slot, const char* vblk, const bf16x8 (&kf)[D / 16],
                                           f32x16 (&dka)[D / 32], f32x16 (&dva)[D / 32], float c, int qt0, int k0,
                                           int w, int r, int h, int lane, bool diag, const Sparse& sp, int hq0,
@@ -589,8 +591,9 @@ __device__ __forceinline__ void dkdv_tile(const char* slot, const char* vblk, co
   f32x16 s = zero16(), dp = zero16();
 #pragma unroll
   for (int t2 = 0; t2 < D / 16; ++t2) {
-    s = mfma(lds_row16<D>(qt, r, 2 * t2 + h), kf[t2], s);                                        // S  [query][key]
-    dp = mfma(lds_row16<D>(dt_, r, 2 * t2 + h), lds_row16<D>(vblk, w * QW + r, 2 * t2 + h), dp);  // dP
+    s = mfma(lds_row16<D>(qt, r, 2 * t2 + h), kf[t2], s);  // S  [query][key]
+    if constexpr ((PART & 2) != 0)
+      dp = mfma(lds_row16<D>(dt_, r, 2 * t2 + h), lds_row16<D>(vblk, w * QW + r, 2 * t2 + h), dp);  // dP
   }
   bool b0 = true, b1 = true;  // layout bits of query rows qt0+[0,16) and qt0+[16,32) vs this key
   if (MASK && sp.layout) {
@@ -614,8 +617,8 @@ __device__ __forceinline__ void dkdv_tile(const char* slot, const char* vblk, co
     const bf16x8 db = acc_to_b(dp, s2);
 #pragma unroll
     for (int t = 0; t < D / 32; ++t) {
-      dva[t] = mfma(lds_trA<D>(dt_, 16 * s2, t, lane), pb, dva[t]);  // dV^T += dO^T P
-      dka[t] = mfma(lds_trA<D>(qt, 16 * s2, t, lane), db, dka[t]);   // dK^T += Q^T dS
+      if constexpr ((PART & 1) != 0) dva[t] = mfma(lds_trA<D>(dt_, 16 * s2, t, lane), pb, dva[t]);  // dV^T += dO^T P
+      if constexpr ((PART & 2) != 0) dka[t] = mfma(lds_trA<D>(qt, 16 * s2, t, lane), db, dka[t]);   // dK^T += Q^T dS
     }
   }
 }
@@ -625,7 +628,7 @@ __device__ __forceinline__ void dkdv_tile(const char* slot, const char* vblk, co
 // half of that, and with B*Hk*Sk/128 ~ 2 workgroups per CU the whole launch waits for block 0
 // (measured 650 us at B4 S2048 H32/8). Splitting the G query heads cuts the longest job by G; the
 // per-head fp32 dK/dV partials [B, Sk, H, D] are summed over G by dkdv_reduce_kernel.
-template <bool SPLIT, int D>
+template <bool SPLIT, int D, int PART = 3>
 __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
     const unsigned short* __restrict__ q, Strides qs, const unsigned short* __restrict__ k, Strides ks,
     const unsigned short* __restrict__ v, Strides vs, const unsigned short* __restrict__ dout, Strides dos,
@@ -669,7 +672,7 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
       glds4(lane < 32 ? (const void*)(lse + lr) : (const void*)(delta + lr), slot + 2 * G_::TILE);
     }
   };
-  tile_glds<QB, D>(vp, vs.s, kb * QB, vblk);
+  if constexpr ((PART & 2) != 0) tile_glds<QB, D>(vp, vs.s, kb * QB, vblk);
   if (total > 0) issue(0, ring);
   bf16x8 kf[D / 16];
 #pragma unroll
@@ -691,7 +694,7 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
     if (active) {
       const char* slot = ring + cur * G_::SLOT;
       const bool diag = causal && (qt0 + qoff < k0 + QW);
-      dkdv_tile<true, D>(slot, vblk, kf, dka, dva, c, qt0, k0, w, r, h, lane, diag, sp, hq0, kbl, qoff);
+      dkdv_tile<true, D, PART>(slot, vblk, kf, dka, dva, c, qt0, k0, w, r, h, lane, diag, sp, hq0, kbl, qoff);
     }
     vm_wait_all();
     __syncthreads();
@@ -710,8 +713,8 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
           a[e] = dka[t][4 * rg + e] * scale;
           cc[e] = dva[t][4 * rg + e];
         }
-        *reinterpret_cast<f32x4*>(kp32 + 32 * t + 8 * rg + 4 * h) = a;
-        *reinterpret_cast<f32x4*>(vp32 + 32 * t + 8 * rg + 4 * h) = cc;
+        if constexpr ((PART & 2) != 0) *reinterpret_cast<f32x4*>(kp32 + 32 * t + 8 * rg + 4 * h) = a;
+        if constexpr ((PART & 1) != 0) *reinterpret_cast<f32x4*>(vp32 + 32 * t + 8 * rg + 4 * h) = cc;
       }
     return;
   }
@@ -727,8 +730,8 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
         pk4[e] = f32_to_bf16(dka[t][4 * rg + e] * scale);
         pv4[e] = f32_to_bf16(dva[t][4 * rg + e]);
       }
-      *reinterpret_cast<u16x4*>(kop + 32 * t + 8 * rg + 4 * h) = pk4;
-      *reinterpret_cast<u16x4*>(vop + 32 * t + 8 * rg + 4 * h) = pv4;
+      if constexpr ((PART & 2) != 0) *reinterpret_cast<u16x4*>(kop + 32 * t + 8 * rg + 4 * h) = pk4;
+      if constexpr ((PART & 1) != 0) *reinterpret_cast<u16x4*>(vop + 32 * t + 8 * rg + 4 * h) = pv4;
     }
 }
 
@@ -896,6 +899,12 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
     set_lds_limit(&fa::dq_kernel<true, D>, 4 * fa::KT * ROWB + kListBytes);
     set_lds_limit(&fa::dkdv_kernel<false, D>, lds_kv_max);
     set_lds_limit(&fa::dkdv_kernel<true, D>, lds_kv_max);
+    if constexpr (D >= 256) {
+      set_lds_limit(&fa::dkdv_kernel<false, D, 1>, lds_kv_max);
+      set_lds_limit(&fa::dkdv_kernel<true, D, 1>, lds_kv_max);
+      set_lds_limit(&fa::dkdv_kernel<false, D, 2>, lds_kv_max);
+      set_lds_limit(&fa::dkdv_kernel<true, D, 2>, lds_kv_max);
+    }
     attr_set = true;
   }
   auto* dqk = sp.layout ? fa::dq_kernel<true, D> : fa::dq_kernel<false, D>;
@@ -932,7 +941,13 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
                        Sq, Sk, (float)scale, causal ? 1 : 0, sp, qoff);
   };
   if (split) {
-    launch(fa::dkdv_kernel<true, D>, H);
+    if constexpr (D >= 256) {
+      launch(fa::dkdv_kernel<true, D, 1>, H);
+      SXE_LAUNCH_CHECK();
+      launch(fa::dkdv_kernel<true, D, 2>, H);
+    } else {
+      launch(fa::dkdv_kernel<true, D>, H);
+    }
     SXE_LAUNCH_CHECK();
     if (partials) {
       const int64_t n8 = (int64_t)B * Sk * Hk * (D / 8);
@@ -941,6 +956,10 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
                          strides_of(dk), reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv), B, Sk, H,
                          Hk);
     }
+  } else if constexpr (D >= 256) {
+    launch(fa::dkdv_kernel<false, D, 1>, Hk);
+    SXE_LAUNCH_CHECK();
+    launch(fa::dkdv_kernel<false, D, 2>, Hk);
   } else {
     launch(fa::dkdv_kernel<false, D>, Hk);
   }
