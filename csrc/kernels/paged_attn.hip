@@ -10,14 +10,21 @@
 //  * one workgroup (4 waves, 256 threads) per (sequence, kv head, KV split): all G = nq/nkv query
 //    heads of the GQA group (x the sequence's new tokens) share every K/V byte loaded, so decode is
 //    pure HBM streaming at the GQA-reduced byte count;
-//  * key phase: lane = key (K row in 16 B vector registers, q rows broadcast from LDS); value phase:
-//    lane = 4 output dims of one of KG V rows per load instruction, the 64 rows' cache offsets
-//    precomputed in the key phase so all V loads of a chunk are in flight together (a per-key
-//    block-table lookup -> load chain made the value phase latency-bound); probabilities hop
-//    through LDS; key-group partial sums fold once per pass with lane shuffles;
+//  * both products on the matrix cores (v_mfma_f32_16x16x32_bf16), 16 query rows (token x head of
+//    the group) per pass: S^T = K Q^T with K fragments loaded straight from the cache into the A
+//    operand (lane = key row of a 16-key tile) and Q^T in the B operand, so each lane holds one
+//    query row's scores (online softmax per lane, max/sum folded over the 4 lane groups with two
+//    shuffles); O^T += V^T P^T takes P^T directly from the score accumulators (the
+//    accumulator-as-operand identity: the 16x16 C layout's k order is matched by the order the V
+//    rows are read) and V^T through ds_read_b64_tr_b16 from a per-wave V image in LDS, loaded by
+//    global_load_lds (no staging registers) with the XOR-swizzled 2D-byte rows; the key rows of a
+//    tile are permuted (0, 8, 4, 12 + e) so each 32-lane half's transposed read is conflict-free;
+//  * decode (4 rows of 16 used for Llama-3's G = 4) wastes MFMA lanes, not bandwidth: the previous
+//    VALU kernel spent 512 FMA instructions per wave per 64 keys on Q K^T alone;
 //  * flash-decoding split over the KV length when (sequences x kv heads) is too small to fill the
 //    256 CUs, merged by a second kernel (fp32 partials);
-//  * causal masking by absolute position (chunked prefill / speculative tokens just work).
+//  * causal masking by absolute position (chunked prefill / speculative tokens just work), sliding
+//    windows skip the key chunks they mask entirely.
 #include "sxe_common.h"
 #include <torch/library.h>
 
@@ -111,169 +118,211 @@ struct Args {
   int64_t out_tok_stride;
   float* part_o;   // [splits, T, nq, D]
   float* part_ml;  // [splits, T, nq, 2]
-  int* counters;   // [S * nkv] self-resetting split counters (nullptr: separate merge kernel)
   int T;
   int window;      // sliding window (Mistral / Qwen2): keys older than `window` positions are masked; 0 = off
 };
 
-// R = query rows (token x head-in-group) per pass: 4 / 8 / 16 picked on the host from the GQA group
-// size so decode rows (q_len = 1) fill one pass without idle row slots.
-template <int D, int R>
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// byte offset of 16-byte chunk `ch` of row `row` in a swizzled [rows][D bf16] image (see flash_attn.hip)
+template <int D>
+__device__ __forceinline__ int soff(int row, int ch) {
+  constexpr int CH = D / 8;
+  const int f = (((row & 3) << 2) | ((row >> 2) & 3)) & (CH >= 16 ? 15 : CH - 1);
+  return row * (2 * D) + 16 * (ch ^ f);
+}
+
+// first key row of lane group g's 4-row block in a 16-key tile (C rows 4g..4g+3 <-> keys kperm(g)+e):
+// the two groups of a 32-lane half read blocks 8 rows apart -> conflict-free transposed reads
+__device__ __forceinline__ int kperm(int g) { return ((g & 1) << 3) | ((g & 2) << 1); }
+
+constexpr int PR = 16;  // query rows per pass
+
+template <int D>
+struct PaGeo {
+  static constexpr int NT = D >= 256 ? 2 : 4;  // 16-key tiles per wave chunk (register budget at D = 256)
+  static constexpr int KC = 16 * NT;           // keys per wave chunk
+  static constexpr int KS = D / 32;            // k-steps of the Q K^T product
+  static constexpr int DT = D / 16;            // 16-wide d tiles of O^T
+  static constexpr int VIMG = KC * 2 * D;      // bytes of one wave's V image
+  static constexpr int MERGE = kWaves * PR * D * 4;
+  static constexpr int LDS = (kWaves * VIMG > MERGE ? kWaves * VIMG : MERGE);
+};
+
+template <int D>
 __global__ __launch_bounds__(256) void paged_attn_kernel(Args a) {
-  constexpr int KV16 = D / 8;   // 16-byte vectors per K row
-  constexpr int LPR = D / 4;    // value phase: lanes per V row (4 dims = 8 bytes each)
-  constexpr int KG = 64 / LPR;  // V rows per wave load instruction
-  __shared__ float q_lds[R][D];
-  __shared__ float p_lds[kWaves][R][64];
-  __shared__ int64_t voff_lds[kWaves][64];
-  __shared__ float mrg_o[kWaves][R][D];
-  __shared__ float mrg_ml[kWaves][R][2];
+  using P = PaGeo<D>;
+  constexpr int NT = P::NT, KC = P::KC, KS = P::KS, DT = P::DT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // V images, then the wave-merge buffer
+  __shared__ int64_t koff_lds[kWaves][KC];
+  __shared__ float mrg_ml[kWaves][PR][2];
 
   const int seq = blockIdx.x / a.nkv, kvh = blockIdx.x - (blockIdx.x / a.nkv) * a.nkv;
   const int split = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int kg = lane / LPR, dl = lane - (lane / LPR) * LPR;
+  const int g = lane >> 4, i = lane & 15;
   const int G = a.nq / a.nkv;
   const int qs = a.q_start[seq], ql = a.q_len[seq], kl = a.kv_len[seq];
   const int k_begin = split * a.keys_per_split;
   const int k_end = min(kl, k_begin + a.keys_per_split);
   const int nrows_total = ql * G;
   const int* bt = a.block_table + (int64_t)seq * a.max_blocks;
-  const int64_t head_stride = (int64_t)a.bs * D;          // between kv heads inside a block half
+  const int64_t head_stride = (int64_t)a.bs * D;             // between kv heads inside a block half
   const int64_t half_stride = (int64_t)a.nkv * head_stride;  // k half -> v half
   const int64_t block_stride = 2 * half_stride;
+  char* vimg = smem + wave * P::VIMG;
+  float* mrg_o = reinterpret_cast<float*>(smem);  // [kWaves][PR][D] after the key loop
+  const int krow = kperm(i >> 2) + (i & 3);        // this lane's key row in a tile (A operand of Q K^T)
 
-  for (int row0 = 0; row0 < nrows_total; row0 += R) {
-    const int nrows = min(R, nrows_total - row0);
-    // ---- q rows -> LDS (fp32, pre-scaled by softmax scale * log2 e) -------------------------
-    for (int i = threadIdx.x; i < R * D; i += 256) {
-      const int r = i / D, d = i - r * D;
-      float v = 0.f;
-      if (r < nrows) {
-        const int row = row0 + r, tok = row / G, g = row - tok * G;
-        v = bf16_to_f32(a.q[(int64_t)(qs + tok) * a.q_tok_stride + (int64_t)(kvh * G + g) * D + d]) * a.scale_log2;
+  for (int row0 = 0; row0 < nrows_total; row0 += PR) {
+    const int nrows = min(PR, nrows_total - row0);
+    // ---- Q^T B operand: lane holds row i's d = 32 ks + 8 g .. +7 ---------------------------------
+    bf16x8 qb[KS];
+    const bool row_ok = i < nrows;
+    int pos = -1;  // absolute position of this lane's query row (causal horizon)
+    {
+      const int row = row0 + (row_ok ? i : 0), tok = row / G, gh = row - tok * G;
+      const unsigned short* qp = a.q + (int64_t)(qs + tok) * a.q_tok_stride + (int64_t)(kvh * G + gh) * D + 8 * g;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        u32x4 v = *reinterpret_cast<const u32x4*>(qp + 32 * ks);
+        if (!row_ok) v = u32x4{0u, 0u, 0u, 0u};
+        qb[ks] = __builtin_bit_cast(bf16x8, v);
       }
-      q_lds[r][d] = v;
+      if (row_ok) pos = kl - ql + tok;
     }
-    __syncthreads();
-    const int max_pos = kl - ql + (row0 + nrows - 1) / G;  // causal horizon of this tile
+    const int max_pos = kl - ql + (row0 + nrows - 1) / G;  // causal horizon of the pass
     const int k_hi = min(k_end, max_pos + 1);
-    // sliding window: keys below the oldest row's window are masked for every row of the pass --
-    // start at the 64-key chunk holding the first visible key (the waves keep their interleave)
     int k_start = k_begin;
-    if (a.window > 0) {
+    if (a.window > 0) {  // first chunk holding a key visible to the pass's oldest row
       const int k_lo = kl - ql + row0 / G - a.window + 1;
-      if (k_lo > k_begin) k_start = k_begin + ((k_lo - k_begin) / 64) * 64;
+      if (k_lo > k_begin) k_start = k_begin + ((k_lo - k_begin) / KC) * KC;
     }
-    float m[R], l[R], acc[R][4];
+    float m = -INFINITY, lsum = 0.f;
+    f32x4 o[DT];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      m[r] = -INFINITY;
-      l[r] = 0.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc[r][e] = 0.f;
-    }
-    for (int kb = k_start + wave * 64; kb < k_hi; kb += kWaves * 64) {
-      // q rows are re-read from LDS every chunk: without this fence LICM hoists all R x D of them
-      // into registers (R = 4 alone would need 512 VGPRs and spill to scratch)
-      asm volatile("" ::: "memory");
-      // ---- key phase: lane = key; invalid lanes re-read key kb (in range) and get p = 0 ------
-      const int key = kb + lane;
-      const bool valid = key < k_hi;
-      const int kc = valid ? key : kb;
-      const int blk = bt[kc / a.bs], off = kc - (kc / a.bs) * a.bs;
-      const int64_t koff = (int64_t)blk * block_stride + kvh * head_stride + (int64_t)off * D;
-      voff_lds[wave][lane] = koff + half_stride;
-      u16x8 kr[KV16];
-#pragma unroll
-      for (int v = 0; v < KV16; ++v) kr[v] = *reinterpret_cast<const u16x8*>(a.cache + koff + v * 8);
-      float s[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) s[r] = 0.f;
-#pragma unroll
-      for (int v = 0; v < KV16; ++v) {
-        float kf[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) kf[e] = bf16_to_f32(kr[v][e]);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          if (r < nrows) {  // (uniform) guard also keeps the scheduler from hoisting all R x D q reads
-            const f32x4 q0 = *reinterpret_cast<const f32x4*>(&q_lds[r][v * 8]);
-            const f32x4 q1 = *reinterpret_cast<const f32x4*>(&q_lds[r][v * 8 + 4]);
-            s[r] += q0[0] * kf[0] + q0[1] * kf[1] + q0[2] * kf[2] + q0[3] * kf[3] + q1[0] * kf[4] + q1[1] * kf[5] +
-                    q1[2] * kf[6] + q1[3] * kf[7];
-          }
-        }
+    for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kb = k_start + wave * KC; kb < k_hi; kb += kWaves * KC) {
+      // ---- cache offsets of the chunk's keys (lane = key; keys past k_hi re-read key kb) ----------
+      if (lane < KC) {
+        const int key = kb + lane;
+        const int kc = key < k_hi ? key : kb;
+        const int blk = bt[kc / a.bs], off = kc - (kc / a.bs) * a.bs;
+        koff_lds[wave][lane] = (int64_t)blk * block_stride + kvh * head_stride + (int64_t)off * D;
       }
-      // ---- online softmax per row -----------------------------------------------------------
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if (r < nrows) {
-          const int pos = kl - ql + (row0 + r) / G;
-          const bool vis = valid && key <= pos && (a.window <= 0 || key > pos - a.window);
-          const float sv = vis ? s[r] : -INFINITY;
-          const float mx = wave_max(sv);
-          const float mn = fmaxf(m[r], mx);
-          float p = 0.f, alpha = 1.f;
-          if (mn != -INFINITY) {
-            p = (sv == -INFINITY) ? 0.f : exp2f(sv - mn);
-            alpha = (m[r] == -INFINITY) ? 0.f : exp2f(m[r] - mn);
-          }
-          l[r] = l[r] * alpha + wave_sum(p);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[r][e] *= alpha;
-          m[r] = mn;
-          p_lds[wave][r][lane] = p;
-        } else {
-          p_lds[wave][r][lane] = 0.f;
-        }
-      }
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): p_lds / voff_lds visible within the wave
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
       __builtin_amdgcn_wave_barrier();
-      // ---- value phase: KG V rows per load, lane = 4 dims of one row; all 64 rows issued
-      //      back to back (offsets precomputed in the key phase, so no dependent block lookups) --
-#pragma unroll 16
-      for (int j0 = 0; j0 < 64; j0 += KG) {
-        const int j = j0 + kg;
-        const uint2 w = *reinterpret_cast<const uint2*>(a.cache + voff_lds[wave][j] + dl * 4);
-        const float v0 = bf16_to_f32(w.x & 0xffff), v1 = bf16_to_f32(w.x >> 16);
-        const float v2 = bf16_to_f32(w.y & 0xffff), v3 = bf16_to_f32(w.y >> 16);
+      // ---- K fragments straight into the A operand: tile t, key row krow, d = 32 ks + 8 g ---------
+      bf16x8 kr[NT][KS];
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const float p = p_lds[wave][r][j];
-          acc[r][0] += p * v0;
-          acc[r][1] += p * v1;
-          acc[r][2] += p * v2;
-          acc[r][3] += p * v3;
+      for (int t = 0; t < NT; ++t) {
+        const unsigned short* kp = a.cache + koff_lds[wave][16 * t + krow] + 8 * g;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) kr[t][ks] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(kp + 32 * ks));
+      }
+      // ---- V rows -> this wave's LDS image (global_load_lds, swizzled source chunk) -------------
+      {
+        constexpr int CH = D / 8, RPK = 64 / CH;  // rows per 1 KiB wave-instruction
+#pragma unroll
+        for (int n = 0; n < KC / RPK; ++n) {
+          const int row = RPK * n + lane / CH;
+          const int cpos = lane % CH;
+          const int ch = cpos ^ ((((row & 3) << 2) | ((row >> 2) & 3)) & (CH >= 16 ? 15 : CH - 1));
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(a.cache + koff_lds[wave][row] + half_stride + ch * 8),
+              (__attribute__((address_space(3))) void*)(vimg + n * 1024), 16, 0, 0);
         }
       }
+      // ---- S^T = K Q^T: lane holds keys 16t + kperm(g) + e of row i ------------------------------
+      f32x4 sc[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        sc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) sc[t] = mfma16(kr[t][ks], qb[ks], sc[t]);
+      }
+      // ---- online softmax of row i over the chunk -------------------------------------------------
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int key = kb + 16 * t + kperm(g) + e;
+          const bool vis = key < k_hi && key <= pos && (a.window <= 0 || key > pos - a.window);
+          const float x = vis ? sc[t][e] * a.scale_log2 : -INFINITY;
+          sc[t][e] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m, mx);
+      const float mref = mn == -INFINITY ? 0.f : mn;
+      const float alpha = m == -INFINITY ? 0.f : exp2f(m - mref);
+      float ps = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float p = exp2f(sc[t][e] - mref);  // exp2(-inf) = 0 for masked keys
+          sc[t][e] = p;
+          ps += p;
+        }
+      lsum = lsum * alpha + ps;
+      m = mn;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's V image has landed
+      __builtin_amdgcn_wave_barrier();
+      // ---- O^T += V^T P^T over key-tile pairs: P^T straight from the score registers -------------
+#pragma unroll
+      for (int pp = 0; pp < NT / 2; ++pp) {
+        bf16x8 pb;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pb[e] = (__bf16)sc[2 * pp][e];
+          pb[4 + e] = (__bf16)sc[2 * pp + 1][e];
+        }
+        const int q4 = i >> 2, p4 = i & 3;
+        const int r0 = 32 * pp + kperm(g) + q4;  // row of this lane's address in the first tile
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int ch = 2 * dt + (p4 >> 1);
+          const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) i16x4*)(vimg + soff<D>(r0, ch) + 8 * (p4 & 1)));
+          const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) i16x4*)(vimg + soff<D>(r0 + 16, ch) + 8 * (p4 & 1)));
+          const i16x8 va = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          o[dt] = mfma16(__builtin_bit_cast(bf16x8, va), pb, o[dt]);
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // the V image is read before the next chunk overwrites it
       __builtin_amdgcn_wave_barrier();
     }
-    // ---- fold the KG key groups of each wave, then merge the 4 waves ---------------------------
+    // ---- fold the row sum over the 4 lane groups; merge the 4 waves through LDS --------------------
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    __syncthreads();  // every wave is done with its V image (the merge buffer aliases it)
+    if (row_ok) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
+      for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-#pragma unroll
-        for (int o = LPR; o < 64; o <<= 1) acc[r][e] += __shfl_xor(acc[r][e], o, 64);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if (r < nrows) {
-        if (kg == 0) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) mrg_o[wave][r][dl * 4 + e] = acc[r][e];
-        }
-        if (lane == 0) {
-          mrg_ml[wave][r][0] = m[r];
-          mrg_ml[wave][r][1] = l[r];
-        }
+        for (int e = 0; e < 4; ++e) mrg_o[(wave * PR + i) * D + 16 * dt + 4 * g + e] = o[dt][e];
+      if (g == 0) {
+        mrg_ml[wave][i][0] = m;
+        mrg_ml[wave][i][1] = lsum;
       }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < nrows * D; i += 256) {
-      const int r = i / D, d = i - r * D;
+    for (int idx = threadIdx.x; idx < nrows * D; idx += 256) {
+      const int r = idx / D, d = idx - r * D;
       float M = -INFINITY;
 #pragma unroll
       for (int w = 0; w < kWaves; ++w) M = fmaxf(M, mrg_ml[w][r][0]);
@@ -282,75 +331,65 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(Args a) {
       for (int w = 0; w < kWaves; ++w) {
         const float mw = mrg_ml[w][r][0];
         const float f = (mw == -INFINITY) ? 0.f : exp2f(mw - M);
-        sum += f * mrg_o[w][r][d];
+        sum += f * mrg_o[(w * PR + r) * D + d];
         L += f * mrg_ml[w][r][1];
       }
-      const int row = row0 + r, tok = row / G, g = row - tok * G;
-      const int t = qs + tok, h = kvh * G + g;
+      const int row = row0 + r, tok = row / G, gh = row - tok * G;
+      const int t = qs + tok, h = kvh * G + gh;
       if (a.splits == 1) {
         a.out[(int64_t)t * a.out_tok_stride + (int64_t)h * D + d] = f32_to_bf16(L > 0.f ? sum / L : 0.f);
       } else {
-        const int64_t idx = ((int64_t)split * a.T + t) * a.nq + h;
-        a.part_o[idx * D + d] = sum;
+        const int64_t pidx = ((int64_t)split * a.T + t) * a.nq + h;
+        a.part_o[pidx * D + d] = sum;
         if (d == 0) {
-          a.part_ml[idx * 2 + 0] = M;
-          a.part_ml[idx * 2 + 1] = L;
+          a.part_ml[pidx * 2 + 0] = M;
+          a.part_ml[pidx * 2 + 1] = L;
         }
       }
     }
     __syncthreads();
-  }
-  // split-KV merge fused in: the LAST workgroup of (seq, kv head) to finish (device-scope counter,
-  // release fence before / acquire fence after the vector atomic) combines every split's partial
-  // o / (max, sum) for this sequence's rows and resets the counter for the next launch. No
-  // workgroup waits on another, so there is nothing to deadlock on.
-  if (a.splits > 1 && a.counters != nullptr) {
-    __shared__ int is_last;
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) is_last = atomicAdd(&a.counters[blockIdx.x], 1) == a.splits - 1;
-    __syncthreads();
-    if (is_last) {
-      __threadfence();
-      for (int i = threadIdx.x; i < nrows_total * D; i += 256) {
-        const int row = i / D, d = i - row * D, tok = row / G, g = row - tok * G;
-        const int64_t th = (int64_t)(qs + tok) * a.nq + kvh * G + g;
-        float M = -INFINITY;
-        for (int s = 0; s < a.splits; ++s) M = fmaxf(M, __builtin_nontemporal_load(&a.part_ml[((int64_t)s * a.T * a.nq + th) * 2]));
-        float acc = 0.f, L = 0.f;
-        for (int s = 0; s < a.splits; ++s) {
-          const int64_t idx = (int64_t)s * a.T * a.nq + th;
-          const float ms = __builtin_nontemporal_load(&a.part_ml[idx * 2]);
-          if (ms == -INFINITY) continue;
-          const float f = exp2f(ms - M);
-          acc += f * __builtin_nontemporal_load(&a.part_o[idx * D + d]);
-          L += f * __builtin_nontemporal_load(&a.part_ml[idx * 2 + 1]);
-        }
-        a.out[(int64_t)(qs + tok) * a.out_tok_stride + (int64_t)(kvh * G + g) * D + d] =
-            f32_to_bf16(L > 0.f ? acc / L : 0.f);
-      }
-      if (threadIdx.x == 0) atomicExch(&a.counters[blockIdx.x], 0);
-    }
   }
 }
 
+// Combine the splits' fp32 partials of one (token, head): every load of a group of up to 16 splits is
+// issued before the first use (a loop that consumes each partial before loading the next makes a
+// chain of dependent ~1 us memory round trips: 10 us at 16 splits).
 template <int D>
-__global__ __launch_bounds__(D) void merge_kernel(const float* __restrict part_o, const float* __restrict part_ml,
-                                                  int splits, int T, int nq, unsigned short* __restrict out,
+__global__ __launch_bounds__(D) void merge_kernel(const float* __restrict__ part_o, const float* __restrict__ part_ml,
+                                                  int splits, int T, int nq, unsigned short* __restrict__ out,
                                                   int64_t out_tok_stride) {
+  constexpr int U = 16;
   const int th = blockIdx.x;  // t * nq + h
   const int t = th / nq, h = th - t * nq;
   const int d = threadIdx.x;
-  float M = -INFINITY;
-  for (int s = 0; s < splits; ++s) M = fmaxf(M, part_ml[((int64_t)s * T * nq + th) * 2]);
-  float acc = 0.f, L = 0.f;
-  for (int s = 0; s < splits; ++s) {
-    const int64_t idx = (int64_t)s * T * nq + th;
-    const float ms = part_ml[idx * 2];
-    if (ms == -INFINITY) continue;
-    const float f = exp2f(ms - M);
-    acc += f * part_o[idx * D + d];
-    L += f * part_ml[idx * 2 + 1];
+  const int64_t sstride = (int64_t)T * nq;
+  float M = -INFINITY, acc = 0.f, L = 0.f;
+  for (int s0 = 0; s0 < splits; s0 += U) {
+    float ms[U], ls[U], os[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int s = min(s0 + u, splits - 1);
+      const int64_t idx = s * sstride + th;
+      ms[u] = part_ml[idx * 2];
+      ls[u] = part_ml[idx * 2 + 1];
+      os[u] = part_o[idx * D + d];
+    }
+    float Mc = M;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (s0 + u < splits) Mc = fmaxf(Mc, ms[u]);
+    const float r = (M == -INFINITY) ? 0.f : exp2f(M - Mc);
+    acc *= r;
+    L *= r;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (s0 + u < splits && ms[u] != -INFINITY) {
+        const float f = exp2f(ms[u] - Mc);
+        acc += f * os[u];
+        L += f * ls[u];
+      }
+    }
+    M = Mc;
   }
   out[(int64_t)t * out_tok_stride + (int64_t)h * D + d] = f32_to_bf16(L > 0.f ? acc / L : 0.f);
 }
@@ -418,28 +457,6 @@ void kv_cache_append(const at::Tensor& qkv, at::Tensor cache, const at::Tensor& 
 }
 
 // q: [T, nq, D] (token stride free); returns out [T, nq, D] bf16
-// Persistent, self-resetting per-(seq, kv head) split counters for the fused merge: allocated zeroed
-// once per device OUTSIDE any stream capture (a buffer first allocated inside a HIP-graph capture
-// would belong to the graph's pool); while capturing with too small a buffer, or without
-// SXE_PA_FUSED_MERGE=1, the separate merge kernel runs instead.
-static int* split_counters(const c10::Device& dev, int64_t need) {
-  static at::Tensor buf[64];
-  // opt-in: measured SLOWER than the separate merge kernel on Llama-3-8B decode (batch 1: 4.56 vs
-  // 4.31 ms/token; batch 16: 7.90 vs 5.97 ms -- the device-scope release/acquire fences write back
-  // and invalidate L2 per workgroup, and the merge serialises into one workgroup per head group)
-  static const bool enabled = [] {
-    const char* e = std::getenv("SXE_PA_FUSED_MERGE");
-    return e && e[0] == '1';
-  }();
-  if (!enabled || dev.index() < 0 || dev.index() >= 64) return nullptr;
-  at::Tensor& b = buf[dev.index()];
-  if (b.defined() && b.numel() >= need) return b.data_ptr<int>();
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(cur_stream(), &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
-  b = at::zeros({std::max<int64_t>(need, 1 << 16)}, at::TensorOptions().device(dev).dtype(at::kInt));
-  return b.data_ptr<int>();
-}
-
 at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const at::Tensor& block_table,
                            const at::Tensor& q_start, const at::Tensor& q_len, const at::Tensor& kv_len, double scale,
                            int64_t max_kv_len, int64_t splits, int64_t window) {
@@ -461,7 +478,7 @@ at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const a
   c10::DeviceGuard g(q.device());
   splits = std::max<int64_t>(1, splits);
   int64_t kps = (std::max<int64_t>(max_kv_len, 1) + splits - 1) / splits;
-  kps = (kps + 63) / 64 * 64;
+  kps = (kps + 63) / 64 * 64;  // whole wave chunks (64 keys; 32 at head dim 256)
   splits = (std::max<int64_t>(max_kv_len, 1) + kps - 1) / kps;
   at::Tensor part_o, part_ml;
   pa::Args a;
@@ -484,34 +501,29 @@ at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const a
   a.T = T;
   a.part_o = nullptr;
   a.part_ml = nullptr;
-  a.counters = nullptr;
   a.window = (int)std::max<int64_t>(0, window);
   if (splits > 1) {
     part_o = at::empty({splits, T, nq, D}, q.options().dtype(at::kFloat));
     part_ml = at::empty({splits, T, nq, 2}, q.options().dtype(at::kFloat));
     a.part_o = part_o.data_ptr<float>();
     a.part_ml = part_ml.data_ptr<float>();
-    a.counters = split_counters(q.device(), S * nkv);
   }
   dim3 grid(S * nkv, splits);
-  const int G = nq / nkv;
   SXE_CHECK(D == 128 || D == 64 || D == 256, "paged_attention: head_dim must be 64, 128 or 256");
-#define SXE_PA_LAUNCH(DD, RR) hipLaunchKernelGGL((pa::paged_attn_kernel<DD, RR>), grid, dim3(256), 0, cur_stream(), a)
-  if (D == 128) {
-    if (G <= 4) SXE_PA_LAUNCH(128, 4);
-    else if (G <= 8) SXE_PA_LAUNCH(128, 8);
-    else SXE_PA_LAUNCH(128, 16);
-  } else if (D == 256) {  // 64 lanes per V row: one row per load; R <= 8 keeps LDS + VGPRs in budget
-    if (G <= 4) SXE_PA_LAUNCH(256, 4);
-    else SXE_PA_LAUNCH(256, 8);
-  } else {
-    if (G <= 4) SXE_PA_LAUNCH(64, 4);
-    else if (G <= 8) SXE_PA_LAUNCH(64, 8);
-    else SXE_PA_LAUNCH(64, 16);
-  }
-#undef SXE_PA_LAUNCH
+  static bool attr_set[3] = {false, false, false};
+  auto launch = [&](void (*kern)(pa::Args), size_t lds, int slot) {
+    if (!attr_set[slot]) {  // > 64 KiB of dynamic LDS must be opted into (gfx950: 160 KiB per CU)
+      SXE_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      attr_set[slot] = true;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, cur_stream(), a);
+  };
+  if (D == 128) launch(pa::paged_attn_kernel<128>, pa::PaGeo<128>::LDS, 0);
+  else if (D == 256) launch(pa::paged_attn_kernel<256>, pa::PaGeo<256>::LDS, 1);
+  else launch(pa::paged_attn_kernel<64>, pa::PaGeo<64>::LDS, 2);
   SXE_LAUNCH_CHECK();
-  if (splits > 1 && a.counters == nullptr) {
+  if (splits > 1) {
     if (D == 128)
       hipLaunchKernelGGL(pa::merge_kernel<128>, dim3(T * nq), dim3(128), 0, cur_stream(), a.part_o, a.part_ml,
                          (int)splits, T, nq, a.out, a.out_tok_stride);

@@ -13,6 +13,11 @@
 //  * one workgroup per 16 output columns, K split over its NW = 4/8 waves (NW = 8 for narrow N,
 //    so more waves per CU stream at once; 16 waves would cap VGPRs at 128 and spill), two super-steps of loads in flight per wave, partial
 //    tiles summed through NW KB of LDS.
+//  * fused prologues (decode, M <= 4): PRO_RMS builds the GEMM input (residual add + RMSNorm) and
+//    PRO_SWIGLU (silu(gate) * up) in LDS inside the GEMM launch -- every workgroup recomputes the
+//    few KB of activations it needs (L2 hits) while its first weight super-step is already in
+//    flight, so the norm / gated-activation launches (4-5 us each at batch 1, latency-bound) are
+//    gone from the decode layer. Workgroup 0 also writes the new residual stream h = x + res.
 #include "sxe_common.h"
 #include <torch/library.h>
 
@@ -27,40 +32,138 @@ struct Frag {
   bf16x8 x[8];
 };
 
-__device__ __forceinline__ void load_ss(Frag& f, const unsigned short* __restrict wrow, bool wok,
-                                        const unsigned short* __restrict xrow, bool xok, int kbase, int K) {
+__device__ __forceinline__ void load_w(Frag& f, const unsigned short* __restrict wrow, bool wok, int kbase, int K) {
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     const int k = kbase + s * 32;
-    const bool in = k < K;
-    f.w[s] = (wok && in) ? *reinterpret_cast<const bf16x8*>(wrow + k) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    f.x[s] = (xok && in) ? *reinterpret_cast<const bf16x8*>(xrow + k) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    f.w[s] = (wok && k < K) ? *reinterpret_cast<const bf16x8*>(wrow + k) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+}
+__device__ __forceinline__ void load_x(Frag& f, const unsigned short* __restrict xrow, bool xok, int kbase, int K) {
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int k = kbase + s * 32;
+    f.x[s] = (xok && k < K) ? *reinterpret_cast<const bf16x8*>(xrow + k) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
   }
 }
 
-template <int NW>
+enum : int { PRO_NONE = 0, PRO_RMS = 1, PRO_SWIGLU = 2 };
+constexpr int kProMaxM = 4;
+
+struct ProArgs {
+  const unsigned short* res;  // RMS: residual added to x (nullptr: none), same row stride as x
+  const unsigned short* gw;   // RMS: norm weight [K]
+  unsigned short* hout;       // RMS: h = x + res [M, K] (written by workgroup 0; nullptr: not wanted)
+  float eps;
+};
+
+// The M x K GEMM input, built in LDS (bf16, row stride K) by the whole workgroup in ONE pass:
+//   PRO_RMS    act = bf16(h * g), h = bf16(x + res) (the unfused norm's rounding); the row's
+//              rsqrt(mean(h^2) + eps) goes to rinv[] and scales the GEMM output in the epilogue
+//   PRO_SWIGLU act = bf16(silu(x[:, :K]) * x[:, K:])
+template <int MODE, int NT>
+__device__ __forceinline__ void build_act(const unsigned short* __restrict x, int64_t ldx, int M, int K,
+                                          const ProArgs& p, unsigned short* act, float* rinv) {
+  __shared__ float red[NT / 64][kProMaxM];
+  const int per = K / 8, n = M * per;
+  if constexpr (MODE == PRO_SWIGLU) {
+    for (int idx = threadIdx.x; idx < n; idx += NT) {
+      const int m = idx / per, c = (idx - m * per) * 8;
+      float gv[8], uv[8], o[8];
+      load8<DT::BF16>(x + (int64_t)m * ldx + c, gv);
+      load8<DT::BF16>(x + (int64_t)m * ldx + K + c, uv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = gv[j] / (1.f + __expf(-gv[j])) * uv[j];
+      store8<DT::BF16>(act + (int64_t)m * K + c, o);
+    }
+  } else {
+    float ss[kProMaxM] = {0.f, 0.f, 0.f, 0.f};
+    for (int idx = threadIdx.x; idx < n; idx += NT) {
+      const int m = idx / per, c = (idx - m * per) * 8;
+      float v[8], gv[8];
+      load8<DT::BF16>(x + (int64_t)m * ldx + c, v);
+      load8<DT::BF16>(p.gw + c, gv);
+      if (p.res != nullptr) {
+        float r[8];
+        load8<DT::BF16>(p.res + (int64_t)m * ldx + c, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = bf16_to_f32(f32_to_bf16(v[j] + r[j]));
+        if (p.hout != nullptr && blockIdx.x == 0) store8<DT::BF16>(p.hout + (int64_t)m * K + c, v);
+      }
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        q += v[j] * v[j];
+        v[j] *= gv[j];
+      }
+#pragma unroll
+      for (int mm = 0; mm < kProMaxM; ++mm)
+        if (mm == m) ss[mm] += q;
+      store8<DT::BF16>(act + (int64_t)m * K + c, v);
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int mm = 0; mm < kProMaxM; ++mm) {
+      const float t = wave_sum(ss[mm]);
+      if (lane == 0) red[wave][mm] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < kProMaxM) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NT / 64; ++w) t += red[w][threadIdx.x];
+      rinv[threadIdx.x] = rsqrtf(t / (float)K + p.eps);
+    }
+  }
+  __syncthreads();
+}
+
+template <int NW, int MODE = PRO_NONE>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(const unsigned short* __restrict x, int64_t ldx,
                                                           const unsigned short* __restrict w, int64_t ldw,
                                                           const unsigned short* __restrict bias,
                                                           unsigned short* __restrict y, int64_t ldy, int M, int N,
-                                                          int K, int ss_per_wave) {
+                                                          int K, int ss_per_wave, ProArgs pro) {
   __shared__ f32x4 red[NW][64];
+  extern __shared__ __attribute__((aligned(16))) unsigned short act_lds[];  // PRO_*: the M x K input
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 16;
   const int col = lane & 15, g = lane >> 4;
   const int n = n0 + col;
   const bool wok = n < N, xok = col < M;
   const unsigned short* wrow = w + (int64_t)(wok ? n : 0) * ldw;
-  const unsigned short* xrow = x + (int64_t)(xok ? col : 0) * ldx;
+  const unsigned short* xrow = MODE == PRO_NONE ? x + (int64_t)(xok ? col : 0) * ldx
+                                                : act_lds + (int64_t)(xok ? col : 0) * K;
   const int ss0 = wave * ss_per_wave;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  __shared__ float rinv[kProMaxM];
   Frag cur, nxt;
-  load_ss(cur, wrow, wok, xrow, xok, ss0 * kSS + g * 8, K);
-  for (int i = 0; i < ss_per_wave; ++i) {
-    if (i + 1 < ss_per_wave) load_ss(nxt, wrow, wok, xrow, xok, (ss0 + i + 1) * kSS + g * 8, K);
+  if constexpr (MODE == PRO_NONE) {
+    load_w(cur, wrow, wok, ss0 * kSS + g * 8, K);
+    load_x(cur, xrow, xok, ss0 * kSS + g * 8, K);
+    for (int i = 0; i < ss_per_wave; ++i) {
+      if (i + 1 < ss_per_wave) {
+        load_w(nxt, wrow, wok, (ss0 + i + 1) * kSS + g * 8, K);
+        load_x(nxt, xrow, xok, (ss0 + i + 1) * kSS + g * 8, K);
+      }
 #pragma unroll
-    for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.x[s], cur.w[s], acc, 0, 0, 0);
-    cur = nxt;
+      for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.x[s], cur.w[s], acc, 0, 0, 0);
+      cur = nxt;
+    }
+  } else {
+    // the weight stream runs two super-steps ahead of the prologue, which builds the input in LDS
+    Frag nx2;
+    load_w(cur, wrow, wok, ss0 * kSS + g * 8, K);
+    if (ss_per_wave > 1) load_w(nxt, wrow, wok, (ss0 + 1) * kSS + g * 8, K);
+    build_act<MODE, NW * 64>(x, ldx, M, K, pro, act_lds, rinv);
+    for (int i = 0; i < ss_per_wave; ++i) {
+      if (i + 2 < ss_per_wave) load_w(nx2, wrow, wok, (ss0 + i + 2) * kSS + g * 8, K);
+      load_x(cur, xrow, xok, (ss0 + i) * kSS + g * 8, K);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.x[s], cur.w[s], acc, 0, 0, 0);
+      cur = nxt;
+      nxt = nx2;
+    }
   }
   // acc: C[row m = 4 g + r][col n] -- sum the 4 waves' K partials
   red[wave][lane] = acc;
@@ -80,7 +183,8 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(const unsigned sho
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = 4 * g + r;
-        if (m < M) y[(int64_t)m * ldy + n] = f32_to_bf16(t[r] + b);
+        const float sc = MODE == PRO_RMS ? rinv[m < kProMaxM ? m : 0] : 1.f;
+        if (m < M) y[(int64_t)m * ldy + n] = f32_to_bf16(t[r] * sc + b);
       }
     }
   }
@@ -110,22 +214,35 @@ __device__ __forceinline__ bf16x8 fp8x8_to_bf16(uint2 w) {
   return r;
 }
 
-template <int NW>
+template <int NW, int MODE = PRO_NONE>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_fp8w_kernel(const unsigned short* __restrict x, int64_t ldx,
                                                                    const uint8_t* __restrict w, int64_t ldw,
                                                                    const float* __restrict wscale,
                                                                    const unsigned short* __restrict bias,
                                                                    unsigned short* __restrict y, int64_t ldy, int M,
-                                                                   int N, int K, int ss_per_wave) {
+                                                                   int N, int K, int ss_per_wave, ProArgs pro) {
   __shared__ f32x4 red[NW][64];
+  extern __shared__ __attribute__((aligned(16))) unsigned short act_lds[];  // PRO_*: the M x K input
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 16;
   const int col = lane & 15, g = lane >> 4;
   const int n = n0 + col;
   const bool wok = n < N, xok = col < M;
   const uint8_t* wrow = w + (int64_t)(wok ? n : 0) * ldw;
-  const unsigned short* xrow = x + (int64_t)(xok ? col : 0) * ldx;
+  const unsigned short* xrow = MODE == PRO_NONE ? x + (int64_t)(xok ? col : 0) * ldx
+                                                : act_lds + (int64_t)(xok ? col : 0) * K;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  __shared__ float rinv[kProMaxM];
+  uint4 wv0[8];  // first super-step's weights: in flight while the prologue builds the input
+  if constexpr (MODE != PRO_NONE) {
+    const int k0 = (wave * ss_per_wave) * kSS8 + 16 * g;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = k0 + 64 * j;
+      wv0[j] = (wok && k < K && ss_per_wave > 0) ? *reinterpret_cast<const uint4*>(wrow + k) : uint4{0u, 0u, 0u, 0u};
+    }
+    build_act<MODE, NW * 64>(x, ldx, M, K, pro, act_lds, rinv);
+  }
   for (int i = 0; i < ss_per_wave; ++i) {
     const int k0 = (wave * ss_per_wave + i) * kSS8 + 16 * g;
     uint4 wv[8];
@@ -134,7 +251,8 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_fp8w_kernel(const unsigne
     for (int j = 0; j < 8; ++j) {
       const int k = k0 + 64 * j;
       const bool in = k < K;
-      wv[j] = (wok && in) ? *reinterpret_cast<const uint4*>(wrow + k) : uint4{0u, 0u, 0u, 0u};
+      if (MODE != PRO_NONE && i == 0) wv[j] = wv0[j];
+      else wv[j] = (wok && in) ? *reinterpret_cast<const uint4*>(wrow + k) : uint4{0u, 0u, 0u, 0u};
       xa[j] = (xok && in) ? *reinterpret_cast<const bf16x8*>(xrow + k) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       xb[j] = (xok && in) ? *reinterpret_cast<const bf16x8*>(xrow + k + 8) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
@@ -162,7 +280,8 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_fp8w_kernel(const unsigne
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = 4 * g + r;
-        if (m < M) y[(int64_t)m * ldy + n] = f32_to_bf16(t[r] * sc + b);
+        const float rs = MODE == PRO_RMS ? rinv[m < kProMaxM ? m : 0] : 1.f;
+        if (m < M) y[(int64_t)m * ldy + n] = f32_to_bf16(t[r] * sc * rs + b);
       }
     }
   }
@@ -201,7 +320,7 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, const c10::opti
   auto* yp = reinterpret_cast<unsigned short*>(y.data_ptr());
 #define SXE_SG_LAUNCH(NW)                                                                                  \
   hipLaunchKernelGGL(sg::skinny_gemm_kernel<NW>, dim3(tiles), dim3(NW * 64), 0, cur_stream(), xp, x.stride(0), \
-                     wp, w.stride(0), bp, yp, y.stride(0), M, N, K, ss_per_wave)
+                     wp, w.stride(0), bp, yp, y.stride(0), M, N, K, ss_per_wave, sg::ProArgs{})
   if (nw == 4) SXE_SG_LAUNCH(4);
   else SXE_SG_LAUNCH(8);
 #undef SXE_SG_LAUNCH
@@ -242,12 +361,107 @@ at::Tensor skinny_gemm_fp8w(const at::Tensor& x, const at::Tensor& wq, const at:
   auto* yp = reinterpret_cast<unsigned short*>(y.data_ptr());
   if (nw == 4)
     hipLaunchKernelGGL(sg::skinny_gemm_fp8w_kernel<4>, dim3(tiles), dim3(256), 0, cur_stream(), xp, x.stride(0), wp,
-                       wq.stride(0), wscale.data_ptr<float>(), bp, yp, y.stride(0), M, N, K, ss_per_wave);
+                       wq.stride(0), wscale.data_ptr<float>(), bp, yp, y.stride(0), M, N, K, ss_per_wave,
+                       sg::ProArgs{});
   else
     hipLaunchKernelGGL(sg::skinny_gemm_fp8w_kernel<8>, dim3(tiles), dim3(512), 0, cur_stream(), xp, x.stride(0), wp,
-                       wq.stride(0), wscale.data_ptr<float>(), bp, yp, y.stride(0), M, N, K, ss_per_wave);
+                       wq.stride(0), wscale.data_ptr<float>(), bp, yp, y.stride(0), M, N, K, ss_per_wave,
+                       sg::ProArgs{});
   SXE_LAUNCH_CHECK();
   return y;
+}
+
+// ---- fused-prologue entry points (decode, M <= 4) ----------------------------------------------
+// mode 1 (rms): x [M, K], res [M, K] or None (same row stride), gw [K], eps -> (y [M, N], h [M, K] = x + res)
+// mode 2 (swiglu): x = gu [M, 2K] (gate | up halves) -> y [M, N]
+// wq: bf16 [N, K] (wscale None) or e4m3 bytes [N, K] with wscale fp32 [N]
+std::vector<at::Tensor> skinny_gemm_pro(const at::Tensor& x, const c10::optional<at::Tensor>& res,
+                                        const c10::optional<at::Tensor>& gw, double eps, const at::Tensor& w,
+                                        const c10::optional<at::Tensor>& wscale, const c10::optional<at::Tensor>& bias,
+                                        int64_t mode) {
+  SXE_CHECK_CUDA(x);
+  SXE_CHECK(mode == sg::PRO_RMS || mode == sg::PRO_SWIGLU, "skinny_gemm_pro: mode 1 (rms) or 2 (swiglu)");
+  SXE_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 &&
+                reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "skinny_gemm_pro: x bf16 [M, *], 16-B rows");
+  const bool fp8 = wscale.has_value() && wscale->defined();
+  SXE_CHECK(w.dim() == 2 && w.stride(1) == 1 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+            "skinny_gemm_pro: w [N, K] row-major, 16-B aligned");
+  SXE_CHECK(fp8 ? w.element_size() == 1 : w.scalar_type() == at::kBFloat16, "skinny_gemm_pro: w bf16 or fp8 bytes");
+  const int M = x.size(0), N = w.size(0), K = w.size(1);
+  SXE_CHECK(M >= 1 && M <= sg::kProMaxM, "skinny_gemm_pro: 1 <= M <= 4");
+  SXE_CHECK(x.size(1) == (mode == sg::PRO_SWIGLU ? 2 * K : K), "skinny_gemm_pro: x width");
+  SXE_CHECK(K % (fp8 ? 16 : 8) == 0 && w.stride(0) % (fp8 ? 16 : 8) == 0, "skinny_gemm_pro: K alignment");
+  sg::ProArgs pro{nullptr, nullptr, nullptr, (float)eps};
+  at::Tensor h;
+  if (mode == sg::PRO_RMS) {
+    SXE_CHECK(gw.has_value() && gw->scalar_type() == at::kBFloat16 && gw->is_contiguous() && gw->numel() == K,
+              "skinny_gemm_pro: norm weight bf16 [K]");
+    pro.gw = reinterpret_cast<const unsigned short*>(gw->data_ptr());
+    if (res.has_value() && res->defined()) {
+      SXE_CHECK(res->scalar_type() == at::kBFloat16 && res->sizes() == x.sizes() && res->strides() == x.strides(),
+                "skinny_gemm_pro: residual like x");
+      pro.res = reinterpret_cast<const unsigned short*>(res->data_ptr());
+      h = at::empty({M, K}, x.options());
+      pro.hout = reinterpret_cast<unsigned short*>(h.data_ptr());
+    }
+  }
+  const unsigned short* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    SXE_CHECK(bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() && bias->numel() == N, "bias: bf16 [N]");
+    bp = reinterpret_cast<const unsigned short*>(bias->data_ptr());
+  }
+  auto y = at::empty({M, N}, x.options());
+  if (N == 0) return {y, h.defined() ? h : x};
+  c10::DeviceGuard gd(x.device());
+  const size_t lds = (size_t)M * K * 2;
+  SXE_CHECK(lds <= 144 * 1024, "skinny_gemm_pro: M x K input exceeds the LDS budget");
+  const int tiles = (N + 15) / 16;
+  auto* xp = reinterpret_cast<const unsigned short*>(x.data_ptr());
+  auto* yp = reinterpret_cast<unsigned short*>(y.data_ptr());
+  static bool attr[2][2][2] = {};
+  auto set = [&](const void* f, int a, int b, int c) {
+    if (!attr[a][b][c]) {
+      SXE_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 144 * 1024));
+      attr[a][b][c] = true;
+    }
+  };
+  const int mi = mode == sg::PRO_RMS ? 0 : 1;
+  if (!fp8) {
+    const int ss_total = (K + sg::kSS - 1) / sg::kSS;
+    int nw = 4;
+    while (nw < 8 && (int64_t)tiles * nw < 4096 && ss_total >= 4 * nw) nw *= 2;
+    const int spw = (ss_total + nw - 1) / nw;
+    auto* wp = reinterpret_cast<const unsigned short*>(w.data_ptr());
+#define SXE_SGP(NW, MODE)                                                                                            \
+  do {                                                                                                               \
+    set(reinterpret_cast<const void*>(&sg::skinny_gemm_kernel<NW, MODE>), 0, NW == 8, mi);                           \
+    hipLaunchKernelGGL((sg::skinny_gemm_kernel<NW, MODE>), dim3(tiles), dim3(NW * 64), lds, cur_stream(), xp,         \
+                       x.stride(0), wp, w.stride(0), bp, yp, y.stride(0), M, N, K, spw, pro);                         \
+  } while (0)
+    if (mode == sg::PRO_RMS) { if (nw == 4) SXE_SGP(4, sg::PRO_RMS); else SXE_SGP(8, sg::PRO_RMS); }
+    else { if (nw == 4) SXE_SGP(4, sg::PRO_SWIGLU); else SXE_SGP(8, sg::PRO_SWIGLU); }
+#undef SXE_SGP
+  } else {
+    SXE_CHECK(wscale->scalar_type() == at::kFloat && wscale->is_contiguous() && wscale->numel() == N,
+              "skinny_gemm_pro: wscale fp32 [N]");
+    const int ss_total = (K + sg::kSS8 - 1) / sg::kSS8;
+    int nw = 4;
+    while (nw < 8 && (int64_t)tiles * nw < 4096 && ss_total >= 2 * nw) nw *= 2;
+    const int spw = (ss_total + nw - 1) / nw;
+    auto* wp = reinterpret_cast<const uint8_t*>(w.data_ptr());
+    const float* sp = wscale->data_ptr<float>();
+#define SXE_SGP8(NW, MODE)                                                                                           \
+  do {                                                                                                               \
+    set(reinterpret_cast<const void*>(&sg::skinny_gemm_fp8w_kernel<NW, MODE>), 1, NW == 8, mi);                      \
+    hipLaunchKernelGGL((sg::skinny_gemm_fp8w_kernel<NW, MODE>), dim3(tiles), dim3(NW * 64), lds, cur_stream(), xp,    \
+                       x.stride(0), wp, w.stride(0), sp, bp, yp, y.stride(0), M, N, K, spw, pro);                     \
+  } while (0)
+    if (mode == sg::PRO_RMS) { if (nw == 4) SXE_SGP8(4, sg::PRO_RMS); else SXE_SGP8(8, sg::PRO_RMS); }
+    else { if (nw == 4) SXE_SGP8(4, sg::PRO_SWIGLU); else SXE_SGP8(8, sg::PRO_SWIGLU); }
+#undef SXE_SGP8
+  }
+  SXE_LAUNCH_CHECK();
+  return {y, h.defined() ? h : x};
 }
 
 }  // namespace sxe
@@ -255,8 +469,11 @@ at::Tensor skinny_gemm_fp8w(const at::Tensor& x, const at::Tensor& wq, const at:
 TORCH_LIBRARY_FRAGMENT(sxe, m) {
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor? bias) -> Tensor");
   m.def("skinny_gemm_fp8w(Tensor x, Tensor wq, Tensor wscale, Tensor? bias) -> Tensor");
+  m.def("skinny_gemm_pro(Tensor x, Tensor? res, Tensor? gw, float eps, Tensor w, Tensor? wscale, Tensor? bias, "
+        "int mode) -> Tensor[]");
 }
 TORCH_LIBRARY_IMPL(sxe, CUDA, m) {
   m.impl("skinny_gemm", &sxe::skinny_gemm);
   m.impl("skinny_gemm_fp8w", &sxe::skinny_gemm_fp8w);
+  m.impl("skinny_gemm_pro", &sxe::skinny_gemm_pro);
 }

@@ -21,6 +21,8 @@ exceeds their count), its KV cache holds only its kv heads, and per layer exactl
 (o_proj, down_proj) plus one logits all-gather per forward cross xGMI. The embedding and norms stay
 replicated. Dense models only (experts run locally, ``ep_size == 1``).
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -193,10 +195,40 @@ class RaggedLlama:
             return self.qw[li][key](x)
         return mod(x)
 
+    # decode (<= 4 tokens): RMSNorm folded into the QKV / gate_up GEMMs and SwiGLU into the down GEMM
+    # (skinny_gemm.hip prologues) -- three latency-bound launches fewer per layer
+    FUSE_MAX_T = 4
+
+    def _fusable(self, T):
+        return (self.tps is None and T <= self.FUSE_MAX_T and not self.is_moe and self.device.type == "cuda" and native.hip_available()
+                and os.environ.get("SXE_DECODE_FUSE", "1") == "1")
+
+    def _wobj(self, mod, li, key):
+        if self.qw is not None and key in self.qw[li]:
+            impl = self.qw[li][key]
+            return getattr(impl, "q", None) if getattr(impl, "q", None) is not None else getattr(impl, "weight", None)
+        return mod.weight
+
+    def _norm_proj(self, norm, x, res, mod, li, key):
+        """(norm(x + res) @ W^T, h) through the fused kernel, else the separate launches."""
+        if self._fusable(x.shape[0]) and getattr(mod, "bias", None) is None:
+            from ....ops.linear import fused_rms_linear
+            r = fused_rms_linear(x, res, norm.weight, norm.eps, self._wobj(mod, li, key))
+            if r is not None:
+                return r
+        a, h = (norm(x), x) if res is None else norm(x, res)
+        return self._proj(mod, a, li, key), h
+
     def _mlp(self, layer, m, li=0):
         if hasattr(layer, "mlp"):
             mlp = layer.mlp
-            return self._proj(mlp.down_proj, swiglu(self._proj(mlp.gate_up_proj, m, li, "gu")), li, "down")
+            gu = m if getattr(self, "_gu_ready", False) else self._proj(mlp.gate_up_proj, m, li, "gu")
+            if self._fusable(gu.shape[0]) and getattr(mlp.down_proj, "bias", None) is None:
+                from ....ops.linear import fused_swiglu_linear
+                y = fused_swiglu_linear(gu, self._wobj(mlp.down_proj, li, "down"))
+                if y is not None:
+                    return y
+            return self._proj(mlp.down_proj, swiglu(gu), li, "down")
         moe = layer.block_sparse_moe if hasattr(layer, "block_sparse_moe") else layer.moe
         return self._moe_dropless(moe.deepspeed_moe, m)
 
@@ -241,19 +273,22 @@ class RaggedLlama:
         x = self.embed_impl(batch.input_ids) if self.embed_impl is not None else model.embed_tokens(batch.input_ids)
         res = None
         for li, layer in enumerate(model.layers):
-            if res is None:
-                a, h = layer.input_layernorm(x), x
-            else:
-                a, h = layer.input_layernorm(x, res)
             attn = layer.self_attn
-            qkv = self._proj(attn.qkv_proj, a, li, "qkv").view(T, self.nq + 2 * self.nkv, self.head_dim)
+            qkv, h = self._norm_proj(layer.input_layernorm, x, res, attn.qkv_proj, li, "qkv")
+            qkv = qkv.view(T, self.nq + 2 * self.nkv, self.head_dim)
             kv_layer = kv_cache.layer(li)
             # RoPE on q/k + append of k/v to the paged cache: one launch (paged_attn.hip)
             rope_kv_cache_append(qkv, rope, batch.positions, kv_layer, batch.slots, self.nq, self.nkv)
             o = self._attention(qkv, kv_layer, batch)
             o = self._proj(attn.o_proj, o.reshape(T, self.nq * self.head_dim), li, "o")
-            m, h2 = layer.post_attention_layernorm(o, h)
-            x, res = self._mlp(layer, m, li), h2
+            if hasattr(layer, "mlp"):
+                gu, h2 = self._norm_proj(layer.post_attention_layernorm, o, h, layer.mlp.gate_up_proj, li, "gu")
+                self._gu_ready = True
+                x, res = self._mlp(layer, gu, li), h2
+                self._gu_ready = False
+            else:
+                m, h2 = layer.post_attention_layernorm(o, h)
+                x, res = self._mlp(layer, m, li), h2
         last = batch.last_idx
         h = model.norm(gather_rows(x, last), gather_rows(res, last))[0]
         if self.tps is not None:  # vocab-parallel head: gather every rank's logit columns

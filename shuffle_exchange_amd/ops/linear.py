@@ -47,6 +47,52 @@ def _skinny(x, weight, bias):
     return torch.ops.sxe.skinny_gemm(x2, weight, bias).view(*x.shape[:-1], weight.shape[0])
 
 
+def _pro_weight(weight):
+    """(w, scale) for the fused-prologue skinny kernels: a bf16 [N, K] tensor or an FP8Weight."""
+    if isinstance(weight, torch.Tensor):
+        if weight.dtype == torch.bfloat16 and weight.dim() == 2 and weight.is_contiguous() and weight.data_ptr() % 16 == 0:
+            return weight, None
+        return None
+    q, sc = getattr(weight, "q", None), getattr(weight, "scale", None)
+    if q is not None and sc is not None and q.element_size() == 1 and q.dim() == 2 and q.is_contiguous():
+        return q.view(torch.uint8), sc
+    return None
+
+
+def _pro_ok(x, rows_max=4):
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and 0 < x.shape[0] <= rows_max
+            and x.stride(1) == 1 and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and not x.requires_grad)
+
+
+def fused_rms_linear(x, residual, norm_weight, eps, weight, bias=None):
+    """Decode (<= 4 rows): ``linear(rms_norm(x + residual), weight)`` in ONE launch
+    (skinny_gemm.hip PRO_RMS). Returns (y, h = x + residual) -- h is x itself without a residual --
+    or None when the fused kernel does not cover the operands (the caller runs the unfused ops)."""
+    wk = _pro_weight(weight)
+    if wk is None or not _pro_ok(x) or norm_weight.dtype != torch.bfloat16 or not norm_weight.is_contiguous():
+        return None
+    if residual is not None and (residual.shape != x.shape or residual.stride() != x.stride()
+                                 or residual.dtype != x.dtype):
+        return None
+    w, sc = wk
+    if x.shape[1] != w.shape[1]:
+        return None
+    y, h = torch.ops.sxe.skinny_gemm_pro(x, residual, norm_weight, float(eps), w, sc, bias, 1)
+    return y, (h if residual is not None else x)
+
+
+def fused_swiglu_linear(gu, weight, bias=None):
+    """Decode (<= 4 rows): ``linear(silu(gu[:, :I]) * gu[:, I:], weight)`` in ONE launch
+    (skinny_gemm.hip PRO_SWIGLU); None when not covered."""
+    wk = _pro_weight(weight)
+    if wk is None or not _pro_ok(gu):
+        return None
+    w, sc = wk
+    if gu.shape[1] != 2 * w.shape[1]:
+        return None
+    return torch.ops.sxe.skinny_gemm_pro(gu, None, None, 0.0, w, sc, bias, 2)[0]
+
+
 # Hand-written weight-gradient GEMM (csrc/kernels/gemm_wgrad.hip: k-major operands read through LDS
 # with ds_read_b64_tr_b16, fp32 accumulate in the epilogue): no transposed copies of dY / X at all.
 # Measured on MI355X at 8192 tokens (tools/wgrad_exp.py, profiles/wgrad_kernel.log): 28672x4096

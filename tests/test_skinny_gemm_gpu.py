@@ -74,3 +74,76 @@ def test_hf_engine_quantized_weights_close_to_bf16(kind, min_cos):
         a, b = e16.put([0], [[t]]), e8.put([0], [[t]])  # decode steps: skinny FP8 / FP6 / FP4-weight kernels
         cos = torch.nn.functional.cosine_similarity(a.float(), b.float()).item()
         assert cos > min_cos, (kind, cos)
+
+
+@pytest.mark.parametrize("M", [1, 3, 4])
+@pytest.mark.parametrize("K,N", [(4096, 6144), (4096, 28672), (512, 200)])
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("with_res", [True, False])
+def test_fused_rms_prologue_vs_fp32(M, K, N, fp8, with_res):
+    """skinny_gemm_pro mode 1: residual add + RMSNorm + GEMM in one launch == the fp32 reference of
+    the separate ops (h rounded to bf16 like the norm kernel), and h = x + res written out."""
+    from shuffle_exchange_amd.ops.fp_quantizer import FP8Weight
+    from shuffle_exchange_amd.ops.linear import fused_rms_linear
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    res = torch.randn(M, K, device="cuda", dtype=torch.bfloat16) if with_res else None
+    g = (1.0 + 0.1 * torch.randn(K, device="cuda")).to(torch.bfloat16)
+    w = (0.02 * torch.randn(N, K, device="cuda")).to(torch.bfloat16)
+    wobj = FP8Weight(w) if fp8 else w
+    y, h = fused_rms_linear(x, res, g, 1e-5, wobj)
+    hr = (x.float() + res.float()).bfloat16().float() if with_res else x.float()
+    a = hr * torch.rsqrt(hr.square().mean(-1, keepdim=True) + 1e-5) * g.float()
+    wr = wobj.dequantize().float() if fp8 else w.float()
+    ref = a @ wr.t()
+    assert torch.equal(h.float(), hr)
+    err = ((y.float() - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("I,N", [(14336, 4096), (512, 256)])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_fused_swiglu_prologue_vs_fp32(M, I, N, fp8):
+    from shuffle_exchange_amd.ops.fp_quantizer import FP8Weight
+    from shuffle_exchange_amd.ops.linear import fused_swiglu_linear
+    torch.manual_seed(1)
+    gu = torch.randn(M, 2 * I, device="cuda", dtype=torch.bfloat16)
+    w = (0.02 * torch.randn(N, I, device="cuda")).to(torch.bfloat16)
+    wobj = FP8Weight(w) if fp8 else w
+    y = fused_swiglu_linear(gu, wobj)
+    g, u = gu.float().chunk(2, dim=-1)
+    a = torch.nn.functional.silu(g) * u
+    wr = wobj.dequantize().float() if fp8 else w.float()
+    ref = a @ wr.t()
+    err = ((y.float() - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
+
+
+def test_decode_fused_layer_matches_unfused(monkeypatch):
+    """Ragged engine decode with the fused prologues == with them disabled (same greedy tokens,
+    logits within bf16 rounding)."""
+    import os
+    from shuffle_exchange_amd.inference.v2 import RaggedInferenceEngineConfig, build_engine
+    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+    torch.manual_seed(0)
+    cfg = llama_config("llama-tiny", hidden_size=512, intermediate_size=1024, num_attention_heads=8,
+                       num_key_value_heads=2, vocab_size=1000, num_hidden_layers=2)
+    model = LlamaForCausalLM(cfg).cuda().bfloat16().eval()
+    prompt = torch.randint(0, cfg.vocab_size, (12,)).tolist()
+    outs = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("SXE_DECODE_FUSE", fuse)
+        eng = build_engine(model, RaggedInferenceEngineConfig(kv_block_size=16, num_kv_blocks=64))
+        logits = eng.put([1], [torch.tensor(prompt)])
+        toks, lg = [], []
+        for _ in range(6):
+            t = int(logits[0].argmax())
+            toks.append(t)
+            logits = eng.put([1], [torch.tensor([t])])
+            lg.append(logits.float())
+        eng.flush(1)
+        outs.append((toks, torch.cat(lg)))
+    assert outs[0][0] == outs[1][0]
+    err = ((outs[0][1] - outs[1][1]).norm() / outs[1][1].norm()).item()
+    assert err < 2e-2, err
