@@ -25,6 +25,9 @@ class MixtralConfig(LlamaConfig):
     capacity_factor: float = 1.25
     router_aux_loss_coef: float = 0.02
     drop_tokens: bool = True
+    min_capacity: int = 4
+    top2_2nd_expert_sampling: bool = True  # reference MoE default (HF Mixtral routes top-2 greedily)
+    enable_expert_tensor_parallelism: bool = False
 
     def num_params(self):
         h, i, L = self.hidden_size, self.intermediate_size, self.num_hidden_layers
@@ -63,8 +66,10 @@ class MixtralDecoderLayer(nn.Module):
         self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         self.block_sparse_moe = MoE(cfg.hidden_size, None, cfg.num_local_experts, cfg.ep_size,
                                     k=cfg.num_experts_per_tok, capacity_factor=cfg.capacity_factor,
-                                    eval_capacity_factor=cfg.capacity_factor, min_capacity=4,
-                                    drop_tokens=cfg.drop_tokens, intermediate_size=cfg.intermediate_size)
+                                    eval_capacity_factor=cfg.capacity_factor, min_capacity=cfg.min_capacity,
+                                    drop_tokens=cfg.drop_tokens, intermediate_size=cfg.intermediate_size,
+                                    top2_2nd_expert_sampling=cfg.top2_2nd_expert_sampling,
+                                    enable_expert_tensor_parallelism=cfg.enable_expert_tensor_parallelism)
 
     def forward(self, x, residual, rope, position_ids=None):
         if residual is None:

@@ -86,9 +86,14 @@ class AutoTP:
 
 
 def broadcast_within_tp(model, tp_group, src_global_rank):
-    """Identical starting weights on every TP rank before sharding."""
+    """Identical starting weights on every TP rank before sharding. Expert weights are left alone:
+    without expert TP the TP ranks hold different experts (and expert-TP shards are cut from
+    each rank's own full init)."""
+    from ..moe.utils import is_moe_param
     with torch.no_grad():
         for p in list(model.parameters()) + list(model.buffers()):
+            if isinstance(p, nn.Parameter) and is_moe_param(p):
+                continue
             dist.broadcast(p.data, src=src_global_rank, group=tp_group)
 
 

@@ -48,10 +48,38 @@ class GroupedSwiGLUExperts(nn.Module):
             p.allreduce = False
             p.group_name = expert_group_name
 
+        self.tp_group = None
+
+    def expert_tp_shard_(self, tp_group):
+        """Expert tensor parallelism (reference MoE ``enable_expert_tensor_parallelism``): keep this
+        TP rank's 1/tp of the gate and up columns and the matching rows of down. The input is then
+        ``copy_to_tp`` (its gradient all-reduced over TP) and the output ``reduce_from_tp``."""
+        from .. import comm as dist
+        tp, r = dist.get_world_size(tp_group), dist.get_rank(tp_group)
+        if tp == 1:
+            return
+        inter = self.w_down.shape[1]
+        assert inter % tp == 0, f"expert intermediate size {inter} not divisible by tp {tp}"
+        s = inter // tp
+        with torch.no_grad():
+            gu = self.w_gate_up.data
+            gu = torch.cat([gu[..., r * s:(r + 1) * s], gu[..., inter + r * s:inter + (r + 1) * s]], -1).contiguous()
+            down = self.w_down.data[:, r * s:(r + 1) * s].contiguous()
+        for name, t in (("w_gate_up", gu), ("w_down", down)):
+            old = getattr(self, name)
+            new = nn.Parameter(t, requires_grad=old.requires_grad)
+            new.allreduce, new.group_name, new.tensor_model_parallel = False, old.group_name, True
+            setattr(self, name, new)
+        self.tp_group = tp_group
+
     def forward(self, x):
         # x: [E_local, C, H] -> [E_local, C, 2I] -> SwiGLU (one HIP launch for all experts) -> [E_local, C, H]
         # (the dense MLP's token-minor weight-gradient scheme, ops/mlp.py, measured no faster here: the
         # experts reduce over only C capacity tokens -- Mixtral-arch 8 layers 311.8 vs 309.9 ms/step)
+        if self.tp_group is not None:
+            from ..module_inject.layers import copy_to_tp, reduce_from_tp
+            x = copy_to_tp(x, self.tp_group)
+            return reduce_from_tp(grouped_mm(swiglu(grouped_mm(x, self.w_gate_up)), self.w_down), self.tp_group)
         return grouped_mm(swiglu(grouped_mm(x, self.w_gate_up)), self.w_down)
 
 

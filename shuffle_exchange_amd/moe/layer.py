@@ -43,9 +43,34 @@ class MoE(nn.Module):
         self._groups_ready = False
 
     def set_deepspeed_parallelism(self, use_data_before_expert_parallel_=False):
-        name = groups.create_expert_and_data_parallel(self.ep_size, self.expert_group_name)
-        self.deepspeed_moe._set_ep_group(groups.get_expert_parallel_group(name))
+        """Create (once) this layer's expert-parallel / expert-data-parallel groups and wire the
+        TP token drop/gather (reference layer.py:98-111, groups.py:240 / :383). With tensor
+        parallelism and ``enable_expert_tensor_parallelism`` the experts are sharded over the TP
+        group here (GroupedSwiGLUExperts: gate/up columns, down rows); without it the EP group
+        spans the TP ranks. The engine calls this after AutoTP and before the model broadcast."""
+        if self._groups_ready:
+            return
+        tp = groups.get_tensor_model_parallel_world_size()
+        expert_tp = self.enable_expert_tensor_parallelism and tp > 1
+        name = groups.create_expert_and_data_parallel(self.ep_size, self.expert_group_name,
+                                                      span_tp=tp > 1 and not expert_tp)
+        tp_group = groups.get_tensor_model_parallel_group() if tp > 1 else None
+        self.deepspeed_moe._set_ep_group(groups.get_expert_parallel_group(name), tp_group, expert_tp)
+        if expert_tp:
+            experts = self.deepspeed_moe.experts
+            if hasattr(experts, "expert_tp_shard_"):
+                experts.expert_tp_shard_(tp_group)
+            for p in experts.parameters():  # user expert modules shard themselves (reference semantics)
+                p.tensor_model_parallel = True
         self._groups_ready = True
+
+    @property
+    def expert_tp_rank(self):
+        """Model-parallel index of this rank's expert shards in checkpoint file names (0 when the
+        experts are not TP-sharded: they are then independent of the TP degree)."""
+        if self.deepspeed_moe.expert_tp:
+            return groups.get_tensor_model_parallel_rank()
+        return 0
 
     def forward(self, hidden_states, used_token=None):
         if not self._groups_ready:

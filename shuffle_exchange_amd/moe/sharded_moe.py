@@ -44,9 +44,11 @@ def multiplicative_jitter(x, device, epsilon=1e-2):
     return x * u
 
 
-def _capacity(num_tokens, num_experts, capacity_factor, min_capacity):
-    c = int(math.ceil(num_tokens / num_experts * capacity_factor))
-    return max(c, int(min_capacity))
+def _capacity(num_tokens, num_experts, capacity_factor, min_capacity, tp=1):
+    c = max(int(math.ceil(num_tokens / num_experts * capacity_factor)), int(min_capacity))
+    # tensor-parallel non-expert layers: the capacity is split over the TP ranks before the a2a
+    # (mappings.drop_tokens), so it is padded to a multiple of tp (reference sharded_moe.py:220)
+    return -(-c // tp) * tp
 
 
 class Routing:
@@ -77,27 +79,28 @@ def _positions(expert_idx, E, mask=None):
     return loc.to(torch.int64)
 
 
-def _max_capacity(exp_counts, ep_group, num_tokens):
+def _max_capacity(exp_counts, ep_group, num_tokens, tp=1):
     new_cap = exp_counts.max().to(torch.int64).reshape(1)
     if ep_group is not None and dist.get_world_size(ep_group) > 1:
         dist.all_reduce(new_cap, op=dist.ReduceOp.MAX, group=ep_group)
-    return int(min(int(new_cap.item()), num_tokens))
+    c = max(1, int(min(int(new_cap.item()), num_tokens)))
+    return -(-c // tp) * tp
 
 
 def top1gating(logits, capacity_factor, min_capacity, used_token=None, noisy_gate_policy=None, drop_tokens=True,
-               use_rts=True, ep_group=None):
+               use_rts=True, ep_group=None, tp=1):
     from ..ops.moe import topk_softmax
     logits_w_noise = logits + gumbel_rsample(logits.shape, logits.device) if noisy_gate_policy == "RSample" else None
     gates, top = topk_softmax(logits, 1)
     S, E = gates.shape
-    capacity = _capacity(S, E, capacity_factor, min_capacity)
+    capacity = _capacity(S, E, capacity_factor, min_capacity, tp)
     idx1 = torch.argmax(logits_w_noise, dim=1) if logits_w_noise is not None else top[:, 0]
     mask1 = F.one_hot(idx1, E)
     if used_token is not None:
         mask1 = mask1 * used_token.unsqueeze(1).to(mask1.dtype)
     exp_counts = mask1.sum(0).detach()
     if not drop_tokens:
-        capacity = _max_capacity(exp_counts, ep_group, S)
+        capacity = _max_capacity(exp_counts, ep_group, S, tp)
     me = gates.mean(0)
     ce = mask1.float().mean(0)
     l_aux = (me * ce).sum() * E
@@ -115,7 +118,8 @@ def top1gating(logits, capacity_factor, min_capacity, used_token=None, noisy_gat
     return Routing(idx1.unsqueeze(1), loc.clamp(max=capacity - 1), keep, gate1, capacity, l_aux, exp_counts)
 
 
-def top2gating(logits, capacity_factor, min_capacity, drop_tokens=True, ep_group=None, top2_2nd_expert_sampling=True):
+def top2gating(logits, capacity_factor, min_capacity, drop_tokens=True, ep_group=None, top2_2nd_expert_sampling=True,
+               tp=1):
     gates = F.softmax(logits, dim=1)
     S, E = gates.shape
     idx1 = torch.argmax(gates, dim=1)
@@ -130,9 +134,9 @@ def top2gating(logits, capacity_factor, min_capacity, drop_tokens=True, ep_group
     idx = torch.stack([idx1, idx2], dim=1)
     loc = _positions(idx, E)
     if drop_tokens:
-        capacity = _capacity(S, E, capacity_factor * 2, min_capacity)
+        capacity = _capacity(S, E, capacity_factor * 2, min_capacity, tp)
     else:
-        capacity = _max_capacity(exp_counts, ep_group, S)
+        capacity = _max_capacity(exp_counts, ep_group, S, tp)
     keep = loc < capacity
     g = torch.stack([(gates * mask1).sum(1), (gates * mask2).sum(1)], dim=1) * keep
     denom = g.sum(1, keepdim=True).clamp(min=torch.finfo(g.dtype).eps)
@@ -140,7 +144,7 @@ def top2gating(logits, capacity_factor, min_capacity, drop_tokens=True, ep_group
     return Routing(idx, loc.clamp(max=capacity - 1), keep, g, capacity, l_aux, exp_counts)
 
 
-def topkgating(logits, k, capacity_factor, min_capacity, drop_tokens=True, ep_group=None, drop_policy="probs"):
+def topkgating(logits, k, capacity_factor, min_capacity, drop_tokens=True, ep_group=None, drop_policy="probs", tp=1):
     from ..ops.moe import topk_softmax
     gates, top_idx = topk_softmax(logits, k)  # one HIP launch on GPU (softmax + top-k per token)
     top_gate = torch.gather(logits, 1, top_idx)
@@ -151,7 +155,7 @@ def topkgating(logits, k, capacity_factor, min_capacity, drop_tokens=True, ep_gr
     ce = mask.float().mean(0)
     l_aux = (me * ce).mean() * E * E / k
     if drop_tokens:
-        capacity = _capacity(S, E, capacity_factor * k, min_capacity)
+        capacity = _capacity(S, E, capacity_factor * k, min_capacity, tp)
         if drop_policy == "probs":
             topk_masked = torch.zeros_like(logits).scatter(1, top_idx, top_gate)
             cidx = torch.topk(topk_masked, k=min(capacity, S), dim=0, sorted=False)[1]
@@ -160,7 +164,7 @@ def topkgating(logits, k, capacity_factor, min_capacity, drop_tokens=True, ep_gr
         elif drop_policy != "position":
             raise ValueError(f"Invalid drop_policy: {drop_policy}")
     else:
-        capacity = _max_capacity(exp_counts, ep_group, S)
+        capacity = _max_capacity(exp_counts, ep_group, S, tp)
     # positions along the token axis per expert (the reference's cumsum over tokens)
     locs = (torch.cumsum(mask.to(torch.int32).t().contiguous(), dim=1).t() - 1).to(torch.int64)
     loc_k = torch.gather(locs, 1, top_idx)
@@ -186,9 +190,11 @@ class TopKGate(nn.Module):
         self.ep_group = ep_group
         self.top2_2nd_expert_sampling = top2_2nd_expert_sampling
         self.drop_policy = drop_policy
+        self.tp = 1
 
-    def _set_ep_group(self, g):
+    def _set_ep_group(self, g, tp=1):
         self.ep_group = g
+        self.tp = tp
 
     def forward(self, x, used_token=None):
         # gating in fp32 (reference sharded_moe.py:500-524)
@@ -200,11 +206,12 @@ class TopKGate(nn.Module):
         if self.k == 1:
             return top1gating(logits, cf, self.min_capacity, used_token,
                               self.noisy_gate_policy if self.training else None, self.drop_tokens, self.use_rts,
-                              self.ep_group)
+                              self.ep_group, self.tp)
         if self.k == 2:
             return top2gating(logits, cf, self.min_capacity, self.drop_tokens, self.ep_group,
-                              self.top2_2nd_expert_sampling and self.training)
-        return topkgating(logits, self.k, cf, self.min_capacity, self.drop_tokens, self.ep_group, self.drop_policy)
+                              self.top2_2nd_expert_sampling and self.training, self.tp)
+        return topkgating(logits, self.k, cf, self.min_capacity, self.drop_tokens, self.ep_group, self.drop_policy,
+                          self.tp)
 
 
 class _AllToAll(torch.autograd.Function):
@@ -233,7 +240,15 @@ def all_to_all(group, x):
 
 
 class MOELayer(nn.Module):
-    """gate -> dispatch -> a2a -> experts -> a2a -> combine (reference sharded_moe.py:587-678)."""
+    """gate -> dispatch -> a2a -> experts -> a2a -> combine (reference sharded_moe.py:587-678).
+
+    Tensor-parallel non-expert layers (``tp_group``): every TP rank routes the same tokens, keeps
+    its 1/tp share of each expert's capacity for the a2a (``drop_tokens``) and all-gathers the
+    shares after the return a2a. With expert TP (``expert_tp``) the EP group lives inside one TP
+    slice and the TP peers of a rank hold the other column/row shards of the SAME experts: the
+    shares are all-gathered before the experts (which run copy_to_tp / reduce_from_tp inside)
+    and dropped again after them. Without it, the EP group spans the TP ranks (different experts
+    per TP rank) and each expert sees only its share."""
 
     def __init__(self, gate: TopKGate, experts, ep_group_name, ep_size, num_local_experts):
         super().__init__()
@@ -246,10 +261,16 @@ class MOELayer(nn.Module):
         self.l_aux = None
         self.exp_counts = None
         self.wall_clock_breakdown = False
+        self.tp_group = None
+        self.tp = 1
+        self.expert_tp = False
 
-    def _set_ep_group(self, ep_group):
+    def _set_ep_group(self, ep_group, tp_group=None, expert_tp=False):
         self.ep_group = ep_group
-        self.gate._set_ep_group(ep_group)
+        self.tp_group = tp_group
+        self.tp = dist.get_world_size(tp_group) if tp_group is not None else 1
+        self.expert_tp = bool(expert_tp) and self.tp > 1
+        self.gate._set_ep_group(ep_group, self.tp)
 
     def forward(self, x, used_token=None):
         shape = x.shape
@@ -265,15 +286,27 @@ class MOELayer(nn.Module):
         # and combine are then atomic-free row gathers (csrc/kernels/moe.hip on the GPU)
         slots, slot_src = routing_tables(r.expert, r.location, r.keep, C, E)
         disp = dispatch(xt, slots, slot_src)
-        # [E, C, H] -> a2a over EP: rank j receives, from every rank, the rows for its local experts
-        disp = all_to_all(self.ep_group, disp.view(self.ep_size, self.num_local_experts * C, H))
-        # local experts see [E_local, ep*C, H]
-        disp = disp.view(self.ep_size, self.num_local_experts, C, H).transpose(0, 1).reshape(
-            self.num_local_experts, self.ep_size * C, H)
+        ep, nle, tp = self.ep_size, self.num_local_experts, self.tp
+        from .mappings import drop_tokens, gather_tokens
+        Cl = C // tp  # capacity share of this TP rank
+        if tp > 1:
+            disp = drop_tokens(disp.view(E, C, H), 1, self.tp_group)
+        # [E, Cl, H] -> a2a over EP: rank j receives, from every rank, the rows for its local experts
+        disp = all_to_all(self.ep_group, disp.reshape(ep, nle * Cl, H))
+        Ce = Cl
+        if self.expert_tp:  # the TP peers hold the other shards of these experts: all see every token
+            disp = gather_tokens(disp.view(ep * nle, Cl, H), 1, self.tp_group)
+            Ce = C
+        # local experts see [E_local, ep*Ce, H]
+        disp = disp.reshape(ep, nle, Ce, H).transpose(0, 1).reshape(nle, ep * Ce, H)
         out = self.experts(disp)
-        out = out.view(self.num_local_experts, self.ep_size, C, H).transpose(0, 1).reshape(self.ep_size,
-                                                                                              self.num_local_experts * C, H)
-        out = all_to_all(self.ep_group, out).reshape(E * C, H)
+        out = out.view(nle, ep, Ce, H).transpose(0, 1).reshape(ep * nle, Ce, H)
+        if self.expert_tp:
+            out = drop_tokens(out, 1, self.tp_group)
+        out = all_to_all(self.ep_group, out.reshape(ep, nle * Cl, H))
+        if tp > 1:
+            out = gather_tokens(out.view(E, Cl, H), 1, self.tp_group)
+        out = out.reshape(E * C, H)
         comb = combine(out, slots, slot_src, r.weight)
         self.l_aux = r.l_aux
         self.exp_counts = r.exp_counts

@@ -21,6 +21,7 @@ class _Registry:
     groups = {}
     ranks = {}
     expert = {}  # name -> (ep_group, ep_ranks, edp_group, edp_ranks)
+    expert_span = {}  # name -> the EP groups span the TP ranks (no expert TP)
     zero_param = None  # hpZ intra group
     mpu = None
 
@@ -50,7 +51,7 @@ def initialize(tensor_parallel_size=1, pipeline_parallel_size=1, sequence_parall
     _Registry.sizes = new
     _Registry.topo = ProcessTopology(["pipe", "data", "seq", "model"], [pp, dp, sp, tp])
     topo = _Registry.topo
-    _Registry.groups, _Registry.ranks, _Registry.expert = {}, {}, {}
+    _Registry.groups, _Registry.ranks, _Registry.expert, _Registry.expert_span = {}, {}, {}, {}
     if mpu is not None:
         _Registry.groups["data"] = mpu.get_data_parallel_group()
         _Registry.ranks["data"] = dist.group_ranks(_Registry.groups["data"])
@@ -161,32 +162,45 @@ def group_ranks(key):
 
 # ---------------------------------------------------------------------------------------------
 # expert parallel (reference utils/groups.py:240-440)
-def create_expert_and_data_parallel(ep_size, group_name=None):
+def create_expert_and_data_parallel(ep_size, group_name=None, span_tp=None):
     """Split every data(-x-seq) parallel group into expert-parallel groups of ``ep_size``
-    consecutive ranks; expert-data-parallel groups join the ranks holding the same experts."""
+    consecutive ranks; expert-data-parallel groups join the ranks holding the same experts.
+
+    ``span_tp`` (tensor parallelism without expert TP; reference groups.py:240
+    ``_create_expert_and_data_parallel``, "E + D"): the groups are cut from the whole data x model
+    plane of a pipeline stage in rank order, so the ranks of one TP group hold DIFFERENT experts and
+    each processes its 1/tp share of the (TP-duplicated) tokens. Without it (the default, and expert
+    TP: groups.py:383 ``_create_expert_data_and_model_parallel``, "E + M + D") the groups stay
+    inside one TP rank's slice."""
     _ensure()
     name = group_name or f"ep_size_{ep_size}"
+    span = bool(span_tp) and _Registry.sizes["tp"] > 1
     if name in _Registry.expert:
+        if span_tp is not None and _Registry.expert_span.get(name, False) != span:
+            raise ValueError(f"expert group {name} already exists with span_tp={_Registry.expert_span.get(name)}: "
+                             "every MoE layer of one ep_size must agree on enable_expert_tensor_parallelism")
         return name
+    _Registry.expert_span[name] = span
     topo = _Registry.topo
     me = dist.get_rank()
     sizes = _Registry.sizes
     mine = [None, [me], None, [me]]
-    for p in range(sizes["pp"]):
-        for m in range(sizes["tp"]):
-            dp_ranks = sorted(topo.filter_match(pipe=p, model=m))
-            n = len(dp_ranks)
-            assert n % ep_size == 0, f"data-parallel size {n} not divisible by ep_size {ep_size}"
-            for i in range(0, n, ep_size):
-                lst = dp_ranks[i:i + ep_size]
-                g = dist.new_group(lst)
-                if me in lst:
-                    mine[0], mine[1] = g, lst
-            for j in range(ep_size):
-                lst = dp_ranks[j::ep_size]
-                g = dist.new_group(lst)
-                if me in lst:
-                    mine[2], mine[3] = g, lst
+    slices = [(p, None) for p in range(sizes["pp"])] if span else \
+        [(p, m) for p in range(sizes["pp"]) for m in range(sizes["tp"])]
+    for p, m in slices:
+        dp_ranks = sorted(topo.filter_match(pipe=p) if m is None else topo.filter_match(pipe=p, model=m))
+        n = len(dp_ranks)
+        assert n % ep_size == 0, f"data-parallel size {n} not divisible by ep_size {ep_size}"
+        for i in range(0, n, ep_size):
+            lst = dp_ranks[i:i + ep_size]
+            g = dist.new_group(lst)
+            if me in lst:
+                mine[0], mine[1] = g, lst
+        for j in range(ep_size):
+            lst = dp_ranks[j::ep_size]
+            g = dist.new_group(lst)
+            if me in lst:
+                mine[2], mine[3] = g, lst
     _Registry.expert[name] = tuple(mine)
     return name
 
@@ -252,7 +266,7 @@ def create_zero_param_parallel_group(size):
 
 def reset():
     _Registry.topo = None
-    _Registry.groups, _Registry.ranks, _Registry.expert = {}, {}, {}
+    _Registry.groups, _Registry.ranks, _Registry.expert, _Registry.expert_span = {}, {}, {}, {}
 
 
 # reference-style private aliases

@@ -90,7 +90,10 @@ def broadcast_coalesced(tensors, src, group, bucket_bytes):
 
 def _split_tp_replicated(model_parameters, tp):
     """Separate TP-sharded from TP-replicated parameters so the global gradient norm counts the
-    replicated ones once (their grads are identical on every TP rank)."""
+    replicated ones once (their grads are identical on every TP rank). Expert parameters count as
+    sharded: expert-TP shards differ per TP rank, and without expert TP the TP ranks hold
+    different experts (the EP group spans them)."""
+    from ..moe.utils import is_moe_param
     plist = list(model_parameters)
     if plist and isinstance(plist[0], dict):
         pgs = plist
@@ -98,8 +101,8 @@ def _split_tp_replicated(model_parameters, tp):
         pgs = [{"params": plist}]
     out = []
     for pg in pgs:
-        sharded = [p for p in pg["params"] if getattr(p, "tensor_model_parallel", False)]
-        repl = [p for p in pg["params"] if not getattr(p, "tensor_model_parallel", False)]
+        sharded = [p for p in pg["params"] if getattr(p, "tensor_model_parallel", False) or is_moe_param(p)]
+        repl = [p for p in pg["params"] if not (getattr(p, "tensor_model_parallel", False) or is_moe_param(p))]
         if sharded:
             out.append({**pg, "params": sharded})
         if repl:
@@ -352,6 +355,12 @@ class SXEEngine(nn.Module):
             # AutoTP training (reference engine.py:450-516 _configure_tensor_parallel)
             from ..module_inject.auto_tp import tp_model_init
             tp_model_init(model, tp, tp_group=groups.get_tensor_model_parallel_group())
+        # MoE groups (and expert-TP sharding) after AutoTP, before the broadcast: the engine owns
+        # the group layout (reference engine.py:1298-1312 set_deepspeed_parallelism)
+        from ..moe.layer import MoE
+        for m in model.modules():
+            if isinstance(m, MoE):
+                m.set_deepspeed_parallelism()
         if not zero_init:
             if dtype != torch.float32:
                 model.to(dtype)
@@ -965,7 +974,90 @@ class SXEEngine(nn.Module):
         prefix = "bf16_" if (self.bfloat16_enabled() and stage == 0) or isinstance(self.optimizer,
                                                                                      BF16_Optimizer) else ""
         optim = os.path.join(d, f"{prefix}zero_pp_rank_{dp}_mp_rank_{mp:02d}_optim_states.pt")
+        moe = self._moe_layers()
+        if moe and stage == 0:
+            # ZeRO-0 + MoE: the whole optimizer differs per expert-parallel rank (reference
+            # engine.py:2969 _get_optimizer_ckpt_name)
+            ep_rank = groups.get_expert_parallel_rank(moe[0][1].expert_group_name)
+            optim = os.path.join(d, f"expp_rank_{ep_rank}_mp_rank_{mp:02d}_optim_states.pt")
         return d, model, optim
+
+    # ------------------------------------------------------------------- MoE checkpoint layout
+    def _moe_layers(self):
+        from ..moe.layer import MoE
+        return [(n, m) for n, m in self.module.named_modules() if isinstance(m, MoE)]
+
+    @staticmethod
+    def _expert_ckpt_name(d, layer_id, expert_id, mp_rank):
+        """reference engine.py:2976 ``_get_expert_ckpt_name``: one file per (MoE layer, global
+        expert, model-parallel rank of the expert shard)."""
+        return os.path.join(d, f"layer_{layer_id}_expert_{expert_id}_mp_rank_{mp_rank:02d}_model_states.pt")
+
+    @staticmethod
+    def _expert_key_prefix(n_module):
+        return f"{n_module}.deepspeed_moe.experts." if n_module else "deepspeed_moe.experts."
+
+    def _split_expert_state(self, sd):
+        """Module state dict -> (non-expert dict, {(layer, global expert): per-expert dict}). Expert
+        keys carry GLOBAL expert ids (``...deepspeed_experts.<gid>.<param>``); the stacked weights
+        of GroupedSwiGLUExperts are split into per-expert slices under the same naming."""
+        from ..moe.experts import GroupedSwiGLUExperts
+        experts = {}
+        rest = dict(sd)
+        for layer_id, (n_module, m) in enumerate(self._moe_layers()):
+            pre = self._expert_key_prefix(n_module)
+            ep_rank = groups.get_expert_parallel_rank(m.expert_group_name)
+            nle = m.num_local_experts
+            grouped = isinstance(m.deepspeed_moe.experts, GroupedSwiGLUExperts)
+            for key in [k for k in rest if k.startswith(pre)]:
+                t = rest.pop(key)
+                sub = key[len(pre):]
+                if grouped:
+                    for i in range(nle):
+                        gid = ep_rank * nle + i
+                        experts.setdefault((layer_id, gid), {})[f"{pre}deepspeed_experts.{gid}.{sub}"] = \
+                            t[i].detach().clone()
+                else:  # deepspeed_experts.<local>.<param>
+                    _, local, tail = sub.split(".", 2)
+                    gid = ep_rank * nle + int(local)
+                    experts.setdefault((layer_id, gid), {})[f"{pre}deepspeed_experts.{gid}.{tail}"] = t.detach().clone()
+        return rest, experts
+
+    def _save_expert_files(self, d, experts):
+        """Every expert is written once: by expert-data-parallel rank 0 of its holders (reference
+        engine.py:3463-3510 _save_moe_checkpoint)."""
+        moe = self._moe_layers()
+        for (layer_id, gid), esd in experts.items():
+            m = moe[layer_id][1]
+            if groups.get_expert_data_parallel_rank(m.expert_group_name) != 0:
+                continue
+            self.checkpoint_engine.save(esd, self._expert_ckpt_name(d, layer_id, gid, m.expert_tp_rank))
+
+    def _load_expert_state(self, d):
+        """This rank's local experts from the per-expert files (global -> local ids; reference
+        engine.py:2840-2895 load_moe_state_dict)."""
+        from ..moe.experts import GroupedSwiGLUExperts
+        out = {}
+        for layer_id, (n_module, m) in enumerate(self._moe_layers()):
+            pre = self._expert_key_prefix(n_module)
+            ep_rank = groups.get_expert_parallel_rank(m.expert_group_name)
+            nle = m.num_local_experts
+            grouped = isinstance(m.deepspeed_moe.experts, GroupedSwiGLUExperts)
+            stacks = {}
+            for i in range(nle):
+                gid = ep_rank * nle + i
+                esd = self.checkpoint_engine.load(self._expert_ckpt_name(d, layer_id, gid, m.expert_tp_rank),
+                                                  map_location="cpu")
+                gpre = f"{pre}deepspeed_experts.{gid}."
+                for k, v in esd.items():
+                    tail = k[len(gpre):]
+                    if grouped:
+                        stacks.setdefault(tail, [None] * nle)[i] = v
+                    else:
+                        out[f"{pre}deepspeed_experts.{i}.{tail}"] = v
+            for tail, parts in stacks.items():
+                out[pre + tail] = torch.stack(parts)
+        return out
 
     def _tp_partitions(self):
         """AutoTP layers: {module name: split_dim / layout / full shape} (reference universal
@@ -1020,9 +1112,14 @@ class SXEEngine(nn.Module):
         names = self._param_names()
         stage = self.zero_optimization_stage()
         write_model = stage == 3 or groups.get_sequence_data_parallel_rank() == 0
+        module_sd = self.module_state_dict(exclude_frozen_parameters) if (write_model or stage < 3) else None
+        moe = self._moe_layers() if stage < 3 else []
+        if moe and module_sd is not None:
+            module_sd, experts = self._split_expert_state(module_sd)
+            self._save_expert_files(d, experts)
         if write_model:
             state = dict(
-                module=self.module_state_dict(exclude_frozen_parameters),
+                module=module_sd,
                 buffer_names=[n for n, _ in self.module.named_buffers()],
                 optimizer=None,
                 param_shapes=[{names[p]: tuple(p.shape) for p in pg["params_orig"]}
@@ -1041,9 +1138,17 @@ class SXEEngine(nn.Module):
             tp_parts = self._tp_partitions()
             if tp_parts:
                 state["tp_partitions"] = tp_parts  # checkpoint/reshape.py re-splits to another TP degree
+            if moe:
+                state["num_experts"] = [m.num_experts for _, m in moe]
             state.update(client_state)
             self.checkpoint_engine.save(state, model_path)
-        if self.optimizer is not None:
+        write_optim = True
+        if moe and stage == 0:
+            # identical on the EDP peers of this model-parallel slice: its first rank writes
+            name = moe[0][1].expert_group_name
+            peers = set(groups._Registry.expert[name][3]) & set(groups.group_ranks("seq_data"))
+            write_optim = self.global_rank == min(peers)
+        if self.optimizer is not None and write_optim:
             osd = self.optimizer.state_dict()
             if hasattr(self.optimizer, "unit_layout"):
                 osd["unit_layout"] = self.optimizer.unit_layout(names)
@@ -1094,6 +1199,8 @@ class SXEEngine(nn.Module):
         d, model_path, optim_path = self._ckpt_names(load_dir, tag)
         ce = self.checkpoint_engine
         state = ce.load(model_path, map_location="cpu")
+        if state.get("module") is not None and self.zero_optimization_stage() < 3 and self._moe_layers():
+            state["module"] = {**state["module"], **self._load_expert_state(d)}
         if state.get("module") is not None:
             if custom_load_fn is not None:
                 custom_load_fn(src=state["module"], dst=self.module)
@@ -1113,7 +1220,7 @@ class SXEEngine(nn.Module):
         dist.barrier()
         skip = {"module", "buffer_names", "optimizer", "param_shapes", "frozen_param_shapes", "lr_scheduler",
                 "sparse_tensor_module_names", "skipped_steps", "global_steps", "global_samples", "dp_world_size",
-                "mp_world_size", "ds_config", "ds_version"}
+                "mp_world_size", "ds_config", "ds_version", "num_experts", "tp_partitions"}
         client = {k: v for k, v in state.items() if k not in skip}
         return os.path.join(load_dir, str(tag)), client
 
@@ -1122,7 +1229,8 @@ class SXEEngine(nn.Module):
         from ..checkpoint.universal import load_universal_into_optimizer
         meta = load_universal_into_optimizer(self.optimizer, universal_dir, self._param_names())
         state = {}
-        files = sorted(f for f in os.listdir(universal_dir) if f.endswith("model_states.pt"))
+        files = sorted((f for f in os.listdir(universal_dir) if f.endswith("model_states.pt")),
+                       key=lambda f: (f.startswith("layer_"), f))  # not a per-expert file
         if files:
             from ..checkpoint.reference_format import load_file
             try:  # weights_only (reference-written model states map their classes to stand-ins)

@@ -55,7 +55,9 @@ class DataParallelOptimizer(ZeroOptimizerBase):
             plists = (list(split_into_units(dense, max(1, int(bucket_size)))) if dense else []) + [[p] for p in sparse]
             for i, plist in enumerate(plists):
                 u = FlatUnit(plist, 1, 0, plist[0].dtype, device, name=f"g{g}u{i}", index=i)
-                u.rgroup, u.rsize = rgroup, rsize
+                # expert grads are summed over their EDP group and divided by the DENSE dp size
+                # (reference engine.py:2713-2716 _reduce_expert_gradients, stage_1_and_2.py:1316)
+                u.rgroup, u.rsize, u.rdiv = rgroup, rsize, self.dp_size
                 u.sparse = getattr(plist[0], "_sxe_sparse", False)
                 u.sparse_parts = []
                 u.dense_seen = False
@@ -77,9 +79,14 @@ class DataParallelOptimizer(ZeroOptimizerBase):
             ep = eps.pop()
             if ep > 1:
                 self.extra_norm_group = groups.get_expert_parallel_group(moe_names[0])
+                # dense duplicates inside the EP group: its members that are data-parallel peers of
+                # this rank (all ep of them, or fewer when the EP group spans the TP ranks)
+                ep_ranks = set(groups.get_expert_parallel_ranks(moe_names[0]))
+                mine = set(dist.group_ranks(self.dp_group)) if self.dp_group is not None else {dist.get_rank()}
+                dup = max(1, len(ep_ranks & mine))
                 for pg in init_optimizer.param_groups:
                     if not pg.get("moe", False):
-                        pg["norm_weight"] = pg.get("norm_weight", 1.0) / ep
+                        pg["norm_weight"] = pg.get("norm_weight", 1.0) / dup
         if hasattr(self.optimizer, "set_segments"):  # layer-wise optimizers (LAMB) on flat masters
             for g, units in enumerate(self.units):
                 segs, base = [], 0
@@ -136,8 +143,8 @@ class DataParallelOptimizer(ZeroOptimizerBase):
         u.sparse_parts = []
         if u.rsize == 1:
             dense.index_add_(0, idx, val)
-            if self.sp_scale != 1.0:
-                dense.mul_(self.sp_scale)
+            if self.sp_scale != u.rdiv:
+                dense.mul_(self.sp_scale / u.rdiv)
             return
         n = torch.tensor([idx.numel()], dtype=torch.long, device=dense.device)
         ns = [torch.zeros_like(n) for _ in range(u.rsize)]
@@ -154,7 +161,7 @@ class DataParallelOptimizer(ZeroOptimizerBase):
         dist.all_gather_into_tensor(av.view(-1), pv.view(-1), group=u.rgroup)
         keep = torch.cat([torch.arange(r * m, r * m + ns[r], device=dense.device) for r in range(u.rsize)])
         dense.index_add_(0, ai[keep], av[keep])
-        dense.mul_(self.sp_scale / u.rsize)
+        dense.mul_(self.sp_scale / u.rdiv)
 
     def _allreduce_unit(self, u):
         if u.sparse and u.dense_seen and u.sparse_parts:
@@ -171,19 +178,24 @@ class DataParallelOptimizer(ZeroOptimizerBase):
             self._sparse_allreduce_unit(u)
             return
         # 1-bit optimizers past their warm-up synchronise compressed momentum themselves
-        if u.rsize == 1 or u.reduced or getattr(self.optimizer, "comm_active", False):
+        if u.reduced or getattr(self.optimizer, "comm_active", False):
             u.reduced = True
+            return
+        if u.rsize == 1:
+            u.reduced = True
+            if self.sp_scale != u.rdiv:  # an expert group of one rank still averages over dp
+                u.grad.mul_(self.sp_scale / u.rdiv)
             return
         u.reduced = True
         st = self.comm_stream
         if st is not None:
             st.wait_stream(torch.cuda.current_stream())
         with get_accelerator().stream(st):
-            if dist.get_backend() == "nccl" and self.sp_scale == 1.0:
+            if dist.get_backend() == "nccl" and self.sp_scale == 1.0 and u.rdiv == u.rsize:
                 dist.all_reduce(u.grad, op=dist.ReduceOp.AVG, group=u.rgroup)
             else:
                 dist.all_reduce(u.grad, group=u.rgroup)
-                u.grad.mul_(self.sp_scale / u.rsize)
+                u.grad.mul_(self.sp_scale / u.rdiv)
 
     def set_gradient_accumulation_boundary(self, flag):
         self.boundary = bool(flag)

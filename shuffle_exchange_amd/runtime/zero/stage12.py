@@ -83,6 +83,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                 gt = self._group_topo(pg)
                 u = FlatUnit(plist, gt.S, gt.offset, dtype, device, name=f"g{g}u{i}", index=i)
                 u.topo = gt
+                u.moe = bool(pg.get("moe", False))
                 if self.fp32_accum:
                     u.staging_dtype = torch.float32
                 units.append(u)
@@ -119,7 +120,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
     def _register_hooks(self):
         for p, u in self.param_unit.items():
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(u)))
-            if self.stage == 2 or u.topo.S == 1:
+            if (self.stage == 2 and u.topo.S > 1) or (u.topo.S == 1 and self._unit_scale(u) == 1.0):
                 # weight-grad GEMMs (ops/linear.py) write into the fp32 accumulator (S == 1) or the
                 # bf16 reduce-scatter staging slot (S > 1) directly
                 p._sxe_grad_target = self._grad_target
@@ -159,7 +160,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
             if unit.topo.S == 1:
                 i = unit.param_index[id(p)]
                 o, n = unit.offsets[i], unit.numels[i]
-                unit.grad[o:o + n].add_(p.grad.reshape(-1))
+                unit.grad[o:o + n].add_(p.grad.reshape(-1), alpha=self._unit_scale(unit))
                 unit.filled[i] = True
                 p.grad = None
                 return
@@ -173,7 +174,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         if unit.topo.S == 1:
             i = unit.param_index[id(p)]
             o, n = unit.offsets[i], unit.numels[i]
-            unit.grad[o:o + n].add_(p.grad.reshape(-1))
+            unit.grad[o:o + n].add_(p.grad.reshape(-1), alpha=self._unit_scale(unit))
         else:
             unit.stage_grad(p, p.grad)  # fp32 staging (staging_dtype), no reduce before the boundary
         p.grad = None
@@ -185,6 +186,14 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         for units in self.units:
             for u in units:
                 u.begin_backward()
+
+    def _unit_scale(self, u):
+        """Gradient averaging factor of a unit. Dense: the mean over its slice (x sp for sequence
+        parallelism). Expert units are SUMMED over their expert-data-parallel group and divided by
+        the dense data-parallel size, so the expert gradients do not depend on ep_size (reference
+        stage_1_and_2.py:1316 divides the whole bucket by the dp group size; engine.py:2713-2716) --
+        an EDP group of one rank (ep == dp) still averages over the dp ranks whose tokens it saw."""
+        return self.sp_scale / (self.topo.S if getattr(u, "moe", False) else u.topo.S)
 
     def _reduce_unit(self, u):
         st = u.staging
@@ -198,7 +207,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
             send = st if (self.comm_dtype is None or st.dtype == self.comm_dtype) else st.to(self.comm_dtype)
             out = torch.empty(u.chunk, dtype=send.dtype, device=send.device)
             dist.reduce_scatter_tensor(out, send, group=u.topo.slice_group)
-            u.grad.add_(out, alpha=self.sp_scale / u.topo.S)
+            u.grad.add_(out, alpha=self._unit_scale(u))
             if stream is not None:
                 st.record_stream(stream)
                 send.record_stream(stream)
@@ -225,7 +234,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                     for i, p in enumerate(u.params):
                         if p.grad is not None:
                             o, n = u.offsets[i], u.numels[i]
-                            u.grad[o:o + n].add_(p.grad.reshape(-1))
+                            u.grad[o:o + n].add_(p.grad.reshape(-1), alpha=self._unit_scale(u))
                             p.grad = None
                     continue
                 if u.pending > 0:

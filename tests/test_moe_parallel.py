@@ -1,0 +1,219 @@
+"""MoE under expert x tensor x data parallelism through the engine (gloo, CPU), checked against ONE
+process training the same Mixtral-tiny on the whole global batch.
+
+Covered (reference deepspeed/moe/sharded_moe.py:615-665 token drop/gather, groups.py:240 / :383
+E+D and E+M+D group layouts, stage_1_and_2.py:1316 / engine.py:2713 expert-gradient averaging by
+the DENSE data-parallel size, engine.py:2840-2895 / 3463-3560 per-expert checkpoint files):
+  * EP=2 over dp=2 (expert-data-parallel groups of ONE rank: the gradient must still be divided
+    by dp), EP=2 over dp=4, ZeRO-0/1/2;
+  * TP=2 without expert TP (the EP group spans the TP ranks, each rank keeps 1/tp of the capacity);
+  * TP=2 with expert TP (gate/up columns and down rows sharded, tokens all-gathered over TP);
+  * gradient clipping: the global norm equals the single-process norm;
+  * save -> load round trips continue bit-identically; ``layer_<l>_expert_<g>_mp_rank_<m>``
+    files; load_module_only restores every expert.
+Routing is made parallelism-invariant: greedy top-2, capacity above the token count (no drops)
+and no router aux loss (its value depends on how tokens are split over ranks)."""
+import os
+
+import pytest
+import torch
+
+from .dist_utils import run_dist
+
+MBS, SEQ, LR = 2, 16, 0.5
+
+
+def _mixtral(ep, expert_tp=False, seed=0):
+    from shuffle_exchange_amd.models.mixtral import MixtralForCausalLM, mixtral_config
+    torch.manual_seed(seed)
+    cfg = mixtral_config("mixtral-tiny", ep_size=ep, router_aux_loss_coef=0.0, capacity_factor=4.0,
+                         min_capacity=256, top2_2nd_expert_sampling=False,
+                         enable_expert_tensor_parallelism=expert_tp)
+    return MixtralForCausalLM(cfg), cfg
+
+
+def _batches(dp, steps, vocab):
+    g = torch.Generator().manual_seed(3)
+    return [torch.randint(0, vocab, (dp * MBS, SEQ), generator=g) for _ in range(steps)]
+
+
+def _load_from_reference(model, ref, ep, tp, expert_tp):
+    """Same weights as the single-process reference: dense by name, this EP rank's experts by
+    their global ids (the engine's AutoTP / expert-TP sharding then cuts them)."""
+    from shuffle_exchange_amd.parallel import groups
+    groups.initialize(tensor_parallel_size=tp)
+    name = groups.create_expert_and_data_parallel(ep, f"ep_size_{ep}", span_tp=tp > 1 and not expert_tp)
+    epr = groups.get_expert_parallel_rank(name)
+    rsd = ref.state_dict()
+    with torch.no_grad():
+        for n, p in model.named_parameters():
+            v = rsd[n]
+            if v.shape != p.shape:  # stacked experts [E, ...] -> this rank's [E/ep, ...]
+                nle = p.shape[0]
+                v = v[epr * nle:(epr + 1) * nle]
+            p.copy_(v)
+
+
+def _full_state(eng, model, tp, expert_tp):
+    """Unsharded state dict: AutoTP linears gathered over TP, experts over TP (expert TP) and EP."""
+    from shuffle_exchange_amd import comm
+    from shuffle_exchange_amd.module_inject.auto_tp import gather_tp_state_dict
+    from shuffle_exchange_amd.moe.layer import MoE
+    from shuffle_exchange_amd.parallel import groups
+    sd = gather_tp_state_dict(model)
+    for n_mod, m in model.named_modules():
+        if not isinstance(m, MoE):
+            continue
+        ex = m.deepspeed_moe.experts
+        for pname in ("w_gate_up", "w_down"):
+            t = getattr(ex, pname).detach().float().contiguous()
+            if expert_tp and tp > 1:
+                parts = [torch.empty_like(t) for _ in range(tp)]
+                comm.all_gather(parts, t, group=groups.get_tensor_model_parallel_group())
+                if pname == "w_gate_up":
+                    s = t.shape[-1] // 2
+                    t = torch.cat([q[..., :s] for q in parts] + [q[..., s:] for q in parts], -1)
+                else:
+                    t = torch.cat(parts, 1)
+            ep_g = m.deepspeed_moe.ep_group
+            epn = comm.get_world_size(ep_g) if ep_g is not None else 1
+            if epn > 1:
+                parts = [torch.empty_like(t) for _ in range(epn)]
+                comm.all_gather(parts, t.contiguous(), group=ep_g)
+                t = torch.cat(parts, 0)
+            sd[f"{n_mod}.deepspeed_moe.experts.{pname}"] = t
+    return {k: v.float() for k, v in sd.items()}
+
+
+def _ds(tp, stage, clip):
+    return {"train_micro_batch_size_per_gpu": MBS, "tensor_parallel": {"autotp_size": tp},
+            "zero_optimization": {"stage": stage}, "gradient_clipping": clip,
+            "optimizer": {"type": "SGD", "params": {"lr": LR}}}
+
+
+def _run(eng, rank_batches):
+    losses = []
+    for local in rank_batches:
+        loss = eng(local, labels=local)
+        eng.backward(loss)
+        eng.step()
+        losses.append(float(loss.detach()))
+    return losses
+
+
+def _local(batches):
+    from shuffle_exchange_amd.parallel import groups
+    dpr = groups.get_data_parallel_rank()
+    return [b[dpr * MBS:(dpr + 1) * MBS] for b in batches]
+
+
+def _case_train(rank, world, tp, ep, expert_tp, stage, steps, clip):
+    import shuffle_exchange_amd as sxe
+    ref, cfg = _mixtral(1)
+    model, _ = _mixtral(ep, expert_tp, seed=11)
+    _load_from_reference(model, ref, ep, tp, expert_tp)
+    eng, _, _, _ = sxe.initialize(model=model, config=_ds(tp, stage, clip))
+    batches = _batches(world // tp, steps, cfg.vocab_size)
+    losses = _run(eng, _local(batches))
+    norm = eng.get_global_grad_norm()
+    return {"losses": losses, "sd": _full_state(eng, model, tp, expert_tp),
+            "norm": float(norm) if norm is not None else None}
+
+
+def _reference(dp, steps, clip):
+    model, cfg = _mixtral(1)
+    opt = torch.optim.SGD(model.parameters(), lr=LR)
+    losses, norm = [], None
+    for b in _batches(dp, steps, cfg.vocab_size):
+        loss = model(b, labels=b)
+        opt.zero_grad()
+        loss.backward()
+        norm = float(torch.nn.utils.clip_grad_norm_(model.parameters(), clip if clip > 0 else 1e30))
+        opt.step()
+        losses.append(float(loss.detach()))
+    return losses, {k: v.float() for k, v in model.state_dict().items()}, norm
+
+
+CASES = [  # world, tp, ep, expert_tp, stage, clip
+    (2, 1, 2, False, 0, 0.0), (2, 1, 2, False, 1, 0.0), (2, 1, 2, False, 2, 1.0),
+    (4, 1, 2, False, 2, 1.0),
+    (2, 2, 2, False, 1, 1.0), (2, 2, 1, True, 2, 1.0),
+    (4, 2, 2, False, 2, 0.0), (4, 2, 2, True, 1, 1.0), (4, 2, 2, True, 0, 1.0), (4, 2, 2, False, 0, 1.0),
+]
+
+
+@pytest.mark.parametrize("world,tp,ep,expert_tp,stage,clip", CASES)
+def test_moe_parallel_matches_single_process(world, tp, ep, expert_tp, stage, clip):
+    steps = 2
+    res = run_dist(_case_train, world, tp, ep, expert_tp, stage, steps, clip)
+    ref_losses, ref_sd, ref_norm = _reference(world // tp, steps, clip)
+    # each rank reports its data-parallel shard's loss (TP peers the same one): the mean over
+    # ranks is the global-batch loss
+    mean = [sum(r["losses"][t] for r in res) / len(res) for t in range(steps)]
+    for a, b in zip(mean, ref_losses):
+        assert a == pytest.approx(b, rel=1e-5, abs=1e-6)
+    for r in res:
+        if clip > 0:
+            assert r["norm"] == pytest.approx(ref_norm, rel=1e-4)
+        for k, v in ref_sd.items():
+            got = r["sd"][k]
+            assert got.shape == v.shape, (k, got.shape, v.shape)
+            d = (got - v).abs().max().item()
+            assert d <= 2e-5 * max(1.0, v.abs().max().item()), f"{k}: {d}"
+
+
+# ---------------------------------------------------------------------------------- checkpoints
+def _case_ckpt(rank, world, tp, ep, expert_tp, stage, tmpdir):
+    import shuffle_exchange_amd as sxe
+    ds = _ds(tp, stage, 1.0)
+    ds["optimizer"] = {"type": "AdamW", "params": {"lr": 5e-3}}
+    model, cfg = _mixtral(ep, expert_tp, seed=0)
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    batches = _local(_batches(world // tp, 4, cfg.vocab_size))
+    _run(eng, batches[:2])
+    eng.save_checkpoint(tmpdir)
+    saved = {n: p.detach().clone() for n, p in model.named_parameters()}
+    cont = _run(eng, batches[2:])
+    after = {n: p.detach().clone() for n, p in model.named_parameters()}
+    model2, _ = _mixtral(ep, expert_tp, seed=123)  # different init: everything comes from the files
+    eng2, _, _, _ = sxe.initialize(model=model2, config=ds)
+    eng2.load_checkpoint(tmpdir)
+    restored = all(torch.equal(p, saved[n]) for n, p in model2.named_parameters())
+    resumed = _run(eng2, batches[2:])
+    same_after = all(torch.equal(p, after[n]) for n, p in model2.named_parameters())
+    model3, _ = _mixtral(ep, expert_tp, seed=77)
+    eng3, _, _, _ = sxe.initialize(model=model3, config=ds)
+    eng3.load_checkpoint(tmpdir, load_module_only=True)
+    module_only = all(torch.equal(p, saved[n]) for n, p in model3.named_parameters())
+    files = sorted(os.listdir(os.path.join(tmpdir, "global_step2")))
+    return {"cont": cont, "resumed": resumed, "restored": restored, "same_after": same_after,
+            "module_only": module_only, "files": files}
+
+
+@pytest.mark.parametrize("world,tp,ep,expert_tp,stage", [
+    (2, 1, 2, False, 0), (2, 1, 2, False, 1), (2, 1, 2, False, 2),
+    (4, 2, 2, True, 1), (4, 2, 2, False, 2), (4, 2, 2, True, 0),
+])
+def test_moe_checkpoint_round_trip(tmp_path, world, tp, ep, expert_tp, stage):
+    res = run_dist(_case_ckpt, world, tp, ep, expert_tp, stage, str(tmp_path))
+    for r in res:
+        assert r["restored"] and r["module_only"]
+        assert r["cont"] == r["resumed"]
+        assert r["same_after"]
+    files = res[0]["files"]
+    n_layers, E = 2, 4
+    mps = range(tp) if expert_tp else [0]
+    for layer in range(n_layers):
+        for e in range(E):
+            for m in mps:
+                assert f"layer_{layer}_expert_{e}_mp_rank_{m:02d}_model_states.pt" in files, files
+    if stage == 0:
+        for e in range(ep):
+            for m in range(tp):
+                assert f"expp_rank_{e}_mp_rank_{m:02d}_optim_states.pt" in files, files
+    # the non-expert model file holds no expert weights
+    import torch as _t
+    sd = _t.load(os.path.join(str(tmp_path), "global_step2", "mp_rank_00_model_states.pt"), map_location="cpu",
+                 weights_only=False)
+    assert not any(".deepspeed_moe.experts." in k for k in sd["module"])
+    assert sd["num_experts"] == [E] * n_layers
