@@ -17,5 +17,11 @@ def build_hf_engine(path_or_model, engine_config: RaggedInferenceEngineConfig = 
     """``weight_quant='fp8'``: row-scaled e4m3 projection / LM-head weights (ops/fp_quantizer.FP8Weight)."""
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
-    model = load_hf_decoder(path_or_model, dtype=dtype, device=device, weight_quant=weight_quant)
+    tp = int(((engine_config.tensor_parallel if engine_config is not None else None) or {}).get("tp_size", 1))
+    tp_group = None
+    if tp > 1:  # every rank loads the checkpoint and keeps its shard (reference sharding/*.py)
+        from .engine_v2 import _tp_group
+        tp_group = _tp_group(tp)
+    model = load_hf_decoder(path_or_model, dtype=dtype, device=device, weight_quant=weight_quant, tp_group=tp_group,
+                            tp_size=tp)
     return InferenceEngineV2(model, engine_config)

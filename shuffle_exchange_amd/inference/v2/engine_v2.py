@@ -65,19 +65,27 @@ class RaggedInferenceEngineConfig:
     implementations: Optional[dict] = None  # pin registry implementations by interface (modules/registry.py)
 
 
+_TP_GROUPS = {}
+
+
 def _tp_group(tp):
-    """Consecutive blocks of `tp` ranks (the ranks of one node share one xGMI mesh)."""
+    """Consecutive blocks of `tp` ranks (the ranks of one node share one xGMI mesh); created once
+    per (tp, world) so build_hf_engine and the engine share it."""
     from ... import comm as dist
     assert dist.is_initialized(), "tensor_parallel.tp_size > 1 needs torch.distributed"
     world, me = dist.get_world_size(), dist.get_rank()
     assert world % tp == 0, f"world size {world} must be a multiple of tp_size {tp}"
     if tp == world:
         return None  # the world group
+    key = (tp, world, id(dist.get_world_group()) if hasattr(dist, "get_world_group") else 0)
+    if key in _TP_GROUPS:
+        return _TP_GROUPS[key]
     mine = None
     for i in range(0, world, tp):
         g = dist.new_group(list(range(i, i + tp)))  # every rank creates every group
         if i <= me < i + tp:
             mine = g
+    _TP_GROUPS[key] = mine
     return mine
 
 

@@ -14,14 +14,16 @@ def ragged_model_for(model, weight_quant=None, tp_group=None, tp_size=1, pins=No
     """Pick the ragged implementation for a model object (``weight_quant='fp8'``: row-scaled e4m3
     projection / LM-head weights for the decode GEMMs; ``tp_group``: tensor-parallel sharding)."""
     if isinstance(model, (RaggedDecoder, RaggedLlama)):
+        if getattr(model, "tp", 1) != tp_size:
+            raise ValueError(f"model was sharded for tp={getattr(model, 'tp', 1)}, engine tp_size={tp_size}: "
+                             "build it with the same tensor_parallel config (build_hf_engine does)")
         return model
-    if tp_size > 1 and not (hasattr(model, "layers") and hasattr(model, "embed_tokens")):
-        raise NotImplementedError("ragged tensor parallelism is implemented for the framework's Llama family")
     if hasattr(model, "config") and hasattr(model.config, "model_type") and hasattr(model.config, "to_dict"):
         p = next(model.parameters())
         dtype = p.dtype if p.dtype in (__import__("torch").bfloat16, __import__("torch").float16,
                                        __import__("torch").float32) else None
-        return load_hf_decoder(model, dtype=dtype, device=p.device, weight_quant=weight_quant)
+        return load_hf_decoder(model, dtype=dtype, device=p.device, weight_quant=weight_quant, tp_group=tp_group,
+                               tp_size=tp_size)
     if hasattr(model, "layers") and hasattr(model.layers[0], "self_attn") and hasattr(model, "embed_tokens"):
         return RaggedLlama(model, weight_quant=weight_quant, tp_group=tp_group, tp_size=tp_size, pins=pins)
     raise NotImplementedError(f"no ragged inference implementation for {type(model).__name__}")

@@ -420,6 +420,78 @@ def dropless_moe(x, router_w, e_gu, e_down, top_k, norm_topk, act="silu"):
     return out
 
 
+# ------------------------------------------------------------------------ tensor parallelism
+def shard_decoder_weights(spec, W, t, r):
+    """This TP rank's share of converted weights (reference inference/v2/model_implementations/
+    sharding/{qkv,attn_out,mlp,moe,unembed}.py): q heads and their kv heads (kv heads replicated
+    when t exceeds their count), o_proj / down / fc2 input columns (row-parallel: partial sums,
+    biases added once after the all-reduce), gate|up / fc1 output rows, every expert's FFN
+    columns (expert TP: routing stays replicated), vocab rows of the LM head (padded to an equal
+    split; logits are all-gathered). Returns (weights, local q heads, local kv heads)."""
+    nq, nkv, D = spec.nq, spec.nkv, spec.head_dim
+    assert nq % t == 0, f"query heads ({nq}) must divide by tp_size ({t})"
+    assert nkv % t == 0 or t % nkv == 0, f"kv heads ({nkv}) and tp_size ({t}) must divide one another"
+    lq, q0 = nq // t, r * (nq // t)
+    if nkv % t == 0:
+        lkv, kv0 = nkv // t, r * (nkv // t)
+    else:  # fewer kv heads than ranks: each rank keeps the kv head its q heads attend to
+        lkv, kv0 = 1, q0 // (nq // nkv)
+
+    def qkv(w):
+        return torch.cat([w[q0 * D:(q0 + lq) * D], w[(nq + kv0) * D:(nq + kv0 + lkv) * D],
+                          w[(nq + nkv + kv0) * D:(nq + nkv + kv0 + lkv) * D]]).contiguous()
+
+    def part(n):
+        assert n % t == 0, f"FFN width {n} must divide by tp_size {t}"
+        return r * (n // t), n // t
+
+    def gate_up(w, dim):  # [gate | up] halves along `dim`: this rank's slice of each
+        n = w.shape[dim] // 2
+        a, c = part(n)
+        return torch.cat([w.narrow(dim, a, c), w.narrow(dim, n + a, c)], dim).contiguous()
+
+    out = {k: v for k, v in W.items() if k != "layers"}
+    out["layers"] = []
+    for L in W["layers"]:
+        M = dict(L)
+        M["qkv_w"] = qkv(L["qkv_w"])
+        if L.get("qkv_b") is not None:
+            M["qkv_b"] = qkv(L["qkv_b"])
+        M["o_w"] = L["o_w"][:, q0 * D:(q0 + lq) * D].contiguous()
+        if "gu_w" in L:
+            M["gu_w"] = gate_up(L["gu_w"], 0)
+            a, c = part(L["down_w"].shape[1])
+            M["down_w"] = L["down_w"][:, a:a + c].contiguous()
+        if "fc1_w" in L:
+            a, c = part(L["fc1_w"].shape[0])
+            M["fc1_w"] = L["fc1_w"][a:a + c].contiguous()
+            if L.get("fc1_b") is not None:
+                M["fc1_b"] = L["fc1_b"][a:a + c].contiguous()
+            M["fc2_w"] = L["fc2_w"][:, a:a + c].contiguous()
+        if "e_gu" in L:
+            M["e_gu"] = gate_up(L["e_gu"], 1)
+            a, c = part(L["e_down"].shape[2])
+            M["e_down"] = L["e_down"][:, :, a:a + c].contiguous()
+        if "sh_gu" in L:
+            M["sh_gu"] = gate_up(L["sh_gu"], 0)
+            a, c = part(L["sh_down"].shape[1])
+            M["sh_down"] = L["sh_down"][:, a:a + c].contiguous()
+        out["layers"].append(M)
+    V = W["lm_head"].shape[0]
+    vs = -(-V // t)
+    lo, hi = min(r * vs, V), min((r + 1) * vs, V)
+
+    def vrows(w):
+        w = w[lo:hi]
+        if hi - lo < vs:  # pad the last shard: every rank gathers the same size
+            w = torch.cat([w, w.new_zeros(vs - (hi - lo), *w.shape[1:])])
+        return w.contiguous()
+    out["lm_head"] = vrows(W["lm_head"])
+    if W.get("lm_head_b") is not None:
+        out["lm_head_b"] = vrows(W["lm_head_b"])
+    return out, lq, lkv
+
+
 # --------------------------------------------------------------------------------- the decoder
 class RaggedDecoder:
     """Engine-facing model (InferenceEngineV2 protocol: num_layers / nkv / head_dim / dtype /
@@ -427,9 +499,17 @@ class RaggedDecoder:
 
     QUANT_KEYS = ("qkv_w", "o_w", "gu_w", "down_w", "fc1_w", "fc2_w", "sh_gu", "sh_down")
 
-    def __init__(self, spec: DecoderSpec, weights, dtype=torch.bfloat16, device=None, weight_quant=None):
+    def __init__(self, spec: DecoderSpec, weights, dtype=torch.bfloat16, device=None, weight_quant=None,
+                 tp_group=None, tp_size=1):
         self.spec = spec
         device = torch.device(device) if device is not None else torch.device("cpu")
+        from .... import comm as dist
+        self.tp, self.tp_group = int(tp_size), tp_group  # tp_group None with tp_size > 1: the world
+        self.tp_rank = dist.get_rank(tp_group) if self.tp > 1 else 0
+        self.nq, self.nkv = spec.nq, spec.nkv
+        if self.tp > 1:
+            assert dist.get_world_size(tp_group) == self.tp, "tp_group size != tp_size"
+            weights, self.nq, self.nkv = shard_decoder_weights(spec, weights, self.tp, self.tp_rank)
 
         def mv(t):
             return t.to(device=device, dtype=dtype).contiguous() if torch.is_tensor(t) else t
@@ -445,7 +525,7 @@ class RaggedDecoder:
                         L[k] = quantized_weight(L[k], weight_quant)
             self.w["lm_head"] = quantized_weight(self.w["lm_head"], weight_quant)
         self.weight_quant = weight_quant
-        self.num_layers, self.nq, self.nkv, self.head_dim = spec.n_layers, spec.nq, spec.nkv, spec.head_dim
+        self.num_layers, self.head_dim = spec.n_layers, spec.head_dim
         self.vocab_size = spec.vocab_size
         self._dtype, self._device = dtype, device
         self.rope = _rope_cache(spec, device) if spec.rotary_dim else None
@@ -472,18 +552,39 @@ class RaggedDecoder:
             return rms_norm(x, w, self.spec.norm_eps, residual=residual)
         return layer_norm(x, w, b, self.spec.norm_eps, residual=residual)
 
-    def _attn(self, a, L, li, batch, kv_cache):
+    def _reduce(self, y, *biases):
+        """Row-parallel epilogue: sum the TP ranks' partial products over xGMI, then add the
+        (replicated) output biases once."""
+        if self.tp > 1:
+            from .... import comm as dist
+            y = y.contiguous()
+            dist.all_reduce(y, group=self.tp_group)
+        for b in biases:
+            if b is not None:
+                y = y + b
+        return y
+
+    def _attn(self, a, L, li, batch, kv_cache, reduce=True):
         s, T = self.spec, a.shape[0]
-        nq, nkv, D = s.nq, s.nkv, s.head_dim
+        nq, nkv, D = self.nq, self.nkv, s.head_dim
         qkv = linear(a, L["qkv_w"], L.get("qkv_b")).view(T, nq + 2 * nkv, D)
         if self.rope is not None:
             apply_rope_tokens_(qkv, self.rope, nq + nkv, batch.positions, rot_dim=s.rotary_dim)
         kv_layer = kv_cache.layer(li)
         kv_cache_append(qkv, kv_layer, batch.slots, nq, nkv)
         o = ragged_attention(qkv, kv_layer, batch, nq, nkv, D, self.scale, s.sliding_window)
-        return linear(o.reshape(T, nq * D), L["o_w"], L.get("o_b"))
+        if self.tp == 1:
+            return linear(o.reshape(T, nq * D), L["o_w"], L.get("o_b"))
+        y = linear(o.reshape(T, nq * D), L["o_w"])
+        return self._reduce(y, L.get("o_b")) if reduce else y
 
-    def _mlp(self, m, L):
+    def _mlp(self, m, L, reduce=True):
+        if self.tp > 1:  # partial sums of this rank's FFN / expert columns
+            y = self._mlp_partial(m, L)
+            return self._reduce(y, L.get("fc2_b")) if reduce else y
+        return self._mlp_partial(m, L, L.get("fc2_b"))
+
+    def _mlp_partial(self, m, L, fc2_b=None):
         s = self.spec
         if "router" in L:
             out = dropless_moe(m, L["router"], L["e_gu"], L["e_down"], s.top_k, s.norm_topk, s.act)
@@ -494,7 +595,7 @@ class RaggedDecoder:
         if "gu_w" in L:
             return linear(gated_act(linear(m, L["gu_w"]), s.act), L["down_w"])
         h = bias_act(linear(m, L["fc1_w"]), L.get("fc1_b"), ACT[s.act])
-        return linear(h, L["fc2_w"], L.get("fc2_b"))
+        return linear(h, L["fc2_w"], fc2_b)
 
     @torch.no_grad()
     def forward(self, batch, kv_cache):
@@ -508,7 +609,11 @@ class RaggedDecoder:
                 h = x if res is None else x + res
                 a = self._norm(h, L["ln1_w"], L.get("ln1_b"))
                 m = self._norm(h, L["ln2_w"], L.get("ln2_b")) if s.two_norms else a
-                x, res = self._attn(a, L, li, batch, kv_cache) + self._mlp(m, L), h
+                if self.tp > 1:  # attention and MLP partials share ONE all-reduce
+                    y = self._attn(a, L, li, batch, kv_cache, reduce=False) + self._mlp(m, L, reduce=False)
+                    x, res = self._reduce(y, L.get("o_b"), L.get("fc2_b")), h
+                else:
+                    x, res = self._attn(a, L, li, batch, kv_cache) + self._mlp(m, L), h
             else:
                 a, h = (self._norm(x, L["ln1_w"], L.get("ln1_b")), x) if res is None else \
                     self._norm(x, L["ln1_w"], L.get("ln1_b"), residual=res)
@@ -518,12 +623,20 @@ class RaggedDecoder:
         last = batch.last_idx
         h = gather_last(x, last, res)  # one HIP gather with the residual add fused
         h = self._norm(h, W["final_w"], W.get("final_b"))
-        return linear(h, W["lm_head"], W.get("lm_head_b")).float()
+        logits = linear(h, W["lm_head"], W.get("lm_head_b")).float()
+        if self.tp > 1:  # vocab-parallel head: gather every rank's logit columns
+            from .... import comm as dist
+            full = torch.empty(self.tp * logits.shape[0], logits.shape[1], dtype=logits.dtype, device=logits.device)
+            dist.all_gather_into_tensor(full, logits.contiguous(), group=self.tp_group)
+            logits = full.view(self.tp, -1, logits.shape[1]).permute(1, 0, 2).reshape(logits.shape[0], -1)
+            logits = logits[:, :self.vocab_size]
+        return logits
 
 
-def load_hf_decoder(model_or_path, dtype=torch.bfloat16, device=None, weight_quant=None):
+def load_hf_decoder(model_or_path, dtype=torch.bfloat16, device=None, weight_quant=None, tp_group=None, tp_size=1):
     """A transformers model instance or a local checkpoint directory (config.json + safetensors /
-    pytorch_model*.bin, loaded without executing pickled code) -> RaggedDecoder."""
+    pytorch_model*.bin, loaded without executing pickled code) -> RaggedDecoder (this rank's
+    tensor-parallel shard when ``tp_size > 1``)."""
     if isinstance(model_or_path, (str, os.PathLike)):
         with open(os.path.join(model_or_path, "config.json")) as f:
             cfg = json.load(f)
@@ -532,4 +645,5 @@ def load_hf_decoder(model_or_path, dtype=torch.bfloat16, device=None, weight_qua
         cfg = model_or_path.config.to_dict()
         sd = {k: v.detach() for k, v in model_or_path.state_dict().items()}
     spec = spec_from_hf_config(cfg)
-    return RaggedDecoder(spec, convert_hf_weights(spec, sd, cfg), dtype=dtype, device=device, weight_quant=weight_quant)
+    return RaggedDecoder(spec, convert_hf_weights(spec, sd, cfg), dtype=dtype, device=device, weight_quant=weight_quant,
+                         tp_group=tp_group, tp_size=tp_size)

@@ -19,7 +19,8 @@ attention output and MLP down projections, :191 all-gather of the vocab-parallel
 holds q heads / kv heads / FFN columns / vocab rows of its 1/t share (kv heads replicated when t
 exceeds their count), its KV cache holds only its kv heads, and per layer exactly two all-reduces
 (o_proj, down_proj) plus one logits all-gather per forward cross xGMI. The embedding and norms stay
-replicated. Dense models only (experts run locally, ``ep_size == 1``).
+replicated. MoE layers shard every expert's FFN columns (routing replicated, one all-reduce after
+the experts); ``weight_quant`` quantizes each rank's slices.
 """
 import os
 
@@ -56,13 +57,23 @@ class _TPShards:
             v = w[(nq + nkv + kv0) * D:(nq + nkv + kv0 + self.nkv) * D]
             d = {"qkv": torch.cat([q, k, v]).contiguous(),
                  "o": a.o_proj.weight[:, q0 * D:(q0 + self.nq) * D].contiguous()}
-            mlp = layer.mlp
-            inter = mlp.gate_up_proj.weight.shape[0] // 2
-            assert inter % t == 0, f"intermediate size ({inter}) must divide by tp_size ({t})"
-            c = inter // t
-            gu = mlp.gate_up_proj.weight
-            d["gu"] = torch.cat([gu[r * c:(r + 1) * c], gu[inter + r * c:inter + (r + 1) * c]]).contiguous()
-            d["down"] = mlp.down_proj.weight[:, r * c:(r + 1) * c].contiguous()
+            if hasattr(layer, "mlp"):
+                mlp = layer.mlp
+                inter = mlp.gate_up_proj.weight.shape[0] // 2
+                assert inter % t == 0, f"intermediate size ({inter}) must divide by tp_size ({t})"
+                c = inter // t
+                gu = mlp.gate_up_proj.weight
+                d["gu"] = torch.cat([gu[r * c:(r + 1) * c], gu[inter + r * c:inter + (r + 1) * c]]).contiguous()
+                d["down"] = mlp.down_proj.weight[:, r * c:(r + 1) * c].contiguous()
+            else:  # MoE: every expert's FFN columns (reference sharding/moe.py); routing replicated
+                moe = (layer.block_sparse_moe if hasattr(layer, "block_sparse_moe") else layer.moe).deepspeed_moe
+                ex = moe.experts
+                inter = ex.w_down.shape[1]
+                assert inter % t == 0, f"expert intermediate size ({inter}) must divide by tp_size ({t})"
+                c = inter // t
+                w = ex.w_gate_up  # [E, H, 2I]: x @ w
+                d["e_gu"] = torch.cat([w[..., r * c:(r + 1) * c], w[..., inter + r * c:inter + (r + 1) * c]], -1).contiguous()
+                d["e_down"] = ex.w_down[:, r * c:(r + 1) * c].contiguous()
             self.layers.append(d)
         V = model.lm_head.weight.shape[0]
         self.vshard = -(-V // t)
@@ -87,21 +98,18 @@ class RaggedLlama:
         self.tp_rank = dist.get_rank(tp_group) if self.tp > 1 else 0
         p0 = next(model.parameters())
         dev = p0.device.type
-        if weight_quant:
+        self._weight_quant, self._pins = weight_quant, pins
+        if weight_quant and self.tp == 1:
             # linear implementations from the registry (modules/heuristics.py): quantized
             # weight-only GEMMs for decode-sized inputs, the bf16 weight on hipBLASLt otherwise
-            def lin(mod):
-                w = mod.weight
-                return H.instantiate_linear(H.LinearConfig(w.shape[1], w.shape[0], w.dtype, weight_quant, dev), w,
-                                            getattr(mod, "bias", None), pins)
             self.qw = []
             for layer in model.layers:
-                d = {"qkv": lin(layer.self_attn.qkv_proj), "o": lin(layer.self_attn.o_proj)}
+                d = {"qkv": self._lin(layer.self_attn.qkv_proj.weight), "o": self._lin(layer.self_attn.o_proj.weight)}
                 if hasattr(layer, "mlp"):
-                    d["gu"] = lin(layer.mlp.gate_up_proj)
-                    d["down"] = lin(layer.mlp.down_proj)
+                    d["gu"] = self._lin(layer.mlp.gate_up_proj.weight)
+                    d["down"] = self._lin(layer.mlp.down_proj.weight)
                 self.qw.append(d)
-            self.qhead = lin(model.lm_head)
+            self.qhead = self._lin(model.lm_head.weight)
         self.cfg = model.cfg
         self.is_moe = hasattr(model.layers[0], "block_sparse_moe") or hasattr(model.layers[0], "moe")
         a0 = model.layers[0].self_attn
@@ -124,19 +132,29 @@ class RaggedLlama:
         self.vocab_size = self.cfg.vocab_size
         self.tps = None
         if self.tp > 1:
-            if self.is_moe:
-                raise NotImplementedError("ragged tensor parallelism covers dense Llama-family models")
-            if weight_quant:
-                raise NotImplementedError("weight_quant with tensor_parallel")
             self._full_heads = (self.nq, self.nkv)
-            self.tps = _TPShards(model, self.tp, self.tp_rank, self.nq, self.nkv, self.head_dim)
+            self._make_shards()
             self.nq, self.nkv = self.tps.nq, self.tps.nkv
+            if self.qw is not None:
+                self.implementations["linear"] = self.qhead.impl_name
+
+    def _lin(self, w, bias=None):
+        from ..modules import heuristics as H
+        return H.instantiate_linear(H.LinearConfig(w.shape[1], w.shape[0], w.dtype, self._weight_quant, w.device.type),
+                                    w, bias, self._pins)
+
+    def _make_shards(self):
+        self.tps = _TPShards(self.model, self.tp, self.tp_rank, *self._full_heads, self.head_dim)
+        if self._weight_quant:  # quantize this rank's slices (row scales are per output row)
+            self.qw = [{k: self._lin(v) for k, v in d.items() if k in ("qkv", "o", "gu", "down")}
+                       for d in self.tps.layers]
+            self.qhead = self._lin(self.tps.head)
 
     def refresh_shards(self):
         """Re-slice the tensor-parallel shards from the (updated) module weights -- the hybrid
         engine calls this before each generation, after training steps changed the weights."""
         if self.tps is not None:
-            self.tps = _TPShards(self.model, self.tp, self.tp_rank, *self._full_heads, self.head_dim)
+            self._make_shards()
 
     @property
     def device(self):
@@ -184,7 +202,10 @@ class RaggedLlama:
 
     def _proj(self, mod, x, li, key):
         if self.tps is not None:
-            y = linear(x, self.tps.layers[li][key])
+            if self.qw is not None:
+                y = self.qw[li][key](x)
+            else:
+                y = linear(x, self.tps.layers[li][key])
             if key in ("o", "down"):  # row-parallel: partial sums over this rank's heads / FFN columns
                 from .... import comm as dist
                 dist.all_reduce(y, group=self.tp_group)
@@ -230,15 +251,23 @@ class RaggedLlama:
                     return y
             return self._proj(mlp.down_proj, swiglu(gu), li, "down")
         moe = layer.block_sparse_moe if hasattr(layer, "block_sparse_moe") else layer.moe
+        if self.tps is not None:  # this rank's expert columns -> partial sums -> one all-reduce
+            d = self.tps.layers[li]
+            y = self._moe_dropless(moe.deepspeed_moe, m, d["e_gu"], d["e_down"])
+            from .... import comm as dist
+            dist.all_reduce(y, group=self.tp_group)
+            return y
         return self._moe_dropless(moe.deepspeed_moe, m)
 
-    def _moe_dropless(self, moe, m):
+    def _moe_dropless(self, moe, m, w_gu=None, w_down=None):
         """Exact top-k routing for inference (no capacity, no dropped tokens): tokens are grouped
         by expert (one argsort), each expert runs its two GEMMs on its rows, results are scattered
         back weighted by the renormalised top-k gate probabilities (reference
         ragged_ops/top_k_gating + moe_scatter + moe_gather)."""
         gate, ex = moe.gate, moe.experts
         assert moe.ep_size == 1, "ragged inference runs experts locally (ep_size == 1)"
+        w_gu = ex.w_gate_up if w_gu is None else w_gu
+        w_down = ex.w_down if w_down is None else w_down
         k = gate.k
         logits = F.linear(m.float(), gate.wg.weight.float())
         if self.moe_impl is not None and self.moe_impl.use_hip_gating and logits.is_cuda:
@@ -260,7 +289,7 @@ class RaggedLlama:
         for e, c in enumerate(counts):
             if c == 0:
                 continue
-            y = torch.matmul(swiglu(torch.matmul(xs[o:o + c], ex.w_gate_up[e])), ex.w_down[e])
+            y = torch.matmul(swiglu(torch.matmul(xs[o:o + c], w_gu[e])), w_down[e])
             out.index_add_(0, tok[o:o + c], y * ws[o:o + c])
             o += c
         return out
@@ -293,7 +322,7 @@ class RaggedLlama:
         h = model.norm(gather_rows(x, last), gather_rows(res, last))[0]
         if self.tps is not None:  # vocab-parallel head: gather every rank's logit columns
             from .... import comm as dist
-            part = linear(h, self.tps.head).float()
+            part = (self.qhead(h) if self.qw is not None else linear(h, self.tps.head)).float()
             full = torch.empty(self.tp * part.shape[0], part.shape[1], dtype=part.dtype, device=part.device)
             dist.all_gather_into_tensor(full, part, group=self.tp_group)
             return full.view(self.tp, -1, part.shape[1]).permute(1, 0, 2).reshape(part.shape[0], -1)[:, :self.tps.vocab]

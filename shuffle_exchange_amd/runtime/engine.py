@@ -1122,7 +1122,7 @@ class SXEEngine(nn.Module):
                 module=module_sd,
                 buffer_names=[n for n, _ in self.module.named_buffers()],
                 optimizer=None,
-                param_shapes=[{names[p]: tuple(p.shape) for p in pg["params_orig"]}
+                param_shapes=[{names[p]: tuple(getattr(p, "ds_shape", p.shape)) for p in pg["params_orig"]}
                               for pg in self._orig_param_groups()],
                 frozen_param_shapes={n: tuple(p.shape) for n, p in self.module.named_parameters() if not p.requires_grad},
                 lr_scheduler=self.lr_scheduler.state_dict() if self.lr_scheduler is not None else None,

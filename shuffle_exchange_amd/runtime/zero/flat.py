@@ -99,6 +99,15 @@ class FlatUnit:
         """Point every parameter's storage at its slot in ``flat``."""
         for p, o, n, s in zip(self.params, self.offsets, self.numels, self.shapes):
             p.data = self.flat[o:o + n].view(s)
+            p.ds_shape, p.ds_numel = torch.Size(s), n
+
+    def unlink_params(self):
+        """Released (ZeRO-3) unit: every parameter becomes an empty tensor -- as in the reference,
+        reading a released parameter yields numel 0 (``ds_shape`` keeps the logical shape)
+        instead of a view into freed memory, which on the GPU would be an illegal access."""
+        empty = self.flat.new_empty(0)
+        for p in self.params:
+            p.data = empty
 
     def param_range_in_shard(self, i):
         """Intersection of param i with this rank's chunk: (param_lo, param_hi, shard_lo) or None."""

@@ -329,6 +329,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             else:
                 u.shard = flat[u.lo:u.hi].clone()
             u.flat.untyped_storage().resize_(0)
+            u.unlink_params()
             u.state = RELEASED
         u.event = None
         u.keep = False
@@ -356,12 +357,12 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         i = u.param_index[id(p)]
         o, n = u.offsets[i], u.numels[i]
         if u.persistent and self.S == 1:
-            return u.grad[o:o + n].view(p.shape), u.acc_valid[i]
+            return u.grad[o:o + n].view(p.ds_shape), u.acc_valid[i]
         if u.staging is None:
             u.staging = torch.empty(u.padded, dtype=u.staging_dtype or u.dtype, device=u.device)
             if u.padded > u.numel:
                 u.staging[u.numel:].zero_()
-        return u.staging[o:o + n].view(p.shape), u.filled[i] or u.carry
+        return u.staging[o:o + n].view(p.ds_shape), u.filled[i] or u.carry
 
     def _grad_done(self, p):
         u = self.param_unit[p]
@@ -490,6 +491,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             st.wait_stream(cur)
         with get_accelerator().stream(st):
             u.flat.untyped_storage().resize_(u.padded * u.flat.element_size())
+            u.link_params()
             swapped = u.swap is not None
             src = u.swap.acquire(u) if swapped else u.shard
             if src.device != u.flat.device:
@@ -569,6 +571,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             u.sec_shard.copy_(u.flat[self.hpz_rank * n:(self.hpz_rank + 1) * n])
             u.sec_valid = True
         u.flat.untyped_storage().resize_(0)
+        u.unlink_params()
         u.state = RELEASED
 
     def _release(self, fg):

@@ -53,7 +53,7 @@ def _fragment(param, which, key=None):
 def _full(param, which, key=None):
     opt, g, u, i = _loc(param)
     frag, rng = _fragment(param, which, key)
-    full = torch.zeros(param.numel(), dtype=torch.float32, device=u.grad.device)
+    full = torch.zeros(u.numels[i], dtype=torch.float32, device=u.grad.device)
     if frag is not None:
         full[rng[0]:rng[1]].copy_(frag.reshape(-1).to(full.device, torch.float32))
     grp = opt.partition_group
