@@ -281,11 +281,19 @@ class FPxWeight:
 
 
 def quantized_weight(w, kind):
-    """Inference weight-only quantization by name: 'fp8' (W8A16), 'fp6' / 'wf6af16' (FP6-LLM), 'fp4'."""
+    """Inference weight quantization by name: 'fp8' (W8A16), 'fp6' / 'wf6af16' (FP6-LLM), 'fp4',
+    'int8' / 'int4' (W8A16 / W4A16 on the mixed-precision grouped kernel), and the OCP-MX formats
+    'mxfp8' / 'mxfp6' / 'mxfp4' (W{8,6,4}A8 on gfx950's block-scaled matrix cores, ops/mx.py)."""
+    if kind in ("int8", "int4"):
+        from .moe import IntWeight
+        return IntWeight(w, 8 if kind == "int8" else 4)
+    if kind in ("mxfp8", "mxfp6", "mxfp6_e2m3", "mxfp4"):
+        from .mx import MXWeight
+        return MXWeight(w, kind)
     if kind == "fp8":
         return FP8Weight(w)
     if kind in ("fp6", "wf6af16"):
         return FPxWeight(w, 6)
     if kind in ("fp4", "wf4af16"):
         return FPxWeight(w, 4)
-    raise ValueError(f"unknown weight quantization {kind!r} (fp8 | fp6 | fp4)")
+    raise ValueError(f"unknown weight quantization {kind!r} (fp8 | fp6 | fp4 | int8 | int4 | mxfp8 | mxfp6 | mxfp4)")

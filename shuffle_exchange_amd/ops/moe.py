@@ -141,3 +141,83 @@ def grouped_gemm(x, w, offsets, row_scale=None):
     if row_scale is not None:
         y = (y.float() * row_scale.reshape(-1, 1).float()).to(x.dtype)
     return y
+
+
+# ------------------------------------------------------------- mixed-precision (int8 / int4) experts
+class QuantizedExperts:
+    """Expert weights [E, N, K] (nn.Linear layout per expert) stored as symmetric int8 or int4 codes
+    with one fp32 scale per (expert, output row, ``group`` K elements); ``group`` defaults to the
+    whole row for int8 (per-channel) and 128 for int4. int4 codes are two's complement, two per
+    byte, low nibble first. Used by ``grouped_gemm`` (csrc/kernels/grouped_gemm.hip
+    grouped_gemm_q_kernel; reference cutlass_ops/mixed_gemm mixed_moe_gemm)."""
+
+    def __init__(self, w, bits=8, group=None):
+        assert bits in (8, 4), "QuantizedExperts: int8 or int4"
+        if w.dim() == 2:
+            w = w.unsqueeze(0)
+        E, N, K = w.shape
+        group = int(group or (K if bits == 8 else 128))
+        assert K % group == 0 and group % 128 == 0, "QuantizedExperts: group a multiple of 128 dividing K"
+        self.bits, self.group, self.shape, self.dtype = bits, group, (E, N, K), w.dtype
+        g = w.detach().float().reshape(E, N, K // group, group)
+        qmax = 127 if bits == 8 else 7
+        scale = (g.abs().amax(-1) / qmax).clamp_min(1e-12)
+        q = torch.clamp(torch.round(g / scale[..., None]), -qmax, qmax).to(torch.int32).reshape(E, N, K)
+        if bits == 4:
+            q = q & 0xF
+            q = (q[..., 0::2] | (q[..., 1::2] << 4))
+        self.q = q.to(torch.uint8).contiguous()
+        self.scale = scale.contiguous()
+
+    def dequantize(self, dtype=torch.bfloat16):
+        E, N, K = self.shape
+        q = self.q.to(torch.int32)
+        if self.bits == 8:
+            q = torch.where(q >= 128, q - 256, q)
+        else:
+            q = torch.stack([q & 0xF, q >> 4], -1).reshape(E, N, K)
+            q = torch.where(q >= 8, q - 16, q)
+        v = q.float().reshape(E, N, K // self.group, self.group) * self.scale[..., None]
+        return v.reshape(E, N, K).to(dtype)
+
+    def to(self, device):
+        self.q, self.scale = self.q.to(device), self.scale.to(device)
+        return self
+
+    @property
+    def nbytes(self):
+        return self.q.numel() + 4 * self.scale.numel()
+
+
+def grouped_gemm_q(x, w: QuantizedExperts, offsets, row_scale=None):
+    """``grouped_gemm`` with int8 / int4 expert weights: one launch, codes widened to bf16 per
+    staged K block inside the kernel (HBM streams 1 or 0.5 bytes per weight). CPU: per-expert loop
+    over the dequantized weights."""
+    E, N, K = w.shape
+    if (_hip(x) and x.dtype == torch.bfloat16 and x.dim() == 2 and w.q.is_cuda and K % 128 == 0 and N % 128 == 0
+            and x.shape[1] == K):
+        rs = None if row_scale is None else row_scale.reshape(-1).float().contiguous()
+        return torch.ops.sxe.grouped_gemm_q(x.contiguous(), w.q, w.scale, w.bits, offsets.to(torch.int32).contiguous(),
+                                            rs)
+    return grouped_gemm(x, w.dequantize(x.dtype), offsets, row_scale)
+
+
+class IntWeight:
+    """Dense int8 / int4 weight-only linear (W8A16 / W4A16) on the mixed-precision grouped kernel
+    with a single group covering all rows (reference inference/v2 mixed_gemm)."""
+
+    def __init__(self, w, bits=8, group=None):
+        self.e = QuantizedExperts(w, bits, group)
+        self.shape, self.dtype, self.bits = tuple(w.shape), w.dtype, bits
+
+    def dequantize(self, dtype=torch.bfloat16):
+        return self.e.dequantize(dtype)[0]
+
+    def linear(self, x, bias=None):
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        offs = torch.tensor([0, x2.shape[0]], dtype=torch.int32, device=x2.device)
+        y = grouped_gemm_q(x2.to(torch.bfloat16) if x2.is_cuda else x2, self.e, offs)
+        if bias is not None:
+            y = y + bias.to(y.dtype)
+        return y.view(*x.shape[:-1], self.shape[0]).to(x.dtype)

@@ -5,7 +5,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/prof
 export PYTHONPATH=$PWD
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 \
  && timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 \
  && timeout -k 10 900 python bench.py --steps ${BENCH_STEPS:-3} --warmup ${BENCH_WARMUP:-1} > gpurun_out/bench.log 2>&1 \
  && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- \
