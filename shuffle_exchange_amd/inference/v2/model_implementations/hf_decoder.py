@@ -394,8 +394,16 @@ def dropless_moe(x, router_w, e_gu, e_down, top_k, norm_topk, act="silu"):
     flat = topi.reshape(-1)
     order = torch.argsort(flat, stable=True)
     tok = order // top_k
-    from ....ops.moe import expert_offsets, grouped_gemm, grouped_gemm_ok
+    from ....ops.moe import QuantizedExperts, expert_offsets, grouped_gemm, grouped_gemm_ok, grouped_gemm_q
     E = e_gu.shape[0]
+    if isinstance(e_gu, QuantizedExperts):
+        # int8 / int4 experts (weight_quant='int8' | 'int4'): the mixed-precision grouped kernel
+        # streams the codes and widens them per staged K block (reference mixed_moe_gemm)
+        offs = expert_offsets(flat, E)
+        xs = x.index_select(0, tok)
+        ws = topw.reshape(-1).index_select(0, order).float()
+        h = gated_act(grouped_gemm_q(xs, e_gu, offs), act)
+        return torch.zeros_like(x).index_add_(0, tok, grouped_gemm_q(h, e_down, offs, ws).to(x.dtype))
     if (grouped_gemm_ok(x, e_gu) and grouped_gemm_ok(x, e_down.transpose(1, 2))
             and flat.numel() <= GROUPED_MAX_ROWS_PER_EXPERT * E):
         # one ragged grouped-GEMM launch per projection (grouped_gemm.hip), routing weight fused
@@ -524,6 +532,12 @@ class RaggedDecoder:
                     if torch.is_tensor(L.get(k)) and L[k].dim() == 2:
                         L[k] = quantized_weight(L[k], weight_quant)
             self.w["lm_head"] = quantized_weight(self.w["lm_head"], weight_quant)
+            if weight_quant in ("int8", "int4"):
+                from ....ops.moe import QuantizedExperts
+                for L in self.w["layers"]:
+                    for k in ("e_gu", "e_down"):
+                        if torch.is_tensor(L.get(k)):
+                            L[k] = QuantizedExperts(L[k], 8 if weight_quant == "int8" else 4)
         self.weight_quant = weight_quant
         self.num_layers, self.head_dim = spec.n_layers, spec.head_dim
         self.vocab_size = spec.vocab_size

@@ -52,8 +52,10 @@ def _native_dim(D):
 
 
 def _aligned(t):
+    # 16-byte aligned rows: base allocations are 512-B aligned, so the element offset decides (and
+    # unlike data_ptr() it is defined on the fake tensors a graph trace runs on)
     return (t.stride(-1) == 1 and t.stride(0) % 8 == 0 and t.stride(1) % 8 == 0 and t.stride(2) % 8 == 0
-            and t.data_ptr() % 16 == 0)
+            and (t.storage_offset() * t.element_size()) % 16 == 0)
 
 
 def hip_supported(q, k, v):

@@ -156,8 +156,8 @@ class QuantizedExperts:
         if w.dim() == 2:
             w = w.unsqueeze(0)
         E, N, K = w.shape
-        group = int(group or (K if bits == 8 else 128))
-        assert K % group == 0 and group % 128 == 0, "QuantizedExperts: group a multiple of 128 dividing K"
+        group = int(group or (K if bits == 8 else min(128, K)))
+        assert K % group == 0, "QuantizedExperts: group must divide K"
         self.bits, self.group, self.shape, self.dtype = bits, group, (E, N, K), w.dtype
         g = w.detach().float().reshape(E, N, K // group, group)
         qmax = 127 if bits == 8 else 7
@@ -195,7 +195,7 @@ def grouped_gemm_q(x, w: QuantizedExperts, offsets, row_scale=None):
     over the dequantized weights."""
     E, N, K = w.shape
     if (_hip(x) and x.dtype == torch.bfloat16 and x.dim() == 2 and w.q.is_cuda and K % 128 == 0 and N % 128 == 0
-            and x.shape[1] == K):
+            and w.group % 128 == 0 and x.shape[1] == K):
         rs = None if row_scale is None else row_scale.reshape(-1).float().contiguous()
         return torch.ops.sxe.grouped_gemm_q(x.contiguous(), w.q, w.scale, w.bits, offsets.to(torch.int32).contiguous(),
                                             rs)

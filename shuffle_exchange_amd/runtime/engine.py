@@ -584,16 +584,18 @@ class SXEEngine(nn.Module):
             from ..profiling.flops_profiler import FlopsProfiler
             prof = FlopsProfiler(self.module, ds_engine=self, recompute_fwd_factor=fp.recompute_fwd_factor)
             prof.start_profile()
+        # the FX graph compiler's module (compile/fx_backend.py) when deepcompile is on at ZeRO 0-2
+        mod = self._fx_module if getattr(self, "_fx_module", None) is not None else self.module
         if self.fp16_enabled() and self._config.model.fp16.auto_cast:
             with torch.autocast(device_type=self.device.type, dtype=torch.float16):
-                out = self.module(*inputs, **kwargs)
+                out = mod(*inputs, **kwargs)
         elif getattr(self, "_offload_activations", False) and self.module.training and torch.is_grad_enabled():
             # schedule-compiler plan (compile/passes.py offload_activation): tensors saved for
             # backward go to pinned host memory during the forward and come back for the backward
             with torch.autograd.graph.save_on_cpu(pin_memory=self.device.type == "cuda"):
-                out = self.module(*inputs, **kwargs)
+                out = mod(*inputs, **kwargs)
         else:
-            out = self.module(*inputs, **kwargs)
+            out = mod(*inputs, **kwargs)
         if prof is not None:
             prof.stop_profile()
             if self.global_rank == 0:
@@ -895,6 +897,13 @@ class SXEEngine(nn.Module):
             opt.prefetch_depth = max(2, opt.prefetch_depth) if cc.get("double_buffer", True) else 1
         if backend == "hipgraph" and self.device.type == "cuda" and self.zero_optimization_stage() < 3:
             self._fwd_graphs = {}
+        if cc.get("deepcompile") and self.zero_optimization_stage() < 3 and hasattr(opt, "grad_ready"):
+            # FX graph compiler (compile/fx_backend.py): Dynamo + AOT autograd graphs whose backward
+            # hands each parameter gradient to the ZeRO buckets right where it is produced
+            from ..compile import CompileConfig
+            from ..compile.fx_backend import compile_fx
+            self._fx_compiler, self._fx_module = compile_fx(self, CompileConfig.from_dict(cc), compile_kwargs)
+            self.compile_plan = {"fx": self._fx_compiler}
         if cc.get("deepcompile") and self.zero_optimization_stage() == 3 and hasattr(opt, "apply_compile_plan"):
             # schedule compiler (compile/): trace the next step(s), then run the passes
             from ..compile import CompileConfig, install_profiler

@@ -111,6 +111,13 @@ class DataParallelOptimizer(ZeroOptimizerBase):
             u.grad[o:o + n].add_(g.reshape(-1))
         p.grad = None
 
+    def grad_ready(self, p):
+        """A gradient delivered outside autograd's AccumulateGrad (the FX graph compiler's in-graph
+        reduce nodes, compile/fx_backend.py): ``p.grad`` is set; run the per-parameter hook."""
+        u = self.param_unit.get(p)
+        if u is not None:
+            self._make_hook(u)(p)
+
     def _make_hook(self, u):
         def hook(p):
             if p.grad is None:

@@ -147,6 +147,13 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         if u.topo.S > 1 and u.pending == 0:
             self._reduce_unit(u)
 
+    def grad_ready(self, p):
+        """A gradient delivered outside autograd's AccumulateGrad (the FX graph compiler's in-graph
+        reduce nodes, compile/fx_backend.py): ``p.grad`` is set; run the per-parameter hook."""
+        u = self.param_unit.get(p)
+        if u is not None:
+            self._make_hook(u)(p)
+
     def _make_hook(self, unit):
         def hook(p):
             if p.grad is None:

@@ -125,3 +125,20 @@ def _case_native_q(rank, world, tp):
     prompts = [torch.randint(0, 301, (n,), generator=g) for n in (5, 11, 3)]
     first = eng.put([1, 2, 3], prompts)
     return {"first": first, "linear": eng.model.implementations["linear"]}
+
+
+@pytest.mark.parametrize("name", ["mixtral", "qwen2_moe"])
+def test_hf_moe_int_weight_quant(name):
+    """weight_quant='int8' / 'int4': dense projections as IntWeight, experts as QuantizedExperts
+    through grouped_gemm_q (reference mixed_gemm / mixed_moe_gemm); logits stay close to the
+    unquantized engine, with TP=2 matching TP=1."""
+    ref = run_dist(_case_hf, 1, name, 1, None)[0]
+    for quant, tol in (("int8", 0.02), ("int4", 0.2)):
+        one = run_dist(_case_hf, 1, name, 1, quant)[0]
+        d = (one["first"] - ref["first"]).abs().max().item()
+        assert d < tol * ref["first"].abs().max().item(), (name, quant, d)
+    two = run_dist(_case_hf, 2, name, 2, "int8")
+    one = run_dist(_case_hf, 1, name, 1, "int8")[0]
+    for r in two:
+        d = (r["first"] - one["first"]).abs().max().item()
+        assert d < 0.05 * one["first"].abs().max().item(), (name, d)
