@@ -12,8 +12,9 @@ flash-attention kernels directly (``flash_attn_fwd_sparse`` / ``flash_attn_bwd_s
 csrc/kernels/flash_attn.hip): every workgroup compacts the list of 64-key (forward, dQ) or 32-query
 (dK/dV) tiles that touch a non-zero block, skips the rest, and masks inside the tiles it visits --
 scores never leave registers and work scales with the layout density. Inputs ``[B, H, S, D]`` are
-consumed through strided views (no transposes). Head dim 128 / bf16 on the GPU; other shapes,
-additive masks and rpe use the fp32 reference path (logged once).
+consumed through strided views (no transposes). Head dims 64 / 128 / 256 run natively, other
+dims up to 256 zero-padded to the next of those; fp16 inputs run in bf16; additive masks and rpe
+use the fp32 reference path (logged once).
 """
 import math
 import random
@@ -258,8 +259,13 @@ def sparse_attention_reference(q, k, v, layout, block, scale, causal=False, key_
     return torch.matmul(p, vf).to(q.dtype)
 
 
+_NATIVE_D = (64, 128, 256)
+
+
 def _hip_ok(q, k, block):
-    return (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] == 128 and q.shape[2] % 128 == 0
+    """Shapes the flash kernels run: any head dim <= 256 (64 / 128 / 256 natively, others zero-padded
+    to the next of those), bf16 or fp16 (fp16 runs in bf16), S a multiple of 128, GQA."""
+    return (q.is_cuda and q.dtype in (torch.bfloat16, torch.float16) and q.shape[-1] <= 256 and q.shape[2] % 128 == 0
             and block % 16 == 0 and q.shape[1] % k.shape[1] == 0)
 
 
@@ -292,7 +298,15 @@ def block_sparse_attention(q, k, v, layout, block, causal=False, softmax_scale=N
         native.require_hip()
         if _hip_ok(q, k, block):
             lay = layout.to(device=q.device, dtype=torch.uint8).contiguous()
-            return _SparseFlash.apply(q, k, v, lay, block, causal, scale)
+            D, dt = q.shape[-1], q.dtype
+            Dn = next(d for d in _NATIVE_D if d >= D)
+            if dt != torch.bfloat16:
+                q, k, v = q.to(torch.bfloat16), k.to(torch.bfloat16), v.to(torch.bfloat16)
+            if Dn != D:  # zero columns change neither q.k nor p.v; the scale stays the caller's
+                pad = torch.nn.functional.pad
+                q, k, v = pad(q, (0, Dn - D)), pad(k, (0, Dn - D)), pad(v, (0, Dn - D))
+            o = _SparseFlash.apply(q, k, v, lay, block, causal, scale)
+            return (o[..., :D] if Dn != D else o).to(dt)
         warning_once(f"block_sparse_attention: D={q.shape[-1]} dtype={q.dtype} not covered by the HIP kernel; "
                      f"using the reference path")
     return sparse_attention_reference(q, k, v, layout, block, scale, causal)

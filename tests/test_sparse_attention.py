@@ -49,20 +49,27 @@ def test_sparse_self_attention_dense_layout_equals_attention():
     assert torch.allclose(out, ref, atol=1e-5)
 
 
+from shuffle_exchange_amd.ops.sparse_attention import sparse_attention_reference as _REF  # noqa: E402
+
+
 def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,causal,hk", [
-    ("fixed16", False, 4), ("bigbird32", False, 4), ("longformer64_uni", True, 4), ("local128", True, 2),
-    ("fixed16", False, 1)])
-def test_block_sparse_flash_matches_reference(cfg, causal, hk):
+@pytest.mark.parametrize("cfg,causal,hk,D", [
+    ("fixed16", False, 4, 128), ("bigbird32", False, 4, 128), ("longformer64_uni", True, 4, 128),
+    ("local128", True, 2, 128), ("fixed16", False, 1, 128), ("fixed16", False, 4, 64), ("bigbird32", True, 2, 64),
+    ("longformer64_uni", True, 4, 96), ("local128", False, 2, 256)])
+def test_block_sparse_flash_matches_reference(cfg, causal, hk, D, monkeypatch):
+    """Every head dim runs the flash kernels (BERT's 64 included): the reference path must not run."""
     from shuffle_exchange_amd.ops import native
     from shuffle_exchange_amd.ops import sparse_attention as sa
     native.require_hip()
     torch.manual_seed(0)
-    B, H, S, D = 2, 4, 512, 128
+    B, H, S = 2, 4, 512
+    monkeypatch.setattr(sa, "sparse_attention_reference", None)
+    ref_fn = _REF
     conf = {"fixed16": lambda: sa.FixedSparsityConfig(H, block=16, num_local_blocks=4, different_layout_per_head=True,
                                                       num_different_global_patterns=2),
             "bigbird32": lambda: sa.BigBirdSparsityConfig(H, block=32, num_random_blocks=1),
@@ -74,7 +81,7 @@ def test_block_sparse_flash_matches_reference(cfg, causal, hk):
     v = torch.randn(B, hk, S, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     o = sa.block_sparse_attention(q, k, v, layout, conf.block, causal=causal)
     q2, k2, v2 = (t.detach().float().requires_grad_() for t in (q, k, v))
-    o2 = sa.sparse_attention_reference(q2, k2, v2, layout.cuda(), conf.block, D ** -0.5, causal)
+    o2 = ref_fn(q2, k2, v2, layout.cuda(), conf.block, D ** -0.5, causal)
     assert _rel(o, o2) < 1e-2
     g = torch.randn_like(o2)
     (o.float() * g).sum().backward()
