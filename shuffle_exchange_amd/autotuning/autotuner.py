@@ -63,7 +63,8 @@ class BaseTuner:
         except Exception as e:  # an OOM / failing config is just a bad point
             exp.error = repr(e)
             exp.metric = None
-        if exp.metric is not None and (self.best is None or exp.metric > self.best.metric):
+        if exp.metric is not None and (self.best is None or (exp.metric < self.best.metric if self.metric == "latency"
+                                                              else exp.metric > self.best.metric)):
             self.best = exp
         return exp.metric
 
@@ -104,34 +105,35 @@ class RandomTuner(GridSearchTuner):
 
 
 class ModelBasedTuner(BaseTuner):
-    """Evaluate a few random points, then always the point the fitted cost model ranks best."""
+    """Evaluate ``warmup`` random points, then mostly the point the refit cost model ranks best,
+    with a ``random_ratio`` share of random exploration (reference autotuning/tuner/
+    model_based_tuner.py: XGBoost cost model over the flattened numeric config values, 0.2 random
+    exploration). The cost model is autotuning/cost_model.py (boosted regression trees)."""
 
-    def __init__(self, *a, warmup=3, seed=1234, **k):
+    def __init__(self, *a, warmup=3, seed=1234, random_ratio=0.2, cost_model="gbt", **k):
         super().__init__(*a, **k)
+        from .cost_model import ConfigFeaturizer, CostModel
+        self._rng = random.Random(seed)
         self._left = list(self.all)
-        random.Random(seed).shuffle(self._left)
-        self.warmup = warmup
+        self._rng.shuffle(self._left)
+        self.warmup, self.random_ratio = warmup, random_ratio
         self._seen = []
-
-    @staticmethod
-    def _feat(e):
-        o = e.overrides
-        mbs = o.get("train_micro_batch_size_per_gpu", 1)
-        st = o.get("zero_optimization", {}).get("stage", 0)
-        return [1.0, math.log2(max(1, mbs)), math.log2(max(1, mbs)) ** 2] + [float(st == s) for s in range(4)]
+        self._feat = ConfigFeaturizer([e.overrides for e in self.all])
+        self.model = CostModel(cost_model, seed=seed)
+        self.lower_is_better = self.metric == "latency"
 
     def next_batch(self, n):
         if not self._left:
             return []
         scored = [e for e in self._seen if e.metric is not None]
-        if len(scored) < self.warmup:
+        if len(scored) < self.warmup or self._rng.random() < self.random_ratio:
             pick = self._left.pop()
         else:
-            X = np.array([self._feat(e) for e in scored])
-            y = np.array([e.metric for e in scored])
-            w, *_ = np.linalg.lstsq(X, y, rcond=None)
-            preds = [float(np.dot(self._feat(e), w)) for e in self._left]
-            pick = self._left.pop(int(np.argmax(preds)))
+            X = [self._feat(e.overrides) for e in scored]
+            y = [e.metric for e in scored]
+            preds = self.model.fit(X, y).predict([self._feat(e.overrides) for e in self._left])
+            i = int(np.argmin(preds) if self.lower_is_better else np.argmax(preds))
+            pick = self._left.pop(i)
         self._seen.append(pick)
         return [pick]
 

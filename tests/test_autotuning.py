@@ -1,5 +1,6 @@
 """Autotuner: memory pruning of infeasible stages, grid / random / model-based search find the best
 (synthetic) configuration, and a real in-process experiment measures engine throughput."""
+import math
 import pytest
 
 
@@ -151,3 +152,36 @@ def test_scheduler_parallel_slots(tmp_path):
     assert time.time() - t0 < 3.9  # a||b, then c, then d would take >= 4 s serially
     assert rm.parse_results().name == "b"
     assert exps[2].metrics["dev"] == "0,1" and exps[3].error
+
+
+def test_cost_model_tuner_finds_optimum_of_nonlinear_space():
+    """Boosted-tree cost model (autotuning/cost_model.py, reference XGBoostCostModel) over generic
+    flattened numeric knobs: on a 3-knob space with an interior optimum it reaches the best point
+    well before exhausting the space, for throughput (max) and latency (min) metrics."""
+    import itertools
+    from shuffle_exchange_amd.autotuning.autotuner import Experiment, ModelBasedTuner
+    from shuffle_exchange_amd.autotuning.cost_model import ConfigFeaturizer, flatten
+    space = [{"train_micro_batch_size_per_gpu": m, "zero_optimization": {"stage": s, "reduce_bucket_size": b}}
+             for m, s, b in itertools.product([1, 2, 4, 8, 16, 32], [0, 1, 2, 3], [1e7, 5e7, 2e8])]
+
+    def tput(e):
+        o = e.overrides
+        m, s, b = o["train_micro_batch_size_per_gpu"], o["zero_optimization"]["stage"], o["zero_optimization"]["reduce_bucket_size"]
+        return 100 - (math.log2(m) - 3) ** 2 * 6 - abs(s - 2) * 9 - abs(math.log10(b) - 7.7) * 4
+
+    exps = [Experiment(f"e{i}", c) for i, c in enumerate(space)]
+    f = ConfigFeaturizer([e.overrides for e in exps])
+    assert f.keys == sorted(flatten(space[0]))
+    best = max(exps, key=tput)
+    hits = 0
+    for seed in range(5):
+        for e in exps:
+            e.metric = None
+        t = ModelBasedTuner(exps, tput, metric="throughput", seed=seed, warmup=4)
+        t.tune(n_trials=30)
+        hits += t.best is best
+    assert hits >= 4
+    for e in exps:
+        e.metric = None
+    t = ModelBasedTuner(exps, lambda e: 1.0 / tput(e), metric="latency", seed=0, warmup=4)
+    assert t.tune(n_trials=30) is best
