@@ -128,7 +128,7 @@ static void xent_checks(const at::Tensor& logits, const at::Tensor& target) {
 
 // Returns (loss [rows] fp32, lse [rows] fp32). If `inplace_grad`, logits are overwritten with
 // scale * (softmax - onehot) where scale = grad_scale * (*scale_t if given).
-std::vector<at::Tensor> xent_fwd(at::Tensor logits, at::Tensor target, int64_t ignore_index, bool inplace_grad,
+std::tuple<at::Tensor, at::Tensor> xent_fwd(at::Tensor logits, at::Tensor target, int64_t ignore_index, bool inplace_grad,
                                  c10::optional<at::Tensor> scale_t, double grad_scale) {
   xent_checks(logits, target);
   const int64_t rows = logits.size(0);
@@ -180,7 +180,7 @@ at::Tensor xent_bwd(at::Tensor logits, at::Tensor target, at::Tensor lse, at::Te
 }  // namespace sxe
 
 TORCH_LIBRARY_FRAGMENT(sxe, m) {
-  m.def("xent_fwd(Tensor(a!) logits, Tensor target, int ignore_index, bool inplace_grad, Tensor? scale, float grad_scale) -> Tensor[]");
+  m.def("xent_fwd(Tensor(a!) logits, Tensor target, int ignore_index, bool inplace_grad, Tensor? scale, float grad_scale) -> (Tensor, Tensor)");
   m.def("xent_bwd(Tensor(a!) logits, Tensor target, Tensor lse, Tensor dloss, int ignore_index, bool inplace) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(sxe, CUDA, m) {

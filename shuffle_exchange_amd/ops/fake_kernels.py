@@ -82,7 +82,7 @@ def _fa_bwd(dout, q, k, v, o, lse, dq, dk, dv, causal, scale, kv_len=-1, causal_
 @_reg("sxe::xent_fwd")
 def _xent_fwd(logits, target, ignore_index, inplace_grad, scale, grad_scale):
     r = logits.shape[0]
-    return [logits.new_empty((r,), dtype=torch.float32), logits.new_empty((r,), dtype=torch.float32)]
+    return logits.new_empty((r,), dtype=torch.float32), logits.new_empty((r,), dtype=torch.float32)
 
 
 @_reg("sxe::xent_bwd")

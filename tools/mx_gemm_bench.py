@@ -1,0 +1,49 @@
+"""MX GEMM (gfx950 block-scaled MFMA, csrc/kernels/mx_gemm.hip) vs bf16 hipBLASLt and FP8
+row-scaled hipBLASLt (_scaled_mm) on Llama-3-8B prefill shapes. Times include the MXFP8
+activation quantisation pass (reported separately too)."""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from shuffle_exchange_amd.ops import mx, native  # noqa: E402
+from shuffle_exchange_amd.ops.fp_quantizer import fp8_linear, quantize_weight_fp8_rowwise  # noqa: E402
+
+
+def t(fn, it=50):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(it):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / it
+
+
+def main():
+    native.require_hip()
+    shapes = [(2048, 6144, 4096), (2048, 4096, 4096), (2048, 28672, 4096), (2048, 4096, 14336), (8192, 4096, 4096),
+              (512, 4096, 4096), (128, 14336, 4096)]
+    for M, N, K in shapes:
+        x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+        w = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
+        fl = 2 * M * N * K
+        tb = t(lambda: torch.nn.functional.linear(x, w))
+        wq8, ws8 = quantize_weight_fp8_rowwise(w)
+        t8 = t(lambda: fp8_linear(x, wq8, ws8))
+        q, s = torch.ops.sxe.mx_quant_fp8(x)
+        tq = t(lambda: torch.ops.sxe.mx_quant_fp8(x))
+        line = f"M={M} N={N} K={K}: bf16 {tb*1e3:.0f} us ({fl/tb/1e9:.0f} TF) | fp8 rowwise {t8*1e3:.0f} us ({fl/t8/1e9:.0f} TF) | act quant {tq*1e3:.0f} us"
+        for fmt in ["mxfp8", "mxfp6", "mxfp4"]:
+            W = mx.MXWeight(w.float(), fmt)
+            code = mx.FORMATS[fmt][0]
+            tg = t(lambda: torch.ops.sxe.mx_gemm(q, s, W.q, W.scale, code, None, None))
+            line += f" | {fmt} {tg*1e3:.0f} us ({fl/tg/1e9:.0f} TF) +q {fl/(tg+tq)/1e9:.0f} TF"
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()
