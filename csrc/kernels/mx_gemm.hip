@@ -18,8 +18,8 @@
 // Both operands are K-contiguous rows -- X as [M, K], W in nn.Linear's [N, K] layout -- so the
 // layouts only decide which bytes of an LDS row a lane reads; no data is ever permuted.
 //
-// Geometry: BM x BN output tile (256x256 / 256x128 / 128x128), 8 waves as 2 (M) x 4 (N), each wave
-// (BM/2) x (BN/4) as 32x32 accumulators; K in stages of 128 (two MFMA k-steps). Operand tiles are
+// Geometry: BM x BN output tile (256x256 / 256x128 / 128x128), WM x WN waves, each wave
+// (BM/WM) x (BN/WN) as 32x32 accumulators; K in stages of 128 (two MFMA k-steps). Operand tiles are
 // staged global -> registers -> LDS with rows padded by 16 B (row strides of 144 / 112 / 80 B put
 // the 16 lanes of a ds_read_b128 phase on distinct banks); the next stage's loads (tiles + the
 // lanes' scale words) are in flight while the current stage's MFMAs run. Workgroups are mapped
@@ -36,7 +36,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int BK = 128, NTHR = 512;
+constexpr int BK = 128;
 constexpr int SA = 128 + 16;  // padded LDS row stride of the fp8 activation tile
 
 // MFMA format codes (cbsz / blgp): 0 e4m3, 1 e5m2, 2 e2m3, 3 e3m2, 4 e2m1
@@ -51,7 +51,7 @@ struct BLayout {
   static constexpr int LB = 4 * BITS;   // bytes one lane feeds per MFMA (32 elements)
 };
 
-template <int ROWS, int CPR, int STRIDE>
+template <int ROWS, int CPR, int STRIDE, int NTHR>
 struct Stager {
   static constexpr int N = (ROWS * CPR + NTHR - 1) / NTHR;
   u32x4 r[N];
@@ -97,13 +97,14 @@ __device__ __forceinline__ i32x8 lds_operand(const char* p, int h) {
   return v;
 }
 
-template <int BM, int BN, int FB>
-__global__ void __launch_bounds__(NTHR, 1)
+template <int BM, int BN, int WM, int WN, int FB>
+__global__ void __launch_bounds__(64 * WM * WN, 1)
     mx_gemm_kernel(const uint8_t* __restrict__ Xq, const uint8_t* __restrict__ Xs, const uint8_t* __restrict__ Wq,
                    const uint8_t* __restrict__ Ws, const unsigned short* __restrict__ bias,
                    const float* __restrict__ col_scale, unsigned short* __restrict__ Y, int M, int N, int K) {
   using L = BLayout<FB>;
-  constexpr int TM = BM / 2, TN = BN / 4, MI = TM / 32, NJ = TN / 32;
+  constexpr int NTHR = 64 * WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NJ = TN / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* lA = smem;
   char* lB = smem + BM * SA;
@@ -115,7 +116,7 @@ __global__ void __launch_bounds__(NTHR, 1)
   const int m0 = (pid % tm) * BM, n0 = (pid / tm) * BN;
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int wm = w >> 2, wn = w & 3, h = lane >> 5, l32 = lane & 31;
+  const int wm = w / WN, wn = w % WN, h = lane >> 5, l32 = lane & 31;
   const int KS = K / 32;          // scale bytes per row
   const int64_t WRB = (int64_t)K * L::BITS / 8;  // weight bytes per row
 
@@ -142,8 +143,8 @@ __global__ void __launch_bounds__(NTHR, 1)
     }
   };
 
-  Stager<BM, 8, SA> stA;
-  Stager<BN, L::CPR, L::SB> stB;
+  Stager<BM, 8, SA, NTHR> stA;
+  Stager<BN, L::CPR, L::SB, NTHR> stB;
   stA.load(Xq, K, m0, M);
   stB.load(Wq, WRB, n0, N);
   load_scales(0);
@@ -238,37 +239,263 @@ __global__ void mx_quant_fp8_kernel(const unsigned short* __restrict__ x, uint8_
   o[1] = u32x4{out[4], out[5], out[6], out[7]};
 }
 
-template <int BM, int BN, int FB>
+
+// ---------------------------------------------------------------------------------------------------
+// Deep-pipelined variant: 256 x 256 output tile, 4 waves (2 x 2, 128 x 128 each: 16 accumulators in
+// AGPRs), every operand byte -- codes AND the lanes' exponent words -- staged by LDS-DMA
+// (global_load_lds, 16 B per lane for codes, 4 B for exponents) into NBUF stage buffers, waited with
+// a counted vmcnt and a raw s_barrier so the next stage's DMA stays in flight across the barrier
+// (cdna_hip_programming.md "Pipelining across barriers"). A glds writes lane i's bytes at the
+// wave-uniform base + i * size, so the LDS image is lane-linear; the bank-conflict swizzle is applied
+// to the SOURCE address instead: 16-byte slot s of row r holds chunk s ^ f(r), with f(r) = (r >> 1) & 7
+// for 128-byte rows (fp8 / padded fp6) and (r >> 2) & 3 for 64-byte rows (fp4), which puts the 16
+// rows a ds_read_b128 phase touches on distinct banks. fp6 rows (96 data bytes) are padded to 128 B.
+namespace dp {
+constexpr int BM = 256, NT = 256;
+template <int FB, int BN> struct L {
+  static constexpr int BITS = fmt_bits(FB);
+  static constexpr int RB = 16 * BITS;                // data bytes per row per 128-K stage
+  static constexpr int RP = BITS == 4 ? 64 : 128;     // LDS row pitch
+  static constexpr int CH = RB / 16;                  // data chunks per row
+  static constexpr int SL = RP / 16;                  // slots per row
+  static constexpr int ROWS_PER_INSTR = 64 / SL;      // rows one wave instruction fills
+  static constexpr int B_INSTR = BN / ROWS_PER_INSTR / 4;  // per wave per stage
+  static constexpr int SI = (BM + BN + 255) / 256;     // exponent instructions per wave (64 rows each)
+  static constexpr int A_BYTES = BM * 128, B_BYTES = BN * RP, S_BYTES = 4 * SI * 64 * 4;
+  static constexpr int STAGE = A_BYTES + B_BYTES + S_BYTES;
+  static constexpr int LOADS = 8 + B_INSTR + SI;       // glds per wave per stage (A, B, exponents)
+};
+__device__ __forceinline__ int fA(int r) { return (r >> 1) & 7; }
+template <int RP> __device__ __forceinline__ int fB(int r) { return RP == 64 ? ((r >> 2) & 3) : ((r >> 1) & 7); }
+
+template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+__device__ __forceinline__ void glds16(const void* g, char* l) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* g, char* l) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 4, 0, 0);
+}
+
+template <int FB, int BN>
+__device__ __forceinline__ void issue_stage(char* buf, const uint8_t* Xq, const uint8_t* Xs, const uint8_t* Wq,
+                                            const uint8_t* Ws, int m0, int n0, int M, int K, int64_t WRB, int KS,
+                                            int kb, int w, int lane) {
+  using G = L<FB, BN>;
+  // A: 32 instructions of 8 rows x 128 B, 8 per wave
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int g = w * 8 + j, row = 8 * g + (lane >> 3), slot = lane & 7;
+    const int gr = min(m0 + row, M - 1);
+    glds16(Xq + (int64_t)gr * K + (int64_t)kb * 128 + 16 * (slot ^ fA(row)), buf + 8 * g * 128);
+  }
+  // B
+#pragma unroll
+  for (int j = 0; j < G::B_INSTR; ++j) {
+    const int g = w * G::B_INSTR + j, row = G::ROWS_PER_INSTR * g + lane / G::SL, slot = lane % G::SL;
+    int ch = slot ^ fB<G::RP>(row);
+    if (ch >= G::CH) ch = 0;  // fp6 padding slots: any in-row chunk, never read
+    glds16(Wq + (int64_t)(n0 + row) * WRB + (int64_t)kb * G::RB + 16 * ch, buf + G::A_BYTES + G::ROWS_PER_INSTR * g * G::RP);
+  }
+  // exponent words (4 E8M0 bytes per row per stage): waves 0-1 the A rows, waves 2-3 the B rows
+  char* sb = buf + G::A_BYTES + G::B_BYTES;
+  // exponent instructions per wave (64 rows each); every wave issues the same count (so one vmcnt
+  // constant fits all), the slots past the A and B rows re-load A rows into a spare area
+#pragma unroll
+  for (int j = 0; j < G::SI; ++j) {
+    const int g = w * G::SI + j;  // A rows 0..BM-1 first, then B rows 0..BN-1, then spares
+    if (g < BM / 64 || g >= (BM + BN) / 64) {
+      const int ga = g < BM / 64 ? g : 0;
+      const int row = 64 * ga + lane, gr = min(m0 + row, M - 1);
+      glds4(Xs + (int64_t)gr * KS + 4 * kb, sb + 64 * g * 4);
+    } else {
+      const int row = 64 * (g - BM / 64) + lane;
+      glds4(Ws + (int64_t)(n0 + row) * KS + 4 * kb, sb + BM * 4 + 64 * (g - BM / 64) * 4);
+    }
+  }
+}
+
+template <int FB, int BN>
+__device__ __forceinline__ i32x8 read_b(const char* bb, int row, int s, int h) {
+  using G = L<FB, BN>;
+  const char* rp = bb + row * G::RP;
+  if constexpr (G::BITS == 8) {
+    const u32x4 a = *reinterpret_cast<const u32x4*>(rp + 16 * ((4 * s + h) ^ fB<G::RP>(row)));
+    const u32x4 b = *reinterpret_cast<const u32x4*>(rp + 16 * ((4 * s + 2 + h) ^ fB<G::RP>(row)));
+    return i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
+  } else if constexpr (G::BITS == 4) {
+    const u32x4 a = *reinterpret_cast<const u32x4*>(rp + 16 * ((2 * s + h) ^ fB<G::RP>(row)));
+    return i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], 0, 0, 0, 0};
+  } else {
+    const int o = 48 * s + 24 * h;
+    u32x2 p[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int oq = o + 8 * q;
+      p[q] = *reinterpret_cast<const u32x2*>(rp + 16 * ((oq >> 4) ^ fB<G::RP>(row)) + (oq & 15));
+    }
+    return i32x8{(int)p[0][0], (int)p[0][1], (int)p[1][0], (int)p[1][1], (int)p[2][0], (int)p[2][1], 0, 0};
+  }
+}
+
+template <int FB, int NBUF, int BN>
+__global__ void __launch_bounds__(NT, 1)
+    mx_gemm_dp_kernel(const uint8_t* __restrict__ Xq, const uint8_t* __restrict__ Xs, const uint8_t* __restrict__ Wq,
+                      const uint8_t* __restrict__ Ws, const unsigned short* __restrict__ bias,
+                      const float* __restrict__ col_scale, unsigned short* __restrict__ Y, int M, int N, int K) {
+  using G = L<FB, BN>;
+  constexpr int NJ = BN / 64;  // 32-column accumulators per wave (wave tile 128 x BN/2)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // bijective XCD-major remap (8 XCDs, round-robin dispatch)
+  const int tm = (M + BM - 1) / BM, tn = N / BN, nwg = tm * tn;
+  const int orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int pid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int m0 = (pid % tm) * BM, n0 = (pid / tm) * BN;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1, h = lane >> 5, l32 = lane & 31;
+  const int KS = K / 32;
+  const int64_t WRB = (int64_t)K * G::BITS / 8;
+  const int nk = K / BK;
+
+  f32x16 acc[4][NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  issue_stage<FB, BN>(smem, Xq, Xs, Wq, Ws, m0, n0, M, K, WRB, KS, 0, w, lane);
+  if (NBUF == 3 && nk > 1) issue_stage<FB, BN>(smem + G::STAGE, Xq, Xs, Wq, Ws, m0, n0, M, K, WRB, KS, 1, w, lane);
+  for (int kb = 0; kb < nk; ++kb) {
+    if (NBUF == 3 && kb + 1 < nk) vm_wait<G::LOADS>(); else vm_wait<0>();
+    raw_barrier();  // stage kb landed for every wave; every wave is done reading stage kb - 1
+    const int ahead = NBUF - 1;
+    if (kb + ahead < nk)
+      issue_stage<FB, BN>(smem + ((kb + ahead) % NBUF) * G::STAGE, Xq, Xs, Wq, Ws, m0, n0, M, K, WRB, KS, kb + ahead, w, lane);
+    const char* buf = smem + (kb % NBUF) * G::STAGE;
+    const char* ba = buf;
+    const char* bb = buf + G::A_BYTES;
+    const unsigned* sc = reinterpret_cast<const unsigned*>(buf + G::A_BYTES + G::B_BYTES);
+    unsigned sa[4], sbw[NJ];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sa[i] = sc[wm * 128 + i * 32 + l32];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) sbw[j] = sc[BM + wn * (BN / 2) + j * 32 + l32];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      i32x8 a[4], b[NJ];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 128 + i * 32 + l32;
+        const char* rp = ba + row * 128;
+        const u32x4 x0 = *reinterpret_cast<const u32x4*>(rp + 16 * ((4 * s + h) ^ fA(row)));
+        const u32x4 x1 = *reinterpret_cast<const u32x4*>(rp + 16 * ((4 * s + 2 + h) ^ fA(row)));
+        a[i] = i32x8{(int)x0[0], (int)x0[1], (int)x0[2], (int)x0[3], (int)x1[0], (int)x1[1], (int)x1[2], (int)x1[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) b[j] = read_b<FB, BN>(bb, wn * (BN / 2) + j * 32 + l32, s, h);
+      const int sh = 8 * (2 * s + h);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+              a[i], b[j], acc[i][j], 0, FB, 0, (int)((sa[i] >> sh) & 0xff), 0, (int)((sbw[j] >> sh) & 0xff));
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int n = n0 + wn * (BN / 2) + j * 32 + l32;
+    const float cs = col_scale ? col_scale[n] : 1.f;
+    const float bv = bias ? bf16_to_f32(bias[n]) : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wm * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (m < M) Y[(int64_t)m * N + n] = f32_to_bf16(acc[i][j][e] * cs + bv);
+      }
+  }
+}
+}  // namespace dp
+
+template <int BM, int BN, int WM, int WN, int FB>
 void launch(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq, const at::Tensor& ws,
             const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& col_scale, at::Tensor& y, int M,
             int N, int K) {
   const size_t lds = (size_t)BM * SA + (size_t)BN * BLayout<FB>::SB;
   static bool attr = [&] {
-    SXE_HIP_CHECK(hipFuncSetAttribute((const void*)mx_gemm_kernel<BM, BN, FB>,
+    SXE_HIP_CHECK(hipFuncSetAttribute((const void*)mx_gemm_kernel<BM, BN, WM, WN, FB>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     return true;
   }();
   (void)attr;
   const int G = ((M + BM - 1) / BM) * (N / BN);
-  hipLaunchKernelGGL((mx_gemm_kernel<BM, BN, FB>), dim3(G), dim3(NTHR), lds, cur_stream(), xq.data_ptr<uint8_t>(),
-                     xs.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), ws.data_ptr<uint8_t>(),
+  hipLaunchKernelGGL((mx_gemm_kernel<BM, BN, WM, WN, FB>), dim3(G), dim3(64 * WM * WN), lds, cur_stream(),
+                     xq.data_ptr<uint8_t>(), xs.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), ws.data_ptr<uint8_t>(),
                      bias ? reinterpret_cast<const unsigned short*>(bias->data_ptr()) : nullptr,
                      col_scale ? col_scale->data_ptr<float>() : nullptr,
                      reinterpret_cast<unsigned short*>(y.data_ptr()), M, N, K);
+}
+
+// tile variants: 0 auto, 1 = 128x128 / 4 waves, 2 = 256x128 / 4 waves, 3 = 256x256 / 4 waves
+// (128x128 per wave, accumulators in AGPRs), 4 = 256x256 / 8 waves, 5 = 256x128 / 8 waves,
+// 6 = 256x256 / 4 waves LDS-DMA pipelined (namespace dp), 7 = the same at 256x128
+static int tile_override() {
+  static int v = [] {
+    const char* e = getenv("SXE_MX_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+template <int FB, int BN>
+void launch_dp(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq, const at::Tensor& ws,
+               const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& cs, at::Tensor& y, int M, int N,
+               int K) {
+  constexpr int NBUF = dp::L<FB, BN>::STAGE * 3 <= 160 * 1024 ? 3 : 2;
+  const size_t lds = (size_t)NBUF * dp::L<FB, BN>::STAGE;
+  static bool attr = [&] {
+    SXE_HIP_CHECK(hipFuncSetAttribute((const void*)dp::mx_gemm_dp_kernel<FB, NBUF, BN>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    return true;
+  }();
+  (void)attr;
+  const int G = ((M + dp::BM - 1) / dp::BM) * (N / BN);
+  hipLaunchKernelGGL((dp::mx_gemm_dp_kernel<FB, NBUF, BN>), dim3(G), dim3(dp::NT), lds, cur_stream(), xq.data_ptr<uint8_t>(),
+                     xs.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), ws.data_ptr<uint8_t>(),
+                     bias ? reinterpret_cast<const unsigned short*>(bias->data_ptr()) : nullptr,
+                     cs ? cs->data_ptr<float>() : nullptr, reinterpret_cast<unsigned short*>(y.data_ptr()), M, N, K);
 }
 
 template <int FB>
 void dispatch_tile(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq, const at::Tensor& ws,
                    const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& cs, at::Tensor& y, int M,
                    int N, int K) {
-  // largest tile that still gives >= 1 workgroup per CU; 128 x 128 for small problems
-  const int64_t g256 = (int64_t)((M + 255) / 256) * (N / 256), g2561 = (int64_t)((M + 255) / 256) * (N / 128);
-  if (N % 256 == 0 && M > 128 && g256 >= kNumCUs)
-    launch<256, 256, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K);
-  else if (M > 128 && g2561 >= kNumCUs)
-    launch<256, 128, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K);
-  else
-    launch<128, 128, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K);
+  int v = tile_override();
+  if (v == 0) {
+    // measured on MI355X (profiles/mx_gemm_bench.log): the LDS-DMA pipelined 256 x 256 tile once it
+    // fills the chip, its 256 x 128 form when that still gives >= half a workgroup per CU, the
+    // register-staged 128 x 128 tile for small problems
+    const int64_t g256 = (int64_t)((M + 255) / 256) * (N / 256), g2561 = (int64_t)((M + 255) / 256) * (N / 128);
+    v = (N % 256 == 0 && M > 256 && g256 >= kNumCUs) ? 6 : (M > 256 && g2561 >= kNumCUs / 2) ? 7 : 1;
+  }
+  if ((v == 3 || v == 4 || v == 6) && N % 256 != 0) v = 2;
+  switch (v) {
+    case 6: launch_dp<FB, 256>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
+    case 7: launch_dp<FB, 128>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
+    case 2: launch<256, 128, 2, 2, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
+    case 3: launch<256, 256, 2, 2, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
+    case 4: launch<256, 256, 2, 4, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
+    case 5: launch<256, 128, 2, 4, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
+    default: launch<128, 128, 2, 2, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
+  }
 }
 
 }  // namespace mx

@@ -24,16 +24,24 @@ def t(fn, it=50):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true", help="two shapes, MX formats only (tile sweeps)")
+    args = ap.parse_args()
     native.require_hip()
     shapes = [(2048, 6144, 4096), (2048, 4096, 4096), (2048, 28672, 4096), (2048, 4096, 14336), (8192, 4096, 4096),
               (512, 4096, 4096), (128, 14336, 4096)]
+    if args.quick:
+        shapes = [(2048, 28672, 4096), (8192, 4096, 4096), (2048, 4096, 4096)]
+    import os
+    print(f"SXE_MX_TILE={os.environ.get('SXE_MX_TILE', '0')}", flush=True)
     for M, N, K in shapes:
         x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
         w = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
         fl = 2 * M * N * K
         tb = t(lambda: torch.nn.functional.linear(x, w))
         wq8, ws8 = quantize_weight_fp8_rowwise(w)
-        t8 = t(lambda: fp8_linear(x, wq8, ws8))
+        t8 = t(lambda: fp8_linear(x, wq8, ws8)) if not args.quick else float("nan")
         q, s = torch.ops.sxe.mx_quant_fp8(x)
         tq = t(lambda: torch.ops.sxe.mx_quant_fp8(x))
         line = f"M={M} N={N} K={K}: bf16 {tb*1e3:.0f} us ({fl/tb/1e9:.0f} TF) | fp8 rowwise {t8*1e3:.0f} us ({fl/t8/1e9:.0f} TF) | act quant {tq*1e3:.0f} us"
