@@ -40,7 +40,11 @@ constexpr int BK = 128;
 constexpr int SA = 128 + 16;  // padded LDS row stride of the fp8 activation tile
 
 // MFMA format codes (cbsz / blgp): 0 e4m3, 1 e5m2, 2 e2m3, 3 e3m2, 4 e2m1
-__host__ __device__ constexpr int fmt_bits(int f) { return f <= 1 ? 8 : (f <= 3 ? 6 : 4); }
+__host__ __device__ constexpr int fmt_bits(int f) { return f <= 1 ? 8 : (f <= 3 || f == 16) ? 6 : 4; }
+// 16 / 17: FPxWeight's bit-plane FP6 (e3m2) / FP4 (e2m1) layout (ops/fp_quantizer.py): transcoded
+// exactly to e4m3 in registers and multiplied as fp8 (both formats embed in e4m3)
+__host__ __device__ constexpr bool is_planes(int f) { return f >= 16; }
+__host__ __device__ constexpr int mfma_fmt(int f) { return is_planes(f) ? 0 : f; }
 
 template <int FB>
 struct BLayout {
@@ -253,15 +257,17 @@ __global__ void mx_quant_fp8_kernel(const unsigned short* __restrict__ x, uint8_
 namespace dp {
 constexpr int BM = 256, NT = 256;
 template <int FB, int BN> struct L {
+  static constexpr bool PL = is_planes(FB);
   static constexpr int BITS = fmt_bits(FB);
   static constexpr int RB = 16 * BITS;                // data bytes per row per 128-K stage
-  static constexpr int RP = BITS == 4 ? 64 : 128;     // LDS row pitch
-  static constexpr int CH = RB / 16;                  // data chunks per row
+  static constexpr int RP = (BITS == 4 || PL) ? 64 : 128;  // LDS row pitch (planes: the nibble plane)
+  static constexpr int CH = PL ? 4 : RB / 16;         // data chunks per row
   static constexpr int SL = RP / 16;                  // slots per row
   static constexpr int ROWS_PER_INSTR = 64 / SL;      // rows one wave instruction fills
-  static constexpr int B_INSTR = BN / ROWS_PER_INSTR / 4;  // per wave per stage
+  static constexpr int CR_INSTR = (PL && BITS == 6) ? BN / 128 : 0;  // crumb-plane (32 B rows) instructions
+  static constexpr int B_INSTR = BN / ROWS_PER_INSTR / 4 + CR_INSTR;  // per wave per stage
   static constexpr int SI = (BM + BN + 255) / 256;     // exponent instructions per wave (64 rows each)
-  static constexpr int A_BYTES = BM * 128, B_BYTES = BN * RP, S_BYTES = 4 * SI * 64 * 4;
+  static constexpr int A_BYTES = BM * 128, B_BYTES = BN * RP + (CR_INSTR ? BN * 32 : 0), S_BYTES = 4 * SI * 64 * 4;
   static constexpr int STAGE = A_BYTES + B_BYTES + S_BYTES;
   static constexpr int LOADS = 8 + B_INSTR + SI;       // glds per wave per stage (A, B, exponents)
 };
@@ -282,8 +288,8 @@ __device__ __forceinline__ void glds4(const void* g, char* l) {
 
 template <int FB, int BN>
 __device__ __forceinline__ void issue_stage(char* buf, const uint8_t* Xq, const uint8_t* Xs, const uint8_t* Wq,
-                                            const uint8_t* Ws, int m0, int n0, int M, int K, int64_t WRB, int KS,
-                                            int kb, int w, int lane) {
+                                            const uint8_t* Wq2, const uint8_t* Ws, int wks, int m0, int n0, int M,
+                                            int K, int64_t WRB, int KS, int kb, int w, int lane) {
   using G = L<FB, BN>;
   // A: 32 instructions of 8 rows x 128 B, 8 per wave
 #pragma unroll
@@ -293,12 +299,27 @@ __device__ __forceinline__ void issue_stage(char* buf, const uint8_t* Xq, const 
     glds16(Xq + (int64_t)gr * K + (int64_t)kb * 128 + 16 * (slot ^ fA(row)), buf + 8 * g * 128);
   }
   // B
+  if constexpr (G::PL) {
+    constexpr int NI = BN / 64;  // nibble plane: 64 B rows, 16 rows per instruction
 #pragma unroll
-  for (int j = 0; j < G::B_INSTR; ++j) {
-    const int g = w * G::B_INSTR + j, row = G::ROWS_PER_INSTR * g + lane / G::SL, slot = lane % G::SL;
-    int ch = slot ^ fB<G::RP>(row);
-    if (ch >= G::CH) ch = 0;  // fp6 padding slots: any in-row chunk, never read
-    glds16(Wq + (int64_t)(n0 + row) * WRB + (int64_t)kb * G::RB + 16 * ch, buf + G::A_BYTES + G::ROWS_PER_INSTR * g * G::RP);
+    for (int j = 0; j < NI; ++j) {
+      const int g = w * NI + j, row = 16 * g + (lane >> 2), ch = (lane & 3) ^ ((row >> 2) & 3);
+      glds16(Wq + (int64_t)(n0 + row) * (K / 2) + (int64_t)kb * 64 + 16 * ch, buf + G::A_BYTES + 16 * g * 64);
+    }
+#pragma unroll
+    for (int j = 0; j < G::CR_INSTR; ++j) {  // crumb plane: 32 B rows, 32 rows per instruction
+      const int g = w * G::CR_INSTR + j, row = 32 * g + (lane >> 1), ch = (lane & 1) ^ ((row >> 3) & 1);
+      glds16(Wq2 + (int64_t)(n0 + row) * (K / 4) + (int64_t)kb * 32 + 16 * ch, buf + G::A_BYTES + BN * 64 + 32 * g * 32);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < G::B_INSTR; ++j) {
+      const int g = w * G::B_INSTR + j, row = G::ROWS_PER_INSTR * g + lane / G::SL, slot = lane % G::SL;
+      int ch = slot ^ fB<G::RP>(row);
+      if (ch >= G::CH) ch = 0;  // fp6 padding slots: any in-row chunk, never read
+      glds16(Wq + (int64_t)(n0 + row) * WRB + (int64_t)kb * G::RB + 16 * ch,
+             buf + G::A_BYTES + G::ROWS_PER_INSTR * g * G::RP);
+    }
   }
   // exponent words (4 E8M0 bytes per row per stage): waves 0-1 the A rows, waves 2-3 the B rows
   char* sb = buf + G::A_BYTES + G::B_BYTES;
@@ -313,16 +334,65 @@ __device__ __forceinline__ void issue_stage(char* buf, const uint8_t* Xq, const 
       glds4(Xs + (int64_t)gr * KS + 4 * kb, sb + 64 * g * 4);
     } else {
       const int row = 64 * (g - BM / 64) + lane;
-      glds4(Ws + (int64_t)(n0 + row) * KS + 4 * kb, sb + BM * 4 + 64 * (g - BM / 64) * 4);
+      glds4(Ws + (int64_t)(n0 + row) * wks + 4 * kb, sb + BM * 4 + 64 * (g - BM / 64) * 4);
     }
   }
+}
+
+// 0xFF in each byte whose (small) value is zero
+__device__ __forceinline__ unsigned zero_bytes(unsigned e) {
+  const unsigned nz = (e | (e >> 1) | (e >> 2)) & 0x01010101u;
+  const unsigned z = nz ^ 0x01010101u;
+  return (z << 8) - z;
+}
+// 4 e3m2 codes (sign|exp nibble per byte, 2 mantissa bits per byte) -> 4 e4m3 bytes, exact. Pure
+// bytewise arithmetic (no carries cross a byte): hipcc 7.2's instcombine crashes on v_perm table
+// lookups in this kernel.
+__device__ __forceinline__ unsigned e3m2x4_to_e4m3(unsigned se, unsigned m) {
+  const unsigned e = se & 0x07070707u, sg = (se & 0x08080808u) << 4;
+  const unsigned nrm = ((e + 0x04040404u) << 3) | (m << 1);
+  const unsigned z = zero_bytes(e);  // subnormal / zero codes: m * 2^-4 = e4m3 00 / 18 / 20 / 24
+  const unsigned b1 = m & 0x01010101u, b2 = (m >> 1) & 0x01010101u;
+  const unsigned sub = ((b1 | b2) << 4) + (m << 3) - ((b1 & b2) << 2);
+  return sg | (z & sub) | (~z & nrm);
+}
+// 4 e2m1 codes (one per byte) -> 4 e4m3 bytes, exact
+__device__ __forceinline__ unsigned e2m1x4_to_e4m3(unsigned x) {
+  const unsigned sg = (x & 0x08080808u) << 4, e = (x >> 1) & 0x03030303u, m = x & 0x01010101u;
+  const unsigned nrm = ((e + 0x06060606u) << 3) | (m << 2);
+  const unsigned z = zero_bytes(e);
+  return sg | (z & ((m << 5) | (m << 4))) | (~z & nrm);
 }
 
 template <int FB, int BN>
 __device__ __forceinline__ i32x8 read_b(const char* bb, int row, int s, int h) {
   using G = L<FB, BN>;
   const char* rp = bb + row * G::RP;
-  if constexpr (G::BITS == 8) {
+  if constexpr (G::PL) {
+    // two 16-value pieces at K = 64 s + 32 p + 16 h of the stage (the fp8 operand's halves)
+    unsigned d[8];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int k0 = 64 * s + 32 * p + 16 * h;
+      const int no = k0 >> 1;  // nibble-plane byte offset (8 B = 16 values)
+      const u32x2 n = *reinterpret_cast<const u32x2*>(rp + 16 * ((no >> 4) ^ ((row >> 2) & 3)) + (no & 15));
+      if constexpr (G::BITS == 6) {
+        const int co = k0 >> 2;  // crumb-plane byte offset (4 B = 16 values)
+        const unsigned c = *reinterpret_cast<const unsigned*>(bb + BN * 64 + row * 32 + 16 * ((co >> 4) ^ ((row >> 3) & 1)) +
+                                                              (co & 15));
+        d[4 * p + 0] = e3m2x4_to_e4m3(n[0] & 0x0F0F0F0Fu, c & 0x03030303u);
+        d[4 * p + 1] = e3m2x4_to_e4m3((n[0] >> 4) & 0x0F0F0F0Fu, (c >> 2) & 0x03030303u);
+        d[4 * p + 2] = e3m2x4_to_e4m3(n[1] & 0x0F0F0F0Fu, (c >> 4) & 0x03030303u);
+        d[4 * p + 3] = e3m2x4_to_e4m3((n[1] >> 4) & 0x0F0F0F0Fu, (c >> 6) & 0x03030303u);
+      } else {
+        d[4 * p + 0] = e2m1x4_to_e4m3(n[0] & 0x0F0F0F0Fu);
+        d[4 * p + 1] = e2m1x4_to_e4m3((n[0] >> 4) & 0x0F0F0F0Fu);
+        d[4 * p + 2] = e2m1x4_to_e4m3(n[1] & 0x0F0F0F0Fu);
+        d[4 * p + 3] = e2m1x4_to_e4m3((n[1] >> 4) & 0x0F0F0F0Fu);
+      }
+    }
+    return i32x8{(int)d[0], (int)d[1], (int)d[2], (int)d[3], (int)d[4], (int)d[5], (int)d[6], (int)d[7]};
+  } else if constexpr (G::BITS == 8) {
     const u32x4 a = *reinterpret_cast<const u32x4*>(rp + 16 * ((4 * s + h) ^ fB<G::RP>(row)));
     const u32x4 b = *reinterpret_cast<const u32x4*>(rp + 16 * ((4 * s + 2 + h) ^ fB<G::RP>(row)));
     return i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
@@ -344,10 +414,12 @@ __device__ __forceinline__ i32x8 read_b(const char* bb, int row, int s, int h) {
 template <int FB, int NBUF, int BN>
 __global__ void __launch_bounds__(NT, 1)
     mx_gemm_dp_kernel(const uint8_t* __restrict__ Xq, const uint8_t* __restrict__ Xs, const uint8_t* __restrict__ Wq,
-                      const uint8_t* __restrict__ Ws, const unsigned short* __restrict__ bias,
-                      const float* __restrict__ col_scale, unsigned short* __restrict__ Y, int M, int N, int K) {
+                      const uint8_t* __restrict__ Wq2, const uint8_t* __restrict__ Ws, int wks,
+                      const unsigned short* __restrict__ bias, const float* __restrict__ col_scale,
+                      unsigned short* __restrict__ Y, int M, int N, int K) {
   using G = L<FB, BN>;
   constexpr int NJ = BN / 64;  // 32-column accumulators per wave (wave tile 128 x BN/2)
+  constexpr int MF = mfma_fmt(FB);  // an immediate operand of the MFMA
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // bijective XCD-major remap (8 XCDs, round-robin dispatch)
   const int tm = (M + BM - 1) / BM, tn = N / BN, nwg = tm * tn;
@@ -368,14 +440,15 @@ __global__ void __launch_bounds__(NT, 1)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  issue_stage<FB, BN>(smem, Xq, Xs, Wq, Ws, m0, n0, M, K, WRB, KS, 0, w, lane);
-  if (NBUF == 3 && nk > 1) issue_stage<FB, BN>(smem + G::STAGE, Xq, Xs, Wq, Ws, m0, n0, M, K, WRB, KS, 1, w, lane);
+  issue_stage<FB, BN>(smem, Xq, Xs, Wq, Wq2, Ws, wks, m0, n0, M, K, WRB, KS, 0, w, lane);
+  if (NBUF == 3 && nk > 1) issue_stage<FB, BN>(smem + G::STAGE, Xq, Xs, Wq, Wq2, Ws, wks, m0, n0, M, K, WRB, KS, 1, w, lane);
   for (int kb = 0; kb < nk; ++kb) {
     if (NBUF == 3 && kb + 1 < nk) vm_wait<G::LOADS>(); else vm_wait<0>();
     raw_barrier();  // stage kb landed for every wave; every wave is done reading stage kb - 1
     const int ahead = NBUF - 1;
     if (kb + ahead < nk)
-      issue_stage<FB, BN>(smem + ((kb + ahead) % NBUF) * G::STAGE, Xq, Xs, Wq, Ws, m0, n0, M, K, WRB, KS, kb + ahead, w, lane);
+      issue_stage<FB, BN>(smem + ((kb + ahead) % NBUF) * G::STAGE, Xq, Xs, Wq, Wq2, Ws, wks, m0, n0, M, K, WRB, KS,
+                          kb + ahead, w, lane);
     const char* buf = smem + (kb % NBUF) * G::STAGE;
     const char* ba = buf;
     const char* bb = buf + G::A_BYTES;
@@ -405,7 +478,7 @@ __global__ void __launch_bounds__(NT, 1)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
-              a[i], b[j], acc[i][j], 0, FB, 0, (int)((sa[i] >> sh) & 0xff), 0, (int)((sbw[j] >> sh) & 0xff));
+              a[i], b[j], acc[i][j], 0, MF, 0, (int)((sa[i] >> sh) & 0xff), 0, (int)((sbw[j] >> sh) & 0xff));
       __builtin_amdgcn_s_setprio(0);
     }
   }
@@ -458,7 +531,7 @@ static int tile_override() {
 template <int FB, int BN>
 void launch_dp(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq, const at::Tensor& ws,
                const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& cs, at::Tensor& y, int M, int N,
-               int K) {
+               int K, const uint8_t* wq2 = nullptr) {
   constexpr int NBUF = dp::L<FB, BN>::STAGE * 3 <= 160 * 1024 ? 3 : 2;
   const size_t lds = (size_t)NBUF * dp::L<FB, BN>::STAGE;
   static bool attr = [&] {
@@ -468,8 +541,9 @@ void launch_dp(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq,
   }();
   (void)attr;
   const int G = ((M + dp::BM - 1) / dp::BM) * (N / BN);
+  const int wks = ws.size(0) == 1 ? 0 : (int)ws.size(1);  // one exponent row shared by all columns
   hipLaunchKernelGGL((dp::mx_gemm_dp_kernel<FB, NBUF, BN>), dim3(G), dim3(dp::NT), lds, cur_stream(), xq.data_ptr<uint8_t>(),
-                     xs.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), ws.data_ptr<uint8_t>(),
+                     xs.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), wq2, ws.data_ptr<uint8_t>(), wks,
                      bias ? reinterpret_cast<const unsigned short*>(bias->data_ptr()) : nullptr,
                      cs ? cs->data_ptr<float>() : nullptr, reinterpret_cast<unsigned short*>(y.data_ptr()), M, N, K);
 }
@@ -518,20 +592,31 @@ std::vector<at::Tensor> mx_quant_fp8(at::Tensor x) {
 }
 
 // y [M, N] bf16 = MX(xq, xs) @ MX(wq, ws)^T (+ bias) (* col_scale); fmt: 0 e4m3, 2 e2m3, 3 e3m2, 4 e2m1
+// fmt 16 / 17: FPxWeight bit planes -- wq = nibble plane [N, K / 2], wq2 = 2-bit plane [N, K / 4] (FP6),
+// ws = E8M0 127s [1, K / 32] (per-row scales go in col_scale)
 at::Tensor mx_gemm(at::Tensor xq, at::Tensor xs, at::Tensor wq, at::Tensor ws, int64_t fmt,
-                   c10::optional<at::Tensor> bias, c10::optional<at::Tensor> col_scale) {
+                   c10::optional<at::Tensor> bias, c10::optional<at::Tensor> col_scale, c10::optional<at::Tensor> wq2) {
   SXE_CHECK_CUDA(xq);
-  SXE_CHECK(fmt == 0 || fmt == 2 || fmt == 3 || fmt == 4, "mx_gemm: weight format 0 (e4m3) / 2 (e2m3) / 3 (e3m2) / 4 (e2m1)");
+  SXE_CHECK(fmt == 0 || fmt == 2 || fmt == 3 || fmt == 4 || fmt == 16 || fmt == 17,
+            "mx_gemm: weight format 0 (e4m3) / 2 (e2m3) / 3 (e3m2) / 4 (e2m1) / 16, 17 (FP6 / FP4 bit planes)");
   SXE_CHECK(xq.dim() == 2 && xq.is_contiguous() && xq.scalar_type() == at::kByte, "mx_gemm: xq uint8 [M, K]");
-  const int64_t M = xq.size(0), K = xq.size(1), N = ws.size(0);
+  SXE_CHECK(wq.dim() == 2, "mx_gemm: wq [N, bytes per row]");
+  const int64_t M = xq.size(0), K = xq.size(1), N = wq.size(0);
+  const bool planes = mx::is_planes((int)fmt);
   const int bits = mx::fmt_bits((int)fmt);
   SXE_CHECK(K % mx::BK == 0, "mx_gemm: K must be a multiple of 128");
   SXE_CHECK(N % 128 == 0, "mx_gemm: N must be a multiple of 128");
   SXE_CHECK(xs.is_contiguous() && xs.scalar_type() == at::kByte && xs.numel() == M * (K / 32), "mx_gemm: xs uint8 [M, K/32]");
-  SXE_CHECK(wq.is_contiguous() && wq.scalar_type() == at::kByte && wq.numel() == N * K * bits / 8,
-            "mx_gemm: wq packed codes [N, K * bits / 8]");
-  SXE_CHECK(ws.dim() == 2 && ws.is_contiguous() && ws.scalar_type() == at::kByte && ws.size(1) == K / 32,
-            "mx_gemm: ws uint8 [N, K/32]");
+  SXE_CHECK(wq.is_contiguous() && wq.scalar_type() == at::kByte && wq.numel() == N * K * (planes ? 4 : bits) / 8,
+            "mx_gemm: wq packed codes [N, K * bits / 8] (planes: nibble plane [N, K / 2])");
+  if (planes && bits == 6) {
+    SXE_CHECK(wq2.has_value() && wq2->defined() && wq2->is_cuda() && wq2->is_contiguous() &&
+                  wq2->scalar_type() == at::kByte && wq2->numel() == N * K / 4,
+              "mx_gemm: FP6 planes need the 2-bit plane [N, K / 4]");
+  }
+  SXE_CHECK(ws.dim() == 2 && ws.is_contiguous() && ws.scalar_type() == at::kByte && ws.size(1) == K / 32 &&
+                (ws.size(0) == N || (planes && ws.size(0) == 1)),
+            "mx_gemm: ws uint8 [N, K/32] (planes: [1, K/32])");
   SXE_CHECK(xs.is_cuda() && wq.is_cuda() && ws.is_cuda(), "mx_gemm: operands on the GPU");
   if (bias.has_value() && bias->defined()) {
     SXE_CHECK(bias->is_cuda() && bias->is_contiguous() && bias->scalar_type() == at::kBFloat16 && bias->numel() == N,
@@ -550,6 +635,19 @@ at::Tensor mx_gemm(at::Tensor xq, at::Tensor xs, at::Tensor wq, at::Tensor ws, i
   c10::DeviceGuard guard(xq.device());
   auto y = at::empty({M, N}, xq.options().dtype(at::kBFloat16));
   if (M == 0) return y;
+  if (planes) {  // the LDS-DMA pipelined tiles (the planes are staged as two sub-tiles)
+    const uint8_t* w2 = bits == 6 ? wq2->data_ptr<uint8_t>() : nullptr;
+    const bool wide = N % 256 == 0 && ((M + 255) / 256) * (N / 256) >= sxe::kNumCUs;
+    if (bits == 6) {
+      wide ? mx::launch_dp<16, 256>(xq, xs, wq, ws, bias, col_scale, y, (int)M, (int)N, (int)K, w2)
+           : mx::launch_dp<16, 128>(xq, xs, wq, ws, bias, col_scale, y, (int)M, (int)N, (int)K, w2);
+    } else {
+      wide ? mx::launch_dp<17, 256>(xq, xs, wq, ws, bias, col_scale, y, (int)M, (int)N, (int)K)
+           : mx::launch_dp<17, 128>(xq, xs, wq, ws, bias, col_scale, y, (int)M, (int)N, (int)K);
+    }
+    SXE_LAUNCH_CHECK();
+    return y;
+  }
   switch (fmt) {
     case 0: mx::dispatch_tile<0>(xq, xs, wq, ws, bias, col_scale, y, (int)M, (int)N, (int)K); break;
     case 2: mx::dispatch_tile<2>(xq, xs, wq, ws, bias, col_scale, y, (int)M, (int)N, (int)K); break;
@@ -564,7 +662,8 @@ at::Tensor mx_gemm(at::Tensor xq, at::Tensor xs, at::Tensor wq, at::Tensor ws, i
 
 TORCH_LIBRARY_FRAGMENT(sxe, m) {
   m.def("mx_quant_fp8(Tensor x) -> Tensor[]");
-  m.def("mx_gemm(Tensor xq, Tensor xs, Tensor wq, Tensor ws, int fmt, Tensor? bias=None, Tensor? col_scale=None) -> Tensor");
+  m.def("mx_gemm(Tensor xq, Tensor xs, Tensor wq, Tensor ws, int fmt, Tensor? bias=None, Tensor? col_scale=None, "
+        "Tensor? wq2=None) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(sxe, CUDA, m) {
   m.impl("mx_quant_fp8", &sxe::mx_quant_fp8);

@@ -14,7 +14,8 @@ MI355X-first:
 * ``FPxWeight`` (FP6-LLM counterpart, reference inference/v2 'wf6af16'): per-output-row scaled
   FP6 or FP4 weights in a bit-plane layout whose decode is byte-parallel in registers; decode-sized
   inputs (<= 16 rows) stream 0.75 (FP6) / 0.5 (FP4) bytes per weight through the skinny MFMA
-  kernel, larger inputs decode the weight to bf16 once per call for hipBLASLt.
+  kernel; larger inputs run the bit planes straight through the block-scaled MFMA GEMM
+  (mx_gemm.hip: exact e3m2 / e2m1 -> e4m3 transcode in registers, MXFP8 activations).
 * ``fp8_linear`` runs the GEMM ON the FP8 matrix cores (hipBLASLt ``_scaled_mm`` with row-wise
   scales: 2.2 PF/s measured on MI355X vs ~1.3-1.5 PF/s for bf16), quantizing activations per row
   with the HIP kernel; ``matmul_fp8`` keeps the reference's weight-only semantics (bf16 activations
@@ -268,16 +269,29 @@ class FPxWeight:
         return (v * self.scale.view(-1, 1)).to(dtype)
 
     def linear(self, x, bias=None):
+        """Decode-sized inputs (<= 16 rows): W{6,4}A16 on the skinny kernel. Larger inputs: the bit
+        planes go straight into the block-scaled MFMA GEMM (mx_gemm.hip, transcoded to e4m3 in
+        registers, activations quantised to MXFP8 on the fly, the per-row scale in the epilogue) --
+        the weight is never widened in HBM. CPU: the dequantised fp32 product."""
         K = x.shape[-1]
         x2 = x.reshape(-1, K)
+        N = self.shape[0]
         if (x2.is_cuda and x2.dtype == torch.bfloat16 and 0 < x2.shape[0] <= 16 and x2.stride(-1) == 1
                 and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0):
             native.require_hip()
             b = bias.to(torch.bfloat16).contiguous() if bias is not None else None
             y = torch.ops.sxe.skinny_gemm_fpxw(x2, self.wa, self.wb, self.scale, b, self.bits)
-            return y.view(*x.shape[:-1], self.shape[0])
+            return y.view(*x.shape[:-1], N)
+        if x2.is_cuda and N % 128 == 0 and x2.shape[0] > 0:
+            native.require_hip()
+            if getattr(self, "_e127", None) is None or self._e127.device != x2.device:
+                self._e127 = torch.full((1, K // 32), 127, dtype=torch.uint8, device=x2.device)
+            q, s = torch.ops.sxe.mx_quant_fp8(x2.to(torch.bfloat16).contiguous())
+            b = bias.to(torch.bfloat16).contiguous() if bias is not None else None
+            y = torch.ops.sxe.mx_gemm(q, s, self.wa, self._e127, 16 if self.bits == 6 else 17, b, self.scale, self.wb)
+            return y.view(*x.shape[:-1], N).to(x.dtype)
         y = torch.nn.functional.linear(x2, self.dequantize(x2.dtype), bias.to(x2.dtype) if bias is not None else None)
-        return y.view(*x.shape[:-1], self.shape[0])
+        return y.view(*x.shape[:-1], N)
 
 
 def quantized_weight(w, kind):

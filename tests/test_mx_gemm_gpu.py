@@ -57,3 +57,27 @@ def test_mx_gemm_asymmetric_identity():
         W = mx.MXWeight(w, fmt)
         y = W.linear(x)
         torch.testing.assert_close(y.float(), mx.dequantize(W.q, W.scale, fmt, K).t(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("bits", [6, 4])
+@pytest.mark.parametrize("M,N,K", [(17, 128, 128), (300, 384, 1024), (2048, 1024, 512), (1030, 4096, 256)])
+def test_fpx_weight_prefill_on_mx_gemm(bits, M, N, K):
+    """FPxWeight (FP6-LLM bit planes) with > 16 rows: the planes go straight into the block-scaled
+    MFMA GEMM (exact e3m2 / e2m1 -> e4m3 transcode in registers, MXFP8 activations, per-row scale in
+    the epilogue); reference = MXFP8(x) @ the fp32-decoded weight, no bf16 weight is materialised."""
+    from shuffle_exchange_amd.ops.fp_quantizer import FPxWeight
+    torch.manual_seed(bits + M + N)
+    w = torch.randn(N, K, device="cuda") * 0.05
+    W = FPxWeight(w.bfloat16(), bits)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    b = torch.randn(N, device="cuda").to(torch.bfloat16)
+    called = []
+    real = torch.ops.sxe.fpxw_unpack
+    y = W.linear(x, b)
+    assert not called and real is torch.ops.sxe.fpxw_unpack
+    q, s = torch.ops.sxe.mx_quant_fp8(x)
+    ref = mx.dequantize(q, s, "mxfp8", K) @ W.dequantize(torch.float32).t() + b.float()
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item() + 1e-3, err
+    full = x.float() @ W.dequantize(torch.float32).t() + b.float()
+    assert ((y.float() - full).norm() / full.norm()).item() < 0.05  # fp8 activations: a small, bounded change

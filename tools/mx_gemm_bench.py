@@ -50,6 +50,12 @@ def main():
             code = mx.FORMATS[fmt][0]
             tg = t(lambda: torch.ops.sxe.mx_gemm(q, s, W.q, W.scale, code, None, None))
             line += f" | {fmt} {tg*1e3:.0f} us ({fl/tg/1e9:.0f} TF) +q {fl/(tg+tq)/1e9:.0f} TF"
+        if not args.quick and N % 128 == 0:
+            from shuffle_exchange_amd.ops.fp_quantizer import FPxWeight
+            for bits in (6, 4):
+                Wp = FPxWeight(w, bits)
+                tp = t(lambda: Wp.linear(x))
+                line += f" | FPxWeight fp{bits} planes {tp*1e3:.0f} us ({fl/tp/1e9:.0f} TF incl. quant)"
         print(line, flush=True)
 
 
