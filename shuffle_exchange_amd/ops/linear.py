@@ -53,8 +53,11 @@ def _pro_weight(weight):
         if weight.dtype == torch.bfloat16 and weight.dim() == 2 and weight.is_contiguous() and weight.data_ptr() % 16 == 0:
             return weight, None
         return None
-    q, sc = getattr(weight, "q", None), getattr(weight, "scale", None)
-    if q is not None and sc is not None and q.element_size() == 1 and q.dim() == 2 and q.is_contiguous():
+    from .fp_quantizer import FP8Weight
+    if not isinstance(weight, FP8Weight):  # other quantized formats (MX, FP6/FP4 planes, int) run unfused
+        return None
+    q, sc = weight.q, weight.scale
+    if q.element_size() == 1 and q.dim() == 2 and q.is_contiguous():
         return q.view(torch.uint8), sc
     return None
 
