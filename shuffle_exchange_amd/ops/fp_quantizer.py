@@ -251,6 +251,9 @@ class FPxWeight:
             self.wa, self.wb = _nibble_words(codes), None
         else:
             self.wa, self.wb = _nibble_words(codes >> 2), _crumb_words(codes & 3)
+        # unit E8M0 block exponents for the MX GEMM (the per-row scale is its epilogue scale); made
+        # here, not lazily, so a HIP-graph capture never allocates it
+        self._e127 = torch.full((1, K // 32), 127, dtype=torch.uint8, device=self.wa.device)
 
     def _codes_back(self):
         N, K = self.shape
@@ -284,8 +287,6 @@ class FPxWeight:
             return y.view(*x.shape[:-1], N)
         if x2.is_cuda and N % 128 == 0 and x2.shape[0] > 0:
             native.require_hip()
-            if getattr(self, "_e127", None) is None or self._e127.device != x2.device:
-                self._e127 = torch.full((1, K // 32), 127, dtype=torch.uint8, device=x2.device)
             q, s = torch.ops.sxe.mx_quant_fp8(x2.to(torch.bfloat16).contiguous())
             b = bias.to(torch.bfloat16).contiguous() if bias is not None else None
             y = torch.ops.sxe.mx_gemm(q, s, self.wa, self._e127, 16 if self.bits == 6 else 17, b, self.scale, self.wb)

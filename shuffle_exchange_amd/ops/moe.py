@@ -216,7 +216,8 @@ class IntWeight:
     def linear(self, x, bias=None):
         K = x.shape[-1]
         x2 = x.reshape(-1, K)
-        offs = torch.tensor([0, x2.shape[0]], dtype=torch.int32, device=x2.device)
+        offs = torch.zeros(2, dtype=torch.int32, device=x2.device)  # no host copy: HIP-graph capturable
+        offs[1:].fill_(x2.shape[0])
         y = grouped_gemm_q(x2.to(torch.bfloat16) if x2.is_cuda else x2, self.e, offs)
         if bias is not None:
             y = y + bias.to(y.dtype)
