@@ -162,6 +162,122 @@ __global__ void __launch_bounds__(NTHR, 2) grouped_gemm_kernel(const unsigned sh
 }
 
 
+
+// ---------------------------------------------------------------------------------------------------
+// Large-expert form (bf16): 256 x 256 output tile, 4 waves (2 x 2, 128 x 128 each = 16 accumulators
+// in AGPRs), K in stages of 64 staged by LDS-DMA (global_load_lds) into two stage buffers with a raw
+// s_barrier, so the next stage's DMA overlaps the current stage's 64 MFMAs per wave -- the same
+// pipeline as the MX GEMM (mx_gemm.hip namespace dp). A glds writes lane-linear LDS, so the
+// bank-conflict swizzle goes on the source address: 16-byte slot s of a 128-byte row r holds chunk
+// s ^ ((r >> 1) & 7). Rows past the expert's range load the range's last row and are not stored.
+namespace dp {
+constexpr int BM = 256, BN = 256, BKD = 64;
+constexpr int TILE = BM * BKD * 2;           // 32 KiB per operand per stage
+constexpr int STAGE = 2 * TILE;
+__device__ __forceinline__ int sw(int r) { return (r >> 1) & 7; }
+__device__ __forceinline__ void glds16(const void* g, char* l) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// WN = waves along N (2 -> 4 waves of 128 x 128; 4 -> 8 waves of 128 x 64, two per SIMD -- the
+// default: 800-903 TF/s vs 713-853 for 4 waves and 472-600 for the 128 x 128 kernel at 1024-4096
+// rows per expert, profiles/grouped_gemm_bench.log)
+template <typename ScaleT, int WN>
+__global__ void __launch_bounds__(128 * WN, 1) grouped_gemm_dp_kernel(const unsigned short* __restrict__ X,
+                                                                const unsigned short* __restrict__ W,
+                                                                const int* __restrict__ offs, int E,
+                                                                const ScaleT* __restrict__ scale,
+                                                                unsigned short* __restrict__ Y, int R, int N, int K) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int idx = blockIdx.x, e = 0, lo = 0, hi = 0;
+  for (; e < E; ++e) {
+    const int a = offs[e], b = offs[e + 1];
+    const int nt = (b - a + BM - 1) / BM;
+    if (idx < nt) {
+      lo = a + idx * BM;
+      hi = min(min(b, lo + BM), R);
+      break;
+    }
+    idx -= nt;
+  }
+  if (e == E || lo < 0 || lo >= hi) return;  // surplus workgroup of the upper-bound grid (uniform)
+  const int n0 = blockIdx.y * BN;
+  const unsigned short* We = W + (int64_t)e * N * K;
+  constexpr int NW = 2 * WN, NJ = 4 * 2 / WN, PI = 32 / NW;  // waves, 32-col tiles per wave, glds per operand
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w / WN, wn = w % WN, h = lane >> 5, l32 = lane & 31;
+
+  auto issue = [&](char* buf, int kb) {
+#pragma unroll
+    for (int j = 0; j < PI; ++j) {  // A: 32 instructions of 8 rows x 128 B
+      const int g = w * PI + j, row = 8 * g + (lane >> 3), slot = lane & 7;
+      const int gr = min(lo + row, hi - 1);
+      glds16(X + (int64_t)gr * K + (int64_t)kb * BKD + 8 * (slot ^ sw(row)), buf + 8 * g * 128);
+    }
+#pragma unroll
+    for (int j = 0; j < PI; ++j) {  // B: the expert's weight rows n0 .. n0 + 255
+      const int g = w * PI + j, row = 8 * g + (lane >> 3), slot = lane & 7;
+      glds16(We + (int64_t)(n0 + row) * K + (int64_t)kb * BKD + 8 * (slot ^ sw(row)), buf + TILE + 8 * g * 128);
+    }
+  };
+
+  f32x16 acc[4][NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = zero16();
+
+  const int nk = K / BKD;
+  issue(smem, 0);
+  for (int kb = 0; kb < nk; ++kb) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();  // stage kb landed for every wave; every wave is done with stage kb - 1
+    if (kb + 1 < nk) issue(smem + ((kb + 1) & 1) * STAGE, kb + 1);
+    const char* ba = smem + (kb & 1) * STAGE;
+    const char* bb = ba + TILE;
+#pragma unroll
+    for (int ks = 0; ks < BKD / 16; ++ks) {
+      bf16x8 a[4], b[NJ];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 128 + i * 32 + l32;
+        a[i] = *reinterpret_cast<const bf16x8*>(ba + row * 128 + 16 * ((2 * ks + h) ^ sw(row)));
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int row = wn * (BN / WN) + j * 32 + l32;
+        b[j] = *reinterpret_cast<const bf16x8*>(bb + row * 128 + 16 * ((2 * ks + h) ^ sw(row)));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int n = n0 + wn * (BN / WN) + j * 32 + l32;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = lo + wm * 128 + i * 32 + acc_row(r, h);
+        if (m < hi) {
+          float v = acc[i][j][r];
+          if (scale) v *= (float)scale[m];
+          Y[(int64_t)m * N + n] = f32_to_bf16(v);
+        }
+      }
+  }
+}
+}  // namespace dp
+
 // Mixed-precision variant: W[e] as int8 / int4 codes [E, N, K * BITS / 8] with fp32 group scales
 // [E, N, K / gs]; everything else as grouped_gemm_kernel.
 template <typename ScaleT, int BITS>
@@ -268,12 +384,51 @@ at::Tensor grouped_gemm(at::Tensor x, at::Tensor w, at::Tensor offsets, c10::opt
   c10::DeviceGuard guard(x.device());
   auto y = at::empty({R, N}, x.options());
   if (R == 0 || N == 0) return y;
-  const size_t lds = 2 * gg::TILE_BYTES;
-  const dim3 grid((unsigned)((R + gg::BM - 1) / gg::BM + E), (unsigned)(N / gg::BN));
   auto X = reinterpret_cast<const unsigned short*>(x.data_ptr());
   auto Wp = reinterpret_cast<const unsigned short*>(w.data_ptr());
   auto Yp = reinterpret_cast<unsigned short*>(y.data_ptr());
   const int* off = offsets.data_ptr<int>();
+  // many rows per expert: the LDS-DMA pipelined 256 x 256 tiles (decided from the shapes only --
+  // the row counts stay on the device; measured crossover in profiles/grouped_gemm_bench.log)
+  const char* force = getenv("SXE_GG_TILE");
+  const bool big = force ? atoi(force) == 256 : (R >= 512 * E && N % gg::dp::BN == 0 && K % gg::dp::BKD == 0);
+  if (big && N % gg::dp::BN == 0 && K % gg::dp::BKD == 0) {
+    const size_t lds_dp = 2 * gg::dp::STAGE;
+    const dim3 grid_dp((unsigned)((R + gg::dp::BM - 1) / gg::dp::BM + E), (unsigned)(N / gg::dp::BN));
+    const char* wne = getenv("SXE_GG_WN");
+    const int wn = wne ? atoi(wne) : 4;
+    auto go = [&](auto kern, int nthr) {
+      SXE_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dp));
+      return nthr;
+    };
+    if (hs && row_scale->scalar_type() == at::kBFloat16) {
+      const __bf16* rs = reinterpret_cast<const __bf16*>(row_scale->data_ptr());
+      if (wn == 2) {
+        go(gg::dp::grouped_gemm_dp_kernel<__bf16, 2>, 256);
+        hipLaunchKernelGGL((gg::dp::grouped_gemm_dp_kernel<__bf16, 2>), grid_dp, dim3(256), lds_dp, cur_stream(), X, Wp,
+                           off, (int)E, rs, Yp, (int)R, (int)N, (int)K);
+      } else {
+        go(gg::dp::grouped_gemm_dp_kernel<__bf16, 4>, 512);
+        hipLaunchKernelGGL((gg::dp::grouped_gemm_dp_kernel<__bf16, 4>), grid_dp, dim3(512), lds_dp, cur_stream(), X, Wp,
+                           off, (int)E, rs, Yp, (int)R, (int)N, (int)K);
+      }
+    } else {
+      const float* rs = hs ? row_scale->data_ptr<float>() : nullptr;
+      if (wn == 2) {
+        go(gg::dp::grouped_gemm_dp_kernel<float, 2>, 256);
+        hipLaunchKernelGGL((gg::dp::grouped_gemm_dp_kernel<float, 2>), grid_dp, dim3(256), lds_dp, cur_stream(), X, Wp,
+                           off, (int)E, rs, Yp, (int)R, (int)N, (int)K);
+      } else {
+        go(gg::dp::grouped_gemm_dp_kernel<float, 4>, 512);
+        hipLaunchKernelGGL((gg::dp::grouped_gemm_dp_kernel<float, 4>), grid_dp, dim3(512), lds_dp, cur_stream(), X, Wp,
+                           off, (int)E, rs, Yp, (int)R, (int)N, (int)K);
+      }
+    }
+    SXE_LAUNCH_CHECK();
+    return y;
+  }
+  const size_t lds = 2 * gg::TILE_BYTES;
+  const dim3 grid((unsigned)((R + gg::BM - 1) / gg::BM + E), (unsigned)(N / gg::BN));
   if (hs && row_scale->scalar_type() == at::kBFloat16) {
     static bool a = [&] {
       SXE_HIP_CHECK(hipFuncSetAttribute((const void*)gg::grouped_gemm_kernel<__bf16>,

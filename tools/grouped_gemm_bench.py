@@ -30,7 +30,9 @@ def t(fn, n=20):
 for name, (E, N, K, tokens, k) in {"mixtral gate_up": (8, 28672, 4096, 4096, 2),
                                    "mixtral down": (8, 4096, 14336, 4096, 2),
                                    "mixtral gate_up decode": (8, 28672, 4096, 64, 2),
-                                   "qwen-moe gate_up": (60, 2816, 2048, 4096, 4)}.items():
+                                   "qwen-moe gate_up": (60, 2816, 2048, 4096, 4),
+                                   "mixtral gate_up 16k": (8, 28672, 4096, 16384, 2),
+                                   "mixtral down 16k": (8, 4096, 14336, 16384, 2)}.items():
     torch.manual_seed(0)
     flat = torch.randint(0, E, (tokens * k,), device="cuda").sort().values
     offs = moe_ops.expert_offsets(flat, E)
@@ -47,7 +49,17 @@ for name, (E, N, K, tokens, k) in {"mixtral gate_up": (8, 28672, 4096, 4096, 2),
         return y
 
     g = t(lambda: torch.ops.sxe.grouped_gemm(x, w, offs, None))
+    os.environ["SXE_GG_TILE"] = "128"
+    g128 = t(lambda: torch.ops.sxe.grouped_gemm(x, w, offs, None))
+    os.environ["SXE_GG_TILE"] = "256"
+    os.environ["SXE_GG_WN"] = "2"
+    g256_4w = t(lambda: torch.ops.sxe.grouped_gemm(x, w, offs, None)) if N % 256 == 0 else float("nan")
+    os.environ["SXE_GG_WN"] = "4"
+    g256 = t(lambda: torch.ops.sxe.grouped_gemm(x, w, offs, None)) if N % 256 == 0 else float("nan")
+    del os.environ["SXE_GG_TILE"], os.environ["SXE_GG_WN"]
     lp = t(loop)
     fl = 2 * R * N * K / 1e9
-    print(f"[{name}] rows {R}: grouped kernel {g:.3f} ms ({fl / g:.0f} TF) | per-expert hipBLASLt loop "
+    print(f"[{name}] rows {R}: grouped kernel (auto) {g:.3f} ms ({fl / g:.0f} TF) | 128x128 {g128:.3f} ms "
+          f"({fl / g128:.0f} TF) | 256x256 LDS-DMA 4 waves {g256_4w:.3f} ms ({fl / g256_4w:.0f} TF), 8 waves "
+          f"{g256:.3f} ms ({fl / g256:.0f} TF) | per-expert hipBLASLt loop "
           f"{lp:.3f} ms ({fl / lp:.0f} TF)", flush=True)
