@@ -391,7 +391,7 @@ at::Tensor grouped_gemm(at::Tensor x, at::Tensor w, at::Tensor offsets, c10::opt
   // many rows per expert: the LDS-DMA pipelined 256 x 256 tiles (decided from the shapes only --
   // the row counts stay on the device; measured crossover in profiles/grouped_gemm_bench.log)
   const char* force = getenv("SXE_GG_TILE");
-  const bool big = force ? atoi(force) == 256 : (R >= 512 * E && N % gg::dp::BN == 0 && K % gg::dp::BKD == 0);
+  const bool big = force ? atoi(force) == 256 : (R >= 256 * E && N % gg::dp::BN == 0 && K % gg::dp::BKD == 0);
   if (big && N % gg::dp::BN == 0 && K % gg::dp::BKD == 0) {
     const size_t lds_dp = 2 * gg::dp::STAGE;
     const dim3 grid_dp((unsigned)((R + gg::dp::BM - 1) / gg::dp::BM + E), (unsigned)(N / gg::dp::BN));
