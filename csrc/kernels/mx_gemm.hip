@@ -256,7 +256,7 @@ __global__ void mx_quant_fp8_kernel(const unsigned short* __restrict__ x, uint8_
 // rows a ds_read_b128 phase touches on distinct banks. fp6 rows (96 data bytes) are padded to 128 B.
 namespace dp {
 constexpr int BM = 256, NT = 256;
-template <int FB, int BN> struct L {
+template <int FB, int BN, int NWV = 4> struct L {
   static constexpr bool PL = is_planes(FB);
   static constexpr int BITS = fmt_bits(FB);
   static constexpr int RB = 16 * BITS;                // data bytes per row per 128-K stage
@@ -264,12 +264,14 @@ template <int FB, int BN> struct L {
   static constexpr int CH = PL ? 4 : RB / 16;         // data chunks per row
   static constexpr int SL = RP / 16;                  // slots per row
   static constexpr int ROWS_PER_INSTR = 64 / SL;      // rows one wave instruction fills
-  static constexpr int CR_INSTR = (PL && BITS == 6) ? BN / 128 : 0;  // crumb-plane (32 B rows) instructions
-  static constexpr int B_INSTR = BN / ROWS_PER_INSTR / 4 + CR_INSTR;  // per wave per stage
-  static constexpr int SI = (BM + BN + 255) / 256;     // exponent instructions per wave (64 rows each)
-  static constexpr int A_BYTES = BM * 128, B_BYTES = BN * RP + (CR_INSTR ? BN * 32 : 0), S_BYTES = 4 * SI * 64 * 4;
+  static constexpr int A_INSTR = BM / 8 / NWV;        // A: 8 rows x 128 B per instruction
+  static constexpr int NI = BN / ROWS_PER_INSTR / NWV; // B codes (planes: the nibble plane)
+  static constexpr int CR_INSTR = (PL && BITS == 6) ? BN / 32 / NWV : 0;  // crumb-plane (32 B rows) instructions
+  static constexpr int B_INSTR = NI + CR_INSTR;        // per wave per stage
+  static constexpr int SI = ((BM + BN) / 64 + NWV - 1) / NWV;  // exponent instructions per wave (64 rows each)
+  static constexpr int A_BYTES = BM * 128, B_BYTES = BN * RP + (CR_INSTR ? BN * 32 : 0), S_BYTES = NWV * SI * 64 * 4;
   static constexpr int STAGE = A_BYTES + B_BYTES + S_BYTES;
-  static constexpr int LOADS = 8 + B_INSTR + SI;       // glds per wave per stage (A, B, exponents)
+  static constexpr int LOADS = A_INSTR + B_INSTR + SI;  // glds per wave per stage (A, B, exponents)
 };
 __device__ __forceinline__ int fA(int r) { return (r >> 1) & 7; }
 template <int RP> __device__ __forceinline__ int fB(int r) { return RP == 64 ? ((r >> 2) & 3) : ((r >> 1) & 7); }
@@ -286,21 +288,21 @@ __device__ __forceinline__ void glds4(const void* g, char* l) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 4, 0, 0);
 }
 
-template <int FB, int BN>
+template <int FB, int BN, int NWV>
 __device__ __forceinline__ void issue_stage(char* buf, const uint8_t* Xq, const uint8_t* Xs, const uint8_t* Wq,
                                             const uint8_t* Wq2, const uint8_t* Ws, int wks, int m0, int n0, int M,
                                             int K, int64_t WRB, int KS, int kb, int w, int lane) {
-  using G = L<FB, BN>;
-  // A: 32 instructions of 8 rows x 128 B, 8 per wave
+  using G = L<FB, BN, NWV>;
+  // A: BM / 8 instructions of 8 rows x 128 B
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int g = w * 8 + j, row = 8 * g + (lane >> 3), slot = lane & 7;
+  for (int j = 0; j < G::A_INSTR; ++j) {
+    const int g = w * G::A_INSTR + j, row = 8 * g + (lane >> 3), slot = lane & 7;
     const int gr = min(m0 + row, M - 1);
     glds16(Xq + (int64_t)gr * K + (int64_t)kb * 128 + 16 * (slot ^ fA(row)), buf + 8 * g * 128);
   }
   // B
   if constexpr (G::PL) {
-    constexpr int NI = BN / 64;  // nibble plane: 64 B rows, 16 rows per instruction
+    constexpr int NI = G::NI;  // nibble plane: 64 B rows, 16 rows per instruction
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int g = w * NI + j, row = 16 * g + (lane >> 2), ch = (lane & 3) ^ ((row >> 2) & 3);
@@ -313,8 +315,8 @@ __device__ __forceinline__ void issue_stage(char* buf, const uint8_t* Xq, const 
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < G::B_INSTR; ++j) {
-      const int g = w * G::B_INSTR + j, row = G::ROWS_PER_INSTR * g + lane / G::SL, slot = lane % G::SL;
+    for (int j = 0; j < G::NI; ++j) {
+      const int g = w * G::NI + j, row = G::ROWS_PER_INSTR * g + lane / G::SL, slot = lane % G::SL;
       int ch = slot ^ fB<G::RP>(row);
       if (ch >= G::CH) ch = 0;  // fp6 padding slots: any in-row chunk, never read
       glds16(Wq + (int64_t)(n0 + row) * WRB + (int64_t)kb * G::RB + 16 * ch,
@@ -411,14 +413,16 @@ __device__ __forceinline__ i32x8 read_b(const char* bb, int row, int s, int h) {
   }
 }
 
-template <int FB, int NBUF, int BN>
-__global__ void __launch_bounds__(NT, 1)
+template <int FB, int NBUF, int BN, int NWV>
+__global__ void __launch_bounds__(64 * NWV, 1)
     mx_gemm_dp_kernel(const uint8_t* __restrict__ Xq, const uint8_t* __restrict__ Xs, const uint8_t* __restrict__ Wq,
                       const uint8_t* __restrict__ Wq2, const uint8_t* __restrict__ Ws, int wks,
                       const unsigned short* __restrict__ bias, const float* __restrict__ col_scale,
                       unsigned short* __restrict__ Y, int M, int N, int K) {
-  using G = L<FB, BN>;
-  constexpr int NJ = BN / 64;  // 32-column accumulators per wave (wave tile 128 x BN/2)
+  using G = L<FB, BN, NWV>;
+  constexpr int WNW = NWV / 2;   // waves along N (2 along M)
+  constexpr int TNW = BN / WNW;  // wave tile 128 x TNW
+  constexpr int NJ = TNW / 32;   // 32-column accumulators per wave
   constexpr int MF = mfma_fmt(FB);  // an immediate operand of the MFMA
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // bijective XCD-major remap (8 XCDs, round-robin dispatch)
@@ -427,7 +431,7 @@ __global__ void __launch_bounds__(NT, 1)
   const int pid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
   const int m0 = (pid % tm) * BM, n0 = (pid / tm) * BN;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int wm = w >> 1, wn = w & 1, h = lane >> 5, l32 = lane & 31;
+  const int wm = w / WNW, wn = w % WNW, h = lane >> 5, l32 = lane & 31;
   const int KS = K / 32;
   const int64_t WRB = (int64_t)K * G::BITS / 8;
   const int nk = K / BK;
@@ -440,14 +444,14 @@ __global__ void __launch_bounds__(NT, 1)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  issue_stage<FB, BN>(smem, Xq, Xs, Wq, Wq2, Ws, wks, m0, n0, M, K, WRB, KS, 0, w, lane);
-  if (NBUF == 3 && nk > 1) issue_stage<FB, BN>(smem + G::STAGE, Xq, Xs, Wq, Wq2, Ws, wks, m0, n0, M, K, WRB, KS, 1, w, lane);
+  issue_stage<FB, BN, NWV>(smem, Xq, Xs, Wq, Wq2, Ws, wks, m0, n0, M, K, WRB, KS, 0, w, lane);
+  if (NBUF == 3 && nk > 1) issue_stage<FB, BN, NWV>(smem + G::STAGE, Xq, Xs, Wq, Wq2, Ws, wks, m0, n0, M, K, WRB, KS, 1, w, lane);
   for (int kb = 0; kb < nk; ++kb) {
     if (NBUF == 3 && kb + 1 < nk) vm_wait<G::LOADS>(); else vm_wait<0>();
     raw_barrier();  // stage kb landed for every wave; every wave is done reading stage kb - 1
     const int ahead = NBUF - 1;
     if (kb + ahead < nk)
-      issue_stage<FB, BN>(smem + ((kb + ahead) % NBUF) * G::STAGE, Xq, Xs, Wq, Wq2, Ws, wks, m0, n0, M, K, WRB, KS,
+      issue_stage<FB, BN, NWV>(smem + ((kb + ahead) % NBUF) * G::STAGE, Xq, Xs, Wq, Wq2, Ws, wks, m0, n0, M, K, WRB, KS,
                           kb + ahead, w, lane);
     const char* buf = smem + (kb % NBUF) * G::STAGE;
     const char* ba = buf;
@@ -457,7 +461,7 @@ __global__ void __launch_bounds__(NT, 1)
 #pragma unroll
     for (int i = 0; i < 4; ++i) sa[i] = sc[wm * 128 + i * 32 + l32];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) sbw[j] = sc[BM + wn * (BN / 2) + j * 32 + l32];
+    for (int j = 0; j < NJ; ++j) sbw[j] = sc[BM + wn * TNW + j * 32 + l32];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       i32x8 a[4], b[NJ];
@@ -470,7 +474,7 @@ __global__ void __launch_bounds__(NT, 1)
         a[i] = i32x8{(int)x0[0], (int)x0[1], (int)x0[2], (int)x0[3], (int)x1[0], (int)x1[1], (int)x1[2], (int)x1[3]};
       }
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) b[j] = read_b<FB, BN>(bb, wn * (BN / 2) + j * 32 + l32, s, h);
+      for (int j = 0; j < NJ; ++j) b[j] = read_b<FB, BN>(bb, wn * TNW + j * 32 + l32, s, h);
       const int sh = 8 * (2 * s + h);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -484,7 +488,7 @@ __global__ void __launch_bounds__(NT, 1)
   }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int n = n0 + wn * (BN / 2) + j * 32 + l32;
+    const int n = n0 + wn * TNW + j * 32 + l32;
     const float cs = col_scale ? col_scale[n] : 1.f;
     const float bv = bias ? bf16_to_f32(bias[n]) : 0.f;
 #pragma unroll
@@ -519,7 +523,8 @@ void launch(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq, co
 
 // tile variants: 0 auto, 1 = 128x128 / 4 waves, 2 = 256x128 / 4 waves, 3 = 256x256 / 4 waves
 // (128x128 per wave, accumulators in AGPRs), 4 = 256x256 / 8 waves, 5 = 256x128 / 8 waves,
-// 6 = 256x256 / 4 waves LDS-DMA pipelined (namespace dp), 7 = the same at 256x128
+// 6 = 256x256 / 8 waves LDS-DMA pipelined (namespace dp), 7 = the same at 256x128 / 4 waves,
+// 8 = 256x256 / 4 waves
 static int tile_override() {
   static int v = [] {
     const char* e = getenv("SXE_MX_TILE");
@@ -528,23 +533,24 @@ static int tile_override() {
   return v;
 }
 
-template <int FB, int BN>
+template <int FB, int BN, int NWV = (BN == 256 ? 8 : 4)>
 void launch_dp(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq, const at::Tensor& ws,
                const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& cs, at::Tensor& y, int M, int N,
                int K, const uint8_t* wq2 = nullptr) {
-  constexpr int NBUF = dp::L<FB, BN>::STAGE * 3 <= 160 * 1024 ? 3 : 2;
-  const size_t lds = (size_t)NBUF * dp::L<FB, BN>::STAGE;
+  using G = dp::L<FB, BN, NWV>;
+  constexpr int NBUF = G::STAGE * 3 <= 160 * 1024 ? 3 : 2;
+  const size_t lds = (size_t)NBUF * G::STAGE;
   static bool attr = [&] {
-    SXE_HIP_CHECK(hipFuncSetAttribute((const void*)dp::mx_gemm_dp_kernel<FB, NBUF, BN>,
+    SXE_HIP_CHECK(hipFuncSetAttribute((const void*)dp::mx_gemm_dp_kernel<FB, NBUF, BN, NWV>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     return true;
   }();
   (void)attr;
-  const int G = ((M + dp::BM - 1) / dp::BM) * (N / BN);
+  const int G_ = ((M + dp::BM - 1) / dp::BM) * (N / BN);
   const int wks = ws.size(0) == 1 ? 0 : (int)ws.size(1);  // one exponent row shared by all columns
-  hipLaunchKernelGGL((dp::mx_gemm_dp_kernel<FB, NBUF, BN>), dim3(G), dim3(dp::NT), lds, cur_stream(), xq.data_ptr<uint8_t>(),
-                     xs.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), wq2, ws.data_ptr<uint8_t>(), wks,
-                     bias ? reinterpret_cast<const unsigned short*>(bias->data_ptr()) : nullptr,
+  hipLaunchKernelGGL((dp::mx_gemm_dp_kernel<FB, NBUF, BN, NWV>), dim3(G_), dim3(64 * NWV), lds, cur_stream(),
+                     xq.data_ptr<uint8_t>(), xs.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), wq2,
+                     ws.data_ptr<uint8_t>(), wks, bias ? reinterpret_cast<const unsigned short*>(bias->data_ptr()) : nullptr,
                      cs ? cs->data_ptr<float>() : nullptr, reinterpret_cast<unsigned short*>(y.data_ptr()), M, N, K);
 }
 
@@ -560,9 +566,10 @@ void dispatch_tile(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor&
     const int64_t g256 = (int64_t)((M + 255) / 256) * (N / 256), g2561 = (int64_t)((M + 255) / 256) * (N / 128);
     v = (N % 256 == 0 && M > 256 && g256 >= kNumCUs) ? 6 : (M > 256 && g2561 >= kNumCUs / 2) ? 7 : 1;
   }
-  if ((v == 3 || v == 4 || v == 6) && N % 256 != 0) v = 2;
+  if ((v == 3 || v == 4 || v == 6 || v == 8) && N % 256 != 0) v = 2;
   switch (v) {
     case 6: launch_dp<FB, 256>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
+    case 8: launch_dp<FB, 256, 4>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
     case 7: launch_dp<FB, 128>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
     case 2: launch<256, 128, 2, 2, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
     case 3: launch<256, 256, 2, 2, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
