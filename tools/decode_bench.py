@@ -21,7 +21,8 @@ def main():
     ap.add_argument("--batches", default="1,8,32,64")
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--modes", default="eager,graphs,graphs+fp8",
-                    help="comma list of eager | graphs | graphs+fp8 (FP8 row-scaled weights, W8A16)")
+                    help="comma list of eager | graphs | graphs+<weight_quant> (fp8 W8A16, fp6 / fp4 FP6-LLM "
+                         "planes, mxfp8 / mxfp6 / mxfp4 OCP-MX, int8 / int4)")
     a = ap.parse_args()
     from shuffle_exchange_amd.inference.v2 import RaggedInferenceEngineConfig, build_engine
     from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
@@ -37,7 +38,7 @@ def main():
         graphs = mode.startswith("graphs")
         eng = build_engine(model, RaggedInferenceEngineConfig(kv_block_size=64, num_kv_blocks=4096,
                                                               decode_graphs=graphs,
-                                                              weight_quant="fp8" if "fp8" in mode else None))
+                                                              weight_quant=mode.split("+", 1)[1] if "+" in mode else None))
         for B in [int(x) for x in a.batches.split(",")]:
             uids = list(range(B))
             g = torch.Generator().manual_seed(B)
