@@ -556,3 +556,154 @@ def has_reduce_scatter_tensor():
 
 def has_all_gather_into_tensor():
     return True
+
+
+# ------------------------------------------------------------------------------------------------
+# the rest of the reference facade (deepspeed/comm/comm.py): list-form collectives, capability
+# queries, environment discovery and the timing decorator
+def is_available():
+    return tdist.is_available()
+
+
+def set_backend(backend_name=None):
+    """Select the backend ``init_distributed`` uses when none is passed (reference set_backend)."""
+    if backend_name:
+        os.environ["SXE_DIST_BACKEND"] = backend_name
+
+
+def init_deepspeed_backend(ds_backend=None, timeout=None, init_method=None):
+    """Reference name for bringing up the communication backend: here always torch.distributed
+    (RCCL over xGMI for GPU tensors, gloo for CPU plumbing)."""
+    init_distributed(dist_backend=ds_backend, timeout=timeout, init_method=init_method)
+
+
+def get_all_ranks_from_group(group=None):
+    return group_ranks(group)
+
+
+def has_all_reduce_coalesced():
+    return hasattr(tdist, "all_reduce_coalesced")
+
+
+def has_coalescing_manager():
+    return hasattr(tdist, "_coalescing_manager")
+
+
+def all_gather_coalesced(output_tensors, input_tensors, group=None, async_op=False):
+    """Gather several tensors at once: their flat concatenation in ONE all-gather (one RCCL launch
+    instead of one per tensor), split back into ``output_tensors[i]`` ([world * numel_i] each)."""
+    n = get_world_size(group)
+    if n == 1:
+        for o, i in zip(output_tensors, input_tensors):
+            o.copy_(i.reshape(o.shape))
+        return None
+    flat = torch.cat([t.reshape(-1) for t in input_tensors])
+    out = torch.empty(n * flat.numel(), dtype=flat.dtype, device=flat.device)
+    all_gather_into_tensor(out, flat, group=group)
+    rows = out.view(n, -1)
+    o = 0
+    for dst, src in zip(output_tensors, input_tensors):
+        k = src.numel()
+        dst.view(n, k).copy_(rows[:, o:o + k])
+        o += k
+    return None
+
+
+def gather(tensor, gather_list=None, dst=0, group=None, async_op=False):
+    if get_world_size(group) == 1:
+        if gather_list:
+            gather_list[0].copy_(tensor)
+        return None
+    return _timed("gather", lambda: tdist.gather(tensor, gather_list, dst=dst, group=group, async_op=async_op), tensor,
+                  group, async_op)
+
+
+def scatter(tensor, scatter_list=None, src=0, group=None, async_op=False):
+    if get_world_size(group) == 1:
+        if scatter_list:
+            tensor.copy_(scatter_list[0])
+        return None
+    return _timed("scatter", lambda: tdist.scatter(tensor, scatter_list, src=src, group=group, async_op=async_op),
+                  tensor, group, async_op, outs=[tensor])
+
+
+def reduce_scatter(output, input_list, op=ReduceOp.SUM, group=None, async_op=False):
+    """List form: the inputs are concatenated and reduce-scattered as one tensor (the reference
+    calls the backend's list reduce_scatter; one contiguous RCCL call is cheaper on xGMI)."""
+    flat = torch.cat([t.reshape(-1) for t in input_list])
+    return reduce_scatter_tensor(output.view(-1), flat, op=op, group=group, async_op=async_op)
+
+
+def timed_op(func):
+    """Decorator recording a call's wall time and payload in the comms logger (reference
+    comm.py timed_op); the facade's own collectives log through ``_timed`` already."""
+    import functools
+
+    @functools.wraps(func)
+    def wrapper(*args, **kwargs):
+        t = kwargs.get("tensor", args[0] if args and torch.is_tensor(args[0]) else None)
+        if t is None or not torch.is_tensor(t):
+            return func(*args, **kwargs)
+        return _timed(func.__name__, lambda: func(*args, **kwargs), t, kwargs.get("group"), False)
+    return wrapper
+
+
+def mpi_discovery(distributed_port=29500, verbose=True):
+    """RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* from an MPI launcher's environment (OpenMPI,
+    MPICH / Intel MPI PMI, Slurm), without mpi4py: the launcher env is enough on one node and the
+    multinode runners export MASTER_ADDR themselves."""
+    env = os.environ
+    for rk, ws, lr in (("OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_RANK"),
+                       ("PMI_RANK", "PMI_SIZE", "MPI_LOCALRANKID"), ("SLURM_PROCID", "SLURM_NTASKS", "SLURM_LOCALID")):
+        if rk in env:
+            env["RANK"], env["WORLD_SIZE"] = env[rk], env.get(ws, "1")
+            env["LOCAL_RANK"] = env.get(lr, "0")
+            break
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    env.setdefault("MASTER_PORT", str(distributed_port))
+    if verbose:
+        log_dist(f"mpi_discovery: rank {env.get('RANK')} / {env.get('WORLD_SIZE')}", ranks=[0])
+
+
+def in_aml():
+    return "AZUREML_EXPERIMENT_ID" in os.environ
+
+
+def in_aws_sm():
+    return "SM_TRAINING_ENV" in os.environ
+
+
+def in_dlts():
+    return "DLTS_JOB_ID" in os.environ
+
+
+def patch_aml_env_for_torch_nccl_backend(master_port=6105, verbose=True):
+    """AzureML: derive the torch.distributed rendezvous env from its OpenMPI variables."""
+    env = os.environ
+    env.setdefault("RANK", env.get("OMPI_COMM_WORLD_RANK", "0"))
+    env.setdefault("WORLD_SIZE", env.get("OMPI_COMM_WORLD_SIZE", "1"))
+    env.setdefault("LOCAL_RANK", env.get("OMPI_COMM_WORLD_LOCAL_RANK", "0"))
+    env.setdefault("MASTER_ADDR", env.get("AZ_BATCH_MASTER_NODE", "127.0.0.1:").split(":")[0] or "127.0.0.1")
+    env.setdefault("MASTER_PORT", str(master_port))
+
+
+def patch_aws_sm_env_for_torch_nccl_backend(verbose=True):
+    """SageMaker: the same from its OpenMPI variables."""
+    env = os.environ
+    env.setdefault("RANK", env.get("OMPI_COMM_WORLD_RANK", "0"))
+    env.setdefault("WORLD_SIZE", env.get("OMPI_COMM_WORLD_SIZE", "1"))
+    env.setdefault("LOCAL_RANK", env.get("OMPI_COMM_WORLD_LOCAL_RANK", "0"))
+
+
+def initialize_mesh_device(mesh_shape, mesh_dim_names):
+    """A torch DeviceMesh over the world (reference initialize_mesh_device); device type from the
+    accelerator (cuda on ROCm = the HIP devices)."""
+    from torch.distributed.device_mesh import init_device_mesh
+    dev = "cuda" if torch.cuda.is_available() and get_backend() == "nccl" else "cpu"
+    return init_device_mesh(dev, tuple(mesh_shape), mesh_dim_names=tuple(mesh_dim_names))
+
+
+def enable_symm_mem_for_group(group_name):
+    """Symmetric-memory collectives are a CUDA/NVSHMEM feature; RCCL over xGMI needs no opt-in here
+    -- kept for API parity, it only records the request."""
+    _State.symm_mem_groups = getattr(_State, "symm_mem_groups", set()) | {group_name}

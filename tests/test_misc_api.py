@@ -145,3 +145,37 @@ def test_packaged_gemm_table_is_lf_and_has_validators():
     keys = [ln.split(",")[1] for ln in raw.decode().splitlines() if ln.startswith("Validator,")]
     assert {"PT_VERSION", "HIP_VERSION", "HIPBLASLT_VERSION", "GCN_ARCH_NAME", "ROCBLAS_VERSION"} <= set(keys)
     assert os.path.getsize(PACKAGED) > 0
+
+
+def _comm_api_case(rank, world):
+    import torch
+    from shuffle_exchange_amd import comm
+    outs = [torch.empty(world * 3), torch.empty(world * 2)]
+    comm.all_gather_coalesced(outs, [torch.full((3,), float(rank)), torch.full((2,), 10.0 + rank)])
+    rs = torch.empty(2)
+    comm.reduce_scatter(rs, [torch.ones(2) * (rank + 1), torch.ones(2) * (rank + 1)])
+    gl = [torch.empty(1) for _ in range(world)] if rank == 0 else None
+    comm.gather(torch.tensor([float(rank)]), gl, dst=0)
+    sc = torch.empty(1)
+    comm.scatter(sc, [torch.tensor([5.0 + r]) for r in range(world)] if rank == 0 else None, src=0)
+    return {"ag": [o.tolist() for o in outs], "rs": rs.tolist(), "gather": [g.item() for g in gl] if gl else None,
+            "scatter": sc.item(), "ranks": comm.get_all_ranks_from_group(None), "avail": comm.is_available()}
+
+
+def test_comm_facade_reference_surface():
+    """The rest of the reference comm API (list-form collectives, gather/scatter, discovery) on gloo."""
+    from .dist_utils import run_dist
+    res = run_dist(_comm_api_case, 2)
+    for r, out in enumerate(res):
+        assert out["ag"] == [[0.0, 0.0, 0.0, 1.0, 1.0, 1.0], [10.0, 10.0, 11.0, 11.0]]
+        assert out["rs"] == [3.0, 3.0]
+        assert out["scatter"] == 5.0 + r
+        assert out["ranks"] == [0, 1] and out["avail"]
+    assert res[0]["gather"] == [0.0, 1.0]
+    import shuffle_exchange_amd.comm as c
+    ref = ["all_gather_coalesced", "gather", "scatter", "reduce_scatter", "get_all_ranks_from_group",
+           "has_all_reduce_coalesced", "has_coalescing_manager", "init_deepspeed_backend", "initialize_mesh_device",
+           "mpi_discovery", "set_backend", "timed_op", "in_aml", "in_aws_sm", "in_dlts", "is_available",
+           "patch_aml_env_for_torch_nccl_backend", "patch_aws_sm_env_for_torch_nccl_backend",
+           "enable_symm_mem_for_group"]
+    assert all(hasattr(c, f) for f in ref)
