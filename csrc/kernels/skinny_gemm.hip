@@ -211,6 +211,17 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(const unsigned sho
   }
 }
 
+// Waves per workgroup: NW = 8 (more waves streaming per CU) while the tiles still fit on the chip
+// in ONE round -- at ~150 VGPRs (bf16) one 8-wave workgroup fits per CU, at ~115 (fp8) two -- and
+// every wave keeps >= `min_ss` super-steps; otherwise NW = 4 (three / four workgroups per CU), so
+// e.g. the 384-tile QKV projection does not run a second, half-empty round of 8-wave workgroups.
+inline int pick_nw(int tiles, int ss_total, int min_ss, int wg8_per_cu) {
+  int nw = 4;
+  while (nw < 8 && (int64_t)tiles * nw < 4096 && ss_total >= min_ss * nw) nw *= 2;
+  if (nw == 8 && tiles > kNumCUs * wg8_per_cu) nw = 4;
+  return nw;
+}
+
 // ---- FP8-weight variant (W8A16: e4m3 weights, per-output-row fp32 scale, bf16 activations) ----
 // Same structure; each lane streams 16 bytes = 16 weights per load and converts them to bf16 in
 // registers (v_cvt_f32_fp8; e4m3 values are exact in bf16), so the weight bytes -- the whole
@@ -330,11 +341,9 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, const c10::opti
   auto y = at::empty({M, N}, x.options());
   if (N == 0) return y;
   c10::DeviceGuard gd(x.device());
-  // K split over NW waves: enough waves in flight (~16 per CU) for narrow N, >= 2 super-steps each
-  const int ss_total = (K + sg::kSS - 1) / sg::kSS;
+    const int ss_total = (K + sg::kSS - 1) / sg::kSS;
   const int tiles = (N + 15) / 16;
-  int nw = 4;
-  while (nw < 8 && (int64_t)tiles * nw < 4096 && ss_total >= 4 * nw) nw *= 2;
+  const int nw = sg::pick_nw(tiles, ss_total, 4, 1);
   const int ss_per_wave = (ss_total + nw - 1) / nw;
   auto* xp = reinterpret_cast<const unsigned short*>(x.data_ptr());
   auto* wp = reinterpret_cast<const unsigned short*>(w.data_ptr());
@@ -374,8 +383,7 @@ at::Tensor skinny_gemm_fp8w(const at::Tensor& x, const at::Tensor& wq, const at:
   c10::DeviceGuard gd(x.device());
   const int ss_total = (K + sg::kSS8 - 1) / sg::kSS8;
   const int tiles = (N + 15) / 16;
-  int nw = 4;
-  while (nw < 8 && (int64_t)tiles * nw < 4096 && ss_total >= 2 * nw) nw *= 2;
+  const int nw = sg::pick_nw(tiles, ss_total, 2, 2);
   const int ss_per_wave = (ss_total + nw - 1) / nw;
   auto* xp = reinterpret_cast<const unsigned short*>(x.data_ptr());
   auto* wp = reinterpret_cast<const uint8_t*>(wq.data_ptr());
@@ -449,8 +457,7 @@ std::vector<at::Tensor> skinny_gemm_pro(const at::Tensor& x, const c10::optional
   const int mi = mode == sg::PRO_RMS ? 0 : 1;
   if (!fp8) {
     const int ss_total = (K + sg::kSS - 1) / sg::kSS;
-    int nw = 4;
-    while (nw < 8 && (int64_t)tiles * nw < 4096 && ss_total >= 4 * nw) nw *= 2;
+    const int nw = sg::pick_nw(tiles, ss_total, 4, 1);
     const int spw = (ss_total + nw - 1) / nw;
     auto* wp = reinterpret_cast<const unsigned short*>(w.data_ptr());
 #define SXE_SGP(NW, MODE)                                                                                            \
@@ -466,8 +473,7 @@ std::vector<at::Tensor> skinny_gemm_pro(const at::Tensor& x, const c10::optional
     SXE_CHECK(wscale->scalar_type() == at::kFloat && wscale->is_contiguous() && wscale->numel() == N,
               "skinny_gemm_pro: wscale fp32 [N]");
     const int ss_total = (K + sg::kSS8 - 1) / sg::kSS8;
-    int nw = 4;
-    while (nw < 8 && (int64_t)tiles * nw < 4096 && ss_total >= 2 * nw) nw *= 2;
+    const int nw = sg::pick_nw(tiles, ss_total, 2, 2);
     const int spw = (ss_total + nw - 1) / nw;
     auto* wp = reinterpret_cast<const uint8_t*>(w.data_ptr());
     const float* sp = wscale->data_ptr<float>();

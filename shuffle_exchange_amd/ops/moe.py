@@ -216,6 +216,14 @@ class IntWeight:
     def linear(self, x, bias=None):
         K = x.shape[-1]
         x2 = x.reshape(-1, K)
+        if (x2.is_cuda and 0 < x2.shape[0] <= 16 and x2.dtype == torch.bfloat16 and K % 128 == 0
+                and self.e.group % 32 == 0 and x2.stride(-1) == 1 and x2.stride(0) % 8 == 0
+                and x2.data_ptr() % 16 == 0):
+            # decode: the skinny kernel streams the codes once (csrc/kernels/skinny_dq.hip)
+            native.require_hip()
+            b = bias.to(torch.bfloat16).contiguous() if bias is not None else None
+            y = torch.ops.sxe.skinny_gemm_dq(x2, self.e.q, self.e.scale, 8 if self.bits == 8 else 9, self.e.group, b)
+            return y.view(*x.shape[:-1], self.shape[0]).to(x.dtype)
         offs = torch.zeros(2, dtype=torch.int32, device=x2.device)  # no host copy: HIP-graph capturable
         offs[1:].fill_(x2.shape[0])
         y = grouped_gemm_q(x2.to(torch.bfloat16) if x2.is_cuda else x2, self.e, offs)

@@ -16,8 +16,10 @@ fp6 four elements per three bytes.
 
 ``MXWeight`` is the inference weight built on it (reference counterparts: inference/v2
 ``wf6af16`` FP6-LLM linear, inference/v2/kernels/core_ops/cuda_linear/linear_kernels_cuda.cu:70,216,
-and ops/fp_quantizer): activations are quantised on the fly to MXFP8 (one HIP pass) and the GEMM
-runs on the FP8/FP6/FP4 matrix cores for every M -- the weight stays in its MX bytes end to end.
+and ops/fp_quantizer): prefill activations are quantised on the fly to MXFP8 (one HIP pass) and
+the GEMM runs on the FP8/FP6/FP4 matrix cores; decode (<= 16 rows) streams the MX codes through a
+skinny kernel that decodes them in registers (csrc/kernels/skinny_dq.hip) -- the weight stays in
+its MX bytes end to end.
 On the CPU the same quantise-then-multiply semantics run in PyTorch (the numerics oracle).
 """
 import torch
@@ -32,6 +34,7 @@ FORMATS = {
     "mxfp4": (4, 2, 1, 4, 6.0),
 }
 BLOCK = 32
+_SKINNY = ("mxfp8", "mxfp6", "mxfp4")  # formats the decode kernel (skinny_dq.hip) reads
 
 
 def _values(ebits, mbits):
@@ -150,9 +153,10 @@ def mx_linear(x, wq, ws, fmt, bias=None, col_scale=None):
 
 class MXWeight:
     """A linear layer's weight [N, K] in an OCP-MX format (``mxfp8`` / ``mxfp6`` / ``mxfp6_e2m3`` /
-    ``mxfp4``), K % 128 == 0 and N % 128 == 0 for the GPU kernel. ``linear`` quantises the input to
-    MXFP8 and runs the block-scaled MFMA GEMM (W{8,6,4}A8); HBM holds bits/8 bytes per weight plus
-    one exponent byte per 32."""
+    ``mxfp4``), K % 128 == 0 and N % 128 == 0 for the GPU kernels. ``linear``: decode-sized inputs
+    run weight-only (bf16 activations) on the skinny dequantising kernel; prefill-sized inputs are
+    quantised to MXFP8 for the block-scaled MFMA GEMM (W{8,6,4}A8). HBM holds bits/8 bytes per
+    weight plus one exponent byte per 32."""
 
     def __init__(self, w, fmt="mxfp6"):
         assert fmt in FORMATS, f"MX format {fmt!r}: one of {sorted(FORMATS)}"
@@ -169,6 +173,17 @@ class MXWeight:
         return dequantize(self.q, self.scale, self.fmt, self.shape[1]).to(dtype)
 
     def linear(self, x, bias=None):
+        """<= 16 rows (decode): weight-only, bf16 activations, the codes decoded in registers by the
+        skinny kernel (csrc/kernels/skinny_dq.hip) -- HBM streams bits/8 bytes per weight. More
+        rows: MXFP8 activations x MX weights on the block-scaled matrix cores (``mx_linear``)."""
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        if (x2.is_cuda and self.fmt in _SKINNY and 0 < x2.shape[0] <= 16 and x2.dtype == torch.bfloat16
+                and x2.stride(-1) == 1 and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0):
+            native.require_hip()
+            b = bias.to(torch.bfloat16).contiguous() if bias is not None else None
+            y = torch.ops.sxe.skinny_gemm_dq(x2, self.q, self.scale, FORMATS[self.fmt][0], 32, b)
+            return y.view(*x.shape[:-1], self.shape[0])
         return mx_linear(x, self.q, self.scale, self.fmt, bias).to(x.dtype)
 
     def to(self, device):

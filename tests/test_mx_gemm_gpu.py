@@ -41,9 +41,11 @@ def test_mx_gemm_matches_fp32(fmt, M, N, K):
     ref = (mx.dequantize(q, s, "mxfp8", K) @ mx.dequantize(W.q, W.scale, fmt, K).t()) * cs + b.float()
     err = (y.float() - ref).abs().max().item()
     assert err <= 1e-2 * ref.abs().max().item() + 1e-3, err
-    # no bias / scale path, through MXWeight.linear
+    # no bias / scale path, through MXWeight.linear (<= 16 rows: weight-only skinny path, bf16
+    # activations; more rows: MXFP8 activations on the block-scaled GEMM)
     y2 = W.linear(x)
-    ref2 = mx.dequantize(q, s, "mxfp8", K) @ W.dequantize(torch.float32).t()
+    xa = x.float() if (M <= 16 and fmt != "mxfp6_e2m3") else mx.dequantize(q, s, "mxfp8", K)
+    ref2 = xa @ W.dequantize(torch.float32).t()
     assert (y2.float() - ref2).abs().max().item() <= 1e-2 * ref2.abs().max().item() + 1e-3
 
 
@@ -81,3 +83,23 @@ def test_fpx_weight_prefill_on_mx_gemm(bits, M, N, K):
     assert err <= 1e-2 * ref.abs().max().item() + 1e-3, err
     full = x.float() @ W.dequantize(torch.float32).t() + b.float()
     assert ((y.float() - full).norm() / full.norm()).item() < 0.05  # fp8 activations: a small, bounded change
+
+
+@pytest.mark.parametrize("kind", ["mxfp8", "mxfp6", "mxfp4", "int8", "int4"])
+@pytest.mark.parametrize("M,N,K", [(1, 128, 128), (5, 384, 1024), (16, 4096, 4096), (3, 1000, 512)])
+def test_skinny_dequant_decode(kind, M, N, K):
+    """<= 16-row GEMMs over MX / int weights (csrc/kernels/skinny_dq.hip): bf16 activations (weight
+    only), codes decoded in registers; reference = x @ the fp32-decoded weight."""
+    from shuffle_exchange_amd.ops.fp_quantizer import quantized_weight
+    if kind.startswith("mx") and N % 128:
+        N = 1024
+    torch.manual_seed(M * 7 + N + K)
+    w = torch.randn(N, K, device="cuda") * 0.05
+    W = quantized_weight(w, kind)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    b = torch.randn(N, device="cuda").to(torch.bfloat16)
+    y = W.linear(x, b)
+    wd = W.dequantize(torch.float32)
+    ref = x.float() @ wd.t() + b.float()
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item() + 2e-3, err
