@@ -11,6 +11,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
+    """A free port BELOW the kernel's ephemeral range (32768+): an ephemeral port released here can
+    be handed to another socket's outgoing connection before rank 0 binds it (EADDRINUSE)."""
+    import random
+    for _ in range(100):
+        p = random.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     p = s.getsockname()[1]
@@ -43,6 +56,15 @@ def _worker(rank, world, port, fn, args, q):
 
 
 def run_dist(fn, world, *args, timeout=240):
+    for attempt in range(3):  # a rendezvous port taken between probe and bind: new port, same run
+        try:
+            return _run_dist(fn, world, *args, timeout=timeout)
+        except RuntimeError as e:
+            if "EADDRINUSE" not in str(e) or attempt == 2:
+                raise
+
+
+def _run_dist(fn, world, *args, timeout=240):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
