@@ -659,12 +659,22 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
   // sparse: SPLIT mode (G == 1), list of the active 32-query tiles of this key block
   const int total = sp.layout ? build_tile_list(sp, hq0, qstart / QT, Sq / QT, QT, kb * QB, kb * QB + QB, false, tlist)
                               : ntq * G;
-  auto qtile_at = [&](int it) { return sp.layout ? tlist[it] * QT : qstart + (it % ntq) * QT; };
   const int kbl = sp.layout ? (k0 + r) / sp.blk : 0;
-
+  // dense tile order: the query tiles qstart .. Sq of head hq0, then of hq0 + 1, ... -- walked by
+  // incremented iterators (a runtime `it % ntq` / `it / ntq` per tile was a scalar division
+  // sequence, a third of the kernel's instructions as SALU)
+  int is_h = hq0, is_q = qstart;  // next tile to issue
+  int c_q = qstart;               // tile being computed
   auto issue = [&](int it, char* slot) {
-    const int hq = sp.layout ? hq0 : hq0 + it / ntq;
-    const int qt0 = qtile_at(it);
+    const int hq = sp.layout ? hq0 : is_h;
+    const int qt0 = sp.layout ? tlist[it] * QT : is_q;
+    if (!sp.layout) {
+      is_q += QT;
+      if (is_q >= Sq) {
+        is_q = qstart;
+        ++is_h;
+      }
+    }
     tile_glds<QT, D>(q + b * qs.b + hq * qs.h, qs.s, qt0, slot);
     tile_glds<QT, D>(dout + b * dos.b + hq * dos.h, dos.s, qt0, slot + G_::TILE);
     if (w == 0) {  // 64 lanes x 4 B: lse[32] then delta[32]
@@ -689,7 +699,8 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
   int cur = 0;
   for (int it = 0; it < total; ++it) {
     if (it + 1 < total) issue(it + 1, ring + (cur ^ 1) * G_::SLOT);
-    const int qt0 = qtile_at(it);
+    const int qt0 = sp.layout ? tlist[it] * QT : c_q;
+    c_q = c_q + QT >= Sq ? qstart : c_q + QT;
     const bool active = !causal || (qt0 + QT - 1 + qoff >= k0);
     if (active) {
       const char* slot = ring + cur * G_::SLOT;
