@@ -456,10 +456,13 @@ void kv_cache_append(const at::Tensor& qkv, at::Tensor cache, const at::Tensor& 
   SXE_LAUNCH_CHECK();
 }
 
-// q: [T, nq, D] (token stride free); returns out [T, nq, D] bf16
-at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const at::Tensor& block_table,
-                           const at::Tensor& q_start, const at::Tensor& q_len, const at::Tensor& kv_len, double scale,
-                           int64_t max_kv_len, int64_t splits, int64_t window) {
+// q: [T, nq, D] (token stride free); returns out [T, nq, D] bf16. parts != nullptr (and splits > 1):
+// no merge launch -- the fp32 partials go to (*parts)[0] = part_o [splits, T, nq, D] and
+// (*parts)[1] = part_ml [splits, T, nq, 2] for a consumer that merges them itself (skinny_gemm_merge)
+static at::Tensor paged_attention_impl(const at::Tensor& q, const at::Tensor& cache, const at::Tensor& block_table,
+                                       const at::Tensor& q_start, const at::Tensor& q_len, const at::Tensor& kv_len,
+                                       double scale, int64_t max_kv_len, int64_t splits, int64_t window,
+                                       std::vector<at::Tensor>* parts) {
   SXE_CHECK_CUDA(q);
   SXE_CHECK(q.scalar_type() == at::kBFloat16 && cache.scalar_type() == at::kBFloat16, "bf16 only");
   SXE_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == q.size(2), "q must be [T, nq, D] with head stride D");
@@ -523,6 +526,10 @@ at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const a
   else if (D == 256) launch(pa::paged_attn_kernel<256>, pa::PaGeo<256>::LDS, 1);
   else launch(pa::paged_attn_kernel<64>, pa::PaGeo<64>::LDS, 2);
   SXE_LAUNCH_CHECK();
+  if (splits > 1 && parts != nullptr) {
+    *parts = {part_o, part_ml};
+    return out;
+  }
   if (splits > 1) {
     if (D == 128)
       hipLaunchKernelGGL(pa::merge_kernel<128>, dim3(T * nq), dim3(128), 0, cur_stream(), a.part_o, a.part_ml,
@@ -538,6 +545,28 @@ at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const a
   return out;
 }
 
+at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const at::Tensor& block_table,
+                           const at::Tensor& q_start, const at::Tensor& q_len, const at::Tensor& kv_len, double scale,
+                           int64_t max_kv_len, int64_t splits, int64_t window) {
+  return paged_attention_impl(q, cache, block_table, q_start, q_len, kv_len, scale, max_kv_len, splits, window, nullptr);
+}
+
+// [out, part_o, part_ml]: with one split `out` is the attention output and the partials are empty;
+// with several, `out` is unwritten and the partials are returned unmerged
+std::vector<at::Tensor> paged_attention_parts(const at::Tensor& q, const at::Tensor& cache,
+                                              const at::Tensor& block_table, const at::Tensor& q_start,
+                                              const at::Tensor& q_len, const at::Tensor& kv_len, double scale,
+                                              int64_t max_kv_len, int64_t splits, int64_t window) {
+  std::vector<at::Tensor> parts;
+  auto out = paged_attention_impl(q, cache, block_table, q_start, q_len, kv_len, scale, max_kv_len, splits, window,
+                                  &parts);
+  if (parts.empty()) {
+    auto e = at::empty({0}, q.options().dtype(at::kFloat));
+    return {out, e, e};
+  }
+  return {out, parts[0], parts[1]};
+}
+
 }  // namespace sxe
 
 TORCH_LIBRARY_FRAGMENT(sxe, m) {
@@ -546,9 +575,12 @@ TORCH_LIBRARY_FRAGMENT(sxe, m) {
         "int nq, int nkv) -> ()");
   m.def("paged_attention(Tensor q, Tensor cache, Tensor block_table, Tensor q_start, Tensor q_len, Tensor kv_len, "
         "float scale, int max_kv_len, int splits, int window=0) -> Tensor");
+  m.def("paged_attention_parts(Tensor q, Tensor cache, Tensor block_table, Tensor q_start, Tensor q_len, "
+        "Tensor kv_len, float scale, int max_kv_len, int splits, int window=0) -> Tensor[]");
 }
 TORCH_LIBRARY_IMPL(sxe, CUDA, m) {
   m.impl("kv_cache_append", &sxe::kv_cache_append);
   m.impl("rope_kv_cache_append", &sxe::rope_kv_cache_append);
   m.impl("paged_attention", &sxe::paged_attention);
+  m.impl("paged_attention_parts", &sxe::paged_attention_parts);
 }

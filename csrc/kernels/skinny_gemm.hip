@@ -47,7 +47,7 @@ __device__ __forceinline__ void load_x(Frag& f, const unsigned short* __restrict
   }
 }
 
-enum : int { PRO_NONE = 0, PRO_RMS = 1, PRO_SWIGLU = 2 };
+enum : int { PRO_NONE = 0, PRO_RMS = 1, PRO_SWIGLU = 2, PRO_MERGE = 3 };
 constexpr int kProMaxM = 4;
 
 struct ProArgs {
@@ -55,15 +55,73 @@ struct ProArgs {
   const unsigned short* gw;   // RMS: norm weight [K]
   unsigned short* hout;       // RMS: h = x + res [M, K] (written by workgroup 0; nullptr: not wanted)
   float eps;
+  const float* po;            // MERGE: split-KV attention partials [splits, M, nq, D] (unnormalised)
+  const float* pml;           // MERGE: their (max, sum) [splits, M, nq, 2], log2 domain
+  int splits, nq;
 };
 
 // The M x K GEMM input, built in LDS (bf16, row stride K) by the whole workgroup in ONE pass:
 //   PRO_RMS    act = bf16(h * g), h = bf16(x + res) (the unfused norm's rounding); the row's
 //              rsqrt(mean(h^2) + eps) goes to rinv[] and scales the GEMM output in the epilogue
 //   PRO_SWIGLU act = bf16(silu(x[:, :K]) * x[:, K:])
+// PRO_MERGE: act[m][h D + d] = the flash-decoding merge of the KV splits' partials (paged_attn.hip
+// merge_kernel's math): sum_s 2^(M_s - M) o_s / sum_s 2^(M_s - M) L_s. One thread per 8 d of one
+// (row, head); every load of a group of 8 splits is issued before the first use.
+template <int NT>
+__device__ __forceinline__ void build_merge(int M, int K, const ProArgs& p, unsigned short* act) {
+  constexpr int U = 8;
+  const int D = K / p.nq, per = K / 8, n = M * per;
+  for (int idx = threadIdx.x; idx < n; idx += NT) {
+    const int m = idx / per, c = (idx - m * per) * 8, h = c / D, d = c - h * D;
+    const int64_t th = (int64_t)m * p.nq + h, sstride = (int64_t)M * p.nq;
+    float Mx = -INFINITY, L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int s0 = 0; s0 < p.splits; s0 += U) {
+      float ms[U], ls[U];
+      f32x4 o0[U], o1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i2 = (int64_t)min(s0 + u, p.splits - 1) * sstride + th;
+        ms[u] = p.pml[i2 * 2];
+        ls[u] = p.pml[i2 * 2 + 1];
+        o0[u] = *reinterpret_cast<const f32x4*>(p.po + i2 * D + d);
+        o1[u] = *reinterpret_cast<const f32x4*>(p.po + i2 * D + d + 4);
+      }
+      float Mc = Mx;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (s0 + u < p.splits) Mc = fmaxf(Mc, ms[u]);
+      const float r = Mx == -INFINITY ? 0.f : exp2f(Mx - Mc);
+      L *= r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] *= r;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (s0 + u < p.splits && ms[u] != -INFINITY) {
+          const float f = exp2f(ms[u] - Mc);
+          L += f * ls[u];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[j] += f * o0[u][j];
+            acc[4 + j] += f * o1[u][j];
+          }
+        }
+      }
+      Mx = Mc;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = L > 0.f ? acc[j] / L : 0.f;
+    store8<DT::BF16>(act + (int64_t)m * K + c, acc);
+  }
+  __syncthreads();
+}
+
 template <int MODE, int NT>
 __device__ __forceinline__ void build_act(const unsigned short* __restrict x, int64_t ldx, int M, int K,
                                           const ProArgs& p, unsigned short* act, float* rinv) {
+  if constexpr (MODE == PRO_MERGE) {
+    build_merge<NT>(M, K, p, act);
+    return;
+  }
   // U chunks of 8 per thread per round, every load of a round issued before the first use: a loop
   // that consumes each chunk before loading the next is a chain of dependent L2 round trips (it made
   // the fused down projection 9 us slower than the separate SwiGLU launch)
@@ -491,6 +549,79 @@ std::vector<at::Tensor> skinny_gemm_pro(const at::Tensor& x, const c10::optional
   return {y, h.defined() ? h : x};
 }
 
+// Decode o_proj with the flash-decoding merge as its prologue (PRO_MERGE): part_o fp32
+// [splits, M, nq, D] and part_ml fp32 [splits, M, nq, 2] from paged_attention_parts; w bf16 [N, K]
+// (wscale None) or e4m3 bytes with wscale fp32 [N]; K = nq * D. One launch instead of merge + GEMM.
+at::Tensor skinny_gemm_merge(const at::Tensor& part_o, const at::Tensor& part_ml, const at::Tensor& w,
+                             const c10::optional<at::Tensor>& wscale, const c10::optional<at::Tensor>& bias) {
+  SXE_CHECK_CUDA(part_o);
+  SXE_CHECK(part_o.scalar_type() == at::kFloat && part_o.dim() == 4 && part_o.is_contiguous() &&
+                part_ml.scalar_type() == at::kFloat && part_ml.is_contiguous() && part_ml.dim() == 4 &&
+                part_ml.size(0) == part_o.size(0) && part_ml.size(1) == part_o.size(1) &&
+                part_ml.size(2) == part_o.size(2) && part_ml.size(3) == 2,
+            "skinny_gemm_merge: part_o fp32 [S, M, nq, D], part_ml fp32 [S, M, nq, 2]");
+  const int S = part_o.size(0), M = part_o.size(1), nq = part_o.size(2), D = part_o.size(3);
+  const bool fp8 = wscale.has_value() && wscale->defined();
+  SXE_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.is_contiguous() && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+            "skinny_gemm_merge: w [N, K] row-major, 16-B aligned");
+  SXE_CHECK(fp8 ? w.element_size() == 1 : w.scalar_type() == at::kBFloat16, "skinny_gemm_merge: w bf16 or fp8 bytes");
+  const int N = w.size(0), K = w.size(1);
+  SXE_CHECK(K == nq * D && D % 8 == 0 && M >= 1 && M <= sg::kProMaxM && S >= 1, "skinny_gemm_merge: K = nq * D, M <= 4");
+  SXE_CHECK(K % (fp8 ? 16 : 8) == 0, "skinny_gemm_merge: K alignment");
+  sg::ProArgs pro{nullptr, nullptr, nullptr, 0.f, part_o.data_ptr<float>(), part_ml.data_ptr<float>(), S, nq};
+  const unsigned short* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    SXE_CHECK(bias->scalar_type() == at::kBFloat16 && bias->is_contiguous() && bias->numel() == N, "bias: bf16 [N]");
+    bp = reinterpret_cast<const unsigned short*>(bias->data_ptr());
+  }
+  auto y = at::empty({M, N}, part_o.options().dtype(at::kBFloat16));
+  if (N == 0) return y;
+  c10::DeviceGuard gd(part_o.device());
+  const size_t lds = (size_t)M * K * 2;
+  SXE_CHECK(lds <= 144 * 1024, "skinny_gemm_merge: M x K input exceeds the LDS budget");
+  const int tiles = (N + 15) / 16;
+  auto* yp = reinterpret_cast<unsigned short*>(y.data_ptr());
+  static bool attr[2][2] = {};
+  auto set = [&](const void* f, int a, int b) {
+    if (!attr[a][b]) {
+      SXE_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 144 * 1024));
+      attr[a][b] = true;
+    }
+  };
+  if (!fp8) {
+    const int ss_total = (K + sg::kSS - 1) / sg::kSS;
+    const int nw = sg::pick_nw(tiles, ss_total, 4, 1);
+    const int spw = (ss_total + nw - 1) / nw;
+    auto* wp = reinterpret_cast<const unsigned short*>(w.data_ptr());
+#define SXE_SGM(NW)                                                                                                  \
+  do {                                                                                                               \
+    set(reinterpret_cast<const void*>(&sg::skinny_gemm_kernel<NW, sg::PRO_MERGE>), 0, NW == 8);                      \
+    hipLaunchKernelGGL((sg::skinny_gemm_kernel<NW, sg::PRO_MERGE>), dim3(tiles), dim3(NW * 64), lds, cur_stream(),    \
+                       nullptr, K, wp, w.stride(0), bp, yp, y.stride(0), M, N, K, spw, pro);                          \
+  } while (0)
+    if (nw == 4) SXE_SGM(4); else SXE_SGM(8);
+#undef SXE_SGM
+  } else {
+    SXE_CHECK(wscale->scalar_type() == at::kFloat && wscale->is_contiguous() && wscale->numel() == N,
+              "skinny_gemm_merge: wscale fp32 [N]");
+    const int ss_total = (K + sg::kSS8 - 1) / sg::kSS8;
+    const int nw = sg::pick_nw(tiles, ss_total, 2, 2);
+    const int spw = (ss_total + nw - 1) / nw;
+    auto* wp = reinterpret_cast<const uint8_t*>(w.data_ptr());
+    const float* sp = wscale->data_ptr<float>();
+#define SXE_SGM8(NW)                                                                                                 \
+  do {                                                                                                               \
+    set(reinterpret_cast<const void*>(&sg::skinny_gemm_fp8w_kernel<NW, sg::PRO_MERGE>), 1, NW == 8);                 \
+    hipLaunchKernelGGL((sg::skinny_gemm_fp8w_kernel<NW, sg::PRO_MERGE>), dim3(tiles), dim3(NW * 64), lds,            \
+                       cur_stream(), nullptr, K, wp, w.stride(0), sp, bp, yp, y.stride(0), M, N, K, spw, pro);        \
+  } while (0)
+    if (nw == 4) SXE_SGM8(4); else SXE_SGM8(8);
+#undef SXE_SGM8
+  }
+  SXE_LAUNCH_CHECK();
+  return y;
+}
+
 }  // namespace sxe
 
 TORCH_LIBRARY_FRAGMENT(sxe, m) {
@@ -498,9 +629,11 @@ TORCH_LIBRARY_FRAGMENT(sxe, m) {
   m.def("skinny_gemm_fp8w(Tensor x, Tensor wq, Tensor wscale, Tensor? bias) -> Tensor");
   m.def("skinny_gemm_pro(Tensor x, Tensor? res, Tensor? gw, float eps, Tensor w, Tensor? wscale, Tensor? bias, "
         "int mode) -> Tensor[]");
+  m.def("skinny_gemm_merge(Tensor part_o, Tensor part_ml, Tensor w, Tensor? wscale, Tensor? bias) -> Tensor");
 }
 TORCH_LIBRARY_IMPL(sxe, CUDA, m) {
   m.impl("skinny_gemm", &sxe::skinny_gemm);
   m.impl("skinny_gemm_fp8w", &sxe::skinny_gemm_fp8w);
   m.impl("skinny_gemm_pro", &sxe::skinny_gemm_pro);
+  m.impl("skinny_gemm_merge", &sxe::skinny_gemm_merge);
 }

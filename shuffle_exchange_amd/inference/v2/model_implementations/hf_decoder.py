@@ -614,6 +614,8 @@ class RaggedDecoder:
     @torch.no_grad()
     def forward(self, batch, kv_cache):
         s, W = self.spec, self.w
+        if self.rope is not None and batch.max_kv_len > self.rope.max_pos:  # HIP RoPE indexes the table unchecked
+            raise ValueError(f"sequence length {batch.max_kv_len} exceeds the RoPE table ({self.rope.max_pos} positions)")
         x = embed(W["embed"], batch.input_ids)
         if s.learned_pos:
             x = x + embed(W["pos_embed"], batch.positions, -s.pos_offset)

@@ -30,7 +30,7 @@ import torch.nn.functional as F
 from ....ops import native
 from ....ops.activation import swiglu
 from ....ops.linear import linear
-from ....ops.paged_attention import paged_attention, rope_kv_cache_append
+from ....ops.paged_attention import paged_attention, paged_attention_parts, rope_kv_cache_append
 from ....ops.rows import embed, gather_rows
 
 FLASH_PREFILL_MIN = 128
@@ -224,6 +224,24 @@ class RaggedLlama:
         return (self.tps is None and T <= self.FUSE_MAX_T and not self.is_moe and self.device.type == "cuda" and native.hip_available()
                 and os.environ.get("SXE_DECODE_FUSE", "1") == "1")
 
+    def _attn_o(self, attn, qkv, kv_layer, batch, li, T):
+        """Attention + o_proj. Decode: the KV-split merge runs inside the o_proj GEMM launch
+        (paged_attention_parts + fused_merge_linear) -- one latency-bound launch fewer per layer."""
+        if self._fusable(T) and getattr(attn.o_proj, "bias", None) is None and native.use_hip(qkv):
+            from ....ops.linear import _pro_weight, fused_merge_linear
+            w = self._wobj(attn.o_proj, li, "o")
+            if _pro_weight(w) is not None:
+                out, parts = paged_attention_parts(qkv[:, :self.nq], kv_layer, batch.block_table, batch.q_start,
+                                                   batch.q_len, batch.kv_len, self.head_dim ** -0.5, batch.max_kv_len)
+                if parts is not None:
+                    y = fused_merge_linear(parts[0], parts[1], w)
+                    if y is not None:
+                        return y
+                    out = self._attention(qkv, kv_layer, batch)
+                return self._proj(attn.o_proj, out.reshape(T, self.nq * self.head_dim), li, "o")
+        o = self._attention(qkv, kv_layer, batch)
+        return self._proj(attn.o_proj, o.reshape(T, self.nq * self.head_dim), li, "o")
+
     def _wobj(self, mod, li, key):
         if self.qw is not None and key in self.qw[li]:
             impl = self.qw[li][key]
@@ -298,6 +316,9 @@ class RaggedLlama:
     def forward(self, batch, kv_cache):
         model = self.model
         rope = model.rope(self.device)
+        if batch.max_kv_len > rope.max_pos:  # the HIP RoPE kernels index the cos/sin table unchecked
+            raise ValueError(f"sequence length {batch.max_kv_len} exceeds the model's RoPE table "
+                             f"({rope.max_pos} positions, max_position_embeddings)")
         T = batch.num_tokens
         x = self.embed_impl(batch.input_ids) if self.embed_impl is not None else model.embed_tokens(batch.input_ids)
         res = None
@@ -308,8 +329,7 @@ class RaggedLlama:
             kv_layer = kv_cache.layer(li)
             # RoPE on q/k + append of k/v to the paged cache: one launch (paged_attn.hip)
             rope_kv_cache_append(qkv, rope, batch.positions, kv_layer, batch.slots, self.nq, self.nkv)
-            o = self._attention(qkv, kv_layer, batch)
-            o = self._proj(attn.o_proj, o.reshape(T, self.nq * self.head_dim), li, "o")
+            o = self._attn_o(attn, qkv, kv_layer, batch, li, T)
             if hasattr(layer, "mlp"):
                 gu, h2 = self._norm_proj(layer.post_attention_layernorm, o, h, layer.mlp.gate_up_proj, li, "gu")
                 self._gu_ready = True

@@ -96,6 +96,19 @@ def fused_swiglu_linear(gu, weight, bias=None):
     return torch.ops.sxe.skinny_gemm_pro(gu, None, None, 0.0, w, sc, bias, 2)[0]
 
 
+def fused_merge_linear(part_o, part_ml, weight, bias=None):
+    """Decode (<= 4 rows): ``linear(merge(part_o, part_ml), weight)`` in ONE launch -- the
+    flash-decoding merge of paged attention's KV-split partials runs as the o_proj skinny GEMM's
+    prologue (skinny_gemm.hip PRO_MERGE). None when the weight is not covered (bf16 / FP8 only)."""
+    wk = _pro_weight(weight)
+    if wk is None or not part_o.is_cuda or part_o.shape[1] > 4:
+        return None
+    w, sc = wk
+    if w.shape[1] != part_o.shape[2] * part_o.shape[3]:
+        return None
+    return torch.ops.sxe.skinny_gemm_merge(part_o, part_ml, w, sc, bias)
+
+
 # Hand-written weight-gradient GEMM (csrc/kernels/gemm_wgrad.hip: k-major operands read through LDS
 # with ds_read_b64_tr_b16, fp32 accumulate in the epilogue): no transposed copies of dY / X at all.
 # Measured on MI355X at 8192 tokens (tools/wgrad_exp.py, profiles/wgrad_kernel.log): 28672x4096

@@ -94,6 +94,18 @@ def choose_splits(num_seqs, nkv, max_kv_len, target_wgs=512):
     return max(1, min(want, math.ceil(max(max_kv_len, 1) / PA_MIN_KEYS)))
 
 
+def paged_attention_parts(q, cache, block_table, q_start, q_len, kv_len, scale, max_kv_len, splits=None):
+    """``paged_attention`` without the split-merge launch (HIP only): returns ``(out, None)`` when the
+    kernel ran one split per (sequence, kv head), else ``(None, (part_o, part_ml))`` -- fp32
+    partials [splits, T, nq, D] / [splits, T, nq, 2] for a consumer that merges them in its own
+    prologue (``ops.linear.fused_merge_linear``: the o_proj skinny GEMM)."""
+    if splits is None:
+        splits = choose_splits(block_table.shape[0], cache.shape[2], max_kv_len)
+    out, po, pml = torch.ops.sxe.paged_attention_parts(q, cache, block_table, q_start, q_len, kv_len, float(scale),
+                                                       int(max_kv_len), int(splits), 0)
+    return (out, None) if po.numel() == 0 else (None, (po, pml))
+
+
 def paged_attention(q, cache, block_table, q_start, q_len, kv_len, scale, max_kv_len, splits=None, window=None):
     """q: [T, nq, D] (head stride D); metadata int32 [S]; returns [T, nq, D]. ``window``: sliding
     window length (keys older than ``window`` positions are masked, Mistral / Qwen2). The HIP kernel

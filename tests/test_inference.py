@@ -106,3 +106,17 @@ def test_v2_tensor_parallel_matches_tp1(nq, nkv):
         assert torch.allclose(r["first"], one["first"], atol=1e-4), (r["first"] - one["first"]).abs().max()
         assert torch.allclose(r["second"], one["second"], atol=1e-4)
         assert r["gen"] == one["gen"]
+
+
+def test_ragged_engine_rejects_positions_beyond_rope_table():
+    """A sequence longer than the RoPE table raises instead of reading cos/sin out of bounds (the HIP
+    RoPE kernels index the table unchecked)."""
+    from shuffle_exchange_amd.inference.v2 import RaggedInferenceEngineConfig, build_engine
+    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+    torch.manual_seed(0)
+    cfg = llama_config("llama-tiny", hidden_size=128, intermediate_size=256, num_attention_heads=4,
+                       num_key_value_heads=2, vocab_size=100, num_hidden_layers=1, max_position_embeddings=64)
+    eng = build_engine(LlamaForCausalLM(cfg).eval(), RaggedInferenceEngineConfig(kv_block_size=16, num_kv_blocks=16))
+    eng.put([1], [torch.randint(0, 100, (60,))])
+    with pytest.raises(ValueError, match="RoPE table"):
+        eng.put([1], [torch.randint(0, 100, (10,))])

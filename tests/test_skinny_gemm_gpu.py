@@ -147,3 +147,71 @@ def test_decode_fused_layer_matches_unfused(monkeypatch):
     assert outs[0][0] == outs[1][0]
     err = ((outs[0][1] - outs[1][1]).norm() / outs[1][1].norm()).item()
     assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("M", [1, 3])
+@pytest.mark.parametrize("splits", [2, 16, 37])
+@pytest.mark.parametrize("nq,D,N", [(32, 128, 4096), (8, 64, 200)])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_fused_merge_prologue_vs_fp32(M, splits, nq, D, N, fp8):
+    """skinny_gemm_merge: the flash-decoding merge of KV-split partials (some splits empty: max -inf)
+    as the o_proj GEMM's prologue == the fp32 merge followed by the GEMM."""
+    from shuffle_exchange_amd.ops.fp_quantizer import FP8Weight
+    from shuffle_exchange_amd.ops.linear import fused_merge_linear
+    torch.manual_seed(2)
+    po = torch.randn(splits, M, nq, D, device="cuda")
+    mx = 4 * torch.randn(splits, M, nq, device="cuda")
+    mx[-1, :, ::3] = float("-inf")  # a split past the sequence's keys
+    ls = torch.rand(splits, M, nq, device="cuda") * 8 + 0.5
+    pml = torch.stack([mx, ls], -1).contiguous()
+    w = (0.02 * torch.randn(N, nq * D, device="cuda")).to(torch.bfloat16)
+    wobj = FP8Weight(w) if fp8 else w
+    y = fused_merge_linear(po, pml, wobj)
+    f = torch.where(mx == float("-inf"), torch.zeros_like(mx), torch.exp2(mx - mx.amax(0, keepdim=True)))
+    o = (f[..., None] * po).sum(0) / (f * ls).sum(0)[..., None]  # [M, nq, D]
+    a = o.reshape(M, nq * D).bfloat16().float()
+    wr = wobj.dequantize().float() if fp8 else w.float()
+    ref = a @ wr.t()
+    err = ((y.float() - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, err
+
+
+def test_decode_merge_fused_o_proj_matches_unfused(monkeypatch):
+    """Ragged engine decode over a context long enough for several KV splits: the merge fused into
+    the o_proj launch == the separate merge kernel + GEMM (same greedy tokens, logits within bf16)."""
+    from shuffle_exchange_amd.inference.v2 import RaggedInferenceEngineConfig, build_engine
+    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+    from shuffle_exchange_amd.ops import paged_attention as pa
+    torch.manual_seed(0)
+    cfg = llama_config("llama-tiny", hidden_size=512, intermediate_size=1024, num_attention_heads=8,
+                       num_key_value_heads=2, vocab_size=1000, num_hidden_layers=2)
+    model = LlamaForCausalLM(cfg).cuda().bfloat16().eval()
+    prompt = torch.randint(0, cfg.vocab_size, (200,)).tolist()  # < max_position_embeddings (256)
+    assert pa.choose_splits(1, 2, 206) > 1
+    import shuffle_exchange_amd.ops.linear as lin
+    calls = {"n": 0}
+    real = lin.fused_merge_linear
+
+    def counting(*a, **k):
+        y = real(*a, **k)
+        calls["n"] += y is not None
+        return y
+    monkeypatch.setattr(lin, "fused_merge_linear", counting)
+    outs = []
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("SXE_DECODE_FUSE", fuse)
+        eng = build_engine(model, RaggedInferenceEngineConfig(kv_block_size=16, num_kv_blocks=64))
+        logits = eng.put([1], [torch.tensor(prompt)])
+        toks, lg = [], []
+        for _ in range(5):
+            t = int(logits[0].argmax())
+            toks.append(t)
+            logits = eng.put([1], [torch.tensor([t])])
+            lg.append(logits.float())
+        eng.flush(1)
+        outs.append((toks, torch.cat(lg)))
+        if fuse == "1":
+            assert calls["n"] > 0  # the fused launch really ran
+    assert outs[0][0] == outs[1][0]
+    err = ((outs[0][1] - outs[1][1]).norm() / outs[1][1].norm()).item()
+    assert err < 2e-2, err
