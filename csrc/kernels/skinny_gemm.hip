@@ -58,7 +58,51 @@ struct ProArgs {
   const float* po;            // MERGE: split-KV attention partials [splits, M, nq, D] (unnormalised)
   const float* pml;           // MERGE: their (max, sum) [splits, M, nq, 2], log2 domain
   int splits, nq;
+  // RMS + RoPE epilogue (rcos != nullptr; the decode QKV projection, head dim 128): the output's q
+  // and k heads are rotated (rotate-half, fp32 cos/sin [max_pos, 64] at rpos[m]) and the rotated k
+  // plus v rows are written to the paged cache [blocks, 2, nkv, bs, 128] at rslots[m] -- the
+  // RoPE + KV-append launch is gone from the decode layer. Each 16-column tile of a q / k head
+  // holds 8 rotation pairs (columns 8 j + c and 64 + 8 j + c), partners 8 lanes apart.
+  const float* rcos;
+  const float* rsin;
+  const int64_t* rpos;
+  const int64_t* rslots;
+  unsigned short* rcache;
+  int rnq, rnkv, rbs;
 };
+
+// output column of lane `col` in tile `tile` (identity unless the RoPE epilogue pairs columns)
+__device__ __forceinline__ int out_col(const ProArgs& p, int tile, int col) {
+  const int h = tile >> 3, j = tile & 7;
+  if (p.rcos == nullptr || h >= p.rnq + p.rnkv) return tile * 16 + col;
+  return h * 128 + (col < 8 ? 8 * j + col : 56 + 8 * j + col);
+}
+
+// Wave-0 epilogue store of output (m, n) = v under the RoPE epilogue; every lane calls it (the pair
+// exchange is a whole-wave shuffle).
+__device__ __forceinline__ void rope_store(const ProArgs& p, float v, int m, int M, int n, int tile, int col,
+                                           unsigned short* __restrict y, int64_t ldy) {
+  const int h = tile >> 3;
+  const float pv = __shfl_xor(v, 8, 64);
+  if (m >= M) return;
+  const int d = n - h * 128;
+  float out = v;
+  if (h < p.rnq + p.rnkv) {
+    const int64_t ps = p.rpos[m];
+    const float c = p.rcos[ps * 64 + (d & 63)], sn = p.rsin[ps * 64 + (d & 63)];
+    out = col < 8 ? v * c - pv * sn : v * c + pv * sn;
+  }
+  const unsigned short ob = f32_to_bf16(out);
+  y[(int64_t)m * ldy + n] = ob;
+  if (h >= p.rnq) {
+    const int64_t slot = p.rslots[m];
+    if (slot >= 0) {
+      const int kv = h >= p.rnq + p.rnkv ? 1 : 0, hh = h - p.rnq - kv * p.rnkv;
+      const int64_t blk = slot / p.rbs, off = slot - blk * p.rbs;
+      p.rcache[(((blk * 2 + kv) * p.rnkv + hh) * p.rbs + off) * 128 + d] = ob;
+    }
+  }
+}
 
 // The M x K GEMM input, built in LDS (bf16, row stride K) by the whole workgroup in ONE pass:
 //   PRO_RMS    act = bf16(h * g), h = bf16(x + res) (the unfused norm's rounding); the row's
@@ -206,9 +250,8 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(const unsigned sho
   __shared__ f32x4 red[NW][64];
   extern __shared__ __attribute__((aligned(16))) unsigned short act_lds[];  // PRO_*: the M x K input
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * 16;
   const int col = lane & 15, g = lane >> 4;
-  const int n = n0 + col;
+  const int n = MODE == PRO_RMS ? out_col(pro, blockIdx.x, col) : blockIdx.x * 16 + col;
   const bool wok = n < N, xok = col < M;
   const unsigned short* wrow = w + (int64_t)(wok ? n : 0) * ldw;
   const unsigned short* xrow = MODE == PRO_NONE ? x + (int64_t)(xok ? col : 0) * ldx
@@ -257,7 +300,13 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(const unsigned sho
       t[2] += u[2];
       t[3] += u[3];
     }
-    if (n < N) {
+    if (MODE == PRO_RMS && pro.rcos != nullptr) {  // RoPE epilogue (no bias: checked on the host)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 4 * g + r;
+        rope_store(pro, t[r] * rinv[m < kProMaxM ? m : 0], m, M, n, blockIdx.x, col, y, ldy);
+      }
+    } else if (n < N) {
       const float b = bias ? bf16_to_f32(bias[n]) : 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -314,9 +363,8 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_fp8w_kernel(const unsigne
   __shared__ f32x4 red[NW][64];
   extern __shared__ __attribute__((aligned(16))) unsigned short act_lds[];  // PRO_*: the M x K input
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * 16;
   const int col = lane & 15, g = lane >> 4;
-  const int n = n0 + col;
+  const int n = MODE == PRO_RMS ? out_col(pro, blockIdx.x, col) : blockIdx.x * 16 + col;
   const bool wok = n < N, xok = col < M;
   const uint8_t* wrow = w + (int64_t)(wok ? n : 0) * ldw;
   const unsigned short* xrow = MODE == PRO_NONE ? x + (int64_t)(xok ? col : 0) * ldx
@@ -364,7 +412,14 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_fp8w_kernel(const unsigne
       t[2] += u[2];
       t[3] += u[3];
     }
-    if (n < N) {
+    if (MODE == PRO_RMS && pro.rcos != nullptr) {  // RoPE epilogue (no bias: checked on the host)
+      const float sc = wscale[n];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 4 * g + r;
+        rope_store(pro, t[r] * sc * rinv[m < kProMaxM ? m : 0], m, M, n, blockIdx.x, col, y, ldy);
+      }
+    } else if (n < N) {
       const float sc = wscale[n];
       const float b = bias ? bf16_to_f32(bias[n]) : 0.f;
 #pragma unroll
@@ -462,10 +517,16 @@ at::Tensor skinny_gemm_fp8w(const at::Tensor& x, const at::Tensor& wq, const at:
 // mode 1 (rms): x [M, K], res [M, K] or None (same row stride), gw [K], eps -> (y [M, N], h [M, K] = x + res)
 // mode 2 (swiglu): x = gu [M, 2K] (gate | up halves) -> y [M, N]
 // wq: bf16 [N, K] (wscale None) or e4m3 bytes [N, K] with wscale fp32 [N]
-std::vector<at::Tensor> skinny_gemm_pro(const at::Tensor& x, const c10::optional<at::Tensor>& res,
-                                        const c10::optional<at::Tensor>& gw, double eps, const at::Tensor& w,
-                                        const c10::optional<at::Tensor>& wscale, const c10::optional<at::Tensor>& bias,
-                                        int64_t mode) {
+struct RopeTensors {
+  const at::Tensor *cos, *sin, *pos, *slots, *cache;
+  int64_t nq, nkv;
+};
+
+static std::vector<at::Tensor> skinny_gemm_pro_impl(const at::Tensor& x, const c10::optional<at::Tensor>& res,
+                                                    const c10::optional<at::Tensor>& gw, double eps,
+                                                    const at::Tensor& w, const c10::optional<at::Tensor>& wscale,
+                                                    const c10::optional<at::Tensor>& bias, int64_t mode,
+                                                    const RopeTensors* rope) {
   SXE_CHECK_CUDA(x);
   SXE_CHECK(mode == sg::PRO_RMS || mode == sg::PRO_SWIGLU, "skinny_gemm_pro: mode 1 (rms) or 2 (swiglu)");
   SXE_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 &&
@@ -479,6 +540,29 @@ std::vector<at::Tensor> skinny_gemm_pro(const at::Tensor& x, const c10::optional
   SXE_CHECK(x.size(1) == (mode == sg::PRO_SWIGLU ? 2 * K : K), "skinny_gemm_pro: x width");
   SXE_CHECK(K % (fp8 ? 16 : 8) == 0 && w.stride(0) % (fp8 ? 16 : 8) == 0, "skinny_gemm_pro: K alignment");
   sg::ProArgs pro{nullptr, nullptr, nullptr, (float)eps};
+  if (rope != nullptr) {
+    SXE_CHECK(mode == sg::PRO_RMS && !(bias.has_value() && bias->defined()), "skinny_gemm_pro_rope: RMS mode, no bias");
+    const int64_t nq = rope->nq, nkv = rope->nkv;
+    SXE_CHECK(nq > 0 && nkv > 0 && w.size(0) == (nq + 2 * nkv) * 128, "skinny_gemm_pro_rope: w rows = (nq + 2 nkv) * 128");
+    const at::Tensor &c = *rope->cos, &sn = *rope->sin, &ps = *rope->pos, &sl = *rope->slots, &kc = *rope->cache;
+    SXE_CHECK(c.scalar_type() == at::kFloat && sn.scalar_type() == at::kFloat && c.is_contiguous() && sn.is_contiguous() &&
+                  c.dim() == 2 && c.size(1) == 64 && sn.sizes() == c.sizes(),
+              "skinny_gemm_pro_rope: cos/sin fp32 [max_pos, 64]");
+    SXE_CHECK(ps.scalar_type() == at::kLong && ps.is_contiguous() && ps.numel() == x.size(0) &&
+                  sl.scalar_type() == at::kLong && sl.is_contiguous() && sl.numel() == x.size(0),
+              "skinny_gemm_pro_rope: pos / slots int64 [M]");
+    SXE_CHECK(kc.scalar_type() == at::kBFloat16 && kc.is_contiguous() && kc.dim() == 5 && kc.size(1) == 2 &&
+                  kc.size(2) == nkv && kc.size(4) == 128,
+              "skinny_gemm_pro_rope: cache bf16 [blocks, 2, nkv, bs, 128]");
+    pro.rcos = c.data_ptr<float>();
+    pro.rsin = sn.data_ptr<float>();
+    pro.rpos = ps.data_ptr<int64_t>();
+    pro.rslots = sl.data_ptr<int64_t>();
+    pro.rcache = reinterpret_cast<unsigned short*>(kc.data_ptr());
+    pro.rnq = (int)nq;
+    pro.rnkv = (int)nkv;
+    pro.rbs = (int)kc.size(3);
+  }
   at::Tensor h;
   if (mode == sg::PRO_RMS) {
     SXE_CHECK(gw.has_value() && gw->scalar_type() == at::kBFloat16 && gw->is_contiguous() && gw->numel() == K,
@@ -547,6 +631,24 @@ std::vector<at::Tensor> skinny_gemm_pro(const at::Tensor& x, const c10::optional
   }
   SXE_LAUNCH_CHECK();
   return {y, h.defined() ? h : x};
+}
+
+std::vector<at::Tensor> skinny_gemm_pro(const at::Tensor& x, const c10::optional<at::Tensor>& res,
+                                        const c10::optional<at::Tensor>& gw, double eps, const at::Tensor& w,
+                                        const c10::optional<at::Tensor>& wscale, const c10::optional<at::Tensor>& bias,
+                                        int64_t mode) {
+  return skinny_gemm_pro_impl(x, res, gw, eps, w, wscale, bias, mode, nullptr);
+}
+
+// The decode QKV projection with residual + RMSNorm prologue AND the RoPE + paged-KV-append
+// epilogue: returns [qkv (q / k rotated), h]; the rotated k and v rows land in `cache`.
+std::vector<at::Tensor> skinny_gemm_pro_rope(const at::Tensor& x, const c10::optional<at::Tensor>& res,
+                                             const at::Tensor& gw, double eps, const at::Tensor& w,
+                                             const c10::optional<at::Tensor>& wscale, const at::Tensor& cos_t,
+                                             const at::Tensor& sin_t, const at::Tensor& pos, const at::Tensor& slots,
+                                             at::Tensor cache, int64_t nq, int64_t nkv) {
+  RopeTensors r{&cos_t, &sin_t, &pos, &slots, &cache, nq, nkv};
+  return skinny_gemm_pro_impl(x, res, gw, eps, w, wscale, c10::nullopt, sg::PRO_RMS, &r);
 }
 
 // Decode o_proj with the flash-decoding merge as its prologue (PRO_MERGE): part_o fp32
@@ -630,10 +732,13 @@ TORCH_LIBRARY_FRAGMENT(sxe, m) {
   m.def("skinny_gemm_pro(Tensor x, Tensor? res, Tensor? gw, float eps, Tensor w, Tensor? wscale, Tensor? bias, "
         "int mode) -> Tensor[]");
   m.def("skinny_gemm_merge(Tensor part_o, Tensor part_ml, Tensor w, Tensor? wscale, Tensor? bias) -> Tensor");
+  m.def("skinny_gemm_pro_rope(Tensor x, Tensor? res, Tensor gw, float eps, Tensor w, Tensor? wscale, Tensor cos, "
+        "Tensor sin, Tensor pos, Tensor slots, Tensor(a!) cache, int nq, int nkv) -> Tensor[]");
 }
 TORCH_LIBRARY_IMPL(sxe, CUDA, m) {
   m.impl("skinny_gemm", &sxe::skinny_gemm);
   m.impl("skinny_gemm_fp8w", &sxe::skinny_gemm_fp8w);
   m.impl("skinny_gemm_pro", &sxe::skinny_gemm_pro);
   m.impl("skinny_gemm_merge", &sxe::skinny_gemm_merge);
+  m.impl("skinny_gemm_pro_rope", &sxe::skinny_gemm_pro_rope);
 }

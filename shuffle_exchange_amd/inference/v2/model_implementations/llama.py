@@ -227,7 +227,8 @@ class RaggedLlama:
     def _attn_o(self, attn, qkv, kv_layer, batch, li, T):
         """Attention + o_proj. Decode: the KV-split merge runs inside the o_proj GEMM launch
         (paged_attention_parts + fused_merge_linear) -- one latency-bound launch fewer per layer."""
-        if self._fusable(T) and getattr(attn.o_proj, "bias", None) is None and native.use_hip(qkv):
+        if (self._fusable(T) and getattr(attn.o_proj, "bias", None) is None and native.use_hip(qkv)
+                and os.environ.get("SXE_DECODE_FUSE_ATTN", "1") == "1"):
             from ....ops.linear import _pro_weight, fused_merge_linear
             w = self._wobj(attn.o_proj, li, "o")
             if _pro_weight(w) is not None:
@@ -324,12 +325,25 @@ class RaggedLlama:
         res = None
         for li, layer in enumerate(model.layers):
             attn = layer.self_attn
-            qkv, h = self._norm_proj(layer.input_layernorm, x, res, attn.qkv_proj, li, "qkv")
-            qkv = qkv.view(T, self.nq + 2 * self.nkv, self.head_dim)
             kv_layer = kv_cache.layer(li)
-            # RoPE on q/k + append of k/v to the paged cache: one launch (paged_attn.hip)
-            rope_kv_cache_append(qkv, rope, batch.positions, kv_layer, batch.slots, self.nq, self.nkv)
-            o = self._attn_o(attn, qkv, kv_layer, batch, li, T)
+            r = None
+            if (self._fusable(T) and self.head_dim == 128 and getattr(attn.qkv_proj, "bias", None) is None
+                    and os.environ.get("SXE_DECODE_FUSE_ATTN", "1") == "1"):
+                # decode: RMSNorm prologue + QKV GEMM + RoPE / KV-append epilogue in one launch
+                from ....ops.linear import fused_rms_rope_linear
+                ln = layer.input_layernorm
+                r = fused_rms_rope_linear(x, res, ln.weight, ln.eps, self._wobj(attn.qkv_proj, li, "qkv"), rope,
+                                          batch.positions, kv_layer, batch.slots, self.nq, self.nkv)
+            if r is not None:
+                qkv, h = r
+                qkv = qkv.view(T, self.nq + 2 * self.nkv, self.head_dim)
+                o = self._attn_o(attn, qkv, kv_layer, batch, li, T)
+            else:
+                qkv, h = self._norm_proj(layer.input_layernorm, x, res, attn.qkv_proj, li, "qkv")
+                qkv = qkv.view(T, self.nq + 2 * self.nkv, self.head_dim)
+                # RoPE on q/k + append of k/v to the paged cache: one launch (paged_attn.hip)
+                rope_kv_cache_append(qkv, rope, batch.positions, kv_layer, batch.slots, self.nq, self.nkv)
+                o = self._attn_o(attn, qkv, kv_layer, batch, li, T)
             if hasattr(layer, "mlp"):
                 gu, h2 = self._norm_proj(layer.post_attention_layernorm, o, h, layer.mlp.gate_up_proj, li, "gu")
                 self._gu_ready = True

@@ -84,6 +84,26 @@ def fused_rms_linear(x, residual, norm_weight, eps, weight, bias=None):
     return y, (h if residual is not None else x)
 
 
+def fused_rms_rope_linear(x, residual, norm_weight, eps, weight, rope, positions, cache, slots, nq, nkv):
+    """Decode (<= 4 rows) QKV projection in ONE launch: residual + RMSNorm prologue, GEMM, and the
+    RoPE + paged-KV-append epilogue (skinny_gemm.hip ``skinny_gemm_pro_rope``; head dim 128).
+    Returns (qkv with q / k rotated, h) -- the rotated k and v are already in ``cache`` -- or None
+    when not covered (the caller runs fused_rms_linear + rope_kv_cache_append)."""
+    wk = _pro_weight(weight)
+    if (wk is None or not _pro_ok(x) or norm_weight.dtype != torch.bfloat16 or not norm_weight.is_contiguous()
+            or rope.cos.shape[-1] != 64 or not cache.is_contiguous() or cache.dim() != 5 or cache.shape[-1] != 128):
+        return None
+    if residual is not None and (residual.shape != x.shape or residual.stride() != x.stride()
+                                 or residual.dtype != x.dtype):
+        return None
+    w, sc = wk
+    if x.shape[1] != w.shape[1] or w.shape[0] != (nq + 2 * nkv) * 128:
+        return None
+    y, h = torch.ops.sxe.skinny_gemm_pro_rope(x, residual, norm_weight, float(eps), w, sc, rope.cos, rope.sin,
+                                              positions.reshape(-1).contiguous().long(), slots, cache, int(nq), int(nkv))
+    return y, (h if residual is not None else x)
+
+
 def fused_swiglu_linear(gu, weight, bias=None):
     """Decode (<= 4 rows): ``linear(silu(gu[:, :I]) * gu[:, I:], weight)`` in ONE launch
     (skinny_gemm.hip PRO_SWIGLU); None when not covered."""

@@ -215,3 +215,43 @@ def test_decode_merge_fused_o_proj_matches_unfused(monkeypatch):
     assert outs[0][0] == outs[1][0]
     err = ((outs[0][1] - outs[1][1]).norm() / outs[1][1].norm()).item()
     assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("M", [1, 3])
+@pytest.mark.parametrize("nq,nkv", [(32, 8), (4, 2)])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_fused_rms_rope_epilogue_vs_separate_ops(M, nq, nkv, fp8):
+    """skinny_gemm_pro_rope (RMSNorm prologue + QKV GEMM + RoPE / KV-append epilogue) == the fused
+    RMS GEMM followed by rope_kv_cache_append (rotation from the fp32 accumulator instead of the
+    bf16-rounded output: within bf16 rounding); slots of -1 leave the cache untouched."""
+    from shuffle_exchange_amd.ops.fp_quantizer import FP8Weight
+    from shuffle_exchange_amd.ops.linear import fused_rms_linear, fused_rms_rope_linear
+    from shuffle_exchange_amd.ops.paged_attention import rope_kv_cache_append
+    from shuffle_exchange_amd.ops.rope import RopeCache
+    torch.manual_seed(3)
+    K, D, bs, nblk = 1024, 128, 16, 8
+    N = (nq + 2 * nkv) * D
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    res = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    g = (1.0 + 0.1 * torch.randn(K, device="cuda")).to(torch.bfloat16)
+    w = (0.05 * torch.randn(N, K, device="cuda")).to(torch.bfloat16)
+    wobj = FP8Weight(w) if fp8 else w
+    rope = RopeCache(D, 4096, 500000.0, device="cuda")
+    pos = torch.randint(0, 4096, (M,), device="cuda")
+    slots = torch.randperm(nblk * bs, device="cuda")[:M].long()
+    if M > 1:
+        slots[1] = -1
+    c_ref = torch.randn(nblk, 2, nkv, bs, D, device="cuda").to(torch.bfloat16)
+    c_f = c_ref.clone()
+    y_ref, h_ref = fused_rms_linear(x, res, g, 1e-5, wobj)
+    q_ref = y_ref.view(M, nq + 2 * nkv, D).clone()
+    rope_kv_cache_append(q_ref, rope, pos, c_ref, slots, nq, nkv)
+    y, h = fused_rms_rope_linear(x, res, g, 1e-5, wobj, rope, pos, c_f, slots, nq, nkv)
+    assert torch.equal(h, h_ref)
+    torch.testing.assert_close(y.view(M, nq + 2 * nkv, D).float(), q_ref.float(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(c_f.float(), c_ref.float(), rtol=2e-2, atol=2e-2)
+    written = torch.zeros(nblk, bs, dtype=torch.bool, device="cuda")
+    ok = slots[slots >= 0]
+    written[ok // bs, ok % bs] = True
+    diff = (c_f != c_ref).any(dim=-1).any(dim=2).any(dim=1)  # [blocks, bs]
+    assert not (diff & ~written).any()  # no stray writes outside the appended slots
