@@ -113,7 +113,8 @@ class _GroupedMM(torch.autograd.Function):
             for e in range(E):
                 torch.mm(dy[e], w[e].t(), out=dx[e])
         if ctx.needs_input_grad[1]:
-            tgt = getattr(w, "_sxe_grad_target", None)
+            from ..ops.linear import grad_target
+            tgt = grad_target(w)
             if tgt is not None:
                 from ..ops.linear import _sxe_wgrad_ok
                 buf, acc = tgt(w)

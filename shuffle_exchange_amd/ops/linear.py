@@ -175,9 +175,22 @@ def data_grad(gy, w):
     return torch.matmul(gy, w)
 
 
+def grad_target(w):
+    """The optimizer's direct weight-grad target of ``w`` (``_sxe_grad_target``), or None when the
+    gradient must take autograd's ``.grad`` path instead: a partial gradient of a tiled / recomputed
+    sub-graph (``_sxe_grad_partial``, set by sequence/tiled.py for every tile but the last -- the
+    reference's ``ds_grad_is_ready = False``, runtime/sequence_parallel/ulysses_sp.py:720-724), or a
+    ``.grad`` that already holds such partial sums (the last tile adds into it, and the ZeRO hook
+    then delivers the total once)."""
+    tgt = getattr(w, "_sxe_grad_target", None)
+    if tgt is None or getattr(w, "_sxe_grad_partial", False) or w.grad is not None:
+        return None
+    return tgt
+
+
 def write_weight_grad(w, gy2, x2):
     """dW = gy2^T @ x2 into the optimizer-provided target of `w`; returns True if handled."""
-    tgt = getattr(w, "_sxe_grad_target", None)
+    tgt = grad_target(w)
     if tgt is None:
         return False
     buf, accumulate = tgt(w)

@@ -44,7 +44,8 @@ def dual_variant(inter):
 def weight_grad_tn(w, gyT, xT):
     """dW = gyT @ xT^T (gyT [N, T], xT [K, T], both token-minor): written into the optimizer's
     target for ``w`` when it has one (returns None), else returned."""
-    tgt = getattr(w, "_sxe_grad_target", None)
+    from .linear import grad_target
+    tgt = grad_target(w)
     dw = None
     if tgt is None:
         return torch.mm(gyT, xT.t())

@@ -49,7 +49,8 @@ class _NormFn(torch.autograd.Function):
         dres = dh.contiguous().view(-1, H) if (ctx.has_res and dh is not None) else None
         dx, dw, db = torch.ops.sxe.norm_bwd(dy2, hin, rstd, mean, weight, dres, bool(ctx.layernorm))
         dx = dx.view(ctx.shape)
-        tgt_fn = getattr(weight, "_sxe_grad_target", None)
+        from .linear import grad_target
+        tgt_fn = grad_target(weight)
         if tgt_fn is not None and ctx.needs_input_grad[2]:
             # the fp32 dgamma goes straight into the optimizer's buffer (no bf16 round trip, no
             # mixed-dtype accumulate in a hook)

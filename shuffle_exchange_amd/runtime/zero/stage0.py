@@ -120,8 +120,8 @@ class DataParallelOptimizer(ZeroOptimizerBase):
 
     def _make_hook(self, u):
         def hook(p):
-            if p.grad is None:
-                return
+            if p.grad is None or getattr(p, "_sxe_grad_partial", False):
+                return  # partial tile gradient: keep summing in .grad until the last tile
             if not self.boundary:
                 if self.fp32_accum:
                     self._take_grad(u, u.param_index[id(p)], p)

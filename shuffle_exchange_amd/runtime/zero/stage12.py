@@ -156,8 +156,8 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
 
     def _make_hook(self, unit):
         def hook(p):
-            if p.grad is None:
-                return
+            if p.grad is None or getattr(p, "_sxe_grad_partial", False):
+                return  # partial tile gradient: keep summing in .grad until the last tile
             if not self.micro_step_boundary and self.stage == 1:
                 # ZeRO-1 keeps accumulating full grads until the boundary: in the bit16 .grad
                 # (autograd's own accumulation), or with fp32_accum in the unit's fp32 buffer
@@ -231,6 +231,11 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                             if p.grad is not None:  # no hook fired (e.g. grads set outside autograd)
                                 self._accumulate_fp32(u, p)
                         if u.staging is not None:
+                            if not u.carry and u.pending > 0:
+                                # slots of params without a gradient in this first micro-step
+                                # are uninitialised (torch.empty staging): zero them before the
+                                # later micro-steps add into them
+                                u.fill_missing()
                             u.carry = True
             return
         for units in self.units:

@@ -460,8 +460,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
 
     def _make_grad_hook(self, unit):
         def hook(p):
-            if p.grad is None:
-                return
+            if p.grad is None or getattr(p, "_sxe_grad_partial", False):
+                return  # partial tile gradient: keep summing in .grad until the last tile
             if unit.persistent and self.S == 1:
                 i = unit.param_index[id(p)]
                 o, n = unit.offsets[i], unit.numels[i]

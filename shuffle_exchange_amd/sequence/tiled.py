@@ -22,6 +22,9 @@ class _TiledCompute(torch.autograd.Function):
     @staticmethod
     def forward(ctx, fn, n_tiles, x, *params):
         ctx.fn, ctx.n_tiles, ctx.n_params = fn, n_tiles, len(params)
+        # parameters whose gradients the tiles accumulate: explicit, else the module's own
+        ctx.grad_params = [p for p in (params or (fn.parameters() if isinstance(fn, torch.nn.Module) else ()))
+                           if p.requires_grad]
         ctx.save_for_backward(x)
         with torch.no_grad():
             outs = [fn(t) for t in x.chunk(n_tiles, dim=-2)]
@@ -32,12 +35,24 @@ class _TiledCompute(torch.autograd.Function):
         (x,) = ctx.saved_tensors
         dx = torch.empty_like(x)
         xs, gs, dxs = x.chunk(ctx.n_tiles, dim=-2), g.chunk(ctx.n_tiles, dim=-2), dx.chunk(ctx.n_tiles, dim=-2)
-        for xt, gt, dxt in zip(xs, gs, dxs):
-            xt = xt.detach().requires_grad_(True)
-            with torch.enable_grad():
-                y = ctx.fn(xt)
-            torch.autograd.backward(y, gt)
-            dxt.copy_(xt.grad)
+        params = ctx.grad_params
+        last = len(xs) - 1
+        try:
+            for t, (xt, gt, dxt) in enumerate(zip(xs, gs, dxs)):
+                # every tile but the last delivers a PARTIAL parameter gradient: the ZeRO hooks and the
+                # direct weight-grad writers leave it summing in .grad (reference ds_grad_is_ready,
+                # runtime/sequence_parallel/ulysses_sp.py:720-724,846-850; honoured at
+                # stage_1_and_2.py:1146 / stage3.py:1280), so a unit is reduced once, with the total
+                for p in params:
+                    p._sxe_grad_partial = t < last
+                xt = xt.detach().requires_grad_(True)
+                with torch.enable_grad():
+                    y = ctx.fn(xt)
+                torch.autograd.backward(y, gt)
+                dxt.copy_(xt.grad)
+        finally:
+            for p in params:
+                p._sxe_grad_partial = False
         return (None, None, dx) + (None,) * ctx.n_params
 
 

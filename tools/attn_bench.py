@@ -1,6 +1,7 @@
 """Time the flash attention kernels alone (fwd, fwd+bwd) vs SDPA, per head dim; for D < 128 also
 the old zero-padded-to-128 path, for Sq != Sk the prefix shape.
-  python tools/attn_bench.py [B]"""
+  python tools/attn_bench.py [B]
+  python tools/attn_bench.py --shapes B,Sq,Sk,H,Hk,D,causal[;...] [--no-sdpa]"""
 import json
 import sys
 import time
@@ -22,7 +23,7 @@ def t(fn, n=10):
     return (time.perf_counter() - t0) / n
 
 
-def run(B, Sq, Sk, H, Hk, D, causal=True):
+def run(B, Sq, Sk, H, Hk, D, causal=True, sdpa=True):
     q = torch.randn(B, Sq, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     k = torch.randn(B, Sk, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     v = torch.randn(B, Sk, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
@@ -34,7 +35,7 @@ def run(B, Sq, Sk, H, Hk, D, causal=True):
     if D < 128:
         qp, kp, vp = (torch.nn.functional.pad(x.detach(), (0, 128 - D)).requires_grad_() for x in (q, k, v))
         paths.append(("hip_padded128", lambda: attention(qp, kp, vp, causal=causal, softmax_scale=D ** -0.5)))
-    if Sq == Sk:
+    if Sq == Sk and sdpa:
         paths.append(("sdpa", lambda: _sdpa(q, k, v, causal, D ** -0.5)))
     for name, f in paths:
         tf = t(f)
@@ -48,6 +49,12 @@ def run(B, Sq, Sk, H, Hk, D, causal=True):
 
 
 def main():
+    if "--shapes" in sys.argv:
+        spec = sys.argv[sys.argv.index("--shapes") + 1]
+        for sh in spec.split(";"):
+            B, Sq, Sk, H, Hk, D, c = (int(x) for x in sh.split(","))
+            run(B, Sq, Sk, H, Hk, D, causal=bool(c), sdpa="--no-sdpa" not in sys.argv)
+        return
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     run(B, 2048, 2048, 32, 8, 128)          # Llama-3-8B training shape
     run(B, 2048, 2048, 32, 8, 64)           # head dim 64 (BERT / GPT-2 / Phi-class)

@@ -1,5 +1,5 @@
 """Flash-attention forward / backward only (B4 S2048 H32/8 D128 causal), 3 dispatches each, for
-rocprofv3 --pmc passes (tools/gpu_pmc_attn.sh)."""
+rocprofv3 --pmc passes (bash tools/gpu_run.sh pmc_attn)."""
 import os
 import sys
 
