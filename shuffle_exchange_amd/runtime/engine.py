@@ -88,11 +88,26 @@ def broadcast_coalesced(tensors, src, group, bucket_bytes):
     return n_coll
 
 
+def _expert_tp_dup(pg, tp):
+    """How many ranks of this rank's TP group hold the same experts as it does (1 = the TP peers
+    hold different experts, tp = the experts are replicated over the TP group). Expert TP shards
+    every expert over the TP group (dup 1); without it the expert-parallel groups span the TP
+    plane (parallel/groups.py ``span_tp``), so the TP peers share experts exactly when they sit
+    in one expert-data-parallel group, e.g. every peer when ep_size = 1."""
+    from ..parallel import groups
+    reg = groups._Registry.expert.get(pg.get("name", ""))
+    tpg = groups.get_tensor_model_parallel_group()
+    if reg is None or tpg is None:
+        return tp
+    return max(1, len(set(dist.group_ranks(tpg)) & set(reg[3])))
+
+
 def _split_tp_replicated(model_parameters, tp):
-    """Separate TP-sharded from TP-replicated parameters so the global gradient norm counts the
-    replicated ones once (their grads are identical on every TP rank). Expert parameters count as
-    sharded: expert-TP shards differ per TP rank, and without expert TP the TP ranks hold
-    different experts (the EP group spans them)."""
+    """Separate TP-sharded from TP-replicated parameters so the global gradient norm (summed over
+    the TP group) counts a replicated gradient once: weight 1 / (number of TP peers holding an
+    identical copy). Dense TP-sharded weights and expert-TP shards count fully; expert parameters
+    without expert TP count 1 / (TP peers with the same experts) -- 1 when ep_size is a multiple
+    of tp, ep/tp when tp is a multiple of ep_size (1/tp at ep_size 1)."""
     from ..moe.utils import is_moe_param
     plist = list(model_parameters)
     if plist and isinstance(plist[0], dict):
@@ -101,10 +116,15 @@ def _split_tp_replicated(model_parameters, tp):
         pgs = [{"params": plist}]
     out = []
     for pg in pgs:
-        sharded = [p for p in pg["params"] if getattr(p, "tensor_model_parallel", False) or is_moe_param(p)]
-        repl = [p for p in pg["params"] if not (getattr(p, "tensor_model_parallel", False) or is_moe_param(p))]
+        sharded = [p for p in pg["params"] if getattr(p, "tensor_model_parallel", False)]
+        rest = [p for p in pg["params"] if not getattr(p, "tensor_model_parallel", False)]
+        experts = [p for p in rest if is_moe_param(p)]
+        repl = [p for p in rest if not is_moe_param(p)]
         if sharded:
             out.append({**pg, "params": sharded})
+        if experts:
+            dup = _expert_tp_dup(pg, tp)
+            out.append({**pg, "params": experts, **({"norm_weight": 1.0 / dup} if dup > 1 else {})})
         if repl:
             out.append({**pg, "params": repl, "norm_weight": 1.0 / tp})
     return out

@@ -139,6 +139,8 @@ CASES = [  # world, tp, ep, expert_tp, stage, clip
     (4, 1, 2, False, 2, 1.0),
     (2, 2, 2, False, 1, 1.0), (2, 2, 1, True, 2, 1.0),
     (4, 2, 2, False, 2, 0.0), (4, 2, 2, True, 1, 1.0), (4, 2, 2, True, 0, 1.0), (4, 2, 2, False, 0, 1.0),
+    # ep_size < tp without expert TP: the TP peers hold identical experts (norm weight ep/tp)
+    (2, 2, 1, False, 0, 1.0), (4, 2, 1, False, 0, 1.0),
 ]
 
 
