@@ -146,15 +146,19 @@ def destroy_process_group(group=None):
     tdist.destroy_process_group(group)
 
 
-def new_group(ranks, cache=True):
+def new_group(ranks, cache=True, tag=None):
     """Collective over the world (every rank must call with the same `ranks`, in the same order).
-    Cached per rank tuple so repeated topologies do not re-create RCCL communicators."""
-    key = tuple(sorted(int(r) for r in ranks))
+    Cached per rank tuple so repeated topologies do not re-create RCCL communicators. ``tag`` names
+    a second, independent communicator over the same ranks (e.g. ZeRO-3's gradient reduce-scatter
+    next to its parameter all-gathers: ProcessGroupNCCL runs every collective of one communicator
+    on one internal stream, so two streams of work on one group serialise)."""
+    ranks_key = tuple(sorted(int(r) for r in ranks))
+    key = (tag,) + ranks_key if tag is not None else ranks_key
     if cache and key in _State.group_cache:
         return _State.group_cache[key]
     if not is_initialized():
         return None
-    g = tdist.new_group(list(key))
+    g = tdist.new_group(list(ranks_key))
     if cache:
         _State.group_cache[key] = g
     return g

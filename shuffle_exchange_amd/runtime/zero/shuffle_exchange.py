@@ -61,6 +61,21 @@ class SliceTopology:
             if me in ranks:
                 self.slice_group, self.slice_ranks = pg, ranks
 
+    def make_reduce_groups(self):
+        """A second communicator per slice (collective: every rank creates every slice's), for
+        gradient reduction that must run concurrently with the parameter all-gathers on
+        ``slice_group``."""
+        if getattr(self, "reduce_group", None) is not None or self.S == 1:
+            return getattr(self, "reduce_group", None)
+        me = dist.get_rank()
+        self.reduce_group = None
+        for g in range(self.num_slices):
+            ranks = self.dp_ranks[g * self.S:(g + 1) * self.S]
+            pg = dist.new_group(ranks, tag="zero_reduce")
+            if me in ranks:
+                self.reduce_group = pg
+        return self.reduce_group
+
     def real(self, slice_idx, offset=None):
         return self.dp_ranks[slice_idx * self.S + (self.offset if offset is None else offset)]
 

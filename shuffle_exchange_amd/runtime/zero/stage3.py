@@ -195,8 +195,10 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         comm = self.S > 1 or self.offload_param or self.pswap is not None
         self.ag_stream = acc.named_stream("zero3_allgather") if acc.gpu and comm else None
         self.rs_stream = acc.named_stream("zero3_reduce") if acc.gpu and comm else None
-        # the optimizer-step stream is created high-priority: HIP serves high-priority streams from
-        # their own queue pool, so it never lands on the compute stream's queue
+        # gradient reduce-scatters (and the qgZ all-to-alls) get their own communicator over the
+        # slice ranks: on the all-gathers' communicator RCCL would queue them behind the backward
+        # prefetch gathers (one internal stream per communicator), whatever HIP stream issues them
+        self.reduce_group = self.topo.make_reduce_groups() if self.S > 1 else None
         self._in_bwd = False
         self._hooks = []
         self.fgroups = []
@@ -638,7 +640,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 self._quantized_reduce_scatter(u, st)
             else:
                 out = torch.empty(u.chunk, dtype=send.dtype, device=send.device)
-                dist.reduce_scatter_tensor(out, send, group=self.topo.slice_group)
+                dist.reduce_scatter_tensor(out, send, group=self.reduce_group)
                 if self.mics:
                     dist.all_reduce(out, group=self._mics_replica)
                     self._accumulate(u, out, self.sp_scale / (self.S * self.topo.num_slices))
@@ -702,8 +704,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         else:
             q, sc = quantize(staging, qg, self.gbits)
         rq, rs = torch.empty_like(q), torch.empty_like(sc)
-        dist.all_to_all_single(rq, q, group=self.topo.slice_group)
-        dist.all_to_all_single(rs, sc, group=self.topo.slice_group)
+        dist.all_to_all_single(rq, q, group=self.reduce_group)
+        dist.all_to_all_single(rs, sc, group=self.reduce_group)
         dequant_reduce(rq, rs, self.S, qg, self.gbits, u.grad, alpha=self.sp_scale / self.S, accumulate=u.rs_valid)
         u.rs_valid = True
         if self.rs_stream is not None:
@@ -783,12 +785,33 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             self._fetch(self.fgroups[j], wait=False)
 
     def _refresh_persistent(self):
+        """Rebuild the full copies of the resident units (persistent small parameters, plan-kept
+        units) after the step: ONE all-gather of all their shards packed back to back -- a
+        Llama-3-8B has ~65 persistent norm-weight units, and as many separate latency-bound
+        gathers cost more than the packed message -- then one strided copy per unit from the
+        rank-major result into its flat buffer."""
         if self.S == 1:
             return
-        for units in self.units:
-            for u in units:
-                if u.persistent or (u.keep and u.state == AVAILABLE):
-                    dist.all_gather_into_tensor(u.flat, u.shard, group=self.topo.slice_group)
+        units = [u for us in self.units for u in us if u.persistent or (u.keep and u.state == AVAILABLE)]
+        if not units:
+            return
+        if len(units) == 1:
+            u = units[0]
+            dist.all_gather_into_tensor(u.flat, u.shard, group=self.topo.slice_group)
+            return
+        total = sum(u.chunk for u in units)
+        send = torch.empty(total, dtype=units[0].dtype, device=units[0].flat.device)
+        off = 0
+        for u in units:
+            send[off:off + u.chunk].copy_(u.shard)
+            off += u.chunk
+        recv = torch.empty(self.S * total, dtype=send.dtype, device=send.device)
+        dist.all_gather_into_tensor(recv, send, group=self.topo.slice_group)
+        rv = recv.view(self.S, total)
+        off = 0
+        for u in units:
+            u.flat.view(self.S, u.chunk).copy_(rv[:, off:off + u.chunk])
+            off += u.chunk
 
     def apply_compile_plan(self, plan):
         """Install a schedule-compiler plan (compile/backend.py): kept groups are no longer

@@ -390,3 +390,31 @@ def case_mixtral_dense_sync(rank, world):
         eng.step()
     from shuffle_exchange_amd.moe.utils import is_moe_param
     return {n: p.detach().float().clone() for n, p in model.named_parameters() if not is_moe_param(p)}
+
+
+def case_zero3_comm_design(rank, world, steps):
+    """ZeRO-3 communicator layout and the post-step refresh collective count."""
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd import comm
+    model, cfg = tiny_llama(0)
+    ds = {"train_micro_batch_size_per_gpu": 1, "zero_optimization": {"stage": 3},
+          "optimizer": {"type": "SGD", "params": {"lr": 0.1}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    opt = eng.optimizer
+    n_persist = sum(1 for us in opt.units for u in us if u.persistent)
+    refresh = []
+    real = opt._refresh_persistent
+
+    def counted():
+        comm.reset_comms_stats()
+        real()
+        refresh.append(sum(n for k, (n, _) in comm.get_comm_volume().items() if "all_gather" in k))
+    opt._refresh_persistent = counted
+    for b in global_batches(cfg, world, 1, 16, steps):
+        local = b[rank:rank + 1]
+        loss = eng(local, labels=local)
+        eng.backward(loss)
+        eng.step()
+    return {"same_group": opt.reduce_group is opt.topo.slice_group,
+            "rs_ranks": comm.group_ranks(opt.reduce_group), "ag_ranks": comm.group_ranks(opt.topo.slice_group),
+            "n_persist": n_persist, "refresh": refresh, "params": full_params(eng)}

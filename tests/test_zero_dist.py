@@ -363,3 +363,18 @@ def test_sparse_marked_weight_with_dense_gradient_stays_in_sync():
         assert torch.equal(a, b)
     for a, b in zip(sp[0], dn[0]):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_zero3_reduce_scatter_has_its_own_communicator_and_one_refresh_gather():
+    """ZeRO-3's gradient reduce-scatter runs on a second communicator over the slice ranks (RCCL
+    serialises every collective of one communicator, so the backward prefetch all-gathers would
+    queue it), and the post-step rebuild of the persistent units is ONE packed all-gather; the
+    trained parameters still match the reference."""
+    world, steps = 2, 2
+    for r in run_dist(C.case_zero3_comm_design, world, steps):
+        assert not r["same_group"]
+        assert r["rs_ranks"] == r["ag_ranks"] == [0, 1]
+        assert r["n_persist"] > 1
+        assert r["refresh"] == [1] * steps, r["refresh"]
+    ref = C.reference_train({"type": "SGD", "params": {"lr": 0.1}}, steps, world, 1, 16)
+    _close(r["params"], ref)
