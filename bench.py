@@ -122,6 +122,27 @@ def comm_model(opt, world, stage, knobs, gas, elem_bytes=2):
     return out
 
 
+def effective_zero(opt):
+    """The ZeRO behaviour the run actually had (config knobs can be inert: e.g. the deferred reduce
+    and the retained gathers need a partition group of more than one rank)."""
+    if opt is None:
+        return {}
+    if hasattr(opt, "fgroups"):  # stage 3
+        units = [u for us in opt.units for u in us]
+        return {"partition_size": opt.S, "defer_reduce": bool(opt.defer_reduce),
+                "retain_params_in_step": bool(opt.retain_params), "prefetch_depth": opt.prefetch_depth,
+                "prefetch_numel": opt.prefetch_numel, "max_reuse_distance": opt.max_reuse_distance,
+                "max_live_parameters": opt.max_live_parameters, "units": len(units),
+                "persistent_units": sum(1 for u in units if u.persistent),
+                "reduce_communicator_separate": opt.reduce_group is not None
+                and opt.reduce_group is not opt.topo.slice_group}
+    if hasattr(opt, "units") and hasattr(opt, "topo"):  # stage 1/2
+        return {"stage": getattr(opt, "stage", None), "partition_size": opt.topo.S,
+                "units": sum(len(us) for us in opt.units),
+                "shuffle_exchange": getattr(opt, "shuffle_exchange_enabled", False)}
+    return {"optimizer": type(opt).__name__}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -241,6 +262,9 @@ def main():
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    final_loss = loss.detach().float().reshape(1)
+    if sp > 1:  # each SP rank holds its sequence shard's share of the loss: the sum is the sample loss
+        dist.all_reduce(final_loss, group=groups.get_sequence_parallel_group())
     tokens = dp * mbs * gas * seq * args.steps
     tps = tokens / elapsed
     if c["family"] == "mixtral":
@@ -279,11 +303,12 @@ def main():
                        "params": n_params, "activation_checkpointing": ac,
                        "optimizer": "AdamW(fp32 master, " + ("C++ CPU Adam on host" if c.get("offload") else
                                                              "fused HIP") + ")",
-                       "zero_knobs": c["knobs"], "zero_optimization": zero, "sequence_parallel_size": sp,
+                       "zero_knobs": c["knobs"], "zero_optimization": zero,
+                       "zero_effective": effective_zero(engine.optimizer), "sequence_parallel_size": sp,
                        "expert_parallel_size": ep},
             "tflops_per_gpu": round(tflops, 1),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if on_gpu else None,
-            "final_loss": round(float(loss.detach()), 4),
+            "final_loss": round(float(final_loss.item()), 4),
             "comm_measured": {op: {"calls_per_step": round(n / args.steps, 2), "bytes_per_step": b // args.steps}
                               for op, (n, b) in sorted(vol.items())},
             "comm_model": comm_model(engine.optimizer, world, stage, c["knobs"], gas),

@@ -16,11 +16,22 @@ MI355X-first:
   inputs (<= 16 rows) stream 0.75 (FP6) / 0.5 (FP4) bytes per weight through the skinny MFMA
   kernel; larger inputs run the bit planes straight through the block-scaled MFMA GEMM
   (mx_gemm.hip: exact e3m2 / e2m1 -> e4m3 transcode in registers, MXFP8 activations).
-* ``fp8_linear`` runs the GEMM ON the FP8 matrix cores (hipBLASLt ``_scaled_mm`` with row-wise
-  scales: 2.2 PF/s measured on MI355X vs ~1.3-1.5 PF/s for bf16), quantizing activations per row
-  with the HIP kernel; ``matmul_fp8`` keeps the reference's weight-only semantics (bf16 activations
-  x group-scaled fp8 weights) by dequantizing the weight tiles to bf16 first.
+* ``fp8_linear`` runs the GEMM on the block-scaled FP8 matrix cores: the hand-written MX kernel
+  (mx_gemm.hip, ``v_mfma_scale_f32_32x32x64_f8f6f4``) with MXFP8 activations (one E8M0 exponent
+  per 32 values, quantised by a HIP pass) against the e4m3 weight codes with unit block exponents
+  and the per-output-row weight scale in its epilogue. Measured (profiles/mx_gemm_bench.log,
+  2048-8192 tokens): 0.83-1.26x bf16 hipBLASLt including the activation pass -- ahead on the
+  Llama-3-8B MLP shapes, behind at N <= 6144; hipBLASLt's row-wise ``_scaled_mm`` (the previous
+  route) ran 0.23-1.37x. Shapes the MX kernel does not tile (N or K not a multiple of 128) keep
+  ``_scaled_mm``.
+* ``matmul_fp8`` keeps the reference's weight-only semantics (bf16 activations x group-scaled
+  fp8 weights, reference fp8_gemm_triton.py:19-67) by dequantising the weight in K slices of at
+  most ``MATMUL_FP8_SLICE`` rows into one reused bf16 buffer and accumulating the slice GEMMs, so
+  no full-size bf16 weight is ever allocated (the Triton kernel dequantises per K tile in
+  registers; here a slice is staged through HBM).
 """
+import math
+
 import torch
 
 from . import native
@@ -140,12 +151,33 @@ def quantize_weight_fp8_rowwise(w):
     return q.view(torch.float8_e4m3fn).view(w.shape), s
 
 
+_UNIT_EXP = {}
+
+
+def _unit_exponents(N, K, device):
+    """E8M0 block exponents of 1.0 for an [N, K] e4m3 weight used as MXFP8 (cached: a HIP-graph
+    capture must not allocate)."""
+    key = (N, K // 32, str(device))
+    t = _UNIT_EXP.get(key)
+    if t is None:
+        t = _UNIT_EXP[key] = torch.full((N, K // 32), 127, dtype=torch.uint8, device=device)
+    return t
+
+
 def fp8_linear(x, w_q, w_scale, bias=None, out_dtype=torch.bfloat16):
-    """y = x @ (w_q * w_scale[:, None])^T with x quantized per row to FP8 and the product on the
-    FP8 MFMA path. x [..., K] bf16/fp32, w_q [N, K] float8_e4m3fn, w_scale [N] fp32."""
+    """y = x @ (w_q * w_scale[:, None])^T on the FP8 matrix cores. x [..., K] bf16/fp32, w_q [N, K]
+    float8_e4m3fn, w_scale [N] fp32. GPU: MXFP8 activations x e4m3 weights on the block-scaled MX
+    GEMM (per-row weight scale in the epilogue); CPU: the same product from dequantised fp32."""
     K = x.shape[-1]
     x2 = x.reshape(-1, K)
-    if x2.is_cuda and K % 16 == 0 and w_q.shape[0] % 16 == 0:
+    N = w_q.shape[0]
+    if x2.is_cuda and K % 128 == 0 and N % 128 == 0:
+        from .mx import mx_linear
+        native.require_hip()
+        wq8 = w_q.view(torch.uint8)
+        y = mx_linear(x2, wq8, _unit_exponents(N, K, x2.device), "mxfp8", bias, col_scale=w_scale)
+        return y.to(out_dtype).view(*x.shape[:-1], N)
+    if x2.is_cuda and K % 16 == 0 and N % 16 == 0:
         native.require_hip()
         q, s = quantize_fp8(x2, K)
         y = torch._scaled_mm(q.view(torch.float8_e4m3fn).view(x2.shape), w_q.t(), scale_a=s.view(-1, 1),
@@ -157,16 +189,37 @@ def fp8_linear(x, w_q, w_scale, bias=None, out_dtype=torch.bfloat16):
         y = (xd @ wd.t()).to(out_dtype)
         if bias is not None:
             y = y + bias.to(out_dtype)
-    return y.view(*x.shape[:-1], w_q.shape[0])
+    return y.view(*x.shape[:-1], N)
+
+
+MATMUL_FP8_SLICE = 1024  # weight rows (K) dequantised per slice in matmul_fp8
 
 
 def matmul_fp8(inp, weight, scale, quantization_group_size):
     """Reference ``matmul_fp8``: inp [M, K] (bf16/fp16) x weight [K, N] stored as fp8 (uint8 codes
-    or float8_e4m3fn) with one scale per ``quantization_group_size`` consecutive weight elements."""
+    or float8_e4m3fn) with one scale per ``quantization_group_size`` consecutive weight elements.
+    The weight is dequantised K-slice by K-slice into one reused buffer (never the whole weight)."""
     wq = weight.view(torch.uint8) if weight.dtype != torch.uint8 else weight
-    wd = dequantize_fp8(wq.reshape(-1), scale.reshape(-1), quantization_group_size, dtype=inp.dtype)
-    return torch.matmul(inp, wd.view(weight.shape))
-
+    K, N = weight.shape
+    g = int(quantization_group_size)
+    flat, sc = wq.reshape(-1), scale.reshape(-1)
+    step = g // math.gcd(g, N)  # slices start on a scale-group boundary: rows * N % g == 0
+    rows = max(step, (MATMUL_FP8_SLICE // step) * step)
+    if rows >= K:
+        return torch.matmul(inp, dequantize_fp8(flat, sc, g, dtype=inp.dtype).view(K, N))
+    buf = torch.empty(rows * N, dtype=inp.dtype, device=inp.device)
+    x2 = inp.reshape(-1, K)
+    out = torch.zeros(x2.shape[0], N, dtype=torch.float32, device=inp.device)  # fp32 sum over slices
+    for k0 in range(0, K, rows):
+        k1 = min(K, k0 + rows)
+        e0, e1 = k0 * N, k1 * N
+        seg = dequantize_fp8(flat[e0:e1], sc[e0 // g:(e1 + g - 1) // g], g, out=buf[:e1 - e0], dtype=inp.dtype)
+        w = seg.view(k1 - k0, N)
+        if out.is_cuda:  # fp32-out GEMM accumulating in its epilogue: no bf16 partial products
+            torch.ops.aten.addmm.dtype_out(out, x2[:, k0:k1], w, torch.float32, beta=1, alpha=1, out=out)
+        else:
+            out.addmm_(x2[:, k0:k1].float(), w.float())
+    return out.to(inp.dtype).view(*inp.shape[:-1], N)
 
 class FP8Weight:
     """Row-scaled FP8 (e4m3) weight of a linear layer, [N, K] -> used through ``ops.linear.linear``:

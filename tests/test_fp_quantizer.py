@@ -49,6 +49,46 @@ def test_fp8_linear_and_matmul_fp8_cpu():
     assert ((out.float() - x @ w).norm() / (x @ w).norm()).item() < 0.05
 
 
+def test_matmul_fp8_never_materialises_the_full_weight(monkeypatch):
+    """Weight-only FP8 GEMM: the weight is dequantised in K slices of at most MATMUL_FP8_SLICE rows
+    (the dequantize op is patched to refuse anything larger) and matches the full product."""
+    import shuffle_exchange_amd.ops.fp_quantizer as fq
+    from shuffle_exchange_amd.ops.quantizer import dequantize_fp8, quantize_fp8
+    torch.manual_seed(0)
+    K, N, g = 5000, 96, 64
+    w, x = torch.randn(K, N), torch.randn(7, K).bfloat16()
+    q, s = quantize_fp8(w.reshape(-1), g)
+    ref = x.float() @ dequantize_fp8(q, s, g, dtype=torch.float32).view(K, N)
+    real = fq.dequantize_fp8
+    seen = []
+
+    def guarded(qq, *a, **k):
+        assert qq.numel() <= fq.MATMUL_FP8_SLICE * N, "full-size dequantised weight"
+        seen.append(qq.numel())
+        return real(qq, *a, **k)
+    monkeypatch.setattr(fq, "dequantize_fp8", guarded)
+    out = fq.matmul_fp8(x, q.view(K, N), s, g).float()
+    assert len(seen) == -(-K // fq.MATMUL_FP8_SLICE)
+    assert ((out - ref).abs().max() / ref.abs().max()).item() < 5e-3
+
+
+@pytest.mark.gpu
+def test_fp8_linear_gpu_on_mx_gemm():
+    """W8A8 prefill on the block-scaled MX GEMM: equals MXFP8(x) @ (e4m3 codes x row scale)^T."""
+    from shuffle_exchange_amd.ops import mx
+    from shuffle_exchange_amd.ops.fp_quantizer import fp8_linear, quantize_weight_fp8_rowwise
+    torch.manual_seed(1)
+    M, N, K = 300, 384, 1024
+    w = torch.randn(N, K, device="cuda") * 0.05
+    wq, ws = quantize_weight_fp8_rowwise(w)
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    b = torch.randn(N, device="cuda").bfloat16()
+    y = fp8_linear(x, wq, ws, b).float()
+    xq, xs = torch.ops.sxe.mx_quant_fp8(x)
+    ref = mx.dequantize(xq, xs, "mxfp8", K) @ (wq.float() * ws.view(-1, 1)).t() + b.float()
+    assert ((y - ref).abs().max() / ref.abs().max()).item() < 1e-2
+
+
 @pytest.mark.gpu
 def test_fp8_linear_gpu_scaled_mm():
     from shuffle_exchange_amd.ops.fp_quantizer import FP8Linear

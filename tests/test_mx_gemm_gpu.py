@@ -63,7 +63,7 @@ def test_mx_gemm_asymmetric_identity():
 
 @pytest.mark.parametrize("bits", [6, 4])
 @pytest.mark.parametrize("M,N,K", [(17, 128, 128), (300, 384, 1024), (2048, 1024, 512), (1030, 4096, 256)])
-def test_fpx_weight_prefill_on_mx_gemm(bits, M, N, K):
+def test_fpx_weight_prefill_on_mx_gemm(bits, M, N, K, monkeypatch):
     """FPxWeight (FP6-LLM bit planes) with > 16 rows: the planes go straight into the block-scaled
     MFMA GEMM (exact e3m2 / e2m1 -> e4m3 transcode in registers, MXFP8 activations, per-row scale in
     the epilogue); reference = MXFP8(x) @ the fp32-decoded weight, no bf16 weight is materialised."""
@@ -73,10 +73,14 @@ def test_fpx_weight_prefill_on_mx_gemm(bits, M, N, K):
     W = FPxWeight(w.bfloat16(), bits)
     x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     b = torch.randn(N, device="cuda").to(torch.bfloat16)
-    called = []
-    real = torch.ops.sxe.fpxw_unpack
+    # the only way to a bf16 weight is FPxWeight.dequantize (fpxw_unpack): refuse it during linear
+    real_deq = FPxWeight.dequantize
+
+    def refuse(self, *a, **k):
+        raise AssertionError("FPxWeight.linear materialised a dequantised weight")
+    monkeypatch.setattr(FPxWeight, "dequantize", refuse)
     y = W.linear(x, b)
-    assert not called and real is torch.ops.sxe.fpxw_unpack
+    monkeypatch.setattr(FPxWeight, "dequantize", real_deq)
     q, s = torch.ops.sxe.mx_quant_fp8(x)
     ref = mx.dequantize(q, s, "mxfp8", K) @ W.dequantize(torch.float32).t() + b.float()
     err = (y.float() - ref).abs().max().item()
