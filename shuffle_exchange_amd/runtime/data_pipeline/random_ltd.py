@@ -20,6 +20,16 @@ class RandomLTDScheduler:
         self.require_steps = cfg.get("require_steps", 100)
         self.current = self.min_value
         self.consumed_layer_tokens = 0
+        # token selection draws from a counter-based stream (seed, draw index) instead of the global
+        # RNG, and the draw index is checkpointed: a resumed run drops the same tokens
+        self.seed = int(config.get("seed", 1234))
+        self.draws = 0
+
+    def generator(self, device):
+        g = torch.Generator(device=device)
+        g.manual_seed((self.seed * 1_000_003 + self.draws) % (1 << 62))
+        self.draws += 1
+        return g
 
     def get_current_seq(self):
         return self.current
@@ -30,11 +40,12 @@ class RandomLTDScheduler:
         return self.current
 
     def state_dict(self):
-        return {"current": self.current, "consumed_layer_tokens": self.consumed_layer_tokens}
+        return {"current": self.current, "consumed_layer_tokens": self.consumed_layer_tokens, "draws": self.draws}
 
     def load_state_dict(self, sd):
         self.current = sd["current"]
         self.consumed_layer_tokens = sd.get("consumed_layer_tokens", 0)
+        self.draws = sd.get("draws", 0)
 
 
 def token_sort_(idx):
@@ -85,7 +96,10 @@ class RandomLayerTokenDrop(nn.Module):
         if not self.training or k >= x.shape[1]:
             return self.layer(x, *args, **kwargs)
         B, S, _ = x.shape
-        idx = token_sort_(torch.rand(B, S, device=x.device).topk(k, dim=1).indices)
+        gen = self.scheduler.generator(x.device) if hasattr(self.scheduler, "generator") else None
+        idx = token_sort_(torch.rand(B, S, device=x.device, generator=gen).topk(k, dim=1).indices)
+        if self.scheduler is not None:
+            self.scheduler.consumed_layer_tokens += B * k
         args = list(args)
         full = {0: x}
         for j, a in enumerate(args):

@@ -221,7 +221,7 @@ class SXEEngine(nn.Module):
             "enabled", True) else {}
         if rltd.get("enabled"):
             from .data_pipeline import RandomLTDScheduler, convert_to_random_ltd
-            self.random_ltd_scheduler = RandomLTDScheduler(rltd)
+            self.random_ltd_scheduler = RandomLTDScheduler({**rltd, "seed": self._de.get("seed", 1234)})
             ids = list(rltd.get("random_ltd_layer_id", []))
             n = convert_to_random_ltd(self.module, ids, self.random_ltd_scheduler)
             if rltd.get("random_ltd_layer_num", n) != n:
@@ -1126,6 +1126,66 @@ class SXEEngine(nn.Module):
             sd[n] = b.detach().cpu().clone()
         return sd
 
+    def _shared_params(self):
+        """{name of a tied parameter that is not stored separately: name of the parameter holding
+        its data} (reference engine.py:3727 ``_get_shared_params``); keyed on the Parameter object,
+        which ZeRO keeps unique per tied weight even while its storage is released."""
+        first, shared = {}, {}
+        for mname, mod in self.module.named_modules():
+            for pname, p in mod.named_parameters(recurse=False):
+                key = f"{mname}.{pname}" if mname else pname
+                if id(p) in first:
+                    shared[key] = first[id(p)]
+                else:
+                    first[id(p)] = key
+        return shared
+
+    def _frozen_param_fragments(self):
+        """Frozen (requires_grad=False) parameters by name, on the host (reference
+        ``_get_zero_frozen_param_attributes(_get_param_fragment_func)``): ZeRO keeps them out of its
+        flat units, so each is whole on every rank."""
+        out = {}
+        for n, p in self.module.named_parameters():
+            if not p.requires_grad and p.numel() > 0:
+                out[n] = p.detach().cpu().clone()
+        return out
+
+    def _copy_recovery_script(self, tag_dir):
+        """Copy the offline consolidation script into the tag directory (reference engine.py:3767
+        ``_copy_recovery_script``): ``python zero_to_fp32.py . out.pt`` there rebuilds the fp32
+        weights with nothing but torch installed."""
+        import shutil
+        import stat
+        src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "utils", "zero_to_fp32.py")
+        dst = os.path.join(tag_dir, "zero_to_fp32.py")
+        shutil.copyfile(src, dst)
+        try:
+            os.chmod(dst, os.stat(dst).st_mode | stat.S_IEXEC)
+        except OSError:
+            pass
+
+    def _dp_writer_group(self, stage):
+        """The ranks that write the (replicated) ZeRO-0/1/2 model-states file together
+        (``checkpoint.writer.data_parallel``: replica / socket / machine, reference
+        runtime/model_checkpointing/data_parallel_writer_factory.py), or None for a rank-0 write.
+        One node: every mode maps to the sequence-data-parallel group."""
+        w = self._config.model.checkpoint.writer or {}
+        mode = w.get("data_parallel")
+        if stage >= 3 or not mode or groups.get_sequence_data_parallel_world_size() == 1:
+            return None
+        if self._moe_layers():
+            return None  # expert files are written per expert-data-parallel group already
+        return groups.get_sequence_data_parallel_group()
+
+    def _save_data_parallel(self, state, path, group):
+        """Write one model-states file with every data-parallel replica writing a disjoint byte
+        range (io/parallel_writer.py): each rank serialises the identical replicated state, the
+        ranks check that their streams agree (size + adler32) and otherwise fall back to a rank-0
+        write."""
+        from ..io.parallel_writer import save_data_parallel
+        self.checkpoint_engine.wait()
+        self.last_dp_write_bytes = save_data_parallel(state, path, group)
+
     def save_checkpoint(self, save_dir, tag=None, client_state=None, save_latest=True,
                         exclude_frozen_parameters=False):
         client_state = client_state or {}
@@ -1146,7 +1206,8 @@ class SXEEngine(nn.Module):
         if moe and module_sd is not None:
             module_sd, experts = self._split_expert_state(module_sd)
             self._save_expert_files(d, experts)
-        if write_model:
+        dpw = self._dp_writer_group(stage)
+        if write_model or dpw is not None:
             state = dict(
                 module=module_sd,
                 buffer_names=[n for n, _ in self.module.named_buffers()],
@@ -1154,7 +1215,13 @@ class SXEEngine(nn.Module):
                 param_shapes=[{names[p]: tuple(getattr(p, "ds_shape", p.shape)) for p in pg["params_orig"]}
                               for pg in self._orig_param_groups()],
                 frozen_param_shapes={n: tuple(p.shape) for n, p in self.module.named_parameters() if not p.requires_grad},
+                shared_params=self._shared_params(),
+                frozen_param_fragments=self._frozen_param_fragments() if (stage >= 2 and not exclude_frozen_parameters)
+                else None,
                 lr_scheduler=self.lr_scheduler.state_dict() if self.lr_scheduler is not None else None,
+                data_sampler=self.curriculum_sampler.state_dict()
+                if getattr(self, "curriculum_sampler", None) is not None else None,
+                random_ltd=self.random_ltd_scheduler.state_dict() if self.random_ltd_enabled() else None,
                 sparse_tensor_module_names=[],
                 skipped_steps=self.skipped_steps,
                 global_steps=self.global_steps,
@@ -1170,7 +1237,10 @@ class SXEEngine(nn.Module):
             if moe:
                 state["num_experts"] = [m.num_experts for _, m in moe]
             state.update(client_state)
-            self.checkpoint_engine.save(state, model_path)
+            if dpw is None:
+                self.checkpoint_engine.save(state, model_path)
+            else:
+                self._save_data_parallel(state, model_path, dpw)
         write_optim = True
         if moe and stage == 0:
             # identical on the EDP peers of this model-parallel slice: its first rank writes
@@ -1181,9 +1251,13 @@ class SXEEngine(nn.Module):
             osd = self.optimizer.state_dict()
             if hasattr(self.optimizer, "unit_layout"):
                 osd["unit_layout"] = self.optimizer.unit_layout(names)
+            if hasattr(self.optimizer, "param_slice_mappings"):
+                osd["param_slice_mappings"] = self.optimizer.param_slice_mappings(names)
             self.checkpoint_engine.save({"optimizer_state_dict": osd, "ds_config": self._config._param_dict,
                                          "ds_version": "sxe-0.1"}, optim_path)
         self.checkpoint_engine.commit(tag)
+        if self.global_rank == 0 and stage > 0:
+            self._copy_recovery_script(d)
         dist.barrier()
         if save_latest and self.global_rank == 0:
             with open(os.path.join(save_dir, "latest"), "w") as f:
@@ -1246,10 +1320,15 @@ class SXEEngine(nn.Module):
             self.global_steps = state.get("global_steps", 0)
             self.global_samples = state.get("global_samples", 0)
             self.skipped_steps = state.get("skipped_steps", 0)
+            if state.get("data_sampler") is not None and getattr(self, "curriculum_sampler", None) is not None:
+                self.curriculum_sampler.load_state_dict(state["data_sampler"])
+            if state.get("random_ltd") is not None and self.random_ltd_enabled():
+                self.random_ltd_scheduler.load_state_dict(state["random_ltd"])
         dist.barrier()
         skip = {"module", "buffer_names", "optimizer", "param_shapes", "frozen_param_shapes", "lr_scheduler",
                 "sparse_tensor_module_names", "skipped_steps", "global_steps", "global_samples", "dp_world_size",
-                "mp_world_size", "ds_config", "ds_version", "num_experts", "tp_partitions"}
+                "mp_world_size", "ds_config", "ds_version", "num_experts", "tp_partitions", "shared_params",
+                "frozen_param_fragments", "data_sampler", "random_ltd"}
         client = {k: v for k, v in state.items() if k not in skip}
         return os.path.join(load_dir, str(tag)), client
 

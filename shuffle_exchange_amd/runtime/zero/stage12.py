@@ -372,6 +372,26 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         return [[{"params": [name_of.get(p, "") for p in u.params], "shapes": u.shapes, "offsets": u.offsets,
                   "numel": u.numel, "padded": u.padded, "chunk": u.chunk} for u in units] for units in self.units]
 
+    def param_slice_mappings(self, name_of):
+        """Per param group {param name: {"numel", "start"}}: the fragment of each parameter held
+        in this rank's flat fp32 partition (reference stage_1_and_2.py:2510 ``param_slice_mappings``
+        of ``fragment_address(numel, start)``), plus ``param_start``, the fragment's first element
+        inside the parameter (the units are not padded per parameter, so a fragment can start
+        mid-parameter on any rank)."""
+        out = []
+        for units in self.units:
+            m, base = {}, 0
+            for u in units:
+                for i, p in enumerate(u.params):
+                    r = u.param_range_in_shard(i)
+                    if r is not None:
+                        plo, phi, slo = r
+                        m[name_of.get(p, f"param_{id(p)}")] = {"numel": phi - plo, "start": base + slo,
+                                                               "param_start": plo}
+                base += u.chunk
+            out.append(m)
+        return out
+
     def state_dict(self):
         self._host_materialize()
         return {

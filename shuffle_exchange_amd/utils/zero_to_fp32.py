@@ -50,11 +50,24 @@ def _optim_files(d):
     return sorted(files, key=key)
 
 
+def _reference_reader():
+    """The reference-layout reader when the package is importable; the copy of this script that
+    save_checkpoint drops into every tag directory runs without it (own checkpoints only)."""
+    try:
+        from shuffle_exchange_amd.checkpoint.reference_format import is_reference_checkpoint, read_reference_checkpoint
+    except ImportError:
+        return None
+    return is_reference_checkpoint, read_reference_checkpoint
+
+
 def get_fp32_state_dict_from_zero_checkpoint(checkpoint_dir, tag=None, exclude_frozen_parameters=False):
-    from ..checkpoint.reference_format import is_reference_checkpoint, read_reference_checkpoint
-    if is_reference_checkpoint(checkpoint_dir, tag):  # written in the reference's ZeRO layout
-        return dict(read_reference_checkpoint(checkpoint_dir, tag)["fp32"])
-    d = _tag_dir(checkpoint_dir, tag)
+    ref = _reference_reader()
+    if ref is not None and ref[0](checkpoint_dir, tag):  # written in the reference's ZeRO layout
+        return dict(ref[1](checkpoint_dir, tag)["fp32"])
+    if tag is None and not os.path.isfile(os.path.join(checkpoint_dir, "latest")) and _optim_files(checkpoint_dir):
+        d = checkpoint_dir  # pointed at the tag directory itself (the copied script: `python zero_to_fp32.py . out`)
+    else:
+        d = _tag_dir(checkpoint_dir, tag)
     files = _optim_files(d)
     if not files:
         raise FileNotFoundError(f"no ZeRO optimizer files in {d}")
@@ -97,9 +110,16 @@ def get_fp32_state_dict_from_zero_checkpoint(checkpoint_dir, tag=None, exclude_f
             if k in mod and k not in sd:
                 sd[k] = mod[k]
         if not exclude_frozen_parameters:
+            frags = ms.get("frozen_param_fragments") or {}
             for k in ms.get("frozen_param_shapes", {}):
-                if k in mod and k not in sd:
+                if k not in sd and k in mod:
                     sd[k] = mod[k].float()
+                elif k not in sd and k in frags:  # ZeRO-2/3 files without a module state
+                    sd[k] = frags[k].float()
+        # tied weights: the parameter that is not stored shares the data of the one that is
+        for k, src in (ms.get("shared_params") or {}).items():
+            if src in sd:
+                sd[k] = sd[src]
     return sd
 
 
