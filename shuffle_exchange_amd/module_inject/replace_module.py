@@ -671,6 +671,173 @@ class FusedCLIPEncoderLayer(_Fused):
         return h + m
 
 
+class FusedMegatronLayer(_Fused):
+    """Megatron-LM GPT ``ParallelTransformerLayer`` (reference containers/megatron_gpt.py
+    ``MegatronLayerPolicy`` + features/megatron.py, and megatron_gpt_moe.py for its MoE form):
+    sequence-first hidden states [S, B, H], pre-LayerNorm, ONE packed QKV GEMM -- Megatron v2
+    stores query_key_value per head as [q_h | k_h | v_h] row blocks; the policy re-packs them to
+    [q | k | v] once (``_align_qkv_transposed``) --, causal flash attention, dense + residual folded
+    into the post-attention LayerNorm, bias-GELU MLP (or the layer's own MoE / expert module, whose
+    first output is kept), residual. ``attention`` (v1) and ``self_attention`` (v2) are both
+    recognised; ``apply_residual_connection_post_layernorm`` is honoured. KV-cache, cross-attention
+    and non-causal masks go to the original layer."""
+
+    def __init__(self, layer, config):
+        super().__init__(layer)
+        at = getattr(layer, "self_attention", None) or layer.attention
+        self.v2 = hasattr(layer, "self_attention")
+        qkv = at.query_key_value
+        H = qkv.weight.shape[1]
+        self.nh = int(getattr(at, "num_attention_heads", getattr(at, "num_attention_heads_per_partition", 0)) or
+                      getattr(config, "num_attention_heads"))
+        self.hd = qkv.weight.shape[0] // (3 * self.nh)
+        w, b = qkv.weight, qkv.bias
+        if self.v2:  # [nh, 3, hd, H] -> [3, nh, hd, H]
+            w = w.view(self.nh, 3, self.hd, H).transpose(0, 1).reshape(3 * self.nh * self.hd, H)
+            b = b.view(self.nh, 3, self.hd).transpose(0, 1).reshape(-1) if b is not None else None
+        self.w_qkv = self._p(w)
+        self.b_qkv = self._p(b) if b is not None else None
+        self.w_o = self._p(at.dense.weight)
+        self.b_o = self._p(at.dense.bias) if at.dense.bias is not None else None
+        li, lp = layer.input_layernorm, layer.post_attention_layernorm
+        self.ln1_w, self.ln1_b, self.eps1 = self._p(li.weight), self._p(li.bias), float(getattr(li, "eps", 1e-5))
+        self.ln2_w, self.ln2_b, self.eps2 = self._p(lp.weight), self._p(lp.bias), float(getattr(lp, "eps", 1e-5))
+        self.post_ln_residual = bool(getattr(layer, "apply_residual_connection_post_layernorm", False))
+        mlp = layer.mlp
+        self.dense_mlp = hasattr(mlp, "dense_h_to_4h")
+        if self.dense_mlp:
+            self.w_fc, self.b_fc = self._p(mlp.dense_h_to_4h.weight), self._p(mlp.dense_h_to_4h.bias)
+            self.w_out, self.b_out = self._p(mlp.dense_4h_to_h.weight), self._p(mlp.dense_4h_to_h.bias)
+        else:
+            self.mlp = mlp  # MoE (megatron_gpt_moe): the expert layer runs as is
+        self.act = _act_name(getattr(config, "hidden_act", "gelu")) if config is not None else "gelu_exact"
+        self._link()
+
+    def _links(self):
+        if self.v2:
+            return []  # the per-head interleaved QKV has no view of the re-packed weight
+        at = self.orig.attention
+        out = [(at.query_key_value.weight, self.w_qkv), (at.dense.weight, self.w_o)]
+        if self.b_qkv is not None:
+            out.append((at.query_key_value.bias, self.b_qkv))
+        return out
+
+    @staticmethod
+    def _is_causal_mask(mask, S):
+        if mask is None:
+            return True
+        if mask.dtype != torch.bool or mask.shape[-1] != S or mask.shape[-2] != S:
+            return False
+        m = mask.reshape(-1, S, S)
+        ref = torch.ones(S, S, dtype=torch.bool, device=mask.device).triu(1)  # True = masked (Megatron)
+        return bool((m == ref).all())
+
+    def forward(self, hidden_states, attention_mask=None, encoder_output=None, enc_dec_attn_mask=None,
+                layer_past=None, get_key_value=False, **kwargs):
+        S, B, H = hidden_states.shape
+        if (encoder_output is not None or layer_past is not None or get_key_value
+                or not self._is_causal_mask(attention_mask, S)):
+            return self._delegate(hidden_states, attention_mask, encoder_output=encoder_output,
+                                  enc_dec_attn_mask=enc_dec_attn_mask, layer_past=layer_past,
+                                  get_key_value=get_key_value, **kwargs)
+        x = hidden_states.transpose(0, 1)  # [B, S, H]
+        ln1 = layer_norm(x, self.ln1_w, self.ln1_b, self.eps1)
+        qkv = linear(ln1, self.w_qkv, self.b_qkv).view(B, S, 3, self.nh, self.hd)
+        o = _attend(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], None, True, 1.0 / math.sqrt(self.hd))
+        a = linear(o.reshape(B, S, self.nh * self.hd), self.w_o, self.b_o)
+        ln2, h = layer_norm(a, self.ln2_w, self.ln2_b, self.eps2, residual=ln1 if self.post_ln_residual else x)
+        if self.dense_mlp:
+            m = linear(bias_act(linear(ln2, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
+        else:
+            m = self.mlp(ln2)
+            m = m[0] if isinstance(m, tuple) else m
+        y = (ln2 if self.post_ln_residual else h) + m
+        return y.transpose(0, 1).contiguous()
+
+
+def _is_causal_additive(mask, Sq, Sk):
+    """An HF additive mask [B, 1, Sq, Sk] that is exactly the bottom-right causal pattern (no padding):
+    the fused causal kernel can replace it."""
+    if mask is None:
+        return True
+    if mask.dim() != 4 or mask.shape[-2] != Sq or mask.shape[-1] != Sk:
+        return False
+    vis = torch.ones(Sq, Sk, dtype=torch.bool, device=mask.device).tril(Sk - Sq)
+    m = mask.reshape(-1, Sq, Sk)
+    return bool(((m == 0) == vis).all())
+
+
+class FusedInternLMLayer(_Fused):
+    """InternLM (v1) ``InternLMDecoderLayer`` (reference containers/internlm.py
+    ``InternLMLayerPolicy``): the Llama structure with biased q/k/v/o projections and the rotary
+    table inside the attention module (``rotary_emb(x, seq_len)`` -> cos/sin indexed by
+    ``position_ids``). RMSNorm -> one packed biased QKV GEMM -> rotate-half RoPE -> causal attention
+    (legacy tuple KV cache) -> o_proj -> residual folded into the post-attention RMSNorm -> gate|up
+    GEMM -> SwiGLU -> down. Returns the HF-v4 tuple ``(hidden, [attn_weights], [present])``."""
+
+    def __init__(self, layer, config):
+        super().__init__(layer)
+        at, mlp = layer.self_attn, layer.mlp
+        self.nh = int(getattr(at, "num_heads", getattr(config, "num_attention_heads", 0)))
+        self.hd = at.q_proj.weight.shape[0] // self.nh
+        self.w_qkv = self._p(torch.cat([at.q_proj.weight, at.k_proj.weight, at.v_proj.weight]))
+        self.b_qkv = (self._p(torch.cat([at.q_proj.bias, at.k_proj.bias, at.v_proj.bias]))
+                      if at.q_proj.bias is not None else None)
+        self.w_o = self._p(at.o_proj.weight)
+        self.b_o = self._p(at.o_proj.bias) if at.o_proj.bias is not None else None
+        self.w_gu = self._p(torch.cat([mlp.gate_proj.weight, mlp.up_proj.weight]))
+        self.w_down = self._p(mlp.down_proj.weight)
+        li, lp = layer.input_layernorm, layer.post_attention_layernorm
+        self.ln1_w, self.eps1 = self._p(li.weight), float(getattr(li, "variance_epsilon", 1e-6))
+        self.ln2_w, self.eps2 = self._p(lp.weight), float(getattr(lp, "variance_epsilon", 1e-6))
+        self._link()
+
+    def _links(self):
+        L, q = self.orig, self.nh * self.hd
+        at, mlp = L.self_attn, L.mlp
+        out = [(at.q_proj.weight, self.w_qkv[:q]), (at.k_proj.weight, self.w_qkv[q:2 * q]),
+               (at.v_proj.weight, self.w_qkv[2 * q:]), (at.o_proj.weight, self.w_o),
+               (mlp.gate_proj.weight, self.w_gu[:self.w_gu.shape[0] // 2]),
+               (mlp.up_proj.weight, self.w_gu[self.w_gu.shape[0] // 2:]), (mlp.down_proj.weight, self.w_down),
+               (L.input_layernorm.weight, self.ln1_w), (L.post_attention_layernorm.weight, self.ln2_w)]
+        if self.b_qkv is not None:
+            out += [(at.q_proj.bias, self.b_qkv[:q]), (at.k_proj.bias, self.b_qkv[q:2 * q]),
+                    (at.v_proj.bias, self.b_qkv[2 * q:])]
+        if self.b_o is not None:
+            out.append((at.o_proj.bias, self.b_o))
+        return out
+
+    def forward(self, hidden_states, attention_mask=None, position_ids=None, past_key_value=None,
+                output_attentions=False, use_cache=False, **kwargs):
+        if output_attentions:
+            return self._delegate(hidden_states, attention_mask=attention_mask, position_ids=position_ids,
+                                  past_key_value=past_key_value, output_attentions=output_attentions,
+                                  use_cache=use_cache, **kwargs)
+        from ..ops.activation import swiglu
+        from ..ops.norm import rms_norm
+        x = hidden_states
+        B, S, H = x.shape
+        past = past_key_value[0].shape[-2] if past_key_value is not None else 0
+        if position_ids is None:
+            position_ids = torch.arange(past, past + S, device=x.device).unsqueeze(0).expand(B, S)
+        qkv = linear(rms_norm(x, self.ln1_w, self.eps1), self.w_qkv, self.b_qkv).view(B, S, 3, self.nh, self.hd)
+        cos, sin = self.orig.self_attn.rotary_emb(qkv, seq_len=past + S)
+        cos, sin = cos.reshape(-1, self.hd)[position_ids], sin.reshape(-1, self.hd)[position_ids]  # [B, S, D]
+        q, k, v = _rope_half(qkv[:, :, 0], cos, sin), _rope_half(qkv[:, :, 1], cos, sin), qkv[:, :, 2]
+        present = None
+        if past_key_value is not None:  # legacy ([B, H, S, D], [B, H, S, D]) cache
+            k = torch.cat([past_key_value[0].transpose(1, 2), k], 1)
+            v = torch.cat([past_key_value[1].transpose(1, 2), v], 1)
+        if use_cache:
+            present = (k.transpose(1, 2), v.transpose(1, 2))
+        causal_only = _is_causal_additive(attention_mask, S, k.shape[1])
+        o = _attend(q, k, v, None if causal_only else attention_mask, causal_only, 1.0 / math.sqrt(self.hd))
+        a = linear(o.reshape(B, S, H), self.w_o, self.b_o)
+        y2, h = rms_norm(a, self.ln2_w, self.eps2, residual=x)
+        out = (h + linear(swiglu(linear(y2, self.w_gu)), self.w_down),)
+        return out + ((present,) if use_cache else ())
+
+
 # layer class name -> fused layer constructor (reference containers/__init__.py policy list)
 POLICIES = {
     "BertLayer": FusedEncoderLayer,
@@ -686,6 +853,8 @@ POLICIES = {
     "BloomBlock": FusedBloomBlock,
     "GPTNeoBlock": FusedGPTNeoBlock,
     "CLIPEncoderLayer": FusedCLIPEncoderLayer,
+    "ParallelTransformerLayer": FusedMegatronLayer,  # Megatron-LM GPT (dense and MoE)
+    "InternLMDecoderLayer": FusedInternLMLayer,
 }
 
 
