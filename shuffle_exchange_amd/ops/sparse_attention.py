@@ -339,6 +339,34 @@ class SparseSelfAttention(nn.Module):
                                           attn_mask, rpe, self.key_padding_mask_mode, self.attn_mask_mode)
 
 
+class BertSparseSelfAttention(nn.Module):
+    """Sparse self-attention layer of a BERT model (reference bert_sparse_self_attention.py:10):
+    query / key / value projections, ``SparseSelfAttention`` with the config's layout, the
+    attention mask applied as a key-padding mask."""
+
+    def __init__(self, config, sparsity_config=None):
+        super().__init__()
+        if config.hidden_size % config.num_attention_heads != 0:
+            raise ValueError(f"The hidden size ({config.hidden_size}) is not a multiple of the number of attention "
+                             f"heads ({config.num_attention_heads})")
+        self.num_attention_heads = config.num_attention_heads
+        self.attention_head_size = config.hidden_size // config.num_attention_heads
+        self.all_head_size = self.num_attention_heads * self.attention_head_size
+        self.query = nn.Linear(config.hidden_size, self.all_head_size)
+        self.key = nn.Linear(config.hidden_size, self.all_head_size)
+        self.value = nn.Linear(config.hidden_size, self.all_head_size)
+        self.sparse_self_attention = SparseSelfAttention(sparsity_config or FixedSparsityConfig(num_heads=4))
+
+    def transpose_for_scores(self, x):
+        return x.view(*x.shape[:-1], self.num_attention_heads, self.attention_head_size).permute(0, 2, 1, 3)
+
+    def forward(self, hidden_states, attention_mask):
+        q, k, v = (self.transpose_for_scores(f(hidden_states)) for f in (self.query, self.key, self.value))
+        ctx = self.sparse_self_attention(q, k, v, key_padding_mask=attention_mask)
+        ctx = ctx.permute(0, 2, 1, 3).contiguous()
+        return ctx.view(*ctx.shape[:-2], self.all_head_size)
+
+
 class SparseAttentionUtils:
     @staticmethod
     def pad_to_block_size(block_size, input_ids, attention_mask=None, pad_token_id=0):
@@ -353,3 +381,6 @@ class SparseAttentionUtils:
     @staticmethod
     def unpad_sequence_output(pad_len, sequence_output):
         return sequence_output[:, :-pad_len] if pad_len > 0 else sequence_output
+
+
+from .sparse_ops import MatMul, Softmax  # noqa: E402,F401  (standalone block-sparse ops)
