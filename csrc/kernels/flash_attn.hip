@@ -204,13 +204,13 @@ __device__ __forceinline__ void glds4(const void* gsrc, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 4, 0, 0);
 }
-template <int ROWS, int D, int NWAVES = NW>
+template <int ROWS, int D>
 __device__ __forceinline__ void tile_glds(const unsigned short* base, int64_t row_stride, int row0, char* lds) {
   constexpr int CH = D / 8, RPK = 64 / CH;  // rows per 1 KiB wave-instruction
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-  for (int i = 0; i < ROWS / RPK / NWAVES; ++i) {
-    const int n = i * NWAVES + w;
+  for (int i = 0; i < ROWS / RPK / NW; ++i) {
+    const int n = i * NW + w;
     const int row = RPK * n + lane / CH;
     const int cpos = lane % CH;
     const int ch = cpos ^ ((((row & 3) << 2) | ((row >> 2) & 3)) & (CH >= 16 ? 15 : CH - 1));
@@ -775,347 +775,6 @@ __global__ void __launch_bounds__(256) dkdv_reduce_kernel(const float* __restric
   }
 }
 
-// =============================================================================================
-// dK, dV, one wave per SIMD: a workgroup = 4 waves = 256 keys of one (batch, KV head, group of
-// HPW query heads); each wave owns 64 keys as two 32-key halves, with dK^T / dV^T of both halves
-// (256 accumulator registers) and its K fragments in the 512-register file. Per 32-query slice
-// the Q / dO row reads (A operands of S and dP) and the transposed dO^T / Q^T reads (A operands of
-// dV^T and dK^T) serve both halves, so LDS traffic and per-slice overhead per MFMA are half those
-// of the 32-keys-per-wave kernel above, and Q/dO are streamed from L2 once per 256 keys instead
-// of per 128. Q/dO/LSE/delta slices arrive by LDS-DMA into a 3-slot ring (two slices in flight
-// behind a counted vmcnt); the V block (256 keys) stays in LDS for the whole sweep.
-// Dense layouts, head dim 64 / 128 (sparse and head dim 256 use dkdv_kernel).
-// =============================================================================================
-constexpr int KB2 = 256;  // keys per workgroup
-constexpr int NSLOT2 = 3;
-
-template <int D, int NWV = 4> struct KVL2 {
-  static constexpr int TILE = QT * 2 * D;
-  static constexpr int SLOT = 2 * TILE + 2 * QT * 4;
-  static constexpr int VBLK = KB2 * 2 * D;
-  static constexpr int LDS = VBLK + NSLOT2 * SLOT;
-  static constexpr int PT = QT / (64 / (D / 8));  // 1 KiB LDS-DMA pieces per Q (or dO) tile
-  static_assert((2 * PT) % NWV == 0, "slice pieces must spread evenly over the waves");
-  // vector-memory ops one wave issues per slice: its Q / dO pieces + one lse/delta piece
-  static constexpr int NVM = 2 * PT / NWV + 1;
-};
-
-// s_waitcnt vmcnt(N) with lgkmcnt / expcnt left at their maxima (gfx9 encoding)
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
-
-// LLVM SchedGroupMask bits for __builtin_amdgcn_sched_group_barrier
-constexpr int SG_VALU = 0x2, SG_MFMA = 0x8, SG_DSR = 0x100;
-#ifndef SXE_FA_SGB
-#define SXE_FA_SGB 1
-#endif
-#if SXE_FA_SGB
-#define SXE_SGB(m, n, id) __builtin_amdgcn_sched_group_barrier(m, n, id)
-#else
-#define SXE_SGB(m, n, id) ((void)0)
-#endif
-
-// Per-lane LDS byte offsets of the operand reads of one 32-row tile, computed once per kernel
-// (hoisted copies per loop would pin three sets of address registers):
-//   row[t2]    A/B operand row read of k-slice t2 (lds_row16 of row r, chunk 2 t2 + h)
-//   tr[t][j]   the two transposed reads of lds_trA for d-tile t (rows +0 / +8); rows 16..31 of
-//              the tile add the constant 16 * ROWB (the swizzle repeats every 16 rows)
-template <int D> struct Offs {
-  int row[D / 16];
-  int tr[D / 32][2];
-  __device__ __forceinline__ void init(int lane) {
-    const int r = lane & 31, h = lane >> 5;
-#pragma unroll
-    for (int t2 = 0; t2 < D / 16; ++t2) row[t2] = soff<D>(r, 2 * t2 + h);
-    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, hh = g >> 1;
-#pragma unroll
-    for (int t = 0; t < D / 32; ++t) {
-      const int ch = 4 * t + 2 * (g & 1) + (p >> 1);
-      tr[t][0] = soff<D>(4 * hh + q, ch) + 8 * (p & 1);
-      tr[t][1] = soff<D>(4 * hh + q + 8, ch) + 8 * (p & 1);
-    }
-  }
-};
-
-template <int D>
-__device__ __forceinline__ bf16x8 trA_at(const char* base, const Offs<D>& o, int s2, int t) {
-  const i16x4 lo = lds_tr(base, o.tr[t][0] + s2 * 16 * 2 * D);
-  const i16x4 hi = lds_tr(base, o.tr[t][1] + s2 * 16 * 2 * D);
-  const i16x8 cc = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8, cc);
-}
-
-template <int D>
-__device__ __forceinline__ bf16x8 row_at(const char* base, const Offs<D>& o, int t2) {
-  return *reinterpret_cast<const bf16x8*>(base + o.row[t2]);
-}
-
-// One 32-key half of a 32-query slice in four scheduling regions, each VALU stage placed under
-// the next MFMA stage (one wave per SIMD: no partner wave hides exposed VALU):
-//   1: S = Q K^T                     (8 MFMAs on a D=128 tile)
-//   2: dP = dO V^T   | P = exp2(c S - lse log2 e), masked, packed to bf16
-//   3: dV^T += dO^T P | dS = P (dP - delta), packed to bf16
-//   4: dK^T += Q^T dS
-// Keys are on the lanes, queries on the accumulator rows; the accumulators of S and dP are the B
-// operands of the dV^T / dK^T products (the accumulator-as-operand identity).
-template <bool MASK, int D>
-__device__ __forceinline__ void dkdv2_half(const char* qt, const char* dot, const char* vrows, const float* lsl,
-                                           const Offs<D>& o, const bf16x8 (&kf)[D / 16], f32x16 (&dva)[D / 32],
-                                           f32x16 (&dka)[D / 32], float c, int qrow0, int key, int h) {
-  constexpr int NM = D / 16;
-  f32x16 s = zero16(), dp = zero16();
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int t2 = 0; t2 < NM; ++t2) s = mfma(row_at<D>(qt, o, t2), kf[t2], s);
-  SXE_SGB(SG_DSR, 2, 0);
-#pragma unroll
-  for (int i = 0; i < NM - 2; ++i) {
-    SXE_SGB(SG_MFMA, 1, 0);
-    SXE_SGB(SG_DSR, 1, 0);
-  }
-  SXE_SGB(SG_MFMA, 2, 0);
-  __builtin_amdgcn_sched_barrier(0);
-  // stage 2
-#pragma unroll
-  for (int t2 = 0; t2 < NM; ++t2) dp = mfma(row_at<D>(dot, o, t2), row_at<D>(vrows, o, t2), dp);
-  f32x4 dl[4];
-  bf16x8 pb[2];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const f32x4 l2 = *reinterpret_cast<const f32x4*>(lsl + 8 * g + 4 * h);
-    dl[g] = *reinterpret_cast<const f32x4*>(lsl + QT + 8 * g + 4 * h);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int i = 4 * g + e;
-      float p = fast_exp2(__builtin_fmaf(s[i], c, -l2[e] * LOG2E));
-      if (MASK && (qrow0 + acc_row(i, h) < key)) p = 0.f;
-      s[i] = p;
-    }
-  }
-  pb[0] = acc_to_b(s, 0);
-  pb[1] = acc_to_b(s, 1);
-  SXE_SGB(SG_DSR, 6, 0);
-#pragma unroll
-  for (int i = 0; i < NM - 2; ++i) {
-    SXE_SGB(SG_MFMA, 1, 0);
-    SXE_SGB(SG_DSR, 2, 0);
-    SXE_SGB(SG_VALU, MASK ? 9 : 5, 0);
-  }
-  SXE_SGB(SG_MFMA, 2, 0);
-  __builtin_amdgcn_sched_barrier(0);
-  // stage 3
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-    for (int t = 0; t < D / 32; ++t) dva[t] = mfma(trA_at<D>(dot, o, s2, t), pb[s2], dva[t]);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) dp[i] = s[i] * (dp[i] - dl[i >> 2][i & 3]);
-  const bf16x8 db0 = acc_to_b(dp, 0), db1 = acc_to_b(dp, 1);
-  SXE_SGB(SG_DSR, 4, 0);
-#pragma unroll
-  for (int i = 0; i < NM - 2; ++i) {
-    SXE_SGB(SG_MFMA, 1, 0);
-    SXE_SGB(SG_DSR, 2, 0);
-    SXE_SGB(SG_VALU, 5, 0);
-  }
-  SXE_SGB(SG_MFMA, 2, 0);
-  __builtin_amdgcn_sched_barrier(0);
-  // stage 4
-#pragma unroll
-  for (int t = 0; t < D / 32; ++t) dka[t] = mfma(trA_at<D>(qt, o, 0, t), db0, dka[t]);
-#pragma unroll
-  for (int t = 0; t < D / 32; ++t) dka[t] = mfma(trA_at<D>(qt, o, 1, t), db1, dka[t]);
-  SXE_SGB(SG_DSR, 4, 0);
-#pragma unroll
-  for (int i = 0; i < NM - 2; ++i) {
-    SXE_SGB(SG_MFMA, 1, 0);
-    SXE_SGB(SG_DSR, 2, 0);
-  }
-  SXE_SGB(SG_MFMA, 2, 0);
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <bool MASK, int D, int NH>
-__device__ __forceinline__ void dkdv2_slice(const char* slot, const char* vw, const Offs<D>& o,
-                                            const bf16x8 (&kf)[NH][D / 16], f32x16 (&dva)[NH][D / 32],
-                                            f32x16 (&dka)[NH][D / 32], float c, int qrow0, const int (&key)[NH],
-                                            int h) {
-  constexpr int TILE = QT * 2 * D;
-  const char* qt = slot;
-  const char* dot = slot + TILE;
-  const float* lsl = reinterpret_cast<const float*>(slot + 2 * TILE);
-#pragma unroll
-  for (int a = 0; a < NH; ++a)
-    dkdv2_half<MASK, D>(qt, dot, vw + a * 32 * 2 * D, lsl, o, kf[a], dva[a], dka[a], c, qrow0, key[a], h);
-}
-
-// KPW keys per wave (64: one wave per SIMD, 512 registers; 32: two waves per SIMD), NWV = 256 / KPW
-template <int D, int KPW>
-__global__ void __launch_bounds__(KB2 / KPW * 64, 1) dkdv2_kernel(
-    const unsigned short* __restrict__ q, Strides qs, const unsigned short* __restrict__ k, Strides ks,
-    const unsigned short* __restrict__ v, Strides vs, const unsigned short* __restrict__ dout, Strides dos,
-    const float* __restrict__ lse, const float* __restrict__ delta, unsigned short* __restrict__ dk, Strides dks,
-    unsigned short* __restrict__ dv, Strides dvs, float* __restrict__ pk, float* __restrict__ pv, int B, int H,
-    int Hk, int Sq, int Sk, float scale, int causal, int qoff, int hpw, int kvlen) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NWV = KB2 / KPW, NH = KPW / 32;
-  using G_ = KVL2<D, NWV>;
-  char* vblk = smem;
-  char* ring = smem + G_::VBLK;
-  // the wave index through readfirstlane: provably wave-uniform, so the per-slice conditions below
-  // are scalar branches (derived from threadIdx they would be divergent exec masks, with the
-  // accumulators copied through every join)
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), r = lane & 31,
-            h = lane >> 5;
-  const int G = H / Hk, ngrp = G / hpw;
-  // heavy-first: key block 0 sees the most queries under causality
-  const int idx = blockIdx.x;
-  const int BHG = B * Hk * ngrp;
-  const int kb = idx / BHG;
-  const int rest = idx - kb * BHG;
-  const int b = rest / (Hk * ngrp);
-  const int kg = rest - b * (Hk * ngrp);  // kh * ngrp + grp
-  const int kh = kg / ngrp, grp = kg - kh * ngrp;
-  const int hq0 = kh * G + grp * hpw;
-  const int kw0 = kb * KB2 + w * KPW;  // this wave's first key
-  const unsigned short* kp = k + b * ks.b + kh * ks.h;
-  const unsigned short* vp = v + b * vs.b + kh * vs.h;
-  const float c = scale * LOG2E;
-  const int qstart = causal ? min(Sq, max(0, kb * KB2 - qoff) / QT * QT) : 0;
-  const int ntq = (Sq - qstart) / QT;
-  const int total = ntq * hpw;
-  int is_h = hq0, is_q = qstart;  // next slice to issue
-  auto issue = [&](char* slot) {
-    const int hq = is_h, qt0 = is_q;
-    is_q += QT;
-    if (is_q >= Sq) {
-      is_q = qstart;
-      ++is_h;
-    }
-    // the slice's 2 * PT pieces (Q then dO) spread over the waves
-    {
-      constexpr int CH = D / 8, RPK = 64 / CH;
-#pragma unroll
-      for (int i = 0; i < 2 * G_::PT / NWV; ++i) {
-        const int n = i * NWV + w;  // wave-uniform
-        const bool isq = n < G_::PT;
-        const int pn = isq ? n : n - G_::PT;
-        const int row = RPK * pn + lane / CH;
-        const int ch = (lane % CH) ^ ((((row & 3) << 2) | ((row >> 2) & 3)) & (CH >= 16 ? 15 : CH - 1));
-        const unsigned short* src = isq ? q + b * qs.b + hq * qs.h + (int64_t)(qt0 + row) * qs.s
-                                        : dout + b * dos.b + hq * dos.h + (int64_t)(qt0 + row) * dos.s;
-        glds16(src + ch * 8, slot + (isq ? 0 : G_::TILE) + pn * 1024);
-      }
-    }
-    // every wave writes the same 256 bytes (lse[32] then delta[32]): a uniform vmcnt per wave
-    const int64_t lr = ((int64_t)b * H + hq) * Sq + qt0 + (lane & 31);
-    glds4(lane < 32 ? (const void*)(lse + lr) : (const void*)(delta + lr), slot + 2 * G_::TILE);
-  };
-  if constexpr (KPW == 64) {
-    // an inline-asm AGPR operand makes the backend select the AGPR-accumulator MFMA forms (its
-    // "may need AGPRs" heuristic) for the 256 dK^T/dV^T accumulators of the 512-register wave
-    float agpr_hint = 0.f;
-    asm volatile("" : "+a"(agpr_hint));
-  }
-  tile_glds<KB2, D, NWV>(vp, vs.s, kb * KB2, vblk);
-  if (total > 0) issue(ring);
-  if (total > 1) issue(ring + G_::SLOT);
-  bf16x8 kf[NH][D / 16];
-#pragma unroll
-  for (int a = 0; a < NH; ++a)
-#pragma unroll
-    for (int t = 0; t < D / 16; ++t)
-      kf[a][t] = *reinterpret_cast<const bf16x8*>(kp + (int64_t)(kw0 + 32 * a + r) * ks.s + 16 * t + 8 * h);
-  f32x16 dka[NH][D / 32], dva[NH][D / 32];
-#pragma unroll
-  for (int a = 0; a < NH; ++a)
-#pragma unroll
-    for (int t = 0; t < D / 32; ++t) {
-      dka[a][t] = zero16();
-      dva[a][t] = zero16();
-    }
-  if (total > 1) vm_wait<G_::NVM>(); else vm_wait<0>();
-  __syncthreads();
-  // masked lanes: query row q sees key when q + qoff >= key; keys >= kv_len never (padded axis)
-  int key[NH];
-#pragma unroll
-  for (int a = 0; a < NH; ++a) key[a] = kw0 + 32 * a + r >= kvlen ? INT32_MAX / 2 : kw0 + 32 * a + r;
-  const int qr_off = causal ? qoff : INT32_MAX / 4;
-  Offs<D> o;
-  o.init(lane);
-  const char* vw = vblk + w * KPW * 2 * D;  // this wave's V rows
-  int it = 0, cur = 0;
-  // one ring step: prefetch slice it + 2, compute slice it (MODE 0: nothing, 1: masked, 2: dense),
-  // wait for slice it + 1 and pass the barrier
-  auto step = [&](auto mode, int qt0) {
-    if (it + 2 < total) issue(ring + ((cur + 2) % NSLOT2) * G_::SLOT);
-    const char* slot = ring + cur * G_::SLOT;
-    if constexpr (decltype(mode)::value == 1)
-      dkdv2_slice<true, D, NH>(slot, vw, o, kf, dva, dka, c, qt0 + qr_off, key, h);
-    if constexpr (decltype(mode)::value == 2)
-      dkdv2_slice<false, D, NH>(slot, vw, o, kf, dva, dka, c, 0, key, h);
-    if (it + 2 < total) vm_wait<G_::NVM>(); else vm_wait<0>();
-    __syncthreads();
-    cur = cur == NSLOT2 - 1 ? 0 : cur + 1;
-    ++it;
-  };
-  // per query head the slices split into three branch-free runs for this wave (causal): before
-  // its keys (no work; only the ring and the barrier), across the diagonal (element mask), after
-  // it (dense). Keeping the accumulators out of any branch keeps them in place in the AGPRs.
-  auto cdiv = [](int x) { return x <= 0 ? 0 : (x + QT - 1) / QT; };
-  const int ja = causal ? min(ntq, cdiv(kw0 - (QT - 1) - qoff - qstart)) : 0;
-  const int jm = (kw0 + KPW - 1 >= kvlen) ? ntq : causal ? max(ja, min(ntq, cdiv(kw0 + KPW - qoff - qstart))) : 0;
-  for (int hh = 0; hh < hpw; ++hh) {
-    int j = 0;
-    for (; j < ja; ++j) step(std::integral_constant<int, 0>{}, 0);
-    for (; j < jm; ++j) step(std::integral_constant<int, 1>{}, qstart + j * QT);
-    for (; j < ntq; ++j) step(std::integral_constant<int, 2>{}, qstart + j * QT);
-  }
-  if (pk != nullptr) {  // fp32 partials [B, Sk, Hk * ngrp, D]
-#pragma unroll
-    for (int a = 0; a < NH; ++a) {
-      const int64_t row = ((int64_t)b * Sk + kw0 + 32 * a + r) * (Hk * ngrp) + kg;
-      float* kp32 = pk + row * D;
-      float* vp32 = pv + row * D;
-#pragma unroll
-      for (int t = 0; t < D / 32; ++t)
-#pragma unroll
-        for (int rg = 0; rg < 4; ++rg) {
-          f32x4 x, y;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            x[e] = dka[a][t][4 * rg + e] * scale;
-            y[e] = dva[a][t][4 * rg + e];
-          }
-          *reinterpret_cast<f32x4*>(kp32 + 32 * t + 8 * rg + 4 * h) = x;
-          *reinterpret_cast<f32x4*>(vp32 + 32 * t + 8 * rg + 4 * h) = y;
-        }
-    }
-    return;
-  }
-#pragma unroll
-  for (int a = 0; a < NH; ++a) {
-    unsigned short* kop = dk + b * dks.b + kh * dks.h + (int64_t)(kw0 + 32 * a + r) * dks.s;
-    unsigned short* vop = dv + b * dvs.b + kh * dvs.h + (int64_t)(kw0 + 32 * a + r) * dvs.s;
-#pragma unroll
-    for (int t = 0; t < D / 32; ++t)
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        u16x4 pk4, pv4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          pk4[e] = f32_to_bf16(dka[a][t][4 * rg + e] * scale);
-          pv4[e] = f32_to_bf16(dva[a][t][4 * rg + e]);
-        }
-        *reinterpret_cast<u16x4*>(kop + 32 * t + 8 * rg + 4 * h) = pk4;
-        *reinterpret_cast<u16x4*>(vop + 32 * t + 8 * rg + 4 * h) = pv4;
-      }
-  }
-}
-
 }  // namespace fa
 
 // ---------------------------------------------------------------------------------------------
@@ -1158,18 +817,6 @@ static bool fwd_narrow() {
   static const bool v = [] {
     const char* e = std::getenv("SXE_FA_FWD_WAVES");
     return e != nullptr && std::atoi(e) == 4;
-  }();
-  return v;
-}
-
-// dK/dV kernel for dense head dim 64 / 128: SXE_FA_DKDV=128 the 128-key, 4-wave kernel
-// (dkdv_kernel); 32 / 64 the 256-key kernel with 32 keys per wave (8 waves) or 64 (4 waves, one
-// per SIMD)
-static int dkdv_kpw() {
-  static const int v = [] {
-    const char* e = std::getenv("SXE_FA_DKDV");
-    const int x = e ? std::atoi(e) : 32;
-    return x == 64 ? 64 : x == 128 ? 0 : 32;
   }();
   return v;
 }
@@ -1284,57 +931,6 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
   SXE_LAUNCH_CHECK();
   // sparse: always one workgroup per query head (per-head tile lists); with GQA the per-head fp32
   // partials are reduced; causal GQA: split to remove the key-block-0 tail (see dkdv_kernel)
-  if constexpr (D <= 128) {
-    const int kpw = dkdv_kpw();
-    if (sp.layout == nullptr && Sk % fa::KB2 == 0 && kpw != 0) {
-      // one-wave-per-SIMD dK/dV over 256-key blocks; HPW query heads per workgroup, halved while
-      // the grid is too small to balance the causal triangle over the CUs (fp32 partials per head
-      // group, summed by dkdv_reduce_kernel)
-      const int G = H / Hk;
-      int hpw = G;
-      const int target = causal ? 1024 : 512;
-      auto nwg = [&](int hp) { return (Sk / fa::KB2) * B * Hk * (G / hp); };
-      while (hpw > 1 && hpw % 2 == 0 && nwg(hpw) < target) hpw /= 2;
-      if (const char* e = std::getenv("SXE_FA_HPW")) {
-        const int want = std::atoi(e);
-        if (want >= 1 && G % want == 0) hpw = want;
-      }
-      const int ngrp = G / hpw;
-      static bool attr2 = false;
-      if (!attr2) {
-        set_lds_limit(&fa::dkdv2_kernel<D, 32>, fa::KVL2<D>::LDS);
-        set_lds_limit(&fa::dkdv2_kernel<D, 64>, fa::KVL2<D>::LDS);
-        attr2 = true;
-      }
-      at::Tensor pk2, pv2;
-      if (ngrp > 1) {
-        pk2 = at::empty({B, Sk, Hk * ngrp, D}, q.options().dtype(at::kFloat));
-        pv2 = at::empty({B, Sk, Hk * ngrp, D}, q.options().dtype(at::kFloat));
-      }
-      auto* kern2 = kpw == 64 ? fa::dkdv2_kernel<D, 64> : fa::dkdv2_kernel<D, 32>;
-      constexpr size_t lds2 = fa::KVL2<D>::LDS;
-      hipLaunchKernelGGL(kern2, dim3(nwg(hpw)), dim3(fa::KB2 / kpw * 64), lds2, cur_stream(),
-                         reinterpret_cast<const unsigned short*>(q.data_ptr()), strides_of(q),
-                         reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
-                         reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),
-                         reinterpret_cast<const unsigned short*>(dout.data_ptr()), strides_of(dout),
-                         lse.data_ptr<float>(), delta.data_ptr<float>(),
-                         reinterpret_cast<unsigned short*>(dk.data_ptr()), strides_of(dk),
-                         reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv),
-                         ngrp > 1 ? pk2.data_ptr<float>() : nullptr, ngrp > 1 ? pv2.data_ptr<float>() : nullptr, B,
-                         H, Hk, Sq, Sk, (float)scale, causal ? 1 : 0, qoff, hpw, kvlen);
-      SXE_LAUNCH_CHECK();
-      if (ngrp > 1) {
-        const int64_t n8 = (int64_t)B * Sk * Hk * (D / 8);
-        hipLaunchKernelGGL(fa::dkdv_reduce_kernel<D>, dim3(stream_grid(n8, 256)), dim3(256), 0, cur_stream(),
-                           pk2.data_ptr<float>(), pv2.data_ptr<float>(),
-                           reinterpret_cast<unsigned short*>(dk.data_ptr()), strides_of(dk),
-                           reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv), B, Sk, Hk * ngrp, Hk);
-        SXE_LAUNCH_CHECK();
-      }
-      return;
-    }
-  }
   const bool split = sp.layout != nullptr || (causal && H > Hk);
   const bool partials = split && H > Hk;
   const size_t lds_kv = G_::VBLK + 2 * G_::SLOT + (sp.layout ? kListBytes : 0);
