@@ -122,12 +122,34 @@ def grouped_gemm_ok(x, w):
             and w.is_cuda and w.shape[2] == x.shape[1] and x.shape[1] % 128 == 0 and w.shape[1] % 128 == 0)
 
 
+GG_LOOP_MIN_ROWS = 1024  # mean rows per expert from which the per-expert hipBLASLt loop is used
+
+
+def _use_expert_loop(x, w):
+    """Dispatch on the measured table (profiles/grouped_gemm_bench.log): with few large experts and
+    many rows each (Mixtral prefill: 2048-4096 rows per expert) the per-expert hipBLASLt GEMMs run
+    1.3-1.6x the ragged kernel (1,081 vs 793 TF at 8k rows, 1,410 vs 899 TF at 32k), at the price of
+    one host read of the offsets; with many small experts (Qwen-MoE: 1/3 the loop's time) or
+    decode-sized inputs the single ragged launch wins, and it is the only choice inside a HIP-graph
+    capture (no host sync allowed). SXE_GG_DISPATCH=kernel|loop forces one."""
+    import os
+    mode = os.environ.get("SXE_GG_DISPATCH", "auto")
+    if mode == "kernel":
+        return False
+    if torch.cuda.is_current_stream_capturing():
+        return False
+    if mode == "loop":
+        return True
+    return x.shape[0] >= GG_LOOP_MIN_ROWS * w.shape[0]
+
+
 def grouped_gemm(x, w, offsets, row_scale=None):
     """y[r] = row_scale[r] * x[r] @ w[e]^T for expert-sorted rows x [R, K], per-expert weights
     w [E, N, K] (nn.Linear layout) and device offsets [E + 1] (``expert_offsets``): ONE launch of
     the ragged MFMA kernel (csrc/kernels/grouped_gemm.hip; reference cutlass_ops/moe_gemm), no host
-    sync. CPU / unsupported shapes: a per-expert loop (reads the offsets on the host)."""
-    if grouped_gemm_ok(x, w):
+    sync -- or, for few experts with many rows each, the per-expert hipBLASLt loop
+    (``_use_expert_loop``). CPU / unsupported shapes: the per-expert loop."""
+    if grouped_gemm_ok(x, w) and not _use_expert_loop(x, w):
         rs = None if row_scale is None else row_scale.reshape(-1).contiguous()
         if rs is not None and rs.dtype not in (torch.float32, torch.bfloat16):
             rs = rs.float()

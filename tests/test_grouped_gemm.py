@@ -17,6 +17,18 @@ def _ref(x, w, offs, scale=None):
     return y
 
 
+def test_expert_loop_dispatch_rule(monkeypatch):
+    """Few experts with >= GG_LOOP_MIN_ROWS rows each -> the per-expert GEMM loop; many small
+    experts -> the ragged kernel; the env knob forces either."""
+    x = torch.empty(8 * moe_ops.GG_LOOP_MIN_ROWS, 16)
+    assert moe_ops._use_expert_loop(x, torch.empty(8, 4, 16))
+    assert not moe_ops._use_expert_loop(x, torch.empty(60, 4, 16))
+    monkeypatch.setenv("SXE_GG_DISPATCH", "kernel")
+    assert not moe_ops._use_expert_loop(x, torch.empty(8, 4, 16))
+    monkeypatch.setenv("SXE_GG_DISPATCH", "loop")
+    assert moe_ops._use_expert_loop(x[:1], torch.empty(60, 4, 16))
+
+
 def test_expert_offsets_and_cpu_fallback():
     torch.manual_seed(0)
     flat = torch.tensor([2, 0, 2, 3, 0, 2])
@@ -28,9 +40,11 @@ def test_expert_offsets_and_cpu_fallback():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dispatch", ["kernel", "loop"])
 @pytest.mark.parametrize("counts", [[0, 300, 1, 128, 0, 77, 513, 2], [1], [0, 0, 0, 5]])
 @pytest.mark.parametrize("scale", [None, "fp32", "bf16"])
-def test_grouped_gemm_vs_fp32(counts, scale):
+def test_grouped_gemm_vs_fp32(counts, scale, dispatch, monkeypatch):
+    monkeypatch.setenv("SXE_GG_DISPATCH", dispatch)
     from shuffle_exchange_amd.ops import native
     native.require_hip()
     torch.manual_seed(0)
