@@ -136,7 +136,7 @@ def _use_expert_loop(x, w):
     mode = os.environ.get("SXE_GG_DISPATCH", "auto")
     if mode == "kernel":
         return False
-    if torch.cuda.is_current_stream_capturing():
+    if x.is_cuda and torch.cuda.is_current_stream_capturing():
         return False
     if mode == "loop":
         return True
