@@ -924,7 +924,14 @@ class SXEEngine(nn.Module):
             from ..compile.fx_backend import compile_fx
             self._fx_compiler, self._fx_module = compile_fx(self, CompileConfig.from_dict(cc), compile_kwargs)
             self.compile_plan = {"fx": self._fx_compiler}
-        if cc.get("deepcompile") and self.zero_optimization_stage() == 3 and hasattr(opt, "apply_compile_plan"):
+        if cc.get("deepcompile") and self.zero_optimization_stage() == 3 and cc.get("fx_zero3"):
+            # ZeRO-3 graph compiler (compile/fx_zero3.py): gather / release / prefetch and the
+            # gradient reduce-scatters placed in Dynamo + AOT autograd graphs
+            from ..compile import CompileConfig
+            from ..compile.fx_zero3 import compile_fx_zero3
+            self._fx_compiler, self._fx_module = compile_fx_zero3(self, CompileConfig.from_dict(cc), compile_kwargs)
+            self.compile_plan = {"fx": self._fx_compiler}
+        elif cc.get("deepcompile") and self.zero_optimization_stage() == 3 and hasattr(opt, "apply_compile_plan"):
             # schedule compiler (compile/): trace the next step(s), then run the passes
             from ..compile import CompileConfig, install_profiler
             self._compile_cfg_obj = CompileConfig.from_dict(cc)

@@ -343,16 +343,48 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
 
     # -------------------------------------------------------------------------------------- hooks
     def _register(self):
+        self._module_hooks = []
         for fg in self.fgroups:
             if fg.name == "#rest":
                 continue
-            self._hooks.append(fg.module.register_forward_pre_hook(self._make_pre(fg)))
-            self._hooks.append(fg.module.register_forward_hook(self._make_post(fg)))
+            self._module_hooks.append(fg.module.register_forward_pre_hook(self._make_pre(fg)))
+            self._module_hooks.append(fg.module.register_forward_hook(self._make_post(fg)))
+        self._hooks.extend(self._module_hooks)
         for p, u in self.param_unit.items():
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_grad_hook(u)))
             # fused weight-grad GEMMs (ops/linear.py) write straight into the unit's buffers
             p._sxe_grad_target = self._grad_target
             p._sxe_grad_done = self._grad_done
+
+    # ---------------------------------------------------------------------- FX graph mode
+    def enter_graph_mode(self):
+        """Hand fetch / release to a compiled graph (compile/fx_zero3.py): the module hooks go, and
+        a released unit keeps its parameters linked as full-shape views of its flat buffer whose
+        STORAGE is freed (``resize_(0)``) -- the traced graph sees fixed parameter shapes, and a
+        gather re-allocates the same storage in place, so the views (and any tensors autograd saved
+        from them) become valid again."""
+        self.graph_mode = True
+        for h in getattr(self, "_module_hooks", []):
+            h.remove()
+        self._module_hooks = []
+        for units in self.units:
+            for u in units:
+                if u.state == RELEASED:  # relink as views (storage stays freed)
+                    u.flat.untyped_storage().resize_(u.padded * u.flat.element_size())
+                    u.link_params()
+                    u.flat.untyped_storage().resize_(0)
+        self.trace = []
+
+    def gather_all_for_trace(self):
+        """Materialise every unit (Dynamo fake-ifies the parameters when it traces)."""
+        for fg in self.fgroups:
+            self._fetch(fg, wait=True)
+
+    def grad_ready(self, p):
+        """A gradient delivered by a compiled graph's reduce node: run the per-parameter hook."""
+        u = self.param_unit.get(p)
+        if u is not None:
+            self._make_grad_hook(u)(p)
 
     def _grad_target(self, p):
         u = self.param_unit[p]
@@ -481,7 +513,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             p.grad = None
             if done:
                 self._reduce_unit(unit)
-                if not unit.persistent and self._in_bwd:
+                if not unit.persistent and self._in_bwd and not getattr(self, "graph_mode", False):
                     self._release_unit(unit)
         return hook
 
@@ -493,7 +525,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             st.wait_stream(cur)
         with get_accelerator().stream(st):
             u.flat.untyped_storage().resize_(u.padded * u.flat.element_size())
-            u.link_params()
+            if not getattr(self, "graph_mode", False):
+                u.link_params()
             swapped = u.swap is not None
             src = u.swap.acquire(u) if swapped else u.shard
             if src.device != u.flat.device:
@@ -573,7 +606,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             u.sec_shard.copy_(u.flat[self.hpz_rank * n:(self.hpz_rank + 1) * n])
             u.sec_valid = True
         u.flat.untyped_storage().resize_(0)
-        u.unlink_params()
+        if not getattr(self, "graph_mode", False):
+            u.unlink_params()
         u.state = RELEASED
 
     def _release(self, fg):
