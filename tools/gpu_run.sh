@@ -24,6 +24,8 @@
 #   gg                tools/grouped_gemm_bench.py
 #   mx                tools/mx_gemm_bench.py ($MX_ARGS)
 #   moe               tools/moe_bench.py ($MOE_ARGS)
+#   compile           tools/compile_bench.py ($COMPILE_ARGS): DeepCompile compiled vs eager step
+#   tune              bounded TunableOp search over the Llama-3-8B GEMM shapes ($TUNE_ARGS)
 #   py=SCRIPT         python SCRIPT ($PY_ARGS)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 3
@@ -79,6 +81,9 @@ run_step() {  # $1 = name, $2 = log file
     gg) timeout -k 10 300 python tools/grouped_gemm_bench.py > "$log" 2>&1 ;;
     mx) timeout -k 10 300 python tools/mx_gemm_bench.py ${MX_ARGS} > "$log" 2>&1 ;;
     moe) timeout -k 10 900 python tools/moe_bench.py ${MOE_ARGS} > "$log" 2>&1 ;;
+    compile) timeout -k 10 900 python tools/compile_bench.py ${COMPILE_ARGS} > "$log" 2>&1 ;;
+    tune) timeout -k 10 ${TUNE_LIMIT:-900} python3 tools/tune_gemms.py gpurun_out/tunableop_llama3_8b.csv ${TUNE_ARGS} \
+      > "$log" 2>&1 ;;
     py) timeout -k 10 ${PY_TIMEOUT:-600} python "$arg" ${PY_ARGS} > "$log" 2>&1 ;;
     *) echo "unknown step $name" > "$log"; return 2 ;;
   esac
