@@ -238,7 +238,8 @@ class RaggedLlama:
                     y = fused_merge_linear(parts[0], parts[1], w)
                     if y is not None:
                         return y
-                    out = self._attention(qkv, kv_layer, batch)
+                    from ....ops.paged_attention import merge_attention_parts
+                    out = merge_attention_parts(parts[0], parts[1], qkv.dtype)  # keep the computed splits
                 return self._proj(attn.o_proj, out.reshape(T, self.nq * self.head_dim), li, "o")
         o = self._attention(qkv, kv_layer, batch)
         return self._proj(attn.o_proj, o.reshape(T, self.nq * self.head_dim), li, "o")
@@ -259,10 +260,12 @@ class RaggedLlama:
         a, h = (norm(x), x) if res is None else norm(x, res)
         return self._proj(mod, a, li, key), h
 
-    def _mlp(self, layer, m, li=0):
+    def _mlp(self, layer, m, li=0, gu=None):
+        """``gu``: the gate_up projection when the caller already ran it (fused with the norm)."""
         if hasattr(layer, "mlp"):
             mlp = layer.mlp
-            gu = m if getattr(self, "_gu_ready", False) else self._proj(mlp.gate_up_proj, m, li, "gu")
+            if gu is None:
+                gu = self._proj(mlp.gate_up_proj, m, li, "gu")
             if self._fusable(gu.shape[0]) and getattr(mlp.down_proj, "bias", None) is None:
                 from ....ops.linear import fused_swiglu_linear
                 y = fused_swiglu_linear(gu, self._wobj(mlp.down_proj, li, "down"))
@@ -346,9 +349,7 @@ class RaggedLlama:
                 o = self._attn_o(attn, qkv, kv_layer, batch, li, T)
             if hasattr(layer, "mlp"):
                 gu, h2 = self._norm_proj(layer.post_attention_layernorm, o, h, layer.mlp.gate_up_proj, li, "gu")
-                self._gu_ready = True
-                x, res = self._mlp(layer, gu, li), h2
-                self._gu_ready = False
+                x, res = self._mlp(layer, None, li, gu=gu), h2
             else:
                 m, h2 = layer.post_attention_layernorm(o, h)
                 x, res = self._mlp(layer, m, li), h2

@@ -106,6 +106,19 @@ def paged_attention_parts(q, cache, block_table, q_start, q_len, kv_len, scale, 
     return (out, None) if po.numel() == 0 else (None, (po, pml))
 
 
+def merge_attention_parts(part_o, part_ml, dtype):
+    """Flash-decoding merge of ``paged_attention_parts``' KV-split partials (the math of
+    paged_attn.hip's merge kernel / skinny_gemm.hip PRO_MERGE): sum_s 2^(M_s - M) o_s /
+    sum_s 2^(M_s - M) L_s over the splits, M the max of the split maxima (log2 domain).
+    part_o [splits, T, nq, D], part_ml [splits, T, nq, 2] fp32 -> [T, nq, D] in ``dtype``."""
+    m, l = part_ml[..., 0], part_ml[..., 1]
+    mx = m.amax(0)
+    f = torch.where(torch.isinf(m), torch.zeros_like(m), torch.exp2(m - torch.where(torch.isinf(mx), 0, mx)))
+    den = (f * l).sum(0)
+    num = (f.unsqueeze(-1) * part_o).sum(0)
+    return torch.where(den.unsqueeze(-1) > 0, num / den.clamp_min(1e-30).unsqueeze(-1), 0.).to(dtype)
+
+
 def paged_attention(q, cache, block_table, q_start, q_len, kv_len, scale, max_kv_len, splits=None, window=None):
     """q: [T, nq, D] (head stride D); metadata int32 [S]; returns [T, nq, D]. ``window``: sliding
     window length (keys older than ``window`` positions are masked, Mistral / Qwen2). The HIP kernel

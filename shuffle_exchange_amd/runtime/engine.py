@@ -559,10 +559,35 @@ class SXEEngine(nn.Module):
                 # param groups since (zero/offload.py split_param_groups)
                 from .zero.offload import expand_scheduler_groups
                 self.lr_scheduler = expand_scheduler_groups(client_lr_scheduler, self.basic_optimizer)
-            return
-        if self._config.scheduler_name:
+        elif self._config.scheduler_name:
             self.lr_scheduler = build_scheduler(self._config.scheduler_name, self.optimizer,
                                                 self._config.scheduler_params)
+        self._hook_scheduler_reads()
+
+    def _hook_scheduler_reads(self):
+        """The bf16 / static-scale step defers its LR advance to the next step (``_defer_skip``: no
+        host sync inside step()). Reads of the schedule through the scheduler object the user
+        holds -- ``get_last_lr()``, ``get_lr()``, ``state_dict()`` -- resolve the pending advance
+        first, so they never see a value one step stale. (A direct read of
+        ``optimizer.param_groups[i]['lr']`` between steps still can: read ``engine.get_lr()`` or
+        the scheduler instead.)"""
+        sched = self.lr_scheduler
+        if sched is None or getattr(type(sched), "_sxe_resolving_reads", False):
+            return
+        engine = self
+        cls = type(sched)
+
+        def wrap(name):
+            base = getattr(cls, name)
+
+            def reader(obj, *a, **k):
+                engine._resolve_skip()
+                return base(obj, *a, **k)
+            reader.__name__ = name
+            return reader
+        # a per-instance subclass: the scheduler's __dict__ (what its state_dict() saves) is untouched
+        methods = {n: wrap(n) for n in ("get_last_lr", "get_lr", "state_dict") if callable(getattr(cls, n, None))}
+        sched.__class__ = type(cls.__name__, (cls,), {"_sxe_resolving_reads": True, **methods})
 
     # ------------------------------------------------------------------------------------- data
     def deepspeed_io(self, dataset, batch_size=None, route=None, pin_memory=True, data_sampler=None,

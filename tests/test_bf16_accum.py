@@ -89,7 +89,7 @@ def _case_skip(rank, world, stage, ckdir):
           "scheduler": {"type": "WarmupLR", "params": {"warmup_min_lr": 0.0, "warmup_max_lr": 1e-2,
                                                        "warmup_num_steps": 10, "warmup_type": "linear"}}}
     eng, _, _, sched = sxe.initialize(model=model, config=ds)
-    lrs, ws = [], []
+    lrs, ws, sched_lrs = [], [], []
     for i in range(4):
         c = torch.ones(N, dtype=torch.bfloat16)
         if i == 2 and rank == 1:
@@ -97,10 +97,12 @@ def _case_skip(rank, world, stage, ckdir):
         loss = eng(c)
         eng.backward(loss)
         eng.step()
+        # the scheduler object the user holds resolves the deferred advance too (not one step stale)
+        sched_lrs.append(sched.get_last_lr()[0])
         lrs.append(eng.get_lr()[0])
         ws.append(model.w.detach().float().clone())
     eng.save_checkpoint(ckdir)
-    return {"lrs": lrs, "skipped": eng.skipped_steps, "ws": ws, "global": eng.global_steps}
+    return {"lrs": lrs, "sched_lrs": sched_lrs, "skipped": eng.skipped_steps, "ws": ws, "global": eng.global_steps}
 
 
 @pytest.mark.parametrize("stage", [0, 1, 3])
@@ -110,6 +112,7 @@ def test_nonfinite_bf16_step_skips_scheduler(tmp_path, stage):
         assert r["skipped"] == 1
         assert r["global"] == 4
         # linear warm-up: lr advances after steps 1, 2, 4 only (step 3 was skipped)
+        assert r["sched_lrs"] == pytest.approx(r["lrs"])
         l0, l1, l2, l3 = r["lrs"]
         assert l1 > l0 and l2 == pytest.approx(l1) and l3 > l2
         assert torch.equal(r["ws"][2], r["ws"][1])  # the skipped step left the weights alone

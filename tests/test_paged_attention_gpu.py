@@ -104,3 +104,22 @@ def test_fused_rope_kv_cache_append_matches_separate_ops():
         torch.testing.assert_close(b, a, rtol=1e-2, atol=1e-2)
         torch.testing.assert_close(c2, c1, rtol=1e-2, atol=1e-2)
         assert torch.equal(c2 == 0, c1 == 0)
+
+
+@pytest.mark.parametrize("splits", [2, 4])
+def test_merge_attention_parts_matches_fused_kernel(splits):
+    """The PyTorch merge of the KV-split partials (v2 llama decode's fallback when the o_proj
+    weight is not covered by the fused merge GEMM) equals the kernel's merged output and the fp32
+    reference."""
+    from shuffle_exchange_amd.ops.paged_attention import (merge_attention_parts, paged_attention,
+                                                          paged_attention_parts, paged_attention_reference)
+    qkv, cache, bt, qs, ql, kl, slots, maxkv = _setup([(700, 1), (1500, 1), (37, 1)], 8, 2, 128, 64)
+    q = qkv[:, :8]
+    scale = 128 ** -0.5
+    out, parts = paged_attention_parts(q, cache, bt, qs, ql, kl, scale, maxkv, splits)
+    assert out is None and parts is not None
+    merged = merge_attention_parts(parts[0], parts[1], q.dtype)
+    fused = paged_attention(q, cache, bt, qs, ql, kl, scale, maxkv, splits)
+    ref = paged_attention_reference(q.float(), cache.float(), bt, qs, ql, kl, scale)
+    torch.testing.assert_close(merged.float(), fused.float(), atol=2e-2, rtol=2e-2)
+    assert ((merged.float() - ref).norm() / ref.norm()).item() < 1e-2
