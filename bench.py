@@ -22,8 +22,10 @@ architecture (no network access for checkpoints/datasets).
   llama70b-infinity   Llama-3-70B, ZeRO-3 + ZeRO-Infinity optimizer offload to pinned host DRAM
                       (C++ AVX-512 Adam), activation checkpointing, seq 2048; 10N layers up to the
                       full 80 (host DRAM of one node bounds the fp32 state: 12 B/param)
-  llama8b-sp32k       Llama-3-8B, Ulysses sequence parallel over all N GPUs, seq 32768, ZeRO-3,
-                      activation checkpointing; one 32k sequence per SP group (strong scaling)
+  llama8b-sp32k       Llama-3-8B, Ulysses sequence parallel over all N GPUs, seq 32768, ZeRO-3; one 32k
+                      sequence per SP group (strong scaling); activation checkpointing by HBM budget
+                      (auto_ac_policy: none when the activations fit -- from 2 GPUs --, else the
+                      MLP-only policy that keeps the attention outputs, else full layers)
 Every JSON line carries the full ZeRO/SP/EP configuration, the measured per-step communication
 volume per collective (``comm_measured``: calls and bytes per rank per step, from the comm facade's
 counters) and an analytic model of it (``comm_model``), so a scaling curve can be checked against the
@@ -51,7 +53,7 @@ CONFIGS = {
                               metric="tokens/sec Llama-3-70B ZeRO-3 + ZeRO-Infinity host offload bf16 "
                                      "(training, whole job)"),
     "llama8b-sp32k": dict(family="llama", model="llama3-8b", seq=32768, mbs=1, gas=1, stage=3, knobs="tuned", sp=True,
-                          ac=True, metric="tokens/sec Llama-3-8B Ulysses SP seq 32k bf16 (training, whole job)"),
+                          ac=True, ac_policy="auto", metric="tokens/sec Llama-3-8B Ulysses SP seq 32k bf16 (training, whole job)"),
 }
 
 
@@ -84,6 +86,28 @@ def zero_knobs(c, cfg, stage):
     if c.get("offload"):
         z["offload_optimizer"] = {"device": "cpu", "pin_memory": True}
     return z
+
+
+# Saved activation bytes per token per Llama decoder layer (bf16, fused kernels of this repo) with
+# no checkpointing / with only the MLP sub-block checkpointed, at hidden 4096 / FFN 14336: the MLP
+# keeps gate_up (2 x 14336), the SwiGLU output and its token-minor copy for the weight gradients.
+ACT_BYTES_PER_TOKEN_LAYER = {"none": 170e3, "mlp": 55e3}
+
+
+def auto_ac_policy(model_name, layers, tokens_per_gpu, world, stage, hbm_bytes=288e9, budget=0.75):
+    """The least recompute that fits: no checkpointing if the saved activations and the ZeRO states
+    fit `budget` of HBM, else the MLP-only policy (attention outputs kept: the flash forward is not
+    re-run), else full-layer checkpointing. 288 GB per MI355X makes 'none' the answer for
+    Llama-3-8B at 32k tokens from 2 GPUs up."""
+    from shuffle_exchange_amd.models import llama_config
+    cfg = llama_config(model_name, **({"num_hidden_layers": layers} if layers else {}))
+    states = 16.0 * cfg.num_params() / (world if stage == 3 else 1)
+    scale = (cfg.hidden_size / 4096 + cfg.intermediate_size / 14336) / 2
+    for policy in ("none", "mlp"):
+        acts = ACT_BYTES_PER_TOKEN_LAYER[policy] * scale * tokens_per_gpu * cfg.num_hidden_layers
+        if states + acts <= budget * hbm_bytes:
+            return policy
+    return "full"
 
 
 def comm_model(opt, world, stage, knobs, gas, elem_bytes=2):
@@ -155,6 +179,9 @@ def main():
     ap.add_argument("--gas", type=int, default=None)
     ap.add_argument("--stage", type=int, default=None)
     ap.add_argument("--ac", action="store_true", help="activation checkpointing")
+    ap.add_argument("--ac-policy", default=None, choices=["full", "mlp", "none", "auto"],
+                    help="what activation checkpointing recomputes (default: the config's; auto = the "
+                         "least recompute whose saved activations fit the HBM budget)")
     ap.add_argument("--layers", type=int, default=None, help="override layer count (a cut model: not the metric)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = plumbing dry-run over gloo (tests only; invalid for the metric)")
@@ -186,8 +213,14 @@ def main():
     dp = world // sp
     layers = args.layers if args.layers is not None else default_layers(args.config, world)
     ac = args.ac or bool(c.get("ac"))
+    policy = args.ac_policy or c.get("ac_policy") or ("full" if ac else "none")
+    if policy == "auto":
+        policy = auto_ac_policy(model_name, layers, seq // sp * mbs, world, stage)
+    ac = policy != "none"
     torch.manual_seed(1234)
     over = {"activation_checkpointing": ac, "max_position_embeddings": max(8192, seq)}
+    if c["family"] == "llama" and policy == "mlp":
+        over["ac_policy"] = "mlp"
     if layers:
         over["num_hidden_layers"] = layers
     if sp > 1:
@@ -300,7 +333,7 @@ def main():
             "data": "synthetic",
             "config": {"name": args.config, "model": model_tag, "global_batch": dp * mbs * gas, "seq_len": seq,
                        "micro_batch_per_gpu": mbs, "grad_accum": gas, "parallelism": "-".join(par),
-                       "params": n_params, "activation_checkpointing": ac,
+                       "params": n_params, "activation_checkpointing": policy if ac else False,
                        "optimizer": "AdamW(fp32 master, " + ("C++ CPU Adam on host" if c.get("offload") else
                                                              "fused HIP") + ")",
                        "zero_knobs": c["knobs"], "zero_optimization": zero,

@@ -69,6 +69,13 @@ struct ProArgs {
   const int64_t* rslots;
   unsigned short* rcache;
   int rnq, rnkv, rbs;
+  // split-K (ks > 1, bf16 kernel): workgroup blockIdx.x covers tile blockIdx.x % tiles and K part
+  // blockIdx.x / tiles; wave 0 of each writes its partial tile to skws and bumps skcnt[tile]; the
+  // last of the ks arrivals sums the partials in K-part order (deterministic), runs the epilogue
+  // and resets the counter for the next launch
+  float* skws;
+  int* skcnt;
+  int ks;
 };
 
 // output column of lane `col` in tile `tile` (identity unless the RoPE epilogue pairs columns)
@@ -112,11 +119,11 @@ __device__ __forceinline__ void rope_store(const ProArgs& p, float v, int m, int
 // merge_kernel's math): sum_s 2^(M_s - M) o_s / sum_s 2^(M_s - M) L_s. One thread per 8 d of one
 // (row, head); every load of a group of 8 splits is issued before the first use.
 template <int NT>
-__device__ __forceinline__ void build_merge(int M, int K, const ProArgs& p, unsigned short* act) {
+__device__ __forceinline__ void build_merge(int M, int K, int klo, int khi, const ProArgs& p, unsigned short* act) {
   constexpr int U = 8;
-  const int D = K / p.nq, per = K / 8, n = M * per;
+  const int D = K / p.nq, per = (khi - klo) / 8, n = M * per;
   for (int idx = threadIdx.x; idx < n; idx += NT) {
-    const int m = idx / per, c = (idx - m * per) * 8, h = c / D, d = c - h * D;
+    const int m = idx / per, c = klo + (idx - m * per) * 8, h = c / D, d = c - h * D;
     const int64_t th = (int64_t)m * p.nq + h, sstride = (int64_t)M * p.nq;
     float Mx = -INFINITY, L = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int s0 = 0; s0 < p.splits; s0 += U) {
@@ -159,26 +166,32 @@ __device__ __forceinline__ void build_merge(int M, int K, const ProArgs& p, unsi
   __syncthreads();
 }
 
+// Only columns [klo, khi) of the input are built (a split-K part needs no more), except under
+// PRO_RMS, whose row norm needs the whole row.
 template <int MODE, int NT>
-__device__ __forceinline__ void build_act(const unsigned short* __restrict x, int64_t ldx, int M, int K,
-                                          const ProArgs& p, unsigned short* act, float* rinv) {
+__device__ __forceinline__ void build_act(const unsigned short* __restrict x, int64_t ldx, int M, int K, int klo,
+                                          int khi, const ProArgs& p, unsigned short* act, float* rinv) {
   if constexpr (MODE == PRO_MERGE) {
-    build_merge<NT>(M, K, p, act);
+    build_merge<NT>(M, K, klo, khi, p, act);
     return;
+  }
+  if constexpr (MODE == PRO_RMS) {
+    klo = 0;
+    khi = K;
   }
   // U chunks of 8 per thread per round, every load of a round issued before the first use: a loop
   // that consumes each chunk before loading the next is a chain of dependent L2 round trips (it made
   // the fused down projection 9 us slower than the separate SwiGLU launch)
   constexpr int U = 4;
   __shared__ float red[NT / 64][kProMaxM];
-  const int per = K / 8, n = M * per;
+  const int per = (khi - klo) / 8, n = M * per;
   float ss[kProMaxM] = {0.f, 0.f, 0.f, 0.f};
   for (int base = 0; base < n; base += U * NT) {
     u16x8 a[U], b[U], gw[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int idx = base + u * NT + threadIdx.x;
-      const int m = idx / per, c = (idx - m * per) * 8;
+      const int m = idx / per, c = klo + (idx - m * per) * 8;
       const bool ok = idx < n;
       const unsigned short* xr = x + (int64_t)(ok ? m : 0) * ldx + (ok ? c : 0);
       a[u] = *reinterpret_cast<const u16x8*>(xr);
@@ -193,7 +206,7 @@ __device__ __forceinline__ void build_act(const unsigned short* __restrict x, in
     for (int u = 0; u < U; ++u) {
       const int idx = base + u * NT + threadIdx.x;
       if (idx >= n) continue;
-      const int m = idx / per, c = (idx - m * per) * 8;
+      const int m = idx / per, c = klo + (idx - m * per) * 8;
       float o[8];
       if constexpr (MODE == PRO_SWIGLU) {
 #pragma unroll
@@ -251,12 +264,15 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(const unsigned sho
   extern __shared__ __attribute__((aligned(16))) unsigned short act_lds[];  // PRO_*: the M x K input
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, g = lane >> 4;
-  const int n = MODE == PRO_RMS ? out_col(pro, blockIdx.x, col) : blockIdx.x * 16 + col;
+  const int ks = pro.ks > 1 ? pro.ks : 1;
+  const int tiles = gridDim.x / ks, tile = blockIdx.x % tiles, kpart = blockIdx.x / tiles;
+  const int n = MODE == PRO_RMS ? out_col(pro, tile, col) : tile * 16 + col;
   const bool wok = n < N, xok = col < M;
   const unsigned short* wrow = w + (int64_t)(wok ? n : 0) * ldw;
   const unsigned short* xrow = MODE == PRO_NONE ? x + (int64_t)(xok ? col : 0) * ldx
                                                 : act_lds + (int64_t)(xok ? col : 0) * K;
-  const int ss0 = wave * ss_per_wave;
+  const int ss_part = NW * ss_per_wave;  // super-steps of one K part
+  const int ss0 = kpart * ss_part + wave * ss_per_wave;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   __shared__ float rinv[kProMaxM];
   Frag cur, nxt;
@@ -277,7 +293,8 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(const unsigned sho
     Frag nx2;
     load_w(cur, wrow, wok, ss0 * kSS + g * 8, K);
     if (ss_per_wave > 1) load_w(nxt, wrow, wok, (ss0 + 1) * kSS + g * 8, K);
-    build_act<MODE, NW * 64>(x, ldx, M, K, pro, act_lds, rinv);
+    build_act<MODE, NW * 64>(x, ldx, M, K, min(K, kpart * ss_part * kSS), min(K, (kpart + 1) * ss_part * kSS), pro,
+                             act_lds, rinv);
     for (int i = 0; i < ss_per_wave; ++i) {
       if (i + 2 < ss_per_wave) load_w(nx2, wrow, wok, (ss0 + i + 2) * kSS + g * 8, K);
       load_x(cur, xrow, xok, (ss0 + i) * kSS + g * 8, K);
@@ -300,11 +317,34 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(const unsigned sho
       t[2] += u[2];
       t[3] += u[3];
     }
+    if (ks > 1) {
+      f32x4* part = reinterpret_cast<f32x4*>(pro.skws) + (int64_t)tile * ks * 64;
+      part[kpart * 64 + lane] = t;
+      __threadfence();  // release the partial before the arrival count (agent scope: all XCDs)
+      int arrived = 0;
+      if (lane == 0) arrived = atomicAdd(pro.skcnt + tile, 1);
+      arrived = __shfl(arrived, 0, 64);
+      if (arrived != ks - 1) return;  // not the last part of this tile
+      __threadfence();  // acquire the other parts' partials
+      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < ks; ++q) {
+        f32x4 u = t;
+        if (q != kpart) {
+          const float* src = reinterpret_cast<const float*>(part + q * 64 + lane);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) u[e] = __hip_atomic_load(src + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sum[e] += u[e];
+      }
+      t = sum;
+      if (lane == 0) __hip_atomic_store(pro.skcnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (MODE == PRO_RMS && pro.rcos != nullptr) {  // RoPE epilogue (no bias: checked on the host)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = 4 * g + r;
-        rope_store(pro, t[r] * rinv[m < kProMaxM ? m : 0], m, M, n, blockIdx.x, col, y, ldy);
+        rope_store(pro, t[r] * rinv[m < kProMaxM ? m : 0], m, M, n, tile, col, y, ldy);
       }
     } else if (n < N) {
       const float b = bias ? bf16_to_f32(bias[n]) : 0.f;
@@ -379,7 +419,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_fp8w_kernel(const unsigne
       const int k = k0 + 64 * j;
       wv0[j] = (wok && k < K && ss_per_wave > 0) ? *reinterpret_cast<const uint4*>(wrow + k) : uint4{0u, 0u, 0u, 0u};
     }
-    build_act<MODE, NW * 64>(x, ldx, M, K, pro, act_lds, rinv);
+    build_act<MODE, NW * 64>(x, ldx, M, K, 0, K, pro, act_lds, rinv);
   }
   for (int i = 0; i < ss_per_wave; ++i) {
     const int k0 = (wave * ss_per_wave + i) * kSS8 + 16 * g;
@@ -432,6 +472,67 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_fp8w_kernel(const unsigne
   }
 }
 
+// Split-K plan for the bf16 kernel. The decode GEMMs with few 16-column tiles (the QKV projection:
+// 384 tiles, o_proj: 256) leave CUs with uneven work (384 tiles = two workgroups on half the CUs,
+// one on the others) or one 4-wave workgroup per CU (too few loads in flight to cover HBM latency);
+// splitting K in ks parts gives every CU the same share and more streams. SXE_SKINNY_SPLITK: 0 off,
+// 1 auto (default), 2 / 4 forced.
+struct SplitWs {
+  at::Tensor ws, cnt;
+};
+
+inline int split_mode() {
+  static const int v = [] {
+    const char* e = std::getenv("SXE_SKINNY_SPLITK");
+    return e == nullptr ? 1 : std::atoi(e);
+  }();
+  return v;
+}
+
+// returns ks (1 = no split) and sets nw / ss_per_wave / the ProArgs split fields
+inline int plan_split(int tiles, int ss_total, int& nw, int& spw, ProArgs& pro, const at::Tensor& like) {
+  int ks = 1;
+  const int mode = split_mode();
+  if (mode == 1 && tiles < 2 * kNumCUs) ks = tiles <= kNumCUs / 2 ? 4 : 2;
+  else if (mode == 2 || mode == 4) ks = mode;
+  while (ks > 1) {
+    const int part = (ss_total + ks - 1) / ks;
+    nw = pick_nw(tiles * ks, part, 4, 1);
+    if (part >= nw) break;
+    ks /= 2;
+  }
+  if (ks > 1) {
+    static std::vector<SplitWs> per_dev;
+    const int dev = like.get_device();
+    if ((int)per_dev.size() <= dev) per_dev.resize(dev + 1);
+    SplitWs& sw = per_dev[dev];
+    const int64_t need = (int64_t)tiles * ks * 64 * 4;
+    if (!sw.ws.defined() || sw.ws.numel() < need || sw.cnt.numel() < tiles) {
+      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+      SXE_HIP_CHECK(hipStreamIsCapturing(cur_stream(), &st));
+      if (st != hipStreamCaptureStatusNone) {
+        ks = 1;  // no workspace allocation inside a graph capture: run unsplit
+      } else {
+        const int64_t cap = std::max<int64_t>(need, (int64_t)4096 * 4 * 64 * 4);
+        sw.ws = at::empty({cap}, like.options().dtype(at::kFloat));
+        sw.cnt = at::zeros({std::max<int64_t>(tiles, 4096)}, like.options().dtype(at::kInt));
+      }
+    }
+    if (ks > 1) {
+      pro.skws = sw.ws.data_ptr<float>();
+      pro.skcnt = sw.cnt.data_ptr<int>();
+      pro.ks = ks;
+      const int part = (ss_total + ks - 1) / ks;
+      spw = (part + nw - 1) / nw;
+      return ks;
+    }
+  }
+  nw = pick_nw(tiles, ss_total, 4, 1);
+  spw = (ss_total + nw - 1) / nw;
+  pro.ks = 1;
+  return 1;
+}
+
 }  // namespace sg
 
 // x [M, K] (row stride free, unit column stride), w [N, K] contiguous rows, bias [N] or None.
@@ -454,16 +555,17 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, const c10::opti
   auto y = at::empty({M, N}, x.options());
   if (N == 0) return y;
   c10::DeviceGuard gd(x.device());
-    const int ss_total = (K + sg::kSS - 1) / sg::kSS;
+  const int ss_total = (K + sg::kSS - 1) / sg::kSS;
   const int tiles = (N + 15) / 16;
-  const int nw = sg::pick_nw(tiles, ss_total, 4, 1);
-  const int ss_per_wave = (ss_total + nw - 1) / nw;
+  int nw = 4, ss_per_wave = 1;
+  sg::ProArgs pro{};
+  const int ks = sg::plan_split(tiles, ss_total, nw, ss_per_wave, pro, x);
   auto* xp = reinterpret_cast<const unsigned short*>(x.data_ptr());
   auto* wp = reinterpret_cast<const unsigned short*>(w.data_ptr());
   auto* yp = reinterpret_cast<unsigned short*>(y.data_ptr());
 #define SXE_SG_LAUNCH(NW)                                                                                  \
-  hipLaunchKernelGGL(sg::skinny_gemm_kernel<NW>, dim3(tiles), dim3(NW * 64), 0, cur_stream(), xp, x.stride(0), \
-                     wp, w.stride(0), bp, yp, y.stride(0), M, N, K, ss_per_wave, sg::ProArgs{})
+  hipLaunchKernelGGL(sg::skinny_gemm_kernel<NW>, dim3(tiles * ks), dim3(NW * 64), 0, cur_stream(), xp,          \
+                     x.stride(0), wp, w.stride(0), bp, yp, y.stride(0), M, N, K, ss_per_wave, pro)
   if (nw == 4) SXE_SG_LAUNCH(4);
   else SXE_SG_LAUNCH(8);
 #undef SXE_SG_LAUNCH
@@ -599,13 +701,13 @@ static std::vector<at::Tensor> skinny_gemm_pro_impl(const at::Tensor& x, const c
   const int mi = mode == sg::PRO_RMS ? 0 : 1;
   if (!fp8) {
     const int ss_total = (K + sg::kSS - 1) / sg::kSS;
-    const int nw = sg::pick_nw(tiles, ss_total, 4, 1);
-    const int spw = (ss_total + nw - 1) / nw;
+    int nw = 4, spw = 1;
+    const int ks = sg::plan_split(tiles, ss_total, nw, spw, pro, x);
     auto* wp = reinterpret_cast<const unsigned short*>(w.data_ptr());
 #define SXE_SGP(NW, MODE)                                                                                            \
   do {                                                                                                               \
     set(reinterpret_cast<const void*>(&sg::skinny_gemm_kernel<NW, MODE>), 0, NW == 8, mi);                           \
-    hipLaunchKernelGGL((sg::skinny_gemm_kernel<NW, MODE>), dim3(tiles), dim3(NW * 64), lds, cur_stream(), xp,         \
+    hipLaunchKernelGGL((sg::skinny_gemm_kernel<NW, MODE>), dim3(tiles * ks), dim3(NW * 64), lds, cur_stream(), xp,    \
                        x.stride(0), wp, w.stride(0), bp, yp, y.stride(0), M, N, K, spw, pro);                         \
   } while (0)
     if (mode == sg::PRO_RMS) { if (nw == 4) SXE_SGP(4, sg::PRO_RMS); else SXE_SGP(8, sg::PRO_RMS); }
@@ -692,13 +794,14 @@ at::Tensor skinny_gemm_merge(const at::Tensor& part_o, const at::Tensor& part_ml
   };
   if (!fp8) {
     const int ss_total = (K + sg::kSS - 1) / sg::kSS;
-    const int nw = sg::pick_nw(tiles, ss_total, 4, 1);
-    const int spw = (ss_total + nw - 1) / nw;
+    int nw = 4, spw = 1;
+    const int ks = sg::plan_split(tiles, ss_total, nw, spw, pro, part_o);
     auto* wp = reinterpret_cast<const unsigned short*>(w.data_ptr());
 #define SXE_SGM(NW)                                                                                                  \
   do {                                                                                                               \
     set(reinterpret_cast<const void*>(&sg::skinny_gemm_kernel<NW, sg::PRO_MERGE>), 0, NW == 8);                      \
-    hipLaunchKernelGGL((sg::skinny_gemm_kernel<NW, sg::PRO_MERGE>), dim3(tiles), dim3(NW * 64), lds, cur_stream(),    \
+    hipLaunchKernelGGL((sg::skinny_gemm_kernel<NW, sg::PRO_MERGE>), dim3(tiles * ks), dim3(NW * 64), lds,             \
+                       cur_stream(),                                                                                 \
                        nullptr, K, wp, w.stride(0), bp, yp, y.stride(0), M, N, K, spw, pro);                          \
   } while (0)
     if (nw == 4) SXE_SGM(4); else SXE_SGM(8);

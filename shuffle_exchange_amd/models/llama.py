@@ -54,6 +54,10 @@ class LlamaConfig:
     tie_word_embeddings: bool = False
     initializer_range: float = 0.02
     activation_checkpointing: bool = False
+    # what activation checkpointing recomputes: "full" = the whole decoder layer (attention
+    # included); "mlp" = only the MLP sub-block (its gate_up / SwiGLU activations, ~70 % of a
+    # layer's saved bytes, are recomputed by GEMMs; the flash-attention forward is NOT re-run)
+    ac_policy: str = "full"
     loss_chunk_tokens: Optional[int] = None
     sequence_parallel: bool = False  # Ulysses: inputs are [B, S/sp] chunks of the SP group
     sp_mode: str = "ulysses"         # "ring" / "ring_zigzag": ring attention (context parallelism) over
@@ -64,6 +68,8 @@ class LlamaConfig:
     extra: dict = field(default_factory=dict)
 
     def __post_init__(self):
+        if self.ac_policy not in ("full", "mlp"):
+            raise ValueError(f"ac_policy must be 'full' or 'mlp', got {self.ac_policy!r}")
         if self.head_dim is None:
             self.head_dim = self.hidden_size // self.num_attention_heads
 
@@ -160,6 +166,7 @@ class LlamaDecoderLayer(nn.Module):
         self.self_attn = LlamaAttention(cfg)
         self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         self.mlp = LlamaMLP(cfg)
+        self.ckpt_mlp = cfg.activation_checkpointing and cfg.ac_policy == "mlp"
 
     def forward(self, x, residual, rope, position_ids=None):
         """(x, residual) -> (mlp_out, new_residual); the true hidden state is x + residual."""
@@ -169,6 +176,8 @@ class LlamaDecoderLayer(nn.Module):
             a, h = self.input_layernorm(x, residual)
         attn = self.self_attn(a, rope, position_ids)
         m, h2 = self.post_attention_layernorm(attn, h)
+        if self.ckpt_mlp and self.training and torch.is_grad_enabled():
+            return checkpoint(self.mlp, m), h2
         return self.mlp(m), h2
 
 
@@ -249,7 +258,8 @@ class LlamaForCausalLM(nn.Module):
         rope = self.rope(x.device)
         res = None
         for layer in self.layers:
-            if self.cfg.activation_checkpointing and self.training and torch.is_grad_enabled():
+            if (self.cfg.activation_checkpointing and self.cfg.ac_policy == "full" and self.training
+                    and torch.is_grad_enabled()):
                 x, res = checkpoint(layer, x, res, rope, position_ids)
             else:
                 x, res = layer(x, res, rope, position_ids)

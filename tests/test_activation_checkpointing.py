@@ -74,3 +74,27 @@ def _case_partitioned_counts(rank, world):
 def test_partition_stores_fraction():
     for r in run_dist(_case_partitioned_counts, 2):
         assert r["part"] == 64 * 64 // 2
+
+
+def test_llama_ac_policies_give_identical_gradients():
+    """Llama activation checkpointing policies (models/llama.py ac_policy): whole-layer ('full') and
+    MLP-only ('mlp', keeps the attention outputs) recompute reproduce the un-checkpointed loss and
+    gradients exactly."""
+    import pytest
+    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+    ids = torch.randint(0, 512, (2, 32), generator=torch.Generator().manual_seed(0))
+    out = {}
+    for name, kw in (("none", {}), ("full", {"activation_checkpointing": True}),
+                     ("mlp", {"activation_checkpointing": True, "ac_policy": "mlp"})):
+        torch.manual_seed(0)
+        model = LlamaForCausalLM(llama_config("llama-tiny", **kw)).train()
+        loss = model(ids, labels=ids)
+        loss.backward()
+        out[name] = (loss.detach(), [p.grad.clone() for p in model.parameters()])
+    assert model.layers[0].ckpt_mlp
+    for name in ("full", "mlp"):
+        assert torch.equal(out[name][0], out["none"][0])
+        for a, b in zip(out[name][1], out["none"][1]):
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
+    with pytest.raises(ValueError):
+        llama_config("llama-tiny", ac_policy="attention")
