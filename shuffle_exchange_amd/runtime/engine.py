@@ -23,6 +23,7 @@ import torch.nn as nn
 
 from .. import comm as dist
 from ..accelerator import get_accelerator
+from ..ops import linear as _linear_ops
 from ..ops import optim as fused
 from ..parallel import groups
 from ..utils.logging import log_dist, logger
@@ -192,6 +193,9 @@ class SXEEngine(nn.Module):
         if optimizer is not None or cfg.optimizer_name is not None:
             self._configure_optimizer(optimizer, model_parameters)
             self._configure_lr_scheduler(lr_scheduler)
+        # transposed weights stay valid across the micro-steps of one optimizer step (ops/linear.py)
+        _linear_ops.WT_CACHE = self.gradient_accumulation_steps() > 1
+        _linear_ops.invalidate_transposed_weights()
         ckpt = cfg.model.checkpoint
         wtype = str((ckpt.writer or {}).get("type", "")).lower()
         if wtype == "fast":  # reference checkpoint.writer {"type": "fast", "io_buffer_size": ...}
@@ -843,6 +847,7 @@ class SXEEngine(nn.Module):
         if off:
             self.optimizer.reload_states()
         self.optimizer.step()
+        _linear_ops.invalidate_transposed_weights()  # the weights changed
         if off:
             self.optimizer.offload_states(include=["optim_states"], non_blocking=True)
         overflow = bool(getattr(self.optimizer, "overflow", False))
@@ -1310,6 +1315,7 @@ class SXEEngine(nn.Module):
 
     def load_checkpoint(self, load_dir, tag=None, load_module_strict=True, load_optimizer_states=True,
                         load_lr_scheduler_states=True, load_module_only=False, custom_load_fn=None):
+        _linear_ops.invalidate_transposed_weights()
         if tag is None:
             latest = os.path.join(load_dir, "latest")
             if not os.path.isfile(latest):

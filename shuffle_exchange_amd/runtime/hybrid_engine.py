@@ -46,12 +46,16 @@ class SXEHybridEngine(SXEEngine):
         return [m for m in self.module.modules() if hasattr(m, "fuse_lora") and hasattr(m, "unfuse_lora")]
 
     def fuse_lora_weight(self):
+        from ..ops.linear import invalidate_transposed_weights
         for m in self._lora_modules():
             m.fuse_lora()
+        invalidate_transposed_weights()  # the base weights changed in place
 
     def unfuse_lora_weight(self):
+        from ..ops.linear import invalidate_transposed_weights
         for m in self._lora_modules():
             m.unfuse_lora()
+        invalidate_transposed_weights()
 
     @torch.no_grad()
     def generate(self, input_ids, max_new_tokens=None, do_sample=False, temperature=1.0, top_k=0, eos_token_id=None,
