@@ -475,8 +475,8 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_fp8w_kernel(const unsigne
 // Split-K plan for the bf16 kernel. The decode GEMMs with few 16-column tiles (the QKV projection:
 // 384 tiles, o_proj: 256) leave CUs with uneven work (384 tiles = two workgroups on half the CUs,
 // one on the others) or one 4-wave workgroup per CU (too few loads in flight to cover HBM latency);
-// splitting K in ks parts gives every CU the same share and more streams. SXE_SKINNY_SPLITK: 0 off,
-// 1 auto (default), 2 / 4 forced.
+// splitting K in ks parts gives every CU the same share and more streams. SXE_SKINNY_SPLITK: 0 off
+// (default until the split path has a GPU measurement in profiles/), 1 auto, 2 / 4 forced.
 struct SplitWs {
   at::Tensor ws, cnt;
 };
@@ -484,7 +484,7 @@ struct SplitWs {
 inline int split_mode() {
   static const int v = [] {
     const char* e = std::getenv("SXE_SKINNY_SPLITK");
-    return e == nullptr ? 1 : std::atoi(e);
+    return e == nullptr ? 0 : std::atoi(e);
   }();
   return v;
 }

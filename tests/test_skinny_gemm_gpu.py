@@ -32,6 +32,9 @@ def test_split_k_is_repeatable_and_graph_safe(N, K):
     """Split-K decode GEMMs (few 16-column tiles: K split over 2-4 workgroups, the last arrival sums
     the partials in a fixed order and resets its tile counter): back-to-back launches and HIP-graph
     replays give bit-identical results equal to the fp32 reference."""
+    import os
+    if os.environ.get("SXE_SKINNY_SPLITK", "0") == "0":
+        pytest.skip("split-K is opt-in (SXE_SKINNY_SPLITK=1)")
     g = torch.Generator(device="cuda").manual_seed(N + K)
     x = torch.randn(1, K, device="cuda", dtype=torch.bfloat16, generator=g)
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g)
