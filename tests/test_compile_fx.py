@@ -151,13 +151,14 @@ def test_fx_compiled_shuffle_exchange_matches_eager(method):
             torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("model_kind", ["mlp", "llama"])
-def test_fx_zero3_graph_compiler_matches_eager(model_kind):
+@pytest.mark.parametrize("model_kind,gas", [("mlp", 1), ("llama", 1), ("llama", 2)])
+def test_fx_zero3_graph_compiler_matches_eager(model_kind, gas):
     """ZeRO-3 under the graph compiler (compile/fx_zero3.py): gather / prefetch / release nodes in
     the forward and backward FX graphs and the reduce-scatters fed by in-graph reduce nodes; the
-    trajectory equals the eager ZeRO-3 engine's (gloo, world 2)."""
-    comp = run_dist(_train, 2, True, 3, 1, model_kind)
-    eager = run_dist(_train, 2, False, 3, 1, model_kind)
+    trajectory equals the eager ZeRO-3 engine's (gloo, world 2), with and without gradient
+    accumulation."""
+    comp = run_dist(_train, 2, True, 3, gas, model_kind)
+    eager = run_dist(_train, 2, False, 3, gas, model_kind)
     for c, e in zip(comp, eager):
         assert c["losses"] == pytest.approx(e["losses"], rel=1e-4, abs=1e-5)
         for x, y in zip(c["params"], e["params"]):
