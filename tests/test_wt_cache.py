@@ -47,20 +47,29 @@ def test_cache_respects_identity_and_cap(counting, monkeypatch):
     assert sum(1 for t in counting if t is w3) == 2  # over the cap: nothing is kept
 
 
-def test_engine_enables_for_accumulation_and_clears_on_step():
+def _case_engine(rank, world):
     import shuffle_exchange_amd as sxe
-    for gas, want in ((1, False), (2, True)):
+    from shuffle_exchange_amd.ops import linear as lin
+    seen = []
+    for gas in (1, 2):
         model = torch.nn.Linear(8, 8)
         ds = {"train_micro_batch_size_per_gpu": 1, "gradient_accumulation_steps": gas,
               "optimizer": {"type": "SGD", "params": {"lr": 0.1}}}
         eng, _, _, _ = sxe.initialize(model=model, config=ds)
-        assert L.WT_CACHE is want
+        seen.append(lin.WT_CACHE)
     w = torch.nn.Parameter(torch.randn(4, 4))
-    L._wt_cache[id(w)] = (None, w)
+    lin._wt_cache[id(w)] = (None, w)
     for _ in range(2):
         eng.backward(eng(torch.randn(1, 8)).sum())
         eng.step()
-    assert not L._wt_cache  # the optimizer step invalidated it
+    return {"seen": seen, "left": len(lin._wt_cache)}
+
+
+def test_engine_enables_for_accumulation_and_clears_on_step():
+    from .dist_utils import run_dist
+    (r,) = run_dist(_case_engine, 1)
+    assert r["seen"] == [False, True]
+    assert r["left"] == 0  # the optimizer step invalidated the cache
 
 
 @pytest.mark.gpu
