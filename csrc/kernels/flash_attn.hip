@@ -417,299 +417,6 @@ __global__ void __launch_bounds__(NWF * 64, (fwd_min_waves<D, NWF>())) fwd_kerne
 }
 
 // =============================================================================================
-// Software-pipelined forward (head dims 64 / 128, 8 waves): K runs one tile ahead of V, so a wave
-// computes the raw scores of tile t+1 (S^T = K Q^T, 16 MFMAs reading K(t+1) from LDS) in the same
-// straight-line block as the softmax of tile t (max / exp / sum / bf16 packs, ~150 VALU issues),
-// then PV(t). The two streams are independent, so the MFMA pipe stays busy while the VALU works
-// through the exps -- in the one-phase loop above both waves of a SIMD run S MFMAs, then both run
-// softmax with the matrix pipe idle, then both run PV. Costs 32 more VGPRs (two score tiles live);
-// the LDS ring is unchanged (slot i holds K(t+1+?) / V(t) with K staged one tile earlier).
-// =============================================================================================
-// Lane-constant LDS byte offsets of the pipelined forward's operand reads, computed once (hipcc
-// otherwise re-derives one per (row block, column block) pair and spills them): K rows of the
-// score MFMAs, k[t2] = soff(r, 2 t2 + h) (+ 32 j rows as an immediate), and the two transposed
-// V reads of the PV MFMAs, v[dt][0 / 1] = rows 4h + q / +8 (+ 32 j + 16 s2 rows as immediates; the
-// swizzle depends only on a row's low 4 bits).
-template <int D>
-struct PipeOffs {
-  int k[D / 16];
-  int v[D / 32][2];
-  __device__ __forceinline__ void init(int lane) {
-    const int r = lane & 31, h = lane >> 5;
-#pragma unroll
-    for (int t2 = 0; t2 < D / 16; ++t2) k[t2] = soff<D>(r, 2 * t2 + h);
-    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, hh = g >> 1;
-#pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt) {
-      const int ch = 4 * dt + 2 * (g & 1) + (p >> 1);
-      v[dt][0] = soff<D>(4 * hh + q, ch) + 8 * (p & 1);
-      v[dt][1] = soff<D>(4 * hh + q + 8, ch) + 8 * (p & 1);
-    }
-#pragma unroll
-    for (int t2 = 0; t2 < D / 16; ++t2) asm volatile("" : "+v"(k[t2]));
-#pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt) asm volatile("" : "+v"(v[dt][0]), "+v"(v[dt][1]));
-  }
-};
-
-template <int D, int J>
-__device__ __forceinline__ void fwd_scores(const char* kt, const bf16x8 (&qf)[D / 16], f32x16 (&s)[J],
-                                           const PipeOffs<D>& of) {
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    s[j] = zero16();
-#pragma unroll
-    for (int t2 = 0; t2 < D / 16; ++t2)
-      s[j] = mfma(*reinterpret_cast<const bf16x8*>(kt + 32 * j * (2 * D) + of.k[t2]), qf[t2], s[j]);
-  }
-}
-
-// transposed V operand of the PV MFMA for rows row0 + [0, 16) (row0 a multiple of 16), column block dt
-template <int D>
-__device__ __forceinline__ bf16x8 vt_operand(const char* vt, int row0, int dt, const PipeOffs<D>& of) {
-  const i16x4 lo = lds_tr(vt + row0 * (2 * D), of.v[dt][0]);
-  const i16x4 hi = lds_tr(vt + row0 * (2 * D), of.v[dt][1]);
-  const i16x8 c = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8, c);
-}
-
-// Online-softmax state of one lane between pipeline steps: m = reference max of the tile about to
-// be exponentiated (mref: the same, 0 while no score was seen), alpha = rescale of O and l that
-// tile brings, grow = whether any lane moved its reference (O needs the rescale at all).
-struct SoftState {
-  float m, mref, alpha;
-  bool grow;
-};
-
-// Mask the raw scores of a tile (MASK) and advance the softmax state by its max (lazy rescale:
-// the reference only moves when the tile max exceeds it by > 2^8, so p <= 256).
-template <bool MASK, int J>
-__device__ __forceinline__ void fwd_tile_max(f32x16 (&s)[J], SoftState& st, float c, int kbase, int qpos, int r,
-                                             int h, bool diag, bool tail, int kvlen, const uint8_t* lrow, int blk) {
-  float mx = -INFINITY;
-  // key - query offsets of this lane's first score row; opaque, so the compares below keep
-  // compile-time row constants instead of 32 hoisted per-row thresholds per mask (VGPRs)
-  int dd = kbase + 4 * h - qpos - r, dl = kbase + 4 * h - kvlen;
-  if (MASK) asm volatile("" : "+v"(dd), "+v"(dl));
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-    bool b0 = true, b1 = true;
-    if (MASK && lrow) {
-      b0 = lrow[(kbase + 32 * j) / blk] != 0;
-      b1 = lrow[(kbase + 32 * j + 16) / blk] != 0;
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float x = s[j][i];
-      if (MASK) {
-        if (diag && dd + 32 * j + acc_row(i, 0) > 0) x = -INFINITY;
-        if (tail && dl + 32 * j + acc_row(i, 0) >= 0) x = -INFINITY;
-        if (!(i < 8 ? b0 : b1)) x = -INFINITY;
-        s[j][i] = x;
-      }
-      mx = fmaxf(mx, x);
-    }
-  }
-  mx = fmaxf(mx, xor32(mx)) * c;
-  const bool grow = mx > st.m + 8.f;
-  const float mnew = grow ? mx : st.m;
-  const float mref = (mnew == -INFINITY) ? 0.f : mnew;
-  st.alpha = fast_exp2(st.m - mref);
-  st.grow = __any(grow);
-  st.m = mnew;
-  st.mref = mref;
-}
-
-// One pipeline step for tile t (its masked scores in `s`, its state in `st`):
-//   phase A: P = exp2(c s - mref) (+ row sum, bf16 packs)  ||  NEXT: scores of tile t+1 into `sn`
-//   phase B: O += P V(t)                                   ||  NEXT: mask + max of tile t+1 -> st
-// The interleave is pinned with sched_group_barrier (hipcc otherwise emits the score MFMAs back to
-// back, each waiting on its own LDS read, and the exps after them): A = 16 x {MFMA, K-row read,
-// ~7 VALU} with the K reads 3 MFMAs ahead; B = 16 x {MFMA, 2 V^T reads, VALU}.
-#ifndef FA_PIPE_SGB
-#define FA_PIPE_SGB 0
-#endif
-template <bool MASKN, bool NEXT, int D, int J>
-__device__ __forceinline__ void fwd_pipe_step(const char* kt_next, const char* vt, const bf16x8 (&qf)[D / 16],
-                                              f32x16 (&s)[J], f32x16 (&sn)[J], f32x16 (&oacc)[D / 32],
-                                              SoftState& st, float& l, float c, int kbn, int qpos, int r, int h,
-                                              const PipeOffs<D>& of, bool diagn, bool tailn, int kvlen,
-                                              const uint8_t* lrow, int blk) {
-  if (st.grow) {
-#pragma unroll
-    for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) oacc[dt][i] *= st.alpha;
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  bf16x8 pb[J][2];
-  float ps = 0.f;
-#pragma unroll
-  for (int j = 0; j < J; ++j) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      s[j][i] = fast_exp2(__builtin_fmaf(s[j][i], c, -st.mref));
-      ps += s[j][i];
-    }
-    pb[j][0] = acc_to_b(s[j], 0);
-    pb[j][1] = acc_to_b(s[j], 1);
-  }
-  if (NEXT) {
-    fwd_scores<D, J>(kt_next, qf, sn, of);
-    constexpr int NM = J * D / 16;  // score MFMAs of the next tile
-    if (FA_PIPE_SGB) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
-#pragma unroll
-    for (int i = 0; i < NM; ++i) {
-      if (!FA_PIPE_SGB) break;
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      if (i + 3 < NM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 64 * J / NM, 0);
-    }
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  l = l * st.alpha + ps;
-#pragma unroll
-  for (int j = 0; j < J; ++j)
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt)
-        oacc[dt] = mfma(vt_operand<D>(vt, 32 * j + 16 * s2, dt, of), pb[j][s2], oacc[dt]);
-  if (NEXT) fwd_tile_max<MASKN, J>(sn, st, c, kbn, qpos, r, h, diagn, tailn, kvlen, lrow, blk);
-  {
-    constexpr int NP = 2 * J * (D / 32);  // PV MFMAs
-    if (FA_PIPE_SGB) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      if (!FA_PIPE_SGB) break;
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      if (i + 2 < NP) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, J * (MASKN ? 80 : 16) / NP, 0);
-    }
-  }
-}
-
-// keys per K/V tile of the pipelined forward: 32 at head dim 128 (two live score tiles of 64 keys
-// would not fit the 256 registers of a wave at two waves per SIMD), 64 at head dim 64
-template <int D>
-constexpr int pipe_kt() { return D >= 128 ? 32 : 64; }
-
-template <int D>
-__global__ void __launch_bounds__(512, 1) fwd_pipe_kernel(
-    const unsigned short* __restrict__ q, Strides qs, const unsigned short* __restrict__ k, Strides ks,
-    const unsigned short* __restrict__ v, Strides vs, unsigned short* __restrict__ o, Strides os,
-    float* __restrict__ lse, int B, int H, int Hk, int Sq, int Sk, float scale, int causal, Sparse sp, int kvlen,
-    int qoff) {
-  static_assert(D <= 128, "pipelined forward: head dims 64 / 128");
-  constexpr bool SPARSE = false;
-  constexpr int NWF = 8;
-  constexpr int KT = pipe_kt<D>(), J = KT / 32;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int ROWB = 2 * D;
-  constexpr int BUF = 2 * KT * ROWB;  // ring slot i: K tile at +0, V tile at +KT*ROWB
-  int* tlist = reinterpret_cast<int*>(smem + 4 * KT * ROWB) + 1;
-  constexpr int QBF = NWF * QW;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-  const int nqb = Sq / QBF;
-  int bh, qb;
-  map_block(nqb, B * H, causal != 0, bh, qb);
-  const int b = bh / H, head = bh - b * H;
-  const int kh = head / (H / Hk);
-  const int q0 = qb * QBF + w * QW;
-  const int qpos = q0 + qoff;
-  const unsigned short* qp = q + b * qs.b + head * qs.h;
-  const unsigned short* kp = k + b * ks.b + kh * ks.h;
-  const unsigned short* vp = v + b * vs.b + kh * vs.h;
-  const float c = scale * LOG2E;
-
-  bf16x8 qf[D / 16];
-#pragma unroll
-  for (int t = 0; t < D / 16; ++t)
-    qf[t] = *reinterpret_cast<const bf16x8*>(qp + (int64_t)(q0 + r) * qs.s + 16 * t + 8 * h);
-  f32x16 oacc[D / 32];
-#pragma unroll
-  for (int t = 0; t < D / 32; ++t) oacc[t] = zero16();
-  SoftState st{-INFINITY, 0.f, 1.f, false};
-  float l = 0.f;
-
-  const int kend = causal ? min(Sk, (qb + 1) * QBF + qoff) : Sk;
-  const int nkt = (max(kend, 0) + KT - 1) / KT;
-  const int ntiles = SPARSE ? build_tile_list(sp, head, 0, nkt, KT, qb * QBF, qb * QBF + QBF, true, tlist) : nkt;
-  auto tile_at = [&](int i) { return SPARSE ? tlist[i] : i; };
-  auto active = [&](int i) { return !causal || tile_at(i) * KT <= qpos + QW - 1; };
-  auto diag_of = [&](int kb) { return causal && (kb + KT - 1 > qpos); };
-  auto tail_of = [&](int kb) { return kb + KT > kvlen; };
-  const uint8_t* lrow = SPARSE ? sp.layout + ((int64_t)head * sp.nb + (q0 + r) / sp.blk) * sp.nb : nullptr;
-  const int blk = SPARSE ? sp.blk : 1;
-
-  PipeOffs<D> of;
-  of.init(lane);
-  f32x16 s0[J], s1[J];
-  // K/V tiles go straight to LDS (global_load_lds, swizzle on the source side): a ring part is
-  // free a whole iteration before it is refilled, so the loads fly under a full tile of compute
-  // with no staging registers (the two live score tiles need them).
-  // prologue: K(0) -> slot 0; scores + max of tile 0 while K(1) -> slot 1 and V(0) -> slot 0 land
-  if (ntiles > 0) tile_glds<KT, D, NWF>(kp, ks.s, tile_at(0) * KT, smem);
-  vm_wait_all();
-  __syncthreads();
-  if (ntiles > 1) tile_glds<KT, D, NWF>(kp, ks.s, tile_at(1) * KT, smem + BUF);
-  if (ntiles > 0) tile_glds<KT, D, NWF>(vp, vs.s, tile_at(0) * KT, smem + KT * ROWB);
-  if (ntiles > 0 && active(0)) {
-    const int kb = tile_at(0) * KT;
-    fwd_scores<D, J>(smem, qf, s0, of);
-    fwd_tile_max<true, J>(s0, st, c, kb, qpos, r, h, diag_of(kb), tail_of(kb), kvlen, lrow, blk);
-  }
-  vm_wait_all();
-  __syncthreads();
-
-  // iteration t: masked scores + state of tile t in `sc` / st; K(t+1) in slot (t+1)&1, V(t) in
-  // slot t&1; K(t+2) and V(t+1) load into the ring parts iteration t - 1 finished with
-  auto body = [&](auto parity, int t, f32x16 (&sc)[J], f32x16 (&sn)[J]) {
-    constexpr int P = decltype(parity)::value;  // t & 1: the ring slots are compile-time offsets
-    const bool k2 = t + 2 < ntiles, v1 = t + 1 < ntiles;
-    if (k2) tile_glds<KT, D, NWF>(kp, ks.s, tile_at(t + 2) * KT, smem + P * BUF);
-    if (v1) tile_glds<KT, D, NWF>(vp, vs.s, tile_at(t + 1) * KT, smem + (P ^ 1) * BUF + KT * ROWB);
-    if (active(t)) {
-      const char* kn = smem + (P ^ 1) * BUF;
-      const char* vt = smem + P * BUF + KT * ROWB;
-      const bool next = v1 && active(t + 1);
-      const int kbn = next ? tile_at(t + 1) * KT : 0;
-      const bool diagn = next && diag_of(kbn), tailn = next && tail_of(kbn);
-      if (!next)
-        fwd_pipe_step<false, false, D, J>(kn, vt, qf, sc, sn, oacc, st, l, c, 0, qpos, r, h, of, false, false, kvlen,
-                                       nullptr, 1);
-      else if (SPARSE || diagn || tailn)
-        fwd_pipe_step<true, true, D, J>(kn, vt, qf, sc, sn, oacc, st, l, c, kbn, qpos, r, h, of, diagn, tailn, kvlen,
-                                     lrow, blk);
-      else
-        fwd_pipe_step<false, true, D, J>(kn, vt, qf, sc, sn, oacc, st, l, c, kbn, qpos, r, h, of, false, false, kvlen,
-                                      nullptr, 1);
-    }
-    vm_wait_all();
-    __syncthreads();
-  };
-  for (int t = 0; t < ntiles; t += 2) {
-    body(std::integral_constant<int, 0>{}, t, s0, s1);
-    if (t + 1 < ntiles) body(std::integral_constant<int, 1>{}, t + 1, s1, s0);
-  }
-  const float m = st.m;
-
-  const float lt = l + __shfl_xor(l, 32, 64);
-  const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  unsigned short* op = o + b * os.b + head * os.h + (int64_t)(q0 + r) * os.s;
-#pragma unroll
-  for (int dt = 0; dt < D / 32; ++dt)
-#pragma unroll
-    for (int rg = 0; rg < 4; ++rg) {
-      u16x4 pk;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) pk[e] = f32_to_bf16(oacc[dt][4 * rg + e] * inv);
-      *reinterpret_cast<u16x4*>(op + 32 * dt + 8 * rg + 4 * h) = pk;
-    }
-  if (h == 0) lse[((int64_t)b * H + head) * Sq + q0 + r] = lt > 0.f ? (m + log2f(lt)) * LN2 : INFINITY;
-}
-
-// =============================================================================================
 // Backward pre-pass: delta[b, h, s] = sum_d dO * O  (fp32); D/8 threads per row
 // =============================================================================================
 template <int D>
@@ -1113,23 +820,13 @@ static fa::Sparse sparse_of(const c10::optional<at::Tensor>& layout, int64_t blo
 
 constexpr size_t kListBytes = (1 + 2048) * sizeof(int) + 16;  // tile list + scratch flags (sparse mode)
 
-// SXE_FA_FWD_WAVES=4 forces the 4-wave forward (A/B measurements)
-static bool fwd_narrow() {
-  static const bool v = [] {
-    const char* e = std::getenv("SXE_FA_FWD_WAVES");
-    return e != nullptr && std::atoi(e) == 4;
-  }();
-  return v;
+// Kernel-variant knob, read on every call (not cached at static init) so a test or an A/B run can
+// switch variants inside one process: SXE_FA_FWD_WAVES=4 forces the 4-wave forward.
+static int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return (e != nullptr && *e != 0) ? std::atoi(e) : dflt;
 }
-
-// SXE_FA_FWD_PIPE=1 selects the software-pipelined 8-wave forward (A/B against the one-phase one)
-static bool fwd_pipe() {
-  static const bool v = [] {
-    const char* e = std::getenv("SXE_FA_FWD_PIPE");
-    return e != nullptr && std::atoi(e) != 0;
-  }();
-  return v;
-}
+static bool fwd_narrow() { return env_int("SXE_FA_FWD_WAVES", 8) == 4; }
 
 template <typename F>
 static void set_lds_limit(F* f, size_t bytes) {
@@ -1155,7 +852,6 @@ static std::vector<at::Tensor> fwd_impl_d(at::Tensor q, at::Tensor k, at::Tensor
     if constexpr (D < 256) {
       set_lds_limit(&fa::fwd_kernel<false, 8, D>, mx);
       set_lds_limit(&fa::fwd_kernel<true, 8, D>, mx);
-      set_lds_limit(&fa::fwd_pipe_kernel<D>, mx);
     }
     attr = true;
   }
@@ -1171,11 +867,6 @@ static std::vector<at::Tensor> fwd_impl_d(at::Tensor q, at::Tensor k, at::Tensor
                        Sq, Sk, (float)scale, causal ? 1 : 0, sp, kvlen, qoff);
   };
   if constexpr (D < 256) {
-    if (wide && fwd_pipe() && !sp.layout) {
-      launch(fa::fwd_pipe_kernel<D>, 8);
-      SXE_LAUNCH_CHECK();
-      return {o, lse};
-    }
     if (wide) {
       sp.layout ? launch(fa::fwd_kernel<true, 8, D>, 8) : launch(fa::fwd_kernel<false, 8, D>, 8);
       SXE_LAUNCH_CHECK();

@@ -196,3 +196,24 @@ def test_flash_cross_and_prefix_lengths(causal, Sq, Sk, D, monkeypatch):
     ol, lse = A.attention_with_lse(q.detach(), k.detach(), v.detach(), causal=causal)
     _, lse2 = A.reference_attention(q2.detach(), k2.detach(), v2.detach(), causal=causal, return_lse=True)
     assert (lse - lse2).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("waves", [4, 8])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("B,Sq,Sk,H,Hk,D", [(2, 256, 256, 4, 4, 128), (1, 512, 512, 8, 2, 128),
+                                            (2, 256, 256, 4, 2, 64), (1, 256, 768, 4, 1, 128),
+                                            (1, 512, 1024, 4, 2, 64), (1, 1024, 1024, 2, 2, 128)])
+def test_flash_fwd_variants(waves, causal, B, Sq, Sk, H, Hk, D, monkeypatch):
+    """Both forward variants (4 and 8 waves per workgroup, SXE_FA_FWD_WAVES, read per call) against
+    the fp32 oracle: head dims 64 / 128, causal / full, q_len != kv_len, GQA."""
+    A = _no_sdpa(monkeypatch)
+    monkeypatch.setenv("SXE_FA_FWD_WAVES", str(waves))
+    torch.manual_seed(2)
+    q = torch.randn(B, Sq, H, D, device="cuda", dtype=torch.bfloat16)
+    k = torch.randn(B, Sk, Hk, D, device="cuda", dtype=torch.bfloat16)
+    v = torch.randn(B, Sk, Hk, D, device="cuda", dtype=torch.bfloat16)
+    assert A.hip_supported(q, k, v)
+    o, lse = A.attention_with_lse(q, k, v, causal=causal)
+    o2, lse2 = A.reference_attention(q.float(), k.float(), v.float(), causal=causal, return_lse=True)
+    assert _rel(o, o2) < 1e-2
+    assert (lse - lse2).abs().max().item() < 2e-2
