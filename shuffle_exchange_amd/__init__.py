@@ -42,6 +42,7 @@ def initialize(args=None, model=None, optimizer=None, model_parameters=None, tra
     if config is None and args is not None:
         config = getattr(args, "deepspeed_config", None) or getattr(args, "sxe_config", None)
     init_distributed(distributed_port=distributed_port, dist_init_required=dist_init_required)
+    config, mesh_device = _mesh_from_args(config, mesh_param)
     pp = getattr(model, "is_pipeline_module", False)
     if pp:
         from .runtime.pipe.engine import PipelineEngine
@@ -60,8 +61,33 @@ def initialize(args=None, model=None, optimizer=None, model_parameters=None, tra
         engine = cls(args=args, model=model, optimizer=optimizer, model_parameters=model_parameters,
                            training_data=training_data, lr_scheduler=lr_scheduler, mpu=mpu,
                            dist_init_required=dist_init_required, collate_fn=collate_fn, config=config,
-                           rings=rings, shuffle_step=shuffle_step, method=method, slice_count=slice_count)
+                           rings=rings, shuffle_step=shuffle_step, method=method, slice_count=slice_count,
+                           mesh_device=mesh_device)
     return engine, engine.optimizer, engine.training_dataloader, engine.lr_scheduler
+
+
+def _mesh_from_args(config, mesh_param):
+    """``mesh_param=(dp, sp)`` -- or both ``data_parallel_size`` and ``sequence_parallel_size`` in the
+    config -- builds a 2-D ("data_parallel", "sequence_parallel") DeviceMesh over the world and sets
+    the engine's sequence-parallel size from it (reference deepspeed/__init__.py:157-166)."""
+    from .runtime.config import _load_raw
+    raw = _load_raw(config) if config is not None else {}
+    if mesh_param is not None:
+        dp, sp = (int(x) for x in mesh_param)
+    elif "data_parallel_size" in raw and "sequence_parallel_size" in raw:
+        dp, sp = int(raw["data_parallel_size"]), int(raw["sequence_parallel_size"])
+    else:
+        return config, None
+    world = comm.get_world_size()
+    if dp * sp != world:
+        raise ValueError(f"mesh (dp={dp}, sp={sp}) does not cover the world of {world} ranks")
+    if raw.get("sequence_parallel_size", sp) != sp:
+        raise ValueError(f"mesh_param sp={sp} contradicts sequence_parallel_size={raw['sequence_parallel_size']}")
+    raw["sequence_parallel_size"] = sp
+    raw["data_parallel_size"] = dp
+    raw.pop("mesh_param", None)
+    logger.info(f"mesh: data_parallel={dp} x sequence_parallel={sp}")
+    return raw, comm.initialize_mesh_device((dp, sp), ("data_parallel", "sequence_parallel"))
 
 
 def add_config_arguments(parser):

@@ -88,8 +88,13 @@ def init_distributed(dist_backend=None, auto_mpi_discovery=True, distributed_por
     env.setdefault("RANK", "0")
     env.setdefault("WORLD_SIZE", "1")
     env.setdefault("LOCAL_RANK", "0")
+    # a world of one with no rendezvous given (a single-GPU job, a test process) needs no TCP store:
+    # an in-process HashStore means two such processes on one machine never meet at a shared
+    # default port (a collision there hangs both in the store handshake)
+    solo = (int(env["WORLD_SIZE"]) == 1 and init_method is None and "MASTER_PORT" not in env)
     env.setdefault("MASTER_ADDR", "127.0.0.1")
-    env.setdefault("MASTER_PORT", str(distributed_port))
+    if not solo:
+        env.setdefault("MASTER_PORT", str(distributed_port))
     # SXE_DIST_BACKEND=gloo: multi-rank rehearsals on a single GPU (RCCL needs one GPU per rank)
     backend = dist_backend or env.get("SXE_DIST_BACKEND") or get_accelerator().communication_backend_name()
     if timeout is None:
@@ -100,8 +105,12 @@ def init_distributed(dist_backend=None, auto_mpi_discovery=True, distributed_por
         torch.cuda.set_device(local_rank)
         # binding the device lets RCCL split sub-communicators from the world comm (cheap new_group)
         kw["device_id"] = torch.device("cuda", local_rank)
-    tdist.init_process_group(backend=backend, init_method=init_method, timeout=timeout,
-                             rank=int(env["RANK"]), world_size=int(env["WORLD_SIZE"]), **kw)
+    if solo:
+        kw["store"] = tdist.HashStore()
+    else:
+        kw["init_method"] = init_method
+    tdist.init_process_group(backend=backend, timeout=timeout, rank=int(env["RANK"]),
+                             world_size=int(env["WORLD_SIZE"]), **kw)
     _State.initialized = True
     _State.backend = backend
     if verbose:

@@ -77,6 +77,25 @@ def byte_range(total, rank, world):
     return lo, lo + base + (1 if rank < rem else 0)
 
 
+def _all_gather_i64(vals, world, group):
+    mine = torch.tensor(vals, dtype=torch.int64)
+    if dist.get_backend(group) == "gloo":
+        parts = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine, group=group)
+        return parts
+    m = mine.cuda()
+    pc = [torch.zeros_like(m) for _ in range(world)]
+    dist.all_gather(pc, m, group=group)
+    return [t.cpu() for t in pc]
+
+
+def _rank0_write(state, path, rank, group):
+    if rank == 0:
+        torch.save(state, path)
+    dist.barrier(group=group)
+    return os.path.getsize(path) if rank == 0 else 0
+
+
 def save_data_parallel(state, path, group=None):
     """Every rank of ``group`` calls this with the same ``state``; returns the bytes this rank wrote."""
     world = dist.get_world_size(group)
@@ -86,28 +105,23 @@ def save_data_parallel(state, path, group=None):
         return os.path.getsize(path)
     sink = _CountingSink()
     torch.save(state, sink)
-    mine = torch.tensor([sink.n, sink.adler], dtype=torch.int64)
-    parts = [torch.zeros_like(mine) for _ in range(world)]
-    dev_ok = dist.get_backend(group) == "gloo"
-    if dev_ok:
-        dist.all_gather(parts, mine, group=group)
-    else:
-        m = mine.cuda()
-        pc = [torch.zeros_like(m) for _ in range(world)]
-        dist.all_gather(pc, m, group=group)
-        parts = [t.cpu() for t in pc]
+    parts = _all_gather_i64([sink.n, sink.adler], world, group)
     agree = all(torch.equal(p, parts[0]) for p in parts)
     total = int(parts[0][0])
     if not agree:
-        if rank == 0:
-            torch.save(state, path)
-        dist.barrier(group=group)
-        return os.path.getsize(path) if rank == 0 else 0
+        return _rank0_write(state, path, rank, group)
     tmp = path + ".dp"
     if rank == 0:
         with open(tmp, "wb") as f:
             f.truncate(total)
     dist.barrier(group=group)
+    # every writer must see rank 0's file: a group spanning nodes whose checkpoint directory is
+    # node-local would otherwise fail in os.open on the other nodes while their peers wait
+    seen = _all_gather_i64([int(os.path.exists(tmp))], world, group)
+    if not all(int(x[0]) for x in seen):
+        if rank == 0:
+            os.remove(tmp)
+        return _rank0_write(state, path, rank, group)
     lo, hi = byte_range(total, rank, world)
     fd = os.open(tmp, os.O_WRONLY)
     try:

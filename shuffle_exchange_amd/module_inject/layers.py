@@ -138,6 +138,7 @@ def gather_from_tp(x, group):
 
 
 class TensorParallelLinearBase(nn.Module):
+    _sxe_lower_precision_safe = True  # torch_autocast: GEMM weights may communicate in bf16 / fp16
     is_tensor_parallel = True
 
     def __init__(self, weight, bias, group, full_shape, split_dim, layout=None):

@@ -187,17 +187,41 @@ def _transpose16(t):
 
 def _transposed_weight(w):
     global _wt_cache_bytes
-    if not WT_CACHE:
+    if not WT_CACHE or not isinstance(w, torch.nn.Parameter):
         return _transpose16(w)
     hit = _wt_cache.get(id(w))
-    if hit is not None and hit[0]() is w and hit[1].shape == w.shape[::-1]:
+    # a weight rebound to other storage (ZeRO-3 gather into a new buffer) or bumped by an in-place
+    # write through the Parameter itself misses instead of returning a stale transpose; writers that
+    # go through other views of a flat buffer call invalidate_transposed_weights()
+    if (hit is not None and hit[0]() is w and hit[1].shape == w.shape[::-1] and hit[2] == w.data_ptr()
+            and hit[3] == w._version):
         return hit[1]
+    if hit is not None:
+        _wt_cache.pop(id(w))
+        _wt_cache_bytes -= hit[1].numel() * hit[1].element_size()
     wt = _transpose16(w)
     nbytes = wt.numel() * wt.element_size()
     if _wt_cache_bytes + nbytes <= WT_CACHE_MAX_BYTES:
-        _wt_cache[id(w)] = (weakref.ref(w), wt)
+        _wt_cache[id(w)] = (weakref.ref(w), wt, w.data_ptr(), w._version)
         _wt_cache_bytes += nbytes
     return wt
+
+
+def transposed_weight_cache_bytes():
+    return _wt_cache_bytes
+
+
+def configure_transposed_weight_cache(enabled, free_bytes=None):
+    """Turn the cache on / off; with ``free_bytes`` (free HBM after the engine is built) the cap is
+    at most a quarter of it, so the cache never takes memory a configuration needs to fit."""
+    global WT_CACHE, WT_CACHE_MAX_BYTES
+    WT_CACHE = bool(enabled)
+    cap = int(float(os.environ.get("SXE_WT_CACHE_GB", "20")) * 2**30)
+    if free_bytes is not None:
+        cap = min(cap, int(free_bytes) // 4)
+    WT_CACHE_MAX_BYTES = cap
+    invalidate_transposed_weights()
+    return cap
 
 
 def data_grad(gy, w):
@@ -256,9 +280,26 @@ def write_weight_grad(w, gy2, x2):
     return True
 
 
+def _autocast_dtype(x):
+    """The torch.autocast compute dtype active for ``x``'s device, or None."""
+    dev = x.device.type
+    if dev in ("cuda", "cpu") and torch.is_autocast_enabled(dev):
+        return torch.get_autocast_dtype(dev)
+    return None
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
+        ctx.param = None
+        ac = _autocast_dtype(x)
+        if ac is not None and weight.dtype != ac:
+            # torch_autocast training (runtime/torch_autocast.py): fp32 master-precision parameters,
+            # GEMMs in the autocast dtype. The fp32 Parameter keeps receiving its gradient through
+            # the optimizer's direct weight-grad target; the bf16 copies are what backward reads.
+            ctx.param = weight
+            x, weight = x.to(ac), weight.to(ac)
+            bias = bias.to(ac) if bias is not None else None
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         return F.linear(x, weight, bias)
@@ -266,13 +307,16 @@ class _Linear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
+        wp = ctx.param if ctx.param is not None else w
+        if gy.dtype != x.dtype:
+            gy = gy.to(x.dtype)
         gy2 = gy.reshape(-1, gy.shape[-1])
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = data_grad(gy, w)
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
-            if not write_weight_grad(w, gy2, x2):
+            if not write_weight_grad(wp, gy2, x2):
                 dw = gy2.t() @ x2
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = gy2.sum(0)
@@ -299,6 +343,8 @@ class Linear(torch.nn.Linear):
     ``init_std``: initialise the weight N(0, init_std) (bias zero) inside the constructor, i.e.
     on the whole tensor before a partitioning ``zero.Init`` cuts it -- the initial model then
     depends only on the seed, not on the number of ranks."""
+
+    _sxe_lower_precision_safe = True  # torch_autocast: GEMM weights may communicate in bf16 / fp16
 
     def __init__(self, in_features, out_features, bias=True, device=None, dtype=None, init_std=None):
         super().__init__(in_features, out_features, bias=bias, device=device, dtype=dtype)

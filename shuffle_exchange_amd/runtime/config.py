@@ -274,6 +274,13 @@ class ElasticityConfig(ConfigModel):
     model_parallel_size: int = 1
 
 
+class TorchAutocastConfig(ConfigModel):
+    """Reference runtime/constants.py:217-226 ``torch_autocast`` block (runtime/torch_autocast.py)."""
+    enabled: bool = False
+    dtype: Optional[str] = None  # bf16 (default) or fp16
+    lower_precision_safe_modules: Optional[List[str]] = None
+
+
 class MoEConfig(ConfigModel):
     ep_size: int = 1
     drop_tokens: bool = True
@@ -325,6 +332,7 @@ class SXEConfigModel(ConfigModel):
     hybrid_engine: HybridEngineConfig = Field(default_factory=HybridEngineConfig)
     elasticity: ElasticityConfig = Field(default_factory=ElasticityConfig)
     moe: MoEConfig = Field(default_factory=MoEConfig)
+    torch_autocast: TorchAutocastConfig = Field(default_factory=TorchAutocastConfig)
     amp: Dict[str, Any] = Field(default_factory=dict)
     compile: Dict[str, Any] = Field(default_factory=dict)
     strict_config: bool = False  # new: unknown keys raise instead of warning
@@ -335,7 +343,7 @@ class SXEConfigModel(ConfigModel):
 RAW_ROOT_KEYS = {
     "data_efficiency", "curriculum_learning", "progressive_layer_drop", "quantize_training", "autotuning",
     "compression_training", "sparse_attention", "eigenvalue", "weight_quantization", "dataloader_drop_last",
-    "bfloat16", "torch_autocast", "nebula", "monitor_config", "data_sampling", "zero_enabled", "deepcompile",
+    "bfloat16", "nebula", "monitor_config", "data_sampling", "zero_enabled", "deepcompile",
     "timers", "use_node_local_storage", "pipeline_stage", "inference", "mesh_param",
 }
 
@@ -405,6 +413,10 @@ class SXEConfig:
         if "bfloat16" in raw and "bf16" not in raw:  # reference alias (runtime/constants.py BFLOAT16_OLD)
             self.model.bf16 = BF16Config(**raw["bfloat16"])
         self.bfloat16_enabled = m.bf16.enabled
+        if "use_node_local_storage" in raw and "use_node_local_storage" not in raw.get("checkpoint", {}):
+            # legacy root-level spelling of checkpoint.use_node_local_storage
+            self.model.checkpoint.use_node_local_storage = bool(raw["use_node_local_storage"])
+        self.torch_autocast_enabled = m.torch_autocast.enabled
         self.unknown_keys = self._check_unknown_keys()
         self.grad_accum_dtype = self._grad_accum_dtype()
         self.ignored_knobs = self._check_ignored_knobs()
@@ -473,6 +485,13 @@ class SXEConfig:
         if self.model.sparse_gradients and zc.stage > 0:
             out.append(("sparse_gradients", "under ZeRO stages 1-3 embedding gradients are reduced densely inside "
                                             "the flat units (same numerics); the sparse all-gather runs at stage 0"))
+        neb = self._param_dict.get("nebula")
+        if isinstance(neb, dict) and neb.get("enabled"):
+            out.append(("nebula", "the Azure Nebula checkpoint service is not available; checkpoints are written by "
+                                  "the torch / fast / decoupled engines (checkpoint.writer, checkpoint.async_save)"))
+        if self._param_dict.get("mesh_param") is not None:
+            out.append(("mesh_param", "a config key has no effect: pass mesh_param=(dp, sp) to initialize(), or set "
+                                      "data_parallel_size and sequence_parallel_size"))
         for k, why in out:
             logger.warning(f"config: '{k}' is accepted but has no effect: {why}")
         return out

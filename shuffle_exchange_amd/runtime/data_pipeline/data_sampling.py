@@ -217,7 +217,8 @@ class CurriculumDataSampler(torch.utils.data.Sampler):
     laid out [gas, dp, micro]: this rank's indices come out as ``gas`` consecutive micro-batches."""
 
     def __init__(self, metric_values, scheduler, global_batch_size, dp_rank=0, dp_size=1, seed=1234,
-                 total_steps=None, gradient_accumulation_steps=1):
+                 total_steps=None, gradient_accumulation_steps=1, metric_name=None):
+        self.metric_name = metric_name
         self.metric = np.asarray(metric_values)
         self.order = np.argsort(self.metric, kind="stable")
         self.sorted_vals = self.metric[self.order]
@@ -236,6 +237,15 @@ class CurriculumDataSampler(torch.utils.data.Sampler):
 
     def state_dict(self):
         return {"step": self.step, "curriculum": self.sched.get_state()}
+
+    def set_custom_curriculum_learning_schedule(self, schedule_func_dict):
+        """{metric name: fn(global_step) -> difficulty} for metrics whose schedule_type is "custom"
+        (reference data_sampling/data_sampler.py:117)."""
+        fn = schedule_func_dict.get(self.metric_name) if self.metric_name is not None else None
+        if fn is None and len(schedule_func_dict) == 1 and self.metric_name is None:
+            fn = next(iter(schedule_func_dict.values()))
+        if fn is not None:
+            self.sched.set_custom_get_difficulty(fn)
 
     def load_state_dict(self, sd):
         self.step = sd["step"]

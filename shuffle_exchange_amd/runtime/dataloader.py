@@ -39,6 +39,9 @@ class SXEDataLoader:
                                      pin_memory=pin_memory, num_workers=num_workers, drop_last=drop_last)
         self.len = len(self.dataloader)
         self.epoch = 0
+        # engine.set_data_post_process_func (reference runtime/dataloader.py:100,120): called on every
+        # batch with the sampler's state (the curriculum difficulty) before the batch is returned
+        self.post_process_func = None
 
     def __len__(self):
         return self.len
@@ -47,7 +50,15 @@ class SXEDataLoader:
         if hasattr(self.data_sampler, "set_epoch"):
             self.data_sampler.set_epoch(self.epoch)
         self.epoch += 1
-        return iter(self.dataloader)
+        it = iter(self.dataloader)
+        if self.post_process_func is None:
+            return it
+        return self._post_processed(it)
+
+    def _post_processed(self, it):
+        for batch in it:
+            state = self.data_sampler.state_dict() if hasattr(self.data_sampler, "state_dict") else {}
+            yield self.post_process_func(batch, state)
 
 
 DeepSpeedDataLoader = SXEDataLoader

@@ -139,11 +139,14 @@ class SXEEngine(nn.Module):
         super().__init__()
         self.client_optimizer = optimizer
         self.client_lr_scheduler = lr_scheduler
+        self.mesh_device = mesh_device  # initialize(mesh_param=(dp, sp)): ("data_parallel", "sequence_parallel")
         self.collate_fn = collate_fn
         self.mpu = mpu
         self.global_steps = 0
         self.global_samples = 0
         self.micro_steps = 0
+        self._gas_base = 0  # micro_steps at the start of the current accumulation window
+        self._step_applied = False
         self.skipped_steps = 0
         self.gradient_average = True
         self._in_no_sync = False
@@ -188,14 +191,20 @@ class SXEEngine(nn.Module):
         self.optimizer = None
         self.basic_optimizer = None
         self.lr_scheduler = None
+        # torch_autocast (runtime/torch_autocast.py): mark the lower-precision-safe parameters before the
+        # optimizer cuts its flat units, so their gradients travel in the autocast dtype
+        self._autocast_dtype = None
+        ta = cfg.model.torch_autocast
+        if ta.enabled:
+            from . import torch_autocast as _ta
+            self._autocast_dtype = _ta.parse_dtype(ta.dtype)
+            _ta.init_autocast_params(self, self._autocast_dtype, ta.lower_precision_safe_modules)
         if model_parameters is None:
             model_parameters = [p for p in model.parameters() if p.requires_grad]
         if optimizer is not None or cfg.optimizer_name is not None:
             self._configure_optimizer(optimizer, model_parameters)
             self._configure_lr_scheduler(lr_scheduler)
-        # transposed weights stay valid across the micro-steps of one optimizer step (ops/linear.py)
-        _linear_ops.WT_CACHE = self.gradient_accumulation_steps() > 1
-        _linear_ops.invalidate_transposed_weights()
+        self._configure_wt_cache()
         ckpt = cfg.model.checkpoint
         wtype = str((ckpt.writer or {}).get("type", "")).lower()
         if wtype == "fast":  # reference checkpoint.writer {"type": "fast", "io_buffer_size": ...}
@@ -213,6 +222,21 @@ class SXEEngine(nn.Module):
             logger.debug(f"monitor disabled: {e}")
         self._auto_se_steps = 0
         self._configure_training_aux()
+
+    def _configure_wt_cache(self):
+        """Transposed weights stay valid across the micro-steps of one optimizer step (ops/linear.py):
+        on with gradient accumulation, off when ZeRO-3 offloads parameters (the cache would hold
+        what the offload frees), capped at a quarter of the HBM still free once the engine is built."""
+        zc = self._config.zero_config
+        offp = zc.offload_param is not None and zc.offload_param.device in ("cpu", "nvme")
+        on = self.gradient_accumulation_steps() > 1 and not (self.zero_optimization_stage() == 3 and offp)
+        free = None
+        if on and self.device.type == "cuda":
+            free = torch.cuda.mem_get_info(self.device)[0]
+        cap = _linear_ops.configure_transposed_weight_cache(on, free)
+        if on:
+            log_dist(f"transposed-weight cache on (gradient_accumulation_steps="
+                     f"{self.gradient_accumulation_steps()}), cap {cap / 2**30:.1f} GiB", ranks=[0])
 
     def _configure_data_efficiency(self):
         raw = self._config._param_dict
@@ -293,7 +317,8 @@ class SXEEngine(nn.Module):
         sched = CurriculumScheduler(mc)
         return CurriculumDataSampler(vals, sched, self.train_batch_size(), dp_rank=groups.get_data_parallel_rank(),
                                      dp_size=groups.get_data_parallel_world_size(), seed=self._de.get("seed", 1234),
-                                     gradient_accumulation_steps=self.gradient_accumulation_steps())
+                                     gradient_accumulation_steps=self.gradient_accumulation_steps(),
+                                     metric_name=name)
 
     def curriculum_enabled_legacy(self):
         return self.curriculum_scheduler_legacy is not None
@@ -473,7 +498,7 @@ class SXEEngine(nn.Module):
             basic = self._configure_basic_optimizer(model_parameters)
         self.basic_optimizer = basic
         dtype = self.model_dtype()
-        scaler = make_scaler(cfg.model.fp16, dtype)
+        scaler = make_scaler(cfg.model.fp16, torch.float16 if self._autocast_dtype == torch.float16 else dtype)
         stage = cfg.zero_optimization_stage
         zc = cfg.zero_config
         dp_ranks = groups.group_ranks("seq_data")
@@ -606,7 +631,7 @@ class SXEEngine(nn.Module):
 
     # --------------------------------------------------------------------------------- train loop
     def is_gradient_accumulation_boundary(self):
-        return (self.micro_steps + 1) % self.gradient_accumulation_steps() == 0
+        return (self.micro_steps - self._gas_base + 1) % self.gradient_accumulation_steps() == 0
 
     def set_gradient_accumulation_boundary(self, is_boundary):
         self._boundary_override = is_boundary
@@ -635,7 +660,14 @@ class SXEEngine(nn.Module):
             prof.start_profile()
         # the FX graph compiler's module (compile/fx_backend.py) when deepcompile is on at ZeRO 0-2
         mod = self._fx_module if getattr(self, "_fx_module", None) is not None else self.module
-        if self.fp16_enabled() and self._config.model.fp16.auto_cast:
+        if self._autocast_dtype is not None or torch.is_autocast_enabled(self.device.type):
+            from .torch_autocast import validate_nested_autocast
+            validate_nested_autocast(self)
+        if self._autocast_dtype is not None:
+            # reference engine.py:2116-2120: fp32 parameters, autocast compute
+            with torch.autocast(device_type=self.device.type, dtype=self._autocast_dtype):
+                out = mod(*inputs, **kwargs)
+        elif self.fp16_enabled() and self._config.model.fp16.auto_cast:
             with torch.autocast(device_type=self.device.type, dtype=torch.float16):
                 out = mod(*inputs, **kwargs)
         elif getattr(self, "_offload_activations", False) and self.module.training and torch.is_grad_enabled():
@@ -669,7 +701,7 @@ class SXEEngine(nn.Module):
         opt.backward_prologue()
         ld = loss.detach()
         self._loss_acc = ld if self._loss_acc is None else self._loss_acc + ld
-        scaled = loss * opt.loss_scale if self.fp16_enabled() else loss
+        scaled = loss * opt.loss_scale if (self.fp16_enabled() or self._autocast_dtype == torch.float16) else loss
         scaled.backward(retain_graph=retain_graph)
         if not self._in_no_sync:
             opt.reduce_gradients()
@@ -690,8 +722,10 @@ class SXEEngine(nn.Module):
         self.timers(STEP_MICRO_TIMER).start()
         boundary = getattr(self, "_boundary_override", None)
         boundary = self.is_gradient_accumulation_boundary() if boundary is None else boundary
+        self._step_applied = False
         if boundary:
             self._take_model_step(lr_kwargs)
+            self._gas_base = self.micro_steps + 1
         self.micro_steps += 1
         self._boundary_override = None
         self.timers(STEP_MICRO_TIMER).stop()
@@ -827,9 +861,14 @@ class SXEEngine(nn.Module):
             ev.synchronize()
         if float(self._skip_host[0]) != 0.0:
             self._skipped_steps += 1
+            if self._step_applied is None:
+                self._step_applied = False
             log_dist(f"step {self.global_steps}: non-finite gradients, update skipped", ranks=[0])
-        elif self.lr_scheduler is not None:
-            self.lr_scheduler.step(**kw)
+        else:
+            if self._step_applied is None:
+                self._step_applied = True
+            if self.lr_scheduler is not None:
+                self.lr_scheduler.step(**kw)
 
     @property
     def skipped_steps(self):
@@ -851,6 +890,7 @@ class SXEEngine(nn.Module):
         if off:
             self.optimizer.offload_states(include=["optim_states"], non_blocking=True)
         overflow = bool(getattr(self.optimizer, "overflow", False))
+        self._step_applied = not overflow
         if self.progressive_layer_drop is not None:
             self.progressive_layer_drop.update_state(self.global_steps + 1)
         if self.quantizer is not None and self.zero_optimization_stage() < 3:
@@ -866,6 +906,7 @@ class SXEEngine(nn.Module):
             # reads the LR, so the schedule matches the reference's per-step host check
             # (engine.py:2376-2390) without a host sync in step()
             self._defer_skip(skip_t, lr_kwargs)
+            self._step_applied = None  # known once the deferred verdict is read
         elif self.lr_scheduler is not None:
             self.lr_scheduler.step(**(lr_kwargs or {}))
         self.global_steps += 1
@@ -1009,6 +1050,104 @@ class SXEEngine(nn.Module):
     def loss_scale(self):
         return self.optimizer.loss_scale
 
+    def torch_autocast_enabled(self):
+        return self._autocast_dtype is not None
+
+    def torch_autocast_dtype(self):
+        return self._autocast_dtype
+
+    def use_node_local_storage(self):
+        return bool(self._config.model.checkpoint.use_node_local_storage)
+
+    # -------------------------------------------------------------- batch size / step / lifecycle
+    def get_batch_info(self):
+        """(train_batch_size, train_micro_batch_size_per_gpu, gradient_accumulation_steps)
+        (reference engine.py:553)."""
+        return self.train_batch_size(), self.train_micro_batch_size_per_gpu(), self.gradient_accumulation_steps()
+
+    def _check_window_start(self, what):
+        if self.micro_steps != self._gas_base:
+            raise RuntimeError(f"{what}: call it between optimizer steps, not inside a gradient accumulation window "
+                               f"({self.micro_steps - self._gas_base} micro-steps of the current window done)")
+
+    def set_train_batch_size(self, train_batch_size):
+        """Change the global batch by changing the number of micro-batches per optimizer step; the
+        micro-batch size stays (reference engine.py:569, used by batch-size ramp-up). Applies from the
+        next accumulation window."""
+        self._check_window_start("set_train_batch_size")
+        mb, dp = self.train_micro_batch_size_per_gpu(), self.dp_world_size
+        if train_batch_size % (mb * dp) != 0:
+            raise ValueError(f"train_batch_size {train_batch_size} must be divisible by micro_batch {mb} x "
+                             f"data-parallel {dp}")
+        self._config.train_batch_size = int(train_batch_size)
+        self._config.gradient_accumulation_steps = int(train_batch_size // (mb * dp))
+        self._batch_changed()
+
+    def set_train_micro_batch_size(self, micro_batch_size):
+        """Change the micro-batch size, keeping gradient_accumulation_steps (reference engine.py:587).
+        The caller feeds micro-batches of the new size."""
+        self._check_window_start("set_train_micro_batch_size")
+        gas = self.gradient_accumulation_steps()
+        self._config.train_micro_batch_size_per_gpu = int(micro_batch_size)
+        self._config.train_batch_size = int(micro_batch_size) * gas * self.dp_world_size
+        self._batch_changed()
+
+    def _batch_changed(self):
+        self.tput_timer.batch_size = self.train_batch_size()
+        self._configure_wt_cache()
+        cs = getattr(self, "curriculum_sampler", None)
+        if cs is not None:
+            cs.gbs = self.train_batch_size()
+            cs.gas = self.gradient_accumulation_steps()
+
+    def was_step_applied(self):
+        """True when the latest ``step()`` updated the parameters: it closed an accumulation window and
+        the gradients were finite (reference engine.py:1906). With bf16 the non-finite verdict stays on
+        the device until read; asking for it here reads it (one host sync)."""
+        if self._step_applied is None:
+            self._resolve_skip()
+        return bool(self._step_applied)
+
+    def set_data_post_process_func(self, post_process_func):
+        """fn(batch, sampler_state) -> batch, applied by the training dataloader to every batch
+        (reference engine.py:598)."""
+        if self.training_dataloader is not None:
+            self.training_dataloader.post_process_func = post_process_func
+
+    def set_custom_curriculum_learning_schedule(self, schedule_func_dict):
+        """{metric: fn(global_step) -> difficulty} for "custom" curriculum schedules (reference
+        engine.py:602)."""
+        cs = getattr(self, "curriculum_sampler", None)
+        if cs is not None and self.curriculum_learning_enabled():
+            cs.set_custom_curriculum_learning_schedule(schedule_func_dict)
+        elif self.curriculum_scheduler_legacy is not None and len(schedule_func_dict) == 1:
+            self.curriculum_scheduler_legacy.set_custom_get_difficulty(next(iter(schedule_func_dict.values())))
+
+    def empty_partition_cache(self):
+        """Release every gathered (non-persistent) ZeRO-3 parameter buffer and return the freed HBM to
+        the device (reference engine.py:3961)."""
+        opt = self.optimizer
+        if opt is not None and hasattr(opt, "empty_partition_cache"):
+            opt.empty_partition_cache()
+        _linear_ops.invalidate_transposed_weights()
+        import gc
+        gc.collect()
+        get_accelerator().empty_cache()
+
+    def destroy(self):
+        """Release what the engine holds beyond Python references (reference engine.py:521): the
+        optimizer's gradient / module hooks and in-flight exchanges, captured HIP graphs, pending
+        decoupled checkpoint writes and the transposed-weight cache. The engine is unusable after."""
+        opt = self.optimizer
+        if opt is not None and hasattr(opt, "destroy"):
+            opt.destroy()
+        ce = getattr(self, "checkpoint_engine", None)
+        if ce is not None:
+            ce.wait()
+        self._fwd_graphs = None
+        _linear_ops.invalidate_transposed_weights()
+        self._destroyed = True
+
     # ---- Shuffle-exchange user hooks (reference stage_1_and_2.py:692-734) ----------------------
     def shuffle_exchange(self):
         if hasattr(self.optimizer, "shuffle_exchange"):
@@ -1017,6 +1156,7 @@ class SXEEngine(nn.Module):
     def synchronization(self):
         if hasattr(self.optimizer, "synchronization"):
             self.optimizer.synchronization()
+            _linear_ops.invalidate_transposed_weights()  # the averaged bit16 weights were rewritten
 
     def reset_rings(self, rings):
         if hasattr(self.optimizer, "reset_rings"):
@@ -1100,20 +1240,50 @@ class SXEEngine(nn.Module):
             self.checkpoint_engine.save(esd, self._expert_ckpt_name(d, layer_id, gid, m.expert_tp_rank))
 
     def _load_expert_state(self, d):
-        """This rank's local experts from the per-expert files (global -> local ids; reference
-        engine.py:2840-2895 load_moe_state_dict)."""
+        """This rank's local experts from the per-expert files (global -> local ids)."""
+        return SXEEngine._load_expert_files(self.module, d, self.checkpoint_engine)
+
+    @staticmethod
+    def load_moe_state_dict(checkpoint_path, tag, state_dict, old_moe_load=False, model=None, mpu=None,
+                            num_experts=1, checkpoint_engine=None):
+        """Add this rank's local experts of ``model`` (read from the per-expert files of checkpoint
+        ``checkpoint_path/tag``, global expert ids mapped to local ones) to ``state_dict`` (reference
+        engine.py:2838-2895). ``old_moe_load``: the layer-less ``expert_<id>_mp_rank_XX`` files of
+        the oldest format, one expert group."""
+        ce = checkpoint_engine if checkpoint_engine is not None else TorchCheckpointEngine()
+        d = os.path.join(checkpoint_path, str(tag)) if tag is not None else checkpoint_path
+        if not old_moe_load:
+            state_dict.update(SXEEngine._load_expert_files(model, d, ce))
+            return state_dict
+        from ..moe.layer import MoE
+        moe = [(n, m) for n, m in model.named_modules() if isinstance(m, MoE)]
+        m0 = moe[0][1]
+        ep_rank = groups.get_expert_parallel_rank(m0.expert_group_name)
+        nle = max(num_experts if isinstance(num_experts, (list, tuple)) else [num_experts]) // \
+            groups.get_expert_parallel_world_size(m0.expert_group_name)
+        mp = groups.get_tensor_model_parallel_rank() if mpu is None else mpu.get_model_parallel_rank()
+        tag_ = "deepspeed_moe.experts.deepspeed_experts."
+        for i in range(nle):
+            gid = ep_rank * nle + i
+            esd = ce.load(os.path.join(d, f"expert_{gid}_mp_rank_{mp:02d}_model_states.pt"), map_location="cpu")
+            for k, v in esd.items():
+                state_dict[k.replace(f"{tag_}{gid}.", f"{tag_}{i}.")] = v
+        return state_dict
+
+    @staticmethod
+    def _load_expert_files(model, d, ce):
         from ..moe.experts import GroupedSwiGLUExperts
+        from ..moe.layer import MoE
         out = {}
-        for layer_id, (n_module, m) in enumerate(self._moe_layers()):
-            pre = self._expert_key_prefix(n_module)
+        for layer_id, (n_module, m) in enumerate((n, x) for n, x in model.named_modules() if isinstance(x, MoE)):
+            pre = SXEEngine._expert_key_prefix(n_module)
             ep_rank = groups.get_expert_parallel_rank(m.expert_group_name)
             nle = m.num_local_experts
             grouped = isinstance(m.deepspeed_moe.experts, GroupedSwiGLUExperts)
             stacks = {}
             for i in range(nle):
                 gid = ep_rank * nle + i
-                esd = self.checkpoint_engine.load(self._expert_ckpt_name(d, layer_id, gid, m.expert_tp_rank),
-                                                  map_location="cpu")
+                esd = ce.load(SXEEngine._expert_ckpt_name(d, layer_id, gid, m.expert_tp_rank), map_location="cpu")
                 gpre = f"{pre}deepspeed_experts.{gid}."
                 for k, v in esd.items():
                     tail = k[len(gpre):]
@@ -1149,19 +1319,68 @@ class SXEEngine(nn.Module):
             sd = {k: v for k, v in sd.items() if k not in names}
         return sd
 
-    def _zero3_consolidated_16bit_state_dict(self):
+    def _zero3_consolidated_16bit_state_dict(self, exclude_frozen_parameters=False, keep=True):
+        """The whole 16-bit model as a host state dict: every fetch group is gathered in turn (a
+        collective: all ranks call this) and copied out, then released -- at most one group's full
+        weights are resident beyond the persistent ones. Tied weights appear under every name (one
+        tensor), frozen (resident, unpartitioned) weights and persistent buffers are included, so the
+        result loads strictly into the unwrapped module (reference engine.py:3830-3905). Ranks called
+        with ``keep=False`` take part in the gathers but keep no host copy (returns None)."""
         opt = self.optimizer
-        sd = {}
-        names = self._param_names()
+        by_param = {}
         for fg in opt.fgroups:
             opt._fetch(fg, wait=True)
-            for u in fg.units:
-                for p in u.params:
-                    sd[names[p]] = p.detach().cpu().clone()
+            if keep:
+                for u in fg.units:
+                    for p in u.params:
+                        by_param[p] = p.detach().cpu().clone()
             opt._release(fg)
-        for n, b in self.module.named_buffers():
-            sd[n] = b.detach().cpu().clone()
+        if not keep:
+            return None
+        sd = {}
+        for n, p in self.module.named_parameters(remove_duplicate=False):
+            if exclude_frozen_parameters and not p.requires_grad:
+                continue
+            t = by_param.get(p)
+            if t is None:  # not held by a ZeRO-3 unit (frozen weights stay resident)
+                t = by_param[p] = p.detach().cpu().clone()
+            sd[n] = t
+        for mname, mod in self.module.named_modules():
+            for bname, b in mod.named_buffers(recurse=False):
+                if b is not None and bname not in mod._non_persistent_buffers_set:
+                    sd[f"{mname}.{bname}" if mname else bname] = b.detach().cpu().clone()
         return sd
+
+    def save_16bit_model(self, save_dir, save_filename="pytorch_model.bin", exclude_frozen_parameters=False):
+        """Write the model's 16-bit weights as one ``torch.save`` state dict that loads into the
+        unwrapped module (reference engine.py:3910-3955; HF Trainer / Accelerate call this to export a
+        ZeRO-3 model). Every rank must call it. Under ZeRO-3 the weights are consolidated only when
+        ``stage3_gather_16bit_weights_on_model_save`` is set (otherwise nothing is written and False is
+        returned, as the reference does). Returns True when the file was written."""
+        path = os.path.join(save_dir, save_filename)
+        # one writer per job, or per node with checkpoint.use_node_local_storage
+        writer = (self.local_rank if self.use_node_local_storage() else dist.get_rank()) == 0
+        if self.zero_optimization_stage() == 3:
+            if not self._config.zero_config.gather_16bit_weights_on_model_save:
+                logger.info(f"not saving {path}: stage3_gather_16bit_weights_on_model_save is False")
+                return False
+            self.optimizer.wait_params()
+            sd = self._zero3_consolidated_16bit_state_dict(exclude_frozen_parameters, keep=writer)
+        else:
+            sd = self.module_state_dict(exclude_frozen_parameters=exclude_frozen_parameters)
+        if writer:
+            os.makedirs(save_dir, exist_ok=True)
+            log_dist(f"saving 16-bit model weights to {path}", ranks=[0])
+            self.checkpoint_engine.save({k: v.detach().cpu() if torch.is_tensor(v) else v for k, v in sd.items()},
+                                        path)
+            self.checkpoint_engine.commit(f"global_step{self.global_steps}")
+            self.checkpoint_engine.wait()
+        dist.barrier()
+        return True
+
+    def save_fp16_model(self, save_dir, save_filename="pytorch_model.bin"):
+        """Old name of ``save_16bit_model`` (reference engine.py:3906)."""
+        return self.save_16bit_model(save_dir, save_filename)
 
     def _shared_params(self):
         """{name of a tied parameter that is not stored separately: name of the parameter holding
@@ -1212,6 +1431,8 @@ class SXEEngine(nn.Module):
             return None
         if self._moe_layers():
             return None  # expert files are written per expert-data-parallel group already
+        if self.use_node_local_storage():
+            return None  # every node writes its own copy
         return groups.get_sequence_data_parallel_group()
 
     def _save_data_parallel(self, state, path, group):
@@ -1231,13 +1452,17 @@ class SXEEngine(nn.Module):
             tag = f"global_step{self.global_steps}"
         tag = str(tag)
         d, model_path, optim_path = self._ckpt_names(save_dir, tag)
-        if self.global_rank == 0:
+        # checkpoint.use_node_local_storage (reference engine.py:1123, 3363): every node keeps a full
+        # checkpoint on its own disk -- the first rank of each node writes the replicated files
+        node_local = self.use_node_local_storage()
+        lead = (self.local_rank if node_local else self.global_rank) == 0
+        if lead:
             os.makedirs(d, exist_ok=True)
         dist.barrier()
         os.makedirs(d, exist_ok=True)
         names = self._param_names()
         stage = self.zero_optimization_stage()
-        write_model = stage == 3 or groups.get_sequence_data_parallel_rank() == 0
+        write_model = stage == 3 or (self.local_rank == 0 if node_local else groups.get_sequence_data_parallel_rank() == 0)
         module_sd = self.module_state_dict(exclude_frozen_parameters) if (write_model or stage < 3) else None
         moe = self._moe_layers() if stage < 3 else []
         if moe and module_sd is not None:
@@ -1293,10 +1518,10 @@ class SXEEngine(nn.Module):
             self.checkpoint_engine.save({"optimizer_state_dict": osd, "ds_config": self._config._param_dict,
                                          "ds_version": "sxe-0.1"}, optim_path)
         self.checkpoint_engine.commit(tag)
-        if self.global_rank == 0 and stage > 0:
+        if lead and stage > 0:
             self._copy_recovery_script(d)
         dist.barrier()
-        if save_latest and self.global_rank == 0:
+        if save_latest and lead:
             with open(os.path.join(save_dir, "latest"), "w") as f:
                 f.write(tag)
         dist.barrier()

@@ -61,6 +61,22 @@ class ZeroOptimizerBase:
         # host or NVMe, update by the C++ CPU kernels; None = everything on the GPU
         self.host_step = None
 
+    def destroy(self):
+        """Remove every hook this optimizer installed on parameters / modules and finish in-flight
+        exchanges (engine.destroy, reference engine.py:521-530)."""
+        if hasattr(self, "wait_params"):
+            self.wait_params()
+        for h in getattr(self, "_hooks", []):
+            h.remove()
+        self._hooks = []
+        self._module_hooks = []
+        for units in self.units:
+            for u in units:
+                for p in u.params:
+                    for a in ("_sxe_grad_target", "_sxe_grad_done"):
+                        if hasattr(p, a):
+                            delattr(p, a)
+
     # --------------------------------------------------------------------------------------------
     def _init_master(self):
         """Create fp32 masters/grad accumulators and re-point the wrapped optimizer at them."""

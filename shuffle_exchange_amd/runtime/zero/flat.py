@@ -57,6 +57,7 @@ class FlatUnit:
         self.grad = None           # fp32 chunk gradient accumulator (view into group grad buffer)
         self.staging = None        # full-size grad staging buffer during backward
         self.staging_dtype = None  # None: the unit dtype; fp32 when gradients carry across micro-steps
+        self.comm_dtype = None     # gradient-reduction dtype override (torch_autocast units)
         self.carry = False         # staging already holds earlier micro-steps' gradients (deferred RS)
         self.filled = None         # per-param "grad copied to staging" flags
         self.pending = 0

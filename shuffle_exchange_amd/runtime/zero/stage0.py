@@ -21,6 +21,7 @@ from ...accelerator import get_accelerator
 from ...utils.logging import log_dist
 from .base import ZeroOptimizerBase
 from .flat import FlatUnit, split_into_units
+from ..torch_autocast import split_by_comm_dtype, unit_comm_dtype
 
 
 class DataParallelOptimizer(ZeroOptimizerBase):
@@ -52,12 +53,14 @@ class DataParallelOptimizer(ZeroOptimizerBase):
                 rsize = groups.get_expert_data_parallel_world_size(name)
             sparse = [p for p in params if getattr(p, "_sxe_sparse", False)]
             dense = [p for p in params if not getattr(p, "_sxe_sparse", False)]
-            plists = (list(split_into_units(dense, max(1, int(bucket_size)))) if dense else []) + [[p] for p in sparse]
+            plists = [pl for run in split_by_comm_dtype(dense) for pl in split_into_units(run, max(1, int(bucket_size)))]
+            plists += [[p] for p in sparse]
             for i, plist in enumerate(plists):
                 u = FlatUnit(plist, 1, 0, plist[0].dtype, device, name=f"g{g}u{i}", index=i)
                 # expert grads are summed over their EDP group and divided by the DENSE dp size
                 # (reference engine.py:2713-2716 _reduce_expert_gradients, stage_1_and_2.py:1316)
                 u.rgroup, u.rsize, u.rdiv = rgroup, rsize, self.dp_size
+                u.comm_dtype = unit_comm_dtype(plist)  # torch_autocast: all-reduce in bf16 / fp16
                 u.sparse = getattr(plist[0], "_sxe_sparse", False)
                 u.sparse_parts = []
                 u.dense_seen = False
@@ -198,11 +201,16 @@ class DataParallelOptimizer(ZeroOptimizerBase):
         if st is not None:
             st.wait_stream(torch.cuda.current_stream())
         with get_accelerator().stream(st):
+            g = u.grad if u.comm_dtype is None else u.grad.to(u.comm_dtype)
             if dist.get_backend() == "nccl" and self.sp_scale == 1.0 and u.rdiv == u.rsize:
-                dist.all_reduce(u.grad, op=dist.ReduceOp.AVG, group=u.rgroup)
+                dist.all_reduce(g, op=dist.ReduceOp.AVG, group=u.rgroup)
             else:
-                dist.all_reduce(u.grad, group=u.rgroup)
-                u.grad.mul_(self.sp_scale / u.rdiv)
+                dist.all_reduce(g, group=u.rgroup)
+                g.mul_(self.sp_scale / u.rdiv)
+            if g is not u.grad:
+                u.grad.copy_(g)
+                if st is not None:
+                    g.record_stream(st)
 
     def set_gradient_accumulation_boundary(self, flag):
         self.boundary = bool(flag)

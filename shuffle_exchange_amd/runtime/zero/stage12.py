@@ -25,6 +25,7 @@ from ...utils.logging import log_dist
 from .base import ZeroOptimizerBase
 from .flat import FlatUnit, split_into_units
 from .shuffle_exchange import ShuffleExchange, SliceTopology
+from ..torch_autocast import split_by_comm_dtype, unit_comm_dtype
 
 
 class ZeroStage12Optimizer(ZeroOptimizerBase):
@@ -79,9 +80,13 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                 continue
             dtype = params[0].dtype
             units = []
-            for i, plist in enumerate(split_into_units(params, max(1, int(reduce_bucket_size)))):
+            # torch_autocast: runs of equal gradient-communication dtype get units of their own
+            plists = [pl for run in split_by_comm_dtype(params)
+                      for pl in split_into_units(run, max(1, int(reduce_bucket_size)))]
+            for i, plist in enumerate(plists):
                 gt = self._group_topo(pg)
                 u = FlatUnit(plist, gt.S, gt.offset, dtype, device, name=f"g{g}u{i}", index=i)
+                u.comm_dtype = unit_comm_dtype(plist)
                 u.topo = gt
                 u.moe = bool(pg.get("moe", False))
                 if self.fp32_accum:
@@ -211,7 +216,8 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         if stream is not None:
             stream.wait_stream(cur)
         with get_accelerator().stream(stream):
-            send = st if (self.comm_dtype is None or st.dtype == self.comm_dtype) else st.to(self.comm_dtype)
+            want = u.comm_dtype or self.comm_dtype
+            send = st if (want is None or st.dtype == want) else st.to(want)
             out = torch.empty(u.chunk, dtype=send.dtype, device=send.device)
             dist.reduce_scatter_tensor(out, send, group=u.topo.slice_group)
             u.grad.add_(out, alpha=self._unit_scale(u))

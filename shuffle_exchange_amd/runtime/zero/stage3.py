@@ -34,6 +34,7 @@ from .base import ZeroOptimizerBase
 from .flat import FlatUnit
 from .partition_parameters import release_construction_partition
 from .shuffle_exchange import ShuffleExchange, SliceTopology
+from ..torch_autocast import unit_comm_dtype
 
 RELEASED, INFLIGHT, AVAILABLE = 0, 1, 2
 
@@ -295,6 +296,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
     def _make_unit(self, params, name, fg):
         dtype = params[0].dtype
         u = FlatUnit(params, self.S, self.topo.offset, dtype, self.device, name=name, materialize_full=False)
+        u.comm_dtype = unit_comm_dtype(params)  # torch_autocast: bf16 reduce-scatter when every param is marked
         u.fg = fg
         u.owner = self
         u.persistent = (self.S == 1 and not self.offload_param) or (
@@ -666,7 +668,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         if rs is not None:
             rs.wait_stream(cur)
         with get_accelerator().stream(rs):
-            want = self.comm_dtype or (u.dtype if self.defer_reduce else None)
+            want = (u.comm_dtype if self.S > 1 else None) or self.comm_dtype or (u.dtype if self.defer_reduce else None)
             send = st if (want is None or st.dtype == want) else st.to(want)
             if self.S == 1:
                 self._accumulate(u, send, 1.0)
@@ -874,6 +876,17 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         self._hold = False
         for fg in self.fgroups:
             self._release(fg)
+
+    def empty_partition_cache(self):
+        """Free every gathered non-persistent unit (engine.empty_partition_cache, reference
+        stage3.py ``empty_partition_cache``): after evaluation or generation outside the training
+        loop, the next forward gathers again."""
+        self.wait_params()
+        self._hold = False
+        for units in self.units:
+            for u in units:
+                if not u.persistent and u.state != RELEASED:
+                    self._release_unit(u)
 
     def gather_params(self, params):
         self.wait_params()
