@@ -320,6 +320,8 @@ def _deferred(fn, outs, async_op):
 
 def _timed(op, fn, tensor, group, async_op, outs=None):
     _fp(op, group, tensor)
+    if op != "all_reduce":  # all_reduce counts under its caller's log_name
+        _State.op_counts[op] += 1
     v = _State.volume[op]
     v[0] += 1
     v[1] += _payload(op, tensor, group)

@@ -20,16 +20,39 @@ class RandomLTDScheduler:
         self.require_steps = cfg.get("require_steps", 100)
         self.current = self.min_value
         self.consumed_layer_tokens = 0
-        # token selection draws from a counter-based stream (seed, draw index) instead of the global
-        # RNG, and the draw index is checkpointed: a resumed run drops the same tokens
+        # token selection draws from a stream keyed by (seed, global step, micro-step, layer) instead
+        # of the global RNG: an activation-checkpoint recompute of the wrapped layer (which restores
+        # only the global RNG) draws the SAME tokens as its forward, and a resumed run -- whose step
+        # counters come from the checkpoint -- drops the same tokens as an uninterrupted one. Outside
+        # an engine (no begin_micro_step) the key falls back to a running draw counter.
         self.seed = int(config.get("seed", 1234))
         self.draws = 0
+        self._key = None
+        self._counted = set()
 
-    def generator(self, device):
+    def begin_micro_step(self, global_step, micro_step):
+        """Called by the engine once per training forward (never by a recompute)."""
+        self._key = (int(global_step), int(micro_step))
+        self._counted = set()
+
+    def generator(self, device, layer_id=0):
         g = torch.Generator(device=device)
-        g.manual_seed((self.seed * 1_000_003 + self.draws) % (1 << 62))
-        self.draws += 1
+        if self._key is None:
+            g.manual_seed((self.seed * 1_000_003 + self.draws) % (1 << 62))
+            self.draws += 1
+            return g
+        step, micro = self._key
+        g.manual_seed(((self.seed * 1_000_003 + step) * 4_099 + micro) * 257 + int(layer_id) & ((1 << 62) - 1))
         return g
+
+    def count_tokens(self, layer_id, n):
+        """consumed_layer_tokens, once per (micro-step, layer): a recompute does not count again."""
+        if self._key is None:
+            self.consumed_layer_tokens += n
+            return
+        if layer_id not in self._counted:
+            self._counted.add(layer_id)
+            self.consumed_layer_tokens += n
 
     def get_current_seq(self):
         return self.current
@@ -96,9 +119,12 @@ class RandomLayerTokenDrop(nn.Module):
         if not self.training or k >= x.shape[1]:
             return self.layer(x, *args, **kwargs)
         B, S, _ = x.shape
-        gen = self.scheduler.generator(x.device) if hasattr(self.scheduler, "generator") else None
+        lid = getattr(self, "layer_id", 0)
+        gen = self.scheduler.generator(x.device, lid) if hasattr(self.scheduler, "generator") else None
         idx = token_sort_(torch.rand(B, S, device=x.device, generator=gen).topk(k, dim=1).indices)
-        if self.scheduler is not None:
+        if hasattr(self.scheduler, "count_tokens"):
+            self.scheduler.count_tokens(lid, B * k)
+        elif self.scheduler is not None:
             self.scheduler.consumed_layer_tokens += B * k
         args = list(args)
         full = {0: x}
@@ -123,9 +149,14 @@ class RandomLayerTokenDrop(nn.Module):
             return scatter_tokens(x, out, idx)
         outs = list(out)
         for j, o in enumerate(outs):
+            if not (torch.is_tensor(o) and o.dim() == 3 and o.shape[:2] == (B, k)):
+                continue
             src = full.get(j, x if j == 0 else None)
-            if src is not None and torch.is_tensor(o) and o.shape[:2] == (B, k):
-                outs[j] = scatter_tokens(src, o, idx)
+            if src is None:
+                # an output stream the layer created (the fused residual of the first layer, whose
+                # input residual is None): dropped tokens carry zero in it, so x + res == x for them
+                src = torch.zeros((B, S) + tuple(o.shape[2:]), dtype=o.dtype, device=o.device)
+            outs[j] = scatter_tokens(src, o, idx)
         return type(out)(outs) if isinstance(out, tuple) else outs
 
 

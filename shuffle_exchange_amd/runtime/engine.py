@@ -651,6 +651,7 @@ class SXEEngine(nn.Module):
             kwargs["curriculum_seqlen"] = self.curriculum_scheduler_legacy.update_difficulty(self.global_steps + 1)
         if self.random_ltd_scheduler is not None and self.module.training:
             self.random_ltd_scheduler.update_seq(self.global_steps)
+            self.random_ltd_scheduler.begin_micro_step(self.global_steps, self.micro_steps - self._gas_base)
         fp = self._config.model.flops_profiler
         prof = None
         if fp.enabled and self.global_steps + 1 == fp.profile_step and self.micro_steps % max(

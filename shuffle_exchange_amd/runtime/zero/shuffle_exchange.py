@@ -161,6 +161,26 @@ class ShuffleExchange:
             dist.all_reduce(f, group=group)
             t.copy_(f)
 
+    @staticmethod
+    def _packed(tensors, fn):
+        """Run ``fn(flat)`` once per dtype over all ``tensors`` packed back to back: one collective per
+        step instead of one per chunk (every RCCL call pays its launch + ring-setup latency over the
+        xGMI links; the pack / unpack copies run at HBM speed). A lone tensor goes in place."""
+        by_dt = {}
+        for t in tensors:
+            by_dt.setdefault(t.dtype, []).append(t)
+        for ts in by_dt.values():
+            if len(ts) == 1 and ts[0].is_contiguous():
+                fn(ts[0])
+                continue
+            flat = torch.cat([t.reshape(-1) for t in ts])
+            fn(flat)
+            o = 0
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[o:o + n].view_as(t))
+                o += n
+
     # -------------------------------------------------------------------------------------------
     def shuffle_exchange(self):
         """User hook (reference stage_1_and_2.py:692): reshuffle every `shuffle_step` calls."""
@@ -211,35 +231,35 @@ class ShuffleExchange:
         tensors = list(shards) + (list(masters) if (self.average_master and masters is not None) else [])
         m = self.method
         if m == "RR":
-            for t in tensors:
-                self._mean_allreduce(t, self.group, self.topo.num_slices)
+            self._packed(tensors, lambda t: self._mean_allreduce(t, self.group, self.topo.num_slices))
         elif m == "shuffle":
-            for t in tensors:
-                self._mean_allreduce(t, self.group, len(self.group_ranks))
+            self._packed(tensors, lambda t: self._mean_allreduce(t, self.group, len(self.group_ranks)))
         elif m == "H-RR":
             # sum up the hierarchy, divide ONCE at the top (pre-dividing every bit16 chunk by n
             # before the sums would round each contribution in bf16 first)
             n = self.topo.num_slices
-            for t in tensors:
+
+            def hrr(t):
                 dist.reduce(t, dst=self.top_node, group=self.group)
                 if self.in_top:
                     dist.all_reduce(t, group=self.top_group)
                     t.div_(n)
                 dist.broadcast(t, src=self.top_node, group=self.group)
+            self._packed(tensors, hrr)
         elif m == "Gossip":
             self._gossip(shards)
 
     def _gossip(self, shards):
         n = self.topo.num_slices
-        senders = torch.bernoulli(torch.full((n,), self.gossip_p), generator=self.gen)
+        # the step's whole plan in two draws (host generator, one .tolist() each): who sends, and to whom
+        senders = torch.bernoulli(torch.full((n,), self.gossip_p), generator=self.gen).tolist()
+        dests = torch.randint(0, n, (n,), generator=self.gen).tolist()
         me = self.topo.slice_id
         ops, recv = [], []
         dev = shards[0].device
         for sid in range(n):
-            if senders[sid].item() != 1:
-                continue
-            dest = int(torch.randint(0, n, (1,), generator=self.gen).item())
-            if dest == sid:
+            dest = int(dests[sid])
+            if senders[sid] != 1 or dest == sid:
                 continue
             if sid == me:
                 self.alpha /= 2
@@ -270,8 +290,7 @@ class ShuffleExchange:
             return False
         if not hasattr(self, "_world_offset_group"):
             self._world_offset_group = self.topo.offset_groups(range(self.topo.num_slices))[0]
-        for t in shards:
-            self._mean_allreduce(t, self._world_offset_group, self.topo.num_slices)
+        self._packed(list(shards), lambda t: self._mean_allreduce(t, self._world_offset_group, self.topo.num_slices))
         return True
 
     def state_dict(self):

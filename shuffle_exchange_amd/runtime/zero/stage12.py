@@ -324,12 +324,10 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         if stream is not None:
             stream.wait_stream(torch.cuda.current_stream())
         with get_accelerator().stream(stream):
-            gossip = self.se is not None and self.se.method == "Gossip"
-            if gossip:  # push-sum draws its senders once per step for all chunks together
+            if self.se is not None:
+                # one packed inter-slice collective per step for all chunks (Gossip: one plan)
                 self.se.sync([u.shard for u in units], masters)
             for i, u in enumerate(units):
-                if self.se is not None and not gossip:
-                    self.se.sync([u.shard], [masters[i]] if masters is not None else None)
                 if u.topo.S > 1:
                     dist.all_gather_into_tensor(u.flat, u.shard, group=u.topo.slice_group)
                 if stream is not None:

@@ -105,6 +105,13 @@ def safe_set_full_fp32_param(param, value):
     if u.flat is not None and u.flat.untyped_storage().size() > 0:
         o, n = u.offsets[i], u.numels[i]
         u.flat[o:o + n].copy_(v.to(u.flat.device, u.flat.dtype))
+    _weights_rewritten()
+
+
+def _weights_rewritten():
+    """The bit16 weights changed outside the optimizer step: drop cached transposes (ops/linear.py)."""
+    from ..ops.linear import invalidate_transposed_weights
+    invalidate_transposed_weights()
 
 
 @torch.no_grad()
@@ -131,6 +138,7 @@ def safe_set_local_fp32_param(param, value):
     if u.master is not None:
         u.master[slo:slo + phi - plo].copy_(value.reshape(-1).to(u.master.device))
     u.shard[slo:slo + phi - plo].copy_(value.reshape(-1).to(u.shard.device, u.shard.dtype))
+    _weights_rewritten()
 
 
 @torch.no_grad()

@@ -171,3 +171,44 @@ def test_distributed_data_analyzer(tmp_path):
     from .dist_utils import run_dist
     run_dist(_case_dist_analyzer, 3, str(tmp_path))
     _check_outputs(str(tmp_path), _Toks())
+
+
+def _case_rltd_ac(rank, world, ac):
+    """Parameters after one random-LTD accumulation window (2 micro-steps, SGD) with or without full
+    activation checkpointing: equal gradients give equal parameters."""
+    import shuffle_exchange_amd as sxe
+    from ._dist_cases import tiny_llama
+    model, cfg = tiny_llama(0, activation_checkpointing=ac, ac_policy="full")
+    ds = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": 2,
+          "optimizer": {"type": "SGD", "params": {"lr": 0.5}}, "zero_optimization": {"stage": 0},
+          "data_efficiency": {"enabled": True, "seed": 3, "data_routing": {"enabled": True, "random_ltd": {
+              "enabled": True, "random_ltd_layer_num": 2, "random_ltd_layer_id": [0, 1],
+              "random_ltd_schedule": {"min_value": 8, "max_value": 32, "schedule_type": "fixed_linear",
+                                      "schedule_config": {"require_steps": 100, "seq_per_step": 8}}}}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    g = torch.Generator().manual_seed(5)
+    for _ in range(2):  # one accumulation window of two micro-steps
+        ids = torch.randint(0, cfg.vocab_size, (2, 32), generator=g)
+        eng.backward(eng(ids, labels=ids))
+        eng.step()
+    return {"params": {n: p.detach().clone() for n, p in eng.module.named_parameters()},
+            "consumed": eng.random_ltd_scheduler.consumed_layer_tokens}
+
+
+def test_random_ltd_with_full_activation_checkpointing_matches():
+    """The recompute of a checkpointed random-LTD layer keeps the forward's tokens (draws keyed by
+    step / micro-step / layer, not a counter), so training equals the uncheckpointed run and the
+    consumed-token count is not doubled."""
+    a = run_dist(_case_rltd_ac, 1, False)[0]
+    b = run_dist(_case_rltd_ac, 1, True)[0]
+    assert a["consumed"] == b["consumed"] == 2 * 2 * 2 * 8
+    moved = 0
+    for n in a["params"]:
+        assert torch.allclose(a["params"][n], b["params"][n], atol=1e-6, rtol=1e-5), n
+        moved += int(not torch.equal(a["params"][n], tiny_llama_param(n)))
+    assert moved > 0
+
+
+def tiny_llama_param(name):
+    from ._dist_cases import tiny_llama
+    return dict(tiny_llama(0)[0].named_parameters())[name.replace(".layer.", ".")].detach()

@@ -161,14 +161,9 @@ def _replay_gossip(seed, n, p, steps):
     g.manual_seed(seed)
     plan = []
     for _ in range(steps):
-        senders = torch.bernoulli(torch.full((n,), p), generator=g)
-        msgs = []
-        for sid in range(n):
-            if senders[sid].item() != 1:
-                continue
-            dest = int(torch.randint(0, n, (1,), generator=g).item())
-            if dest != sid:
-                msgs.append((sid, dest))
+        senders = torch.bernoulli(torch.full((n,), p), generator=g).tolist()
+        dests = torch.randint(0, n, (n,), generator=g).tolist()
+        msgs = [(sid, int(dests[sid])) for sid in range(n) if senders[sid] == 1 and dests[sid] != sid]
         plan.append(msgs)
     return plan
 
@@ -227,3 +222,40 @@ def test_rr_bf16_rounding_vs_fp32_mean(w8):
                 exp = _mean([w8[q][k]["log"][c]["before"][i] for q in _same_offset(w8, k, r)])
                 ulp = torch.ldexp(torch.ones_like(exp), torch.frexp(exp.abs().clamp_min(1e-30))[1] - 8)
                 assert ((after - exp).abs() <= 4 * ulp).all(), (c, r, ((after - exp).abs() / ulp).max())
+
+
+def _case_op_counts(rank, world, method, stage):
+    """Collectives issued by one post-step inter-slice exchange with many flat units."""
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd import comm
+    model, cfg = tiny_llama(0)
+    ds = {"train_micro_batch_size_per_gpu": 1, "optimizer": {"type": "SGD", "params": {"lr": 0.05}},
+          "zero_optimization": {"stage": stage, "reduce_bucket_size": 20000, "stage3_param_persistence_threshold": 0}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds, method=method, slice_count=2, rings=2, shuffle_step=2)
+    b = global_batches(cfg, world, 1, 16, 1)[0][rank:rank + 1]
+    eng.backward(eng(b, labels=b))
+    se = eng.optimizer.se
+    real = se.sync
+    counts = {}
+
+    def counted(shards, masters=None):
+        comm.reset_comms_stats()
+        real(shards, masters)
+        counts.update(comm.get_op_counts())
+        counts["chunks"] = len(shards)
+    se.sync = counted
+    eng.step()
+    return counts
+
+
+@pytest.mark.parametrize("method,stage", [("RR", 2), ("RR", 1), ("shuffle", 2), ("H-RR", 2)])
+def test_inter_slice_exchange_is_one_collective_per_step(method, stage):
+    """RR / shuffle: ONE all-reduce per step over all chunks packed together (not one per chunk);
+    H-RR: one reduce + one broadcast (+ one all-reduce on the top ranks)."""
+    res = run_dist(_case_op_counts, W, method, stage)
+    for r, c in enumerate(res):
+        assert c["chunks"] > 1, c  # several flat units: the packing is what keeps it at one call
+        if method in ("RR", "shuffle"):
+            assert c.get("all_reduce", 0) == 1, (r, c)
+        else:
+            assert c.get("reduce", 0) == 1 and c.get("broadcast", 0) == 1 and c.get("all_reduce", 0) <= 1, (r, c)

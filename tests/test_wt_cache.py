@@ -47,6 +47,44 @@ def test_cache_respects_identity_and_cap(counting, monkeypatch):
     assert sum(1 for t in counting if t is w3) == 2  # over the cap: nothing is kept
 
 
+def test_inplace_write_or_rebinding_misses(counting):
+    """A write through the Parameter (version bump) or a rebind to other storage (ZeRO-3 gathers
+    into a new buffer) is a miss even without an explicit invalidation."""
+    w = torch.nn.Parameter(torch.randn(64, 32))
+    L._transposed_weight(w)
+    with torch.no_grad():
+        w.add_(1.0)
+    assert torch.equal(L._transposed_weight(w), w.t()) and len(counting) == 2
+    w.data = torch.randn(64, 32)
+    assert torch.equal(L._transposed_weight(w), w.t()) and len(counting) == 3
+    assert L.transposed_weight_cache_bytes() == 64 * 32 * 4  # the stale entry's bytes were released
+
+
+def _case_writers(rank, world):
+    """Every bit16 weight writer outside the optimizer step drops the cache."""
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd.ops import linear as lin
+    from shuffle_exchange_amd.utils.tensor_fragment import safe_set_full_fp32_param, safe_set_local_fp32_param
+    model = torch.nn.Linear(8, 8)
+    ds = {"train_micro_batch_size_per_gpu": 1, "gradient_accumulation_steps": 2, "zero_optimization": {"stage": 1},
+          "optimizer": {"type": "SGD", "params": {"lr": 0.1}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds, method="RR", slice_count=1)
+    out = {}
+    for name, fn in (("synchronization", eng.synchronization),
+                     ("safe_set_full", lambda: safe_set_full_fp32_param(model.weight, torch.ones(8, 8))),
+                     ("safe_set_local", lambda: safe_set_local_fp32_param(model.weight, torch.ones(64)))):
+        lin._wt_cache[id(model.weight)] = (None, model.weight)
+        fn()
+        out[name] = len(lin._wt_cache)
+    return out
+
+
+def test_weight_writers_invalidate():
+    from .dist_utils import run_dist
+    (r,) = run_dist(_case_writers, 1)
+    assert r == {"synchronization": 0, "safe_set_full": 0, "safe_set_local": 0}
+
+
 def _case_engine(rank, world):
     import shuffle_exchange_amd as sxe
     from shuffle_exchange_amd.ops import linear as lin
