@@ -137,6 +137,11 @@ class HostOptimizerStep:
         self.d2h = acc.named_stream("offload_d2h") if acc.gpu else None
         self.h2d = acc.named_stream("offload_h2d") if acc.gpu else None
         self._h2d_done = None
+        # SXE_OFFLOAD_TRACE=1: per-step host timeline of the streamed update (wall time waiting for
+        # gradient D2H copies, in the C++ update kernel, waiting for free H2D slots) -- logged and
+        # kept in ``self.trace`` (tools/offload_timeline.py turns it into a table)
+        self.trace_on = os.environ.get("SXE_OFFLOAD_TRACE", "0") == "1"
+        self.trace = []
 
     # ------------------------------------------------------------------------------------ layout
     def _kinds(self, opt):
@@ -259,6 +264,9 @@ class HostOptimizerStep:
                 for i, u, off in zip(range(len(units)), units, _offsets(units))]
         NS = len(self.gslots)
         d2h_ev = {}
+        import time as _time
+        tr = {"t0": _time.perf_counter(), "d2h_wait": 0.0, "cpu": 0.0, "h2d_wait": 0.0, "units": len(flat),
+              "elems": sum(x[2].chunk for x in flat)} if self.trace_on else None
 
         def issue_d2h(k):
             u = flat[k][2]
@@ -293,7 +301,11 @@ class HostOptimizerStep:
                 gn, iN, un, _ = flat[k + 1]
                 pend[k + 1] = self.swapper.read((k + 1) % nslot, gn, iN, un.chunk)
             if k in d2h_ev:
+                if tr is not None:
+                    t = _time.perf_counter()
                 d2h_ev.pop(k).synchronize()
+                if tr is not None:
+                    tr["d2h_wait"] += _time.perf_counter() - t
             slot = k % NS
             grad = self.gslots[slot][:u.chunk]
             if nvme:
@@ -304,11 +316,19 @@ class HostOptimizerStep:
                 master, states = u.master, self._state_views(opt, g, off, u.chunk)
             if u.shard_is_cuda():
                 if self._lslot_ev[slot] is not None:
+                    if tr is not None:
+                        t = _time.perf_counter()
                     self._lslot_ev[slot].synchronize()  # its previous H2D has drained
+                    if tr is not None:
+                        tr["h2d_wait"] += _time.perf_counter() - t
                 lp = self.lslots[slot][:u.chunk]
             else:
                 lp = u.shard_for_overwrite()  # pinned host shard, or an NVMe swap buffer
+            if tr is not None:
+                t = _time.perf_counter()
             self._host_kernel(opt, pg, st, master, grad, states, lp, coef)
+            if tr is not None:
+                tr["cpu"] += _time.perf_counter() - t
             if nvme:
                 self.swapper.write(k % nslot, g, i, u.chunk)
             if k + NS < len(flat):
@@ -326,6 +346,17 @@ class HostOptimizerStep:
         if cur is not None:
             cur.wait_stream(self.d2h)  # zero_grad_buffers() must not overtake the copies
             cur.wait_stream(self.h2d)
+        if tr is not None:
+            if cur is not None:
+                torch.cuda.synchronize()
+            tr["wall"] = _time.perf_counter() - tr["t0"]
+            tr["threads"] = torch.get_num_threads()
+            self.trace.append(tr)
+            gb = tr["elems"] * 4 / 1e9
+            log_dist(f"offload step: wall {tr['wall'] * 1e3:.0f} ms | C++ update {tr['cpu'] * 1e3:.0f} ms "
+                     f"({gb * 4 / max(tr['cpu'], 1e-9):.0f} GB/s of fp32 state) | waiting on grad D2H "
+                     f"{tr['d2h_wait'] * 1e3:.0f} ms | waiting on H2D slots {tr['h2d_wait'] * 1e3:.0f} ms | "
+                     f"{tr['units']} units, {tr['elems'] / 1e9:.2f} G elements, {tr['threads']} threads", ranks=[0])
 
     def _update_mirrored(self, opt, cur, coef):
         """Generic (torch) optimizers: full host mirrors of grads / bit16 params."""

@@ -55,10 +55,11 @@ run_step() {  # $1 = name, $2 = log file
     smoke) timeout -k 10 300 python __graft_entry__.py smoke > "$log" 2>&1 ;;
     bench) timeout -k 10 900 python bench.py ${BENCH_ARGS:---steps 3 --warmup 1} > "$log" 2>&1 ;;
     prof)
-      mkdir -p gpurun_out/prof
-      timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- \
+      local pd=${PROF_DIR:-gpurun_out/prof}
+      mkdir -p "$pd"
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$pd" -o bench -- \
         python3 bench.py ${BENCH_ARGS:---steps 1 --warmup 1} > "$log" 2>&1
-      local rc=$?; find gpurun_out/prof -name "*kernel_trace.csv" -size +50M -delete; return $rc ;;
+      local rc=$?; find "$pd" -name "*kernel_trace.csv" -size +50M -delete; return $rc ;;
     attn) timeout -k 10 300 python tools/attn_bench.py ${ATTN_ARGS:-4} > "$log" 2>&1 ;;
     attnprof)
       mkdir -p gpurun_out/attnprof
