@@ -19,6 +19,7 @@
 //    flight, so the norm / gated-activation launches (4-5 us each at batch 1, latency-bound) are
 //    gone from the decode layer. Workgroup 0 also writes the new residual stream h = x + res.
 #include "sxe_common.h"
+#include <map>
 #include <torch/library.h>
 
 namespace sxe {
@@ -475,18 +476,24 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_fp8w_kernel(const unsigne
 // Split-K plan for the bf16 kernel. The decode GEMMs with few 16-column tiles (the QKV projection:
 // 384 tiles, o_proj: 256) leave CUs with uneven work (384 tiles = two workgroups on half the CUs,
 // one on the others) or one 4-wave workgroup per CU (too few loads in flight to cover HBM latency);
-// splitting K in ks parts gives every CU the same share and more streams. SXE_SKINNY_SPLITK: 0 off
-// (default until the split path has a GPU measurement in profiles/), 1 auto, 2 / 4 forced.
+// splitting K in ks parts gives every CU the same share and more streams. SXE_SKINNY_SPLITK (read per
+// call): 0 off, 1 auto (shapes with fewer than two tiles per CU), 2 / 4 forced.
+//
+// Workspace ownership (partials [tiles, ks, 64 lanes, 4] fp32 + one arrival counter per tile, reset
+// by the tile's last arrival):
+//  * eager launches use a workspace per (device, stream): two streams never share counters, and a
+//    workspace that must grow is replaced through the stream-ordered caching allocator (its last
+//    user ran on the same stream);
+//  * a launch being captured into a HIP graph gets a workspace of its own, allocated inside the
+//    capture from the graph's private pool (zeroed counters by a captured memset): it lives as long
+//    as the graph, and no later eager call can free or resize what a graph replays.
 struct SplitWs {
   at::Tensor ws, cnt;
 };
 
 inline int split_mode() {
-  static const int v = [] {
-    const char* e = std::getenv("SXE_SKINNY_SPLITK");
-    return e == nullptr ? 0 : std::atoi(e);
-  }();
-  return v;
+  const char* e = std::getenv("SXE_SKINNY_SPLITK");
+  return (e == nullptr || *e == 0) ? 0 : std::atoi(e);
 }
 
 // returns ks (1 = no split) and sets nw / ss_per_wave / the ProArgs split fields
@@ -502,30 +509,39 @@ inline int plan_split(int tiles, int ss_total, int& nw, int& spw, ProArgs& pro, 
     ks /= 2;
   }
   if (ks > 1) {
-    static std::vector<SplitWs> per_dev;
-    const int dev = like.get_device();
-    if ((int)per_dev.size() <= dev) per_dev.resize(dev + 1);
-    SplitWs& sw = per_dev[dev];
     const int64_t need = (int64_t)tiles * ks * 64 * 4;
-    if (!sw.ws.defined() || sw.ws.numel() < need || sw.cnt.numel() < tiles) {
-      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-      SXE_HIP_CHECK(hipStreamIsCapturing(cur_stream(), &st));
-      if (st != hipStreamCaptureStatusNone) {
-        ks = 1;  // no workspace allocation inside a graph capture: run unsplit
-      } else {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long cap_id = 0;
+    SXE_HIP_CHECK(hipStreamGetCaptureInfo(cur_stream(), &st, &cap_id));
+    if (st != hipStreamCaptureStatusNone) {
+      // graph-owned workspace (the caching allocator serves captures from the graph's pool), shared
+      // by the capture's launches -- they replay in stream order -- and grown by a new allocation
+      // (earlier nodes keep theirs: nothing a graph references is ever freed)
+      static std::map<unsigned long long, SplitWs> per_capture;
+      static std::vector<SplitWs> retired;
+      SplitWs& sw = per_capture[cap_id];
+      if (!sw.ws.defined() || sw.ws.numel() < need || sw.cnt.numel() < tiles) {
+        if (sw.ws.defined()) retired.push_back(sw);
+        sw.ws = at::empty({need}, like.options().dtype(at::kFloat));
+        sw.cnt = at::zeros({tiles}, like.options().dtype(at::kInt));
+      }
+      pro.skws = sw.ws.data_ptr<float>();
+      pro.skcnt = sw.cnt.data_ptr<int>();
+    } else {
+      static std::map<std::pair<int, hipStream_t>, SplitWs> per_stream;
+      SplitWs& sw = per_stream[{like.get_device(), cur_stream()}];
+      if (!sw.ws.defined() || sw.ws.numel() < need || sw.cnt.numel() < tiles) {
         const int64_t cap = std::max<int64_t>(need, (int64_t)4096 * 4 * 64 * 4);
         sw.ws = at::empty({cap}, like.options().dtype(at::kFloat));
         sw.cnt = at::zeros({std::max<int64_t>(tiles, 4096)}, like.options().dtype(at::kInt));
       }
-    }
-    if (ks > 1) {
       pro.skws = sw.ws.data_ptr<float>();
       pro.skcnt = sw.cnt.data_ptr<int>();
-      pro.ks = ks;
-      const int part = (ss_total + ks - 1) / ks;
-      spw = (part + nw - 1) / nw;
-      return ks;
     }
+    pro.ks = ks;
+    const int part = (ss_total + ks - 1) / ks;
+    spw = (part + nw - 1) / nw;
+    return ks;
   }
   nw = pick_nw(tiles, ss_total, 4, 1);
   spw = (ss_total + nw - 1) / nw;

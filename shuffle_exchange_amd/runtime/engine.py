@@ -661,6 +661,9 @@ class SXEEngine(nn.Module):
             prof.start_profile()
         # the FX graph compiler's module (compile/fx_backend.py) when deepcompile is on at ZeRO 0-2
         mod = self._fx_module if getattr(self, "_fx_module", None) is not None else self.module
+        z3_graph = getattr(self.optimizer, "graph_mode", False)
+        if z3_graph:
+            self.optimizer.graph_relink()
         if self._autocast_dtype is not None or torch.is_autocast_enabled(self.device.type):
             from .torch_autocast import validate_nested_autocast
             validate_nested_autocast(self)
@@ -678,6 +681,8 @@ class SXEEngine(nn.Module):
                 out = mod(*inputs, **kwargs)
         else:
             out = mod(*inputs, **kwargs)
+        if z3_graph and not (self.module.training and torch.is_grad_enabled()):
+            self.optimizer.graph_unlink()  # no backward follows this forward
         if prof is not None:
             prof.stop_profile()
             if self.global_rank == 0:
@@ -706,6 +711,8 @@ class SXEEngine(nn.Module):
         scaled.backward(retain_graph=retain_graph)
         if not self._in_no_sync:
             opt.reduce_gradients()
+        if getattr(opt, "graph_mode", False) and not retain_graph:
+            opt.graph_unlink()
         self.timers(BACKWARD_MICRO_TIMER).stop()
         return loss
 

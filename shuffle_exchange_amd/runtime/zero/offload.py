@@ -142,6 +142,20 @@ class HostOptimizerStep:
         # kept in ``self.trace`` (tools/offload_timeline.py turns it into a table)
         self.trace_on = os.environ.get("SXE_OFFLOAD_TRACE", "0") == "1"
         self.trace = []
+        # Asynchronous update (SXE_OFFLOAD_ASYNC, default on; optimizers that declare
+        # ``supports_async_host_step``, i.e. ZeRO-3): every unit's gradient crosses PCIe into a pinned
+        # host mirror, then a worker thread runs the C++ update unit by unit in the order the next
+        # forward needs them and copies each updated bit16 shard back on the H2D stream; step()
+        # returns at once and the next forward waits per unit (``wait_units``) instead of for the
+        # whole update -- the host update of the later units runs under the forward of the earlier
+        # ones. Results are bit-identical to the synchronous path (same kernels, same order).
+        self.async_update = os.environ.get("SXE_OFFLOAD_ASYNC", "1") == "1" and self.device == "cpu"
+        self._worker = None
+        self._ready = {}
+        self._h2d_ev = {}
+        self._pending = False
+        self._error = None
+        self.ghost = None
 
     # ------------------------------------------------------------------------------------ layout
     def _kinds(self, opt):
@@ -262,6 +276,8 @@ class HostOptimizerStep:
         # copies are in flight ahead of the CPU update
         flat = [(g, i, u, off) for g, units in enumerate(opt.units) if g in self.groups
                 for i, u, off in zip(range(len(units)), units, _offsets(units))]
+        if self._async_ok(opt, flat):
+            return self._update_async(opt, cur, coef, flat)
         NS = len(self.gslots)
         d2h_ev = {}
         import time as _time
@@ -358,6 +374,170 @@ class HostOptimizerStep:
                      f"{tr['d2h_wait'] * 1e3:.0f} ms | waiting on H2D slots {tr['h2d_wait'] * 1e3:.0f} ms | "
                      f"{tr['units']} units, {tr['elems'] / 1e9:.2f} G elements, {tr['threads']} threads", ranks=[0])
 
+    # ------------------------------------------------------------------------ asynchronous update
+    def _async_ok(self, opt, flat):
+        if not (self.async_update and flat and getattr(opt, "supports_async_host_step", False)):
+            return False
+        if getattr(opt, "pswap", None) is not None:
+            return False  # NVMe parameter tier: its swap buffers are driven from the main thread
+        if self.ghost is not None:
+            return True
+        need = sum(x[2].chunk for x in flat) * 4
+        try:
+            import psutil
+            avail = psutil.virtual_memory().available
+        except Exception:
+            return False
+        if need > avail // 2:  # the mirror must leave the host room: else stream through the slot ring
+            log_dist(f"offload: {need / 2**30:.1f} GiB gradient mirror does not fit host memory; "
+                     "synchronous host update", ranks=[0])
+            self.async_update = False
+            return False
+        return True
+
+    def _update_async(self, opt, cur, coef, flat):
+        import threading
+        import time as _time
+        self.wait_all()
+        order = getattr(opt, "host_unit_order", None)
+        if order is not None:  # the next forward's order: its first units are ready first
+            rank = {id(u): r for r, u in enumerate(order())}
+            flat = sorted(flat, key=lambda x: rank.get(id(x[2]), len(rank)))
+        total = sum(x[2].chunk for x in flat)
+        if self.ghost is None or self.ghost.numel() < total:
+            self.ghost = _pinned(total, torch.float32)
+        t0 = _time.perf_counter()
+        if cur is not None:
+            self.d2h.wait_stream(cur)
+        d2h, o = [], 0
+        for g, i, u, off in flat:
+            dst = self.ghost[o:o + u.chunk]
+            o += u.chunk
+            if cur is None:
+                dst.copy_(u.grad)
+                d2h.append((dst, None))
+                continue
+            with get_accelerator().stream(self.d2h):
+                dst.copy_(u.grad, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.d2h)
+            d2h.append((dst, ev))
+        for g in self.groups:
+            st = opt.optimizer.state[opt.master[g]]
+            if opt.kind in ("adam", "adagrad"):
+                st["step"] = int(st.get("step", 0)) + 1
+        self._ready = {id(x[2]): threading.Event() for x in flat}
+        self._h2d_ev = {}
+        self._error = None
+        self._pending = True
+        tr = {"t0": t0, "units": [], "waits": [], "elems": total} if self.trace_on else None
+        self._cur_trace = tr
+        dev = opt.device if cur is not None else None
+
+        def work():
+            try:
+                if dev is not None:
+                    torch.cuda.set_device(dev)
+                NS = len(self.gslots)
+                for k, ((g, i, u, off), (grad, ev)) in enumerate(zip(flat, d2h)):
+                    ta = _time.perf_counter()
+                    if ev is not None:
+                        ev.synchronize()
+                    tb = _time.perf_counter()
+                    pg = opt.optimizer.param_groups[g]
+                    st = opt.optimizer.state[opt.master[g]]
+                    slot = k % NS
+                    if u.shard_is_cuda():
+                        if self._lslot_ev[slot] is not None:
+                            self._lslot_ev[slot].synchronize()  # its previous H2D has drained
+                        lp = self.lslots[slot][:u.chunk]
+                    else:
+                        lp = u.shard_for_overwrite()
+                    self._host_kernel(opt, pg, st, u.master, grad, self._state_views(opt, g, off, u.chunk), lp, coef)
+                    tc = _time.perf_counter()
+                    if u.shard_is_cuda():
+                        with get_accelerator().stream(self.h2d):
+                            u.shard.copy_(lp, non_blocking=True)
+                            hev = torch.cuda.Event()
+                            hev.record(self.h2d)
+                        self._lslot_ev[slot] = hev
+                        self._h2d_ev[id(u)] = hev
+                    if tr is not None:
+                        tr["units"].append((u.name, u.chunk, ta - t0, tb - t0, tc - t0))
+                    self._ready[id(u)].set()
+            except BaseException as e:  # surfaced by wait_unit / wait_all on the main thread
+                self._error = e
+                for e2 in self._ready.values():
+                    e2.set()
+
+        self._worker = threading.Thread(target=work, name="sxe-host-adam", daemon=True)
+        self._worker.start()
+
+    def _raise(self):
+        if self._error is not None:
+            e, self._error = self._error, None
+            raise RuntimeError("host optimizer update failed") from e
+
+    def wait_unit(self, u):
+        """The calling stream may read unit ``u``'s bit16 shard (async update finished for it)."""
+        if not self._pending:
+            return
+        ev = self._ready.get(id(u))
+        if ev is None:
+            return
+        if not ev.is_set():
+            import time as _time
+            t = _time.perf_counter()
+            ev.wait()
+            tr = getattr(self, "_cur_trace", None)
+            if tr is not None:
+                tr["waits"].append((u.name, t - tr["t0"], _time.perf_counter() - tr["t0"]))
+        self._raise()
+        h = self._h2d_ev.get(id(u))
+        if h is not None:
+            torch.cuda.current_stream().wait_event(h)
+
+    def wait_units(self, units):
+        for u in units:
+            self.wait_unit(u)
+
+    def wait_all(self):
+        """Finish the asynchronous update: every shard final, the compute stream ordered after it."""
+        if self._worker is not None:
+            self._worker.join()
+            self._worker = None
+        self._raise()
+        if self._pending:
+            if self.h2d is not None and torch.cuda.is_available():
+                torch.cuda.current_stream().wait_stream(self.h2d)
+            self._pending = False
+            tr = getattr(self, "_cur_trace", None)
+            if tr is not None and tr["units"]:
+                self._log_async_trace(tr)
+                self._cur_trace = None
+
+    def before_backward(self):
+        """The backward rewrites the fp32 gradient accumulators: the D2H copies of the previous
+        asynchronous update must have read them."""
+        if self.d2h is not None and torch.cuda.is_available():
+            torch.cuda.current_stream().wait_stream(self.d2h)
+
+    def _log_async_trace(self, tr):
+        self.trace.append(tr)
+        path = os.environ.get("SXE_OFFLOAD_TRACE_FILE")
+        if path and self.rank == 0:  # host timeline of every step, JSON lines (tools/offload_timeline.py)
+            import json
+            with open(path, "a") as f:
+                f.write(json.dumps({"units": tr["units"], "waits": tr["waits"], "elems": tr["elems"]}) + "\n")
+        last = tr["units"][-1]
+        cpu = sum(c - b for _, _, _, b, c in tr["units"])
+        d2h_wait = sum(b - a for _, _, a, b, _ in tr["units"])
+        fwd_wait = sum(b - a for _, a, b in tr["waits"])
+        log_dist(f"offload async step: host update done at {last[4] * 1e3:.0f} ms | C++ update {cpu * 1e3:.0f} ms "
+                 f"({tr['elems'] * 16 / 1e9 / max(cpu, 1e-9):.0f} GB/s of fp32 state) | worker waiting on grad D2H "
+                 f"{d2h_wait * 1e3:.0f} ms | next forward waited {fwd_wait * 1e3:.0f} ms on {len(tr['waits'])} units",
+                 ranks=[0])
+
     def _update_mirrored(self, opt, cur, coef):
         """Generic (torch) optimizers: full host mirrors of grads / bit16 params."""
         if self._h2d_done is not None:
@@ -417,7 +597,8 @@ class HostOptimizerStep:
     # ------------------------------------------------------------------------- checkpoint support
     def materialize(self, opt):
         """NVMe: read every record into full host tensors (master + optimizer state) so the usual
-        state_dict() sees them. No-op for cpu offload."""
+        state_dict() sees them. No-op for cpu offload (beyond finishing an asynchronous update)."""
+        self.wait_all()
         if self.device != "nvme" or self.materialized:
             return
         sw = self.swapper
@@ -462,6 +643,7 @@ class HostOptimizerStep:
 
     def write_master(self, opt, u):
         """After an external edit of a unit's bit16 shard: refresh its fp32 master."""
+        self.wait_all()
         if self.device == "cpu":
             u.master.copy_(u.shard.float().cpu() if u.shard.is_cuda else u.shard.float())
             return

@@ -377,6 +377,31 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                     u.flat.untyped_storage().resize_(0)
         self.trace = []
 
+    def graph_relink(self):
+        """Before a compiled forward: released units show their parameters as full-shape views of the
+        freed flat storage again (the shapes the traced graphs were specialised on)."""
+        self._in_graph_step = True
+        for units in self.units:
+            for u in units:
+                if getattr(u, "graph_unlinked", False):
+                    if u.state == RELEASED:
+                        st = u.flat.untyped_storage()
+                        st.resize_(u.padded * u.flat.element_size())  # views need in-bounds storage
+                        u.link_params()
+                        st.resize_(0)
+                    u.graph_unlinked = False
+
+    def graph_unlink(self):
+        """After a compiled step (backward done, or a no-grad forward): released parameters read as
+        empty tensors (numel 0) -- as in eager ZeRO-3 -- instead of full-shape views over freed
+        storage that a read outside GatheredParameters would dereference."""
+        self._in_graph_step = False
+        for units in self.units:
+            for u in units:
+                if u.state == RELEASED and not u.persistent and not getattr(u, "graph_unlinked", False):
+                    u.unlink_params()
+                    u.graph_unlinked = True
+
     def gather_all_for_trace(self):
         """Materialise every unit (Dynamo fake-ifies the parameters when it traces)."""
         for fg in self.fgroups:
@@ -419,6 +444,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         def pre(mod, args):
             if not self._in_bwd:
                 self._observed.append(fg.idx)
+            if self.host_step is not None:
+                self.host_step.wait_units(fg.units)  # asynchronous host update (zero/offload.py)
             self._fetch(fg, wait=True)
             self._prefetch_after(fg, backward=self._in_bwd)
             if self.tracer is not None and not self._in_bwd:
@@ -521,14 +548,17 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
 
     # ------------------------------------------------------------------------------ fetch/release
     def _launch_gather(self, u):
+        if self.host_step is not None:
+            self.host_step.wait_unit(u)  # the shard is final once the host update reached it
         cur = torch.cuda.current_stream() if u.flat.is_cuda else None  # shard may be host-resident (offload_param)
         st = self.ag_stream
         if st is not None:
             st.wait_stream(cur)
         with get_accelerator().stream(st):
             u.flat.untyped_storage().resize_(u.padded * u.flat.element_size())
-            if not getattr(self, "graph_mode", False):
+            if not getattr(self, "graph_mode", False) or getattr(u, "graph_unlinked", False):
                 u.link_params()
+                u.graph_unlinked = False
             swapped = u.swap is not None
             src = u.swap.acquire(u) if swapped else u.shard
             if src.device != u.flat.device:
@@ -610,6 +640,9 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         u.flat.untyped_storage().resize_(0)
         if not getattr(self, "graph_mode", False):
             u.unlink_params()
+        elif not getattr(self, "_in_graph_step", False):  # a gather outside a compiled step
+            u.unlink_params()
+            u.graph_unlinked = True
         u.state = RELEASED
 
     def _release(self, fg):
@@ -756,6 +789,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             self.tracer.on_forward_start()
 
     def backward_prologue(self):
+        if self.host_step is not None:
+            self.host_step.before_backward()
         for units in self.units:
             for u in units:
                 u.begin_backward()
@@ -791,8 +826,25 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             self.tracer.on_backward_end()
 
     # ------------------------------------------------------------------------------------------ step
+    supports_async_host_step = True
+
     def wait_params(self):
-        """Nothing in flight across steps: the update runs on the compute stream."""
+        """Nothing in flight across steps on the device (the update runs on the compute stream);
+        an asynchronous host-offload update (zero/offload.py) is finished here."""
+        if self.host_step is not None:
+            self.host_step.wait_all()
+
+    def host_unit_order(self):
+        """Units in the order the next forward needs them: the ``#rest`` group (parameters read
+        outside any hooked module) first, then the recorded forward trace, then the rest."""
+        seen, out = set(), []
+        rest = [fg for fg in self.fgroups if fg.name == "#rest"]
+        for fg in rest + [self.fgroups[j] for j in self.trace] + list(self.fgroups):
+            for u in fg.units:
+                if id(u) not in seen:
+                    seen.add(id(u))
+                    out.append(u)
+        return out
 
     def step(self, closure=None, lr_kwargs=None):
         self.wait_params()
@@ -807,6 +859,12 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             return
         self._fused_update(coef, skip)
         self.zero_grad_buffers()
+        if self.host_step is not None:
+            for fg in self.fgroups:
+                if fg.name == "#rest":  # read outside any module hook: final before the next forward
+                    self.host_step.wait_units(fg.units)
+            if self.se is not None:
+                self.wait_params()
         if self.se is not None:
             self.se.sync([u.shard for units in self.units for u in units], self._device_masters())
         self._refresh_persistent()
@@ -829,6 +887,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         if self.S == 1:
             return
         units = [u for us in self.units for u in us if u.persistent or (u.keep and u.state == AVAILABLE)]
+        if units:
+            self.wait_params()  # their shards come from the (possibly asynchronous) host update
         if not units:
             return
         if len(units) == 1:

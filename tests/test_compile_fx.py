@@ -55,8 +55,19 @@ def _train(rank, world, compiled, stage, gas, model_kind):
             out["z3"] = {k: {kk: v.get(kk) for kk in ("fw", "bw", "reduces", "params")} for k, v in fx.graphs.items()}
             out["stats"] = dict(fx.stats)
     if stage == 3:
+        from shuffle_exchange_amd.runtime.zero.stage3 import RELEASED
+        released = [p for us in eng.optimizer.units for u in us if u.state == RELEASED for p in u.params]
+        # between steps a released parameter reads as an empty tensor (eager ZeRO-3 semantics), in
+        # graph mode too -- never as a full-shape view of freed storage
+        out["released_numels"] = sorted({p.numel() for p in released})
         out["params"] = [v for _, v in sorted(eng._zero3_consolidated_16bit_state_dict().items())
                          if v.dtype.is_floating_point]
+        if compiled:  # and the next compiled step still runs (relinked before the forward)
+            x = torch.randint(0, 128, (2, 16), generator=g) if model_kind == "llama" else torch.randn(2, 16, generator=g)
+            loss = eng(x, labels=x) if model_kind == "llama" else eng(x).pow(2).mean()
+            eng.backward(loss)
+            eng.step()
+            out["after_extra_step"] = sorted({p.numel() for p in released})
     return out
 
 
@@ -168,3 +179,5 @@ def test_fx_zero3_graph_compiler_matches_eager(model_kind, gas):
         assert fw > 0 and bw > 0, c["z3"]
         assert sum(v["reduces"] for v in c["z3"].values()) >= 1
         assert c["stats"]["fetch"] > 0 and c["stats"]["release"] > 0
+        assert c["released_numels"] == [0] and e["released_numels"] == [0], (c["released_numels"], e["released_numels"])
+        assert c["after_extra_step"] == [0]

@@ -202,3 +202,36 @@ def test_client_scheduler_survives_twin_flow_split():
         opt.step()
         sch.step()
     assert [g["lr"] for g in opt.param_groups] == [0.25, 0.25, 2.0 * 0.2]
+
+
+def _case_async(rank, world, async_on, gas, clip):
+    os.environ["SXE_OFFLOAD_ASYNC"] = "1" if async_on else "0"
+    os.environ["SXE_OFFLOAD_TRACE"] = "1"
+    import shuffle_exchange_amd as sxe
+    from ._dist_cases import global_batches, tiny_llama, full_params
+    model, cfg = tiny_llama(0)
+    ds = _cfg(3, clip=clip)
+    ds["gradient_accumulation_steps"] = gas
+    ds["zero_optimization"]["stage3_param_persistence_threshold"] = 0
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    hs = eng.optimizer.host_step
+    for b in global_batches(cfg, world * gas, 2, 16, 3):
+        for m in range(gas):
+            part = b[m * 2 * world:(m + 1) * 2 * world]
+            x = part[rank * 2:(rank + 1) * 2]
+            eng.backward(eng(x, labels=x))
+            eng.step()
+    was_async = hs._worker is not None or bool(hs.trace and "waits" in hs.trace[-1])
+    return {"params": full_params(eng), "async": was_async}
+
+
+@pytest.mark.parametrize("gas,clip", [(1, 0.0), (2, 1.0)])
+def test_async_host_update_is_bit_identical(gas, clip):
+    """ZeRO-3 + CPU optimizer offload: the asynchronous host update (worker thread, per-unit waits in
+    the next forward) gives exactly the parameters of the synchronous one."""
+    a = run_dist(_case_async, 2, True, gas, clip)
+    s = run_dist(_case_async, 2, False, gas, clip)
+    assert a[0]["async"] and not s[0]["async"]
+    for ra, rs in zip(a, s):
+        for k in rs["params"]:
+            assert torch.equal(ra["params"][k], rs["params"][k]), k
