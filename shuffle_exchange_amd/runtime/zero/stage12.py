@@ -29,6 +29,7 @@ from ..torch_autocast import split_by_comm_dtype, unit_comm_dtype
 
 
 class ZeroStage12Optimizer(ZeroOptimizerBase):
+    supports_overlapped_step = True  # zero/base.py _overlapped_update
     def __init__(self, init_optimizer, *, stage=2, loss_scaler, clip_grad=0.0, dp_ranks=None, dp_group=None,
                  reduce_bucket_size=500_000_000, communication_data_type=None, overlap_comm=True,
                  shuffle_exchange_cfg=None, method=None, slice_count=None, rings=None, shuffle_step=None,
@@ -195,6 +196,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         self.micro_step_boundary = bool(flag)
 
     def backward_prologue(self):
+        self.drain_step()  # the update read the fp32 gradient accumulators the backward rewrites
         for units in self.units:
             for u in units:
                 u.begin_backward()
@@ -323,11 +325,23 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         stream = self.comm_stream if self._module_units is not None else None
         if stream is not None:
             stream.wait_stream(torch.cuda.current_stream())
+        evs = self.__dict__.get("_step_events") or {}
+        if evs and (self.se is not None or stream is None):
+            self.drain_step()  # chunks needed all at once (inter-slice sync) / no per-unit consumer
+            if stream is not None:
+                stream.wait_stream(torch.cuda.current_stream())
+            evs = {}
         with get_accelerator().stream(stream):
             if self.se is not None:
                 # one packed inter-slice collective per step for all chunks (Gossip: one plan)
                 self.se.sync([u.shard for u in units], masters)
             for i, u in enumerate(units):
+                ev = evs.pop(u, None)  # this unit's overlapped update (zero/base.py)
+                if ev is not None and u.topo.S > 1:
+                    stream.wait_event(ev)
+                elif ev is not None:  # nothing to gather: the forward hook of its module waits
+                    self._pending_events[u] = ev
+                    continue
                 if u.topo.S > 1:
                     dist.all_gather_into_tensor(u.flat, u.shard, group=u.topo.slice_group)
                 if stream is not None:
@@ -341,6 +355,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         self._drain_pending()
 
     def _drain_pending(self):
+        self.drain_step()
         if self._pending_events:
             cur = torch.cuda.current_stream()
             for ev in self._pending_events.values():

@@ -446,6 +446,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 self._observed.append(fg.idx)
             if self.host_step is not None:
                 self.host_step.wait_units(fg.units)  # asynchronous host update (zero/offload.py)
+            for u in fg.units:
+                self.wait_step_unit(u)  # overlapped device update (zero/base.py)
             self._fetch(fg, wait=True)
             self._prefetch_after(fg, backward=self._in_bwd)
             if self.tracer is not None and not self._in_bwd:
@@ -553,7 +555,10 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         cur = torch.cuda.current_stream() if u.flat.is_cuda else None  # shard may be host-resident (offload_param)
         st = self.ag_stream
         if st is not None:
+            self.wait_step_unit(u, st)
             st.wait_stream(cur)
+        elif cur is not None:
+            self.wait_step_unit(u)
         with get_accelerator().stream(st):
             u.flat.untyped_storage().resize_(u.padded * u.flat.element_size())
             if not getattr(self, "graph_mode", False) or getattr(u, "graph_unlinked", False):
@@ -789,6 +794,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             self.tracer.on_forward_start()
 
     def backward_prologue(self):
+        self.drain_step()
         if self.host_step is not None:
             self.host_step.before_backward()
         for units in self.units:
@@ -827,10 +833,15 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
 
     # ------------------------------------------------------------------------------------------ step
     supports_async_host_step = True
+    supports_overlapped_step = True  # zero/base.py _overlapped_update
+
+    def step_unit_order(self):
+        return self.host_unit_order()
 
     def wait_params(self):
         """Nothing in flight across steps on the device (the update runs on the compute stream);
         an asynchronous host-offload update (zero/offload.py) is finished here."""
+        self.drain_step()
         if self.host_step is not None:
             self.host_step.wait_all()
 
@@ -859,12 +870,14 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             return
         self._fused_update(coef, skip)
         self.zero_grad_buffers()
-        if self.host_step is not None:
-            for fg in self.fgroups:
-                if fg.name == "#rest":  # read outside any module hook: final before the next forward
+        for fg in self.fgroups:
+            if fg.name == "#rest":  # read outside any module hook: final before the next forward
+                if self.host_step is not None:
                     self.host_step.wait_units(fg.units)
-            if self.se is not None:
-                self.wait_params()
+                for u in fg.units:
+                    self.wait_step_unit(u)
+        if self.se is not None:
+            self.wait_params()
         if self.se is not None:
             self.se.sync([u.shard for units in self.units for u in units], self._device_masters())
         self._refresh_persistent()
