@@ -73,3 +73,33 @@ def test_v02_world_size_from_env(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "16")
     b, valid, mb = compute_elastic_config(cfg, return_microbatch=True)
     assert (b, mb) == (960, 4)
+
+
+def test_elastic_agent_monitor_decisions():
+    """The agent's monitor tick (reference elasticity/elastic_agent.py:127-189): failures and shrunk
+    membership (dead heartbeat / fewer participants) restart against max_restarts, grown membership
+    restarts for free, success exits."""
+    from shuffle_exchange_amd.elasticity.elastic_agent import (FAIL, RESTART, RESTART_FREE, SUCCEED, CONTINUE,
+                                                               monitor_decision)
+    assert monitor_decision("SUCCEEDED", 2, 2, 0, 0, 3) == SUCCEED
+    assert monitor_decision("HEALTHY", 2, 2, 0, 0, 3) == CONTINUE
+    assert monitor_decision("HEALTHY", 2, 2, 0, 1, 0) == RESTART_FREE     # joiners: not counted
+    assert monitor_decision("FAILED", 2, 2, 0, 0, 1) == RESTART
+    assert monitor_decision("UNHEALTHY", 2, 2, 0, 0, 0) == FAIL
+    assert monitor_decision("HEALTHY", 3, 2, 0, 0, 1) == RESTART          # a participant left
+    assert monitor_decision("HEALTHY", 2, 2, 1, 0, 1) == RESTART          # a dead heartbeat
+    assert monitor_decision("HEALTHY", 2, 2, 1, 0, 0) == FAIL
+
+
+def test_elastic_agent_rdzv_view_counts_dead_heartbeats():
+    import datetime
+    import types
+    from shuffle_exchange_amd.elasticity.elastic_agent import _rdzv_view
+    now = datetime.datetime(2026, 1, 1, 12, 0, 0)
+    st = types.SimpleNamespace(participants={"a": 0, "b": 1},
+                               last_heartbeats={"a": now, "b": now - datetime.timedelta(seconds=100)})
+    h = types.SimpleNamespace(_state_holder=types.SimpleNamespace(state=st),
+                              _settings=types.SimpleNamespace(keep_alive_interval=datetime.timedelta(seconds=5),
+                                                              keep_alive_max_attempt=3))
+    assert _rdzv_view(h, now) == (2, 1)
+    assert _rdzv_view(types.SimpleNamespace()) == (None, 0)

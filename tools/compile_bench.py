@@ -7,7 +7,7 @@ graph executed as generated Python over the same HIP kernels, gradients handed t
 by in-graph reduce nodes -- against the eager engine with its autograd hooks. The ZeRO-3
 gather / release / prefetch placement itself is pinned by the gloo tests
 (tests/test_compile_fx.py).
-  python tools/compile_bench.py [--layers 4] [--seq 2048] [--mbs 2] [--stages 1,2,3] [--steps 5]
+  python tools/compile_bench.py [--layers 4] [--seq 2048] [--mbs 2] [--stages 1,2,3] [--steps 5] [--offload-param]
 """
 import argparse
 import gc
@@ -27,10 +27,14 @@ def run(stage, compiled, a):
     cfg = llama_config("llama3-8b", num_hidden_layers=a.layers)
     torch.manual_seed(0)
     model = LlamaForCausalLM(cfg).to(device="cuda", dtype=torch.bfloat16)
+    z = {"stage": stage, "reduce_bucket_size": 500_000_000}
+    if stage == 3 and a.offload_param:
+        # parameters on the host: even one GPU gathers every unit (H2D) per use, which is where the
+        # graph compiler's in-graph prefetch / release placement can show up
+        z.update({"offload_param": {"device": "cpu", "pin_memory": True}, "stage3_param_persistence_threshold": 0})
     ds = {"train_micro_batch_size_per_gpu": a.mbs, "bf16": {"enabled": True},
           "optimizer": {"type": "AdamW", "params": {"lr": 1e-5}},
-          "zero_optimization": {"stage": stage, "reduce_bucket_size": 500_000_000},
-          "compile": {"deepcompile": True, "fx_zero3": True}}
+          "zero_optimization": z, "compile": {"deepcompile": True, "fx_zero3": True}}
     eng, _, _, _ = sxe.initialize(model=model, config=ds)
     if compiled:
         eng.compile()
@@ -51,7 +55,8 @@ def run(stage, compiled, a):
         loss = step()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / a.steps
-    out = {"stage": stage, "compiled": compiled, "ms_per_step": round(ms, 2),
+    out = {"stage": stage, "offload_param": bool(stage == 3 and a.offload_param), "compiled": compiled,
+           "ms_per_step": round(ms, 2),
            "tokens_per_s": round(a.mbs * a.seq * 1e3 / ms, 1), "loss": round(float(loss.detach()), 4)}
     if compiled:
         fx = eng.compile_plan["fx"]
@@ -72,6 +77,7 @@ def main():
     ap.add_argument("--stages", default="1,2,3")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--offload-param", action="store_true", help="ZeRO-3 with offload_param cpu")
     a = ap.parse_args()
     import shuffle_exchange_amd as sxe
     sxe.init_distributed(verbose=False)
