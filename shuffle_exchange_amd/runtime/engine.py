@@ -902,6 +902,8 @@ class SXEEngine(nn.Module):
         if self.progressive_layer_drop is not None:
             self.progressive_layer_drop.update_state(self.global_steps + 1)
         if self.quantizer is not None and self.zero_optimization_stage() < 3:
+            if hasattr(self.optimizer, "drain_step"):
+                self.optimizer.drain_step()  # MoQ rewrites the weights the overlapped update writes
             self.quantizer.quantize([[p for p in self.module.parameters() if p.requires_grad]], overflow)
         self.optimizer.zero_grad()
         skip_t = getattr(self.optimizer, "_skip_t", None)

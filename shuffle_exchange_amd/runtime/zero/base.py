@@ -291,6 +291,7 @@ class ZeroOptimizerBase:
             self._step_events = {}
         ss = self._step_stream
         ss.wait_stream(torch.cuda.current_stream())
+        self._step_inflight = True
         rank = {id(u): r for r, u in enumerate(self.step_unit_order())}
         order = sorted(units, key=lambda u: rank.get(id(u), len(rank)))
         with acc.stream(ss):
@@ -314,12 +315,12 @@ class ZeroOptimizerBase:
             (stream or torch.cuda.current_stream()).wait_event(ev)
 
     def drain_step(self):
-        """The current stream waits for every pending overlapped update."""
-        evs = self.__dict__.get("_step_events")
-        if evs:
-            cur = torch.cuda.current_stream()
-            cur.wait_stream(self._step_stream)
-            evs.clear()
+        """The current stream waits for every pending overlapped update (and the accumulator
+        zeroing queued behind it), whether or not its per-unit events were consumed."""
+        if self.__dict__.get("_step_inflight"):
+            torch.cuda.current_stream().wait_stream(self._step_stream)
+            self._step_events.clear()
+            self._step_inflight = False
 
     def _lamb_segments(self, g):
         """Per-parameter segments of group g's flat master on this rank (cached): LAMB's trust
@@ -453,6 +454,13 @@ class ZeroOptimizerBase:
         self._offloaded = {}
 
     def zero_grad_buffers(self):
+        if self.__dict__.get("_step_inflight"):
+            # the overlapped update still reads the accumulators: zero them behind it, on its stream
+            from ...accelerator import get_accelerator
+            with get_accelerator().stream(self._step_stream):
+                for gr in self.grads:
+                    gr.zero_()
+            return
         for gr in self.grads:
             gr.zero_()
 

@@ -412,6 +412,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         return out
 
     def state_dict(self):
+        self.wait_params()
         self._host_materialize()
         return {
             "loss_scaler": self.loss_scaler.state_dict(),
@@ -429,6 +430,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         }
 
     def load_state_dict(self, sd, load_optimizer_states=True, load_from_fp32_weights=True):
+        self.wait_params()
         self.loss_scaler.load_state_dict(sd["loss_scaler"])
         self.clip_grad = sd.get("clip_grad", self.clip_grad)
         self._host_materialize()
