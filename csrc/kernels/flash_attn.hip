@@ -234,10 +234,14 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const b
                                          f32x16 (&oacc)[D / 32], float& m, float& l, float c, int kbase, int qpos,
                                          int r, int h, int lane, bool diag, bool tail, int kvlen, const uint8_t* lrow,
                                          int blk) {
+  // causal diagonal tile whose second 32-key half lies entirely above this wave's last query
+  // (the wave's queries start at the tile's first key): that half's QK^T and PV MFMAs are skipped
+  const bool skip1 = MASK && diag && !tail && lrow == nullptr && kbase + 32 > qpos + QW - 1;
   f32x16 s[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     s[j] = zero16();
+    if (j == 1 && skip1) break;
 #pragma unroll
     for (int t2 = 0; t2 < D / 16; ++t2) s[j] = mfma(lds_row16<D>(kt, 32 * j + r, 2 * t2 + h), qf[t2], s[j]);
   }
@@ -292,13 +296,15 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const b
       for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
   }
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int j = 0; j < 2; ++j) {
+    if (j == 1 && skip1) break;  // its p are all exp2(-inf) = 0
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 pb = acc_to_b(s[j], s2);
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt) oacc[dt] = mfma(lds_trA<D>(vt, 32 * j + 16 * s2, dt, lane), pb, oacc[dt]);
     }
+  }
 }
 
 // Waves per workgroup (each 32 queries): NWF = 8 (256 queries; one workgroup of 2 waves per SIMD
@@ -455,8 +461,10 @@ __device__ __forceinline__ void dq_tile(const char* kt, const char* vt, const bf
                                         int kvlen, const uint8_t* lay_row, int blk) {
   int dd = kbase + 4 * h - qpos - r, dl = kbase + 4 * h - kvlen;  // see fwd_tile
   if (MASK) asm volatile("" : "+v"(dd), "+v"(dl));
+  const bool skip1 = MASK && diag && !tail && lay_row == nullptr && kbase + 32 > qpos + QW - 1;  // see fwd_tile
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
+    if (j == 1 && skip1) break;
     f32x16 s = zero16(), dp = zero16();
 #pragma unroll
     for (int t2 = 0; t2 < D / 16; ++t2) {
