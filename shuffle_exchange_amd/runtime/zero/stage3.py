@@ -847,14 +847,17 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
 
     def host_unit_order(self):
         """Units in the order the next forward needs them: the ``#rest`` group (parameters read
-        outside any hooked module) first, then the recorded forward trace, then the rest."""
+        outside any hooked module) first -- after the small resident units the post-step refresh
+        all-gathers when the partition has several ranks --, then the recorded forward trace,
+        then the rest."""
         seen, out = set(), []
         rest = [fg for fg in self.fgroups if fg.name == "#rest"]
-        for fg in rest + [self.fgroups[j] for j in self.trace] + list(self.fgroups):
-            for u in fg.units:
-                if id(u) not in seen:
-                    seen.add(id(u))
-                    out.append(u)
+        groups = rest + [self.fgroups[j] for j in self.trace] + list(self.fgroups)
+        resident = [u for fg in groups for u in fg.units if u.persistent or u.keep]  # _refresh_persistent's
+        for u in (resident if self.S > 1 else []) + [u for fg in groups for u in fg.units]:
+            if id(u) not in seen:
+                seen.add(id(u))
+                out.append(u)
         return out
 
     def step(self, closure=None, lr_kwargs=None):
@@ -900,10 +903,14 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         if self.S == 1:
             return
         units = [u for us in self.units for u in us if u.persistent or (u.keep and u.state == AVAILABLE)]
-        if units:
-            self.wait_params()  # their shards come from the (possibly asynchronous) host update
         if not units:
             return
+        # their shards come from the (possibly asynchronous) update: wait for exactly these units,
+        # which the update order puts first (host_unit_order), not for the whole update
+        if self.host_step is not None:
+            self.host_step.wait_units(units)
+        for u in units:
+            self.wait_step_unit(u)
         if len(units) == 1:
             u = units[0]
             dist.all_gather_into_tensor(u.flat, u.shard, group=self.topo.slice_group)
