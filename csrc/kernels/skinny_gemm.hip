@@ -19,7 +19,6 @@
 //    flight, so the norm / gated-activation launches (4-5 us each at batch 1, latency-bound) are
 //    gone from the decode layer. Workgroup 0 also writes the new residual stream h = x + res.
 #include "sxe_common.h"
-#include <map>
 #include <torch/library.h>
 
 namespace sxe {
@@ -70,13 +69,6 @@ struct ProArgs {
   const int64_t* rslots;
   unsigned short* rcache;
   int rnq, rnkv, rbs;
-  // split-K (ks > 1, bf16 kernel): workgroup blockIdx.x covers tile blockIdx.x % tiles and K part
-  // blockIdx.x / tiles; wave 0 of each writes its partial tile to skws and bumps skcnt[tile]; the
-  // last of the ks arrivals sums the partials in K-part order (deterministic), runs the epilogue
-  // and resets the counter for the next launch
-  float* skws;
-  int* skcnt;
-  int ks;
 };
 
 // output column of lane `col` in tile `tile` (identity unless the RoPE epilogue pairs columns)
@@ -265,15 +257,13 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(const unsigned sho
   extern __shared__ __attribute__((aligned(16))) unsigned short act_lds[];  // PRO_*: the M x K input
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, g = lane >> 4;
-  const int ks = pro.ks > 1 ? pro.ks : 1;
-  const int tiles = gridDim.x / ks, tile = blockIdx.x % tiles, kpart = blockIdx.x / tiles;
+  const int tile = blockIdx.x;
   const int n = MODE == PRO_RMS ? out_col(pro, tile, col) : tile * 16 + col;
   const bool wok = n < N, xok = col < M;
   const unsigned short* wrow = w + (int64_t)(wok ? n : 0) * ldw;
   const unsigned short* xrow = MODE == PRO_NONE ? x + (int64_t)(xok ? col : 0) * ldx
                                                 : act_lds + (int64_t)(xok ? col : 0) * K;
-  const int ss_part = NW * ss_per_wave;  // super-steps of one K part
-  const int ss0 = kpart * ss_part + wave * ss_per_wave;
+  const int ss0 = wave * ss_per_wave;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   __shared__ float rinv[kProMaxM];
   Frag cur, nxt;
@@ -294,8 +284,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(const unsigned sho
     Frag nx2;
     load_w(cur, wrow, wok, ss0 * kSS + g * 8, K);
     if (ss_per_wave > 1) load_w(nxt, wrow, wok, (ss0 + 1) * kSS + g * 8, K);
-    build_act<MODE, NW * 64>(x, ldx, M, K, min(K, kpart * ss_part * kSS), min(K, (kpart + 1) * ss_part * kSS), pro,
-                             act_lds, rinv);
+    build_act<MODE, NW * 64>(x, ldx, M, K, 0, K, pro, act_lds, rinv);
     for (int i = 0; i < ss_per_wave; ++i) {
       if (i + 2 < ss_per_wave) load_w(nx2, wrow, wok, (ss0 + i + 2) * kSS + g * 8, K);
       load_x(cur, xrow, xok, (ss0 + i) * kSS + g * 8, K);
@@ -317,29 +306,6 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(const unsigned sho
       t[1] += u[1];
       t[2] += u[2];
       t[3] += u[3];
-    }
-    if (ks > 1) {
-      f32x4* part = reinterpret_cast<f32x4*>(pro.skws) + (int64_t)tile * ks * 64;
-      part[kpart * 64 + lane] = t;
-      __threadfence();  // release the partial before the arrival count (agent scope: all XCDs)
-      int arrived = 0;
-      if (lane == 0) arrived = atomicAdd(pro.skcnt + tile, 1);
-      arrived = __shfl(arrived, 0, 64);
-      if (arrived != ks - 1) return;  // not the last part of this tile
-      __threadfence();  // acquire the other parts' partials
-      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-      for (int q = 0; q < ks; ++q) {
-        f32x4 u = t;
-        if (q != kpart) {
-          const float* src = reinterpret_cast<const float*>(part + q * 64 + lane);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) u[e] = __hip_atomic_load(src + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sum[e] += u[e];
-      }
-      t = sum;
-      if (lane == 0) __hip_atomic_store(pro.skcnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (MODE == PRO_RMS && pro.rcos != nullptr) {  // RoPE epilogue (no bias: checked on the host)
 #pragma unroll
@@ -473,80 +439,12 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_fp8w_kernel(const unsigne
   }
 }
 
-// Split-K plan for the bf16 kernel. The decode GEMMs with few 16-column tiles (the QKV projection:
-// 384 tiles, o_proj: 256) leave CUs with uneven work (384 tiles = two workgroups on half the CUs,
-// one on the others) or one 4-wave workgroup per CU (too few loads in flight to cover HBM latency);
-// splitting K in ks parts gives every CU the same share and more streams. SXE_SKINNY_SPLITK (read per
-// call): 0 off, 1 auto (shapes with fewer than two tiles per CU), 2 / 4 forced.
-//
-// Workspace ownership (partials [tiles, ks, 64 lanes, 4] fp32 + one arrival counter per tile, reset
-// by the tile's last arrival):
-//  * eager launches use a workspace per (device, stream): two streams never share counters, and a
-//    workspace that must grow is replaced through the stream-ordered caching allocator (its last
-//    user ran on the same stream);
-//  * a launch being captured into a HIP graph gets a workspace of its own, allocated inside the
-//    capture from the graph's private pool (zeroed counters by a captured memset): it lives as long
-//    as the graph, and no later eager call can free or resize what a graph replays.
-struct SplitWs {
-  at::Tensor ws, cnt;
-};
-
-inline int split_mode() {
-  const char* e = std::getenv("SXE_SKINNY_SPLITK");
-  return (e == nullptr || *e == 0) ? 0 : std::atoi(e);
-}
-
-// returns ks (1 = no split) and sets nw / ss_per_wave / the ProArgs split fields
-inline int plan_split(int tiles, int ss_total, int& nw, int& spw, ProArgs& pro, const at::Tensor& like) {
-  int ks = 1;
-  const int mode = split_mode();
-  if (mode == 1 && tiles < 2 * kNumCUs) ks = tiles <= kNumCUs / 2 ? 4 : 2;
-  else if (mode == 2 || mode == 4) ks = mode;
-  while (ks > 1) {
-    const int part = (ss_total + ks - 1) / ks;
-    nw = pick_nw(tiles * ks, part, 4, 1);
-    if (part >= nw) break;
-    ks /= 2;
-  }
-  if (ks > 1) {
-    const int64_t need = (int64_t)tiles * ks * 64 * 4;
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    unsigned long long cap_id = 0;
-    SXE_HIP_CHECK(hipStreamGetCaptureInfo(cur_stream(), &st, &cap_id));
-    if (st != hipStreamCaptureStatusNone) {
-      // graph-owned workspace (the caching allocator serves captures from the graph's pool), shared
-      // by the capture's launches -- they replay in stream order -- and grown by a new allocation
-      // (earlier nodes keep theirs: nothing a graph references is ever freed)
-      static std::map<unsigned long long, SplitWs> per_capture;
-      static std::vector<SplitWs> retired;
-      SplitWs& sw = per_capture[cap_id];
-      if (!sw.ws.defined() || sw.ws.numel() < need || sw.cnt.numel() < tiles) {
-        if (sw.ws.defined()) retired.push_back(sw);
-        sw.ws = at::empty({need}, like.options().dtype(at::kFloat));
-        sw.cnt = at::zeros({tiles}, like.options().dtype(at::kInt));
-      }
-      pro.skws = sw.ws.data_ptr<float>();
-      pro.skcnt = sw.cnt.data_ptr<int>();
-    } else {
-      static std::map<std::pair<int, hipStream_t>, SplitWs> per_stream;
-      SplitWs& sw = per_stream[{like.get_device(), cur_stream()}];
-      if (!sw.ws.defined() || sw.ws.numel() < need || sw.cnt.numel() < tiles) {
-        const int64_t cap = std::max<int64_t>(need, (int64_t)4096 * 4 * 64 * 4);
-        sw.ws = at::empty({cap}, like.options().dtype(at::kFloat));
-        sw.cnt = at::zeros({std::max<int64_t>(tiles, 4096)}, like.options().dtype(at::kInt));
-      }
-      pro.skws = sw.ws.data_ptr<float>();
-      pro.skcnt = sw.cnt.data_ptr<int>();
-    }
-    pro.ks = ks;
-    const int part = (ss_total + ks - 1) / ks;
-    spw = (part + nw - 1) / nw;
-    return ks;
-  }
+// Waves per workgroup and super-steps per wave of the bf16 kernel. (A split-K variant -- K split
+// over 2-4 workgroups with a last-arrival reduction -- was measured and removed: 5.9 vs 3.7 ms per
+// batch-1 decode step, profiles/r05/decode_splitk_ab.log.)
+inline void plan(int tiles, int ss_total, int& nw, int& spw) {
   nw = pick_nw(tiles, ss_total, 4, 1);
   spw = (ss_total + nw - 1) / nw;
-  pro.ks = 1;
-  return 1;
 }
 
 }  // namespace sg
@@ -575,12 +473,12 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, const c10::opti
   const int tiles = (N + 15) / 16;
   int nw = 4, ss_per_wave = 1;
   sg::ProArgs pro{};
-  const int ks = sg::plan_split(tiles, ss_total, nw, ss_per_wave, pro, x);
+  sg::plan(tiles, ss_total, nw, ss_per_wave);
   auto* xp = reinterpret_cast<const unsigned short*>(x.data_ptr());
   auto* wp = reinterpret_cast<const unsigned short*>(w.data_ptr());
   auto* yp = reinterpret_cast<unsigned short*>(y.data_ptr());
 #define SXE_SG_LAUNCH(NW)                                                                                  \
-  hipLaunchKernelGGL(sg::skinny_gemm_kernel<NW>, dim3(tiles * ks), dim3(NW * 64), 0, cur_stream(), xp,          \
+  hipLaunchKernelGGL(sg::skinny_gemm_kernel<NW>, dim3(tiles), dim3(NW * 64), 0, cur_stream(), xp,               \
                      x.stride(0), wp, w.stride(0), bp, yp, y.stride(0), M, N, K, ss_per_wave, pro)
   if (nw == 4) SXE_SG_LAUNCH(4);
   else SXE_SG_LAUNCH(8);
@@ -718,12 +616,12 @@ static std::vector<at::Tensor> skinny_gemm_pro_impl(const at::Tensor& x, const c
   if (!fp8) {
     const int ss_total = (K + sg::kSS - 1) / sg::kSS;
     int nw = 4, spw = 1;
-    const int ks = sg::plan_split(tiles, ss_total, nw, spw, pro, x);
+    sg::plan(tiles, ss_total, nw, spw);
     auto* wp = reinterpret_cast<const unsigned short*>(w.data_ptr());
 #define SXE_SGP(NW, MODE)                                                                                            \
   do {                                                                                                               \
     set(reinterpret_cast<const void*>(&sg::skinny_gemm_kernel<NW, MODE>), 0, NW == 8, mi);                           \
-    hipLaunchKernelGGL((sg::skinny_gemm_kernel<NW, MODE>), dim3(tiles * ks), dim3(NW * 64), lds, cur_stream(), xp,    \
+    hipLaunchKernelGGL((sg::skinny_gemm_kernel<NW, MODE>), dim3(tiles), dim3(NW * 64), lds, cur_stream(), xp,         \
                        x.stride(0), wp, w.stride(0), bp, yp, y.stride(0), M, N, K, spw, pro);                         \
   } while (0)
     if (mode == sg::PRO_RMS) { if (nw == 4) SXE_SGP(4, sg::PRO_RMS); else SXE_SGP(8, sg::PRO_RMS); }
@@ -811,12 +709,12 @@ at::Tensor skinny_gemm_merge(const at::Tensor& part_o, const at::Tensor& part_ml
   if (!fp8) {
     const int ss_total = (K + sg::kSS - 1) / sg::kSS;
     int nw = 4, spw = 1;
-    const int ks = sg::plan_split(tiles, ss_total, nw, spw, pro, part_o);
+    sg::plan(tiles, ss_total, nw, spw);
     auto* wp = reinterpret_cast<const unsigned short*>(w.data_ptr());
 #define SXE_SGM(NW)                                                                                                  \
   do {                                                                                                               \
     set(reinterpret_cast<const void*>(&sg::skinny_gemm_kernel<NW, sg::PRO_MERGE>), 0, NW == 8);                      \
-    hipLaunchKernelGGL((sg::skinny_gemm_kernel<NW, sg::PRO_MERGE>), dim3(tiles * ks), dim3(NW * 64), lds,             \
+    hipLaunchKernelGGL((sg::skinny_gemm_kernel<NW, sg::PRO_MERGE>), dim3(tiles), dim3(NW * 64), lds,                  \
                        cur_stream(),                                                                                 \
                        nullptr, K, wp, w.stride(0), bp, yp, y.stride(0), M, N, K, spw, pro);                          \
   } while (0)

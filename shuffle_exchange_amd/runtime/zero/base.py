@@ -270,17 +270,19 @@ class ZeroOptimizerBase:
                     u.shard.copy_(u.master)
 
     # ------------------------------------------------------------ overlapped device update
-    # SXE_STEP_OVERLAP (default on for ZeRO-1/2/3 with fused Adam on the GPU): the update runs on a
-    # side stream as one launch per unit in the order the next forward needs the units, and every
-    # consumer waits for exactly its own units' event (forward pre-hooks, the post-step gathers), so
-    # the HBM-bound update of the later units overlaps the MFMA-bound forward of the earlier ones
-    # instead of running before it. Same kernel, same math per element: bit-identical results.
+    # SXE_STEP_OVERLAP=1 (opt-in, ZeRO-1/2/3 with fused Adam on the GPU): the update runs on a side
+    # stream as one launch per unit in the order the next forward needs the units, and every
+    # consumer waits for exactly its own units' event (forward pre-hooks, the post-step gathers),
+    # so the HBM-bound update of the later units can run beside the MFMA-bound forward of the
+    # earlier ones. Same kernel, same math per element: bit-identical results. Off by default: on
+    # one MI355X the hipBLASLt GEMMs leave no room for concurrent update workgroups -- 25,363 vs
+    # 25,387 tokens/s (Llama-3-8B) and 24,962 vs 25,020 (Mixtral), profiles/r05/step_overlap_*.log.
     def _overlap_step_ok(self, units):
         if not getattr(self, "supports_overlapped_step", False) or not units or not units[0].master.is_cuda:
             return False
         if not hasattr(self, "_overlap_on"):
             import os
-            self._overlap_on = os.environ.get("SXE_STEP_OVERLAP", "1") == "1"
+            self._overlap_on = os.environ.get("SXE_STEP_OVERLAP", "0") == "1"
         return self._overlap_on
 
     def _overlapped_update(self, units, adam, coef, skip):

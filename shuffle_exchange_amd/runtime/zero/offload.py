@@ -142,14 +142,18 @@ class HostOptimizerStep:
         # kept in ``self.trace`` (tools/offload_timeline.py turns it into a table)
         self.trace_on = os.environ.get("SXE_OFFLOAD_TRACE", "0") == "1"
         self.trace = []
-        # Asynchronous update (SXE_OFFLOAD_ASYNC, default on; optimizers that declare
+        # Asynchronous update (SXE_OFFLOAD_ASYNC=1, opt-in; optimizers that declare
         # ``supports_async_host_step``, i.e. ZeRO-3): every unit's gradient crosses PCIe into a pinned
         # host mirror, then a worker thread runs the C++ update unit by unit in the order the next
         # forward needs them and copies each updated bit16 shard back on the H2D stream; step()
         # returns at once and the next forward waits per unit (``wait_units``) instead of for the
-        # whole update -- the host update of the later units runs under the forward of the earlier
-        # ones. Results are bit-identical to the synchronous path (same kernels, same order).
-        self.async_update = os.environ.get("SXE_OFFLOAD_ASYNC", "1") == "1" and self.device == "cpu"
+        # whole update. Results are bit-identical to the synchronous path (same kernels, same
+        # order). Off by default: on the 1-GPU box the forward only waits for the update (the host
+        # update is 10x the forward's time) and the worker's OpenMP team ran the update 6-30 %
+        # slower than the main thread's, 3,765 vs 4,020 tokens/s on llama70b-infinity
+        # (profiles/r05/llama70b-infinity_async_{on,off}.log, timeline
+        # llama70b-infinity_async_trace.jsonl).
+        self.async_update = os.environ.get("SXE_OFFLOAD_ASYNC", "0") == "1" and self.device == "cpu"
         self._worker = None
         self._ready = {}
         self._h2d_ev = {}

@@ -27,72 +27,6 @@ def test_skinny_gemm_matches_fp32(M, N, K, with_bias):
     assert err <= 1e-2 * ref.abs().max().item() + 1e-2, err
 
 
-@pytest.mark.parametrize("mode", ["1", "2", "4"])
-@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 4096), (1000, 14336)])
-def test_split_k_is_repeatable_and_graph_safe(N, K, mode, monkeypatch):
-    """Split-K decode GEMMs (K split over 2-4 workgroups, the last arrival sums the partials in a
-    fixed order and resets its tile counter), forced on through SXE_SKINNY_SPLITK (read per call):
-    back-to-back launches and HIP-graph replays are bit-identical and equal the fp32 reference --
-    also after an eager call on a much larger shape has grown (and replaced) the eager workspace,
-    which a graph must never reference."""
-    monkeypatch.setenv("SXE_SKINNY_SPLITK", mode)
-    g = torch.Generator(device="cuda").manual_seed(N + K)
-    x = torch.randn(1, K, device="cuda", dtype=torch.bfloat16, generator=g)
-    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g)
-    ys = [torch.ops.sxe.skinny_gemm(x, w, None) for _ in range(3)]
-    ref = x.float() @ w.float().t()
-    assert (ys[0].float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item() + 1e-2
-    assert all(torch.equal(ys[0], y) for y in ys[1:])
-    monkeypatch.setenv("SXE_SKINNY_SPLITK", "0")
-    unsplit = torch.ops.sxe.skinny_gemm(x, w, None)
-    monkeypatch.setenv("SXE_SKINNY_SPLITK", mode)
-    assert (ys[0].float() - unsplit.float()).abs().max().item() <= 1e-2 * ref.abs().max().item() + 1e-2
-    out = torch.empty_like(ys[0])
-    graph = torch.cuda.CUDAGraph()
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        torch.ops.sxe.skinny_gemm(x, w, None)  # warm the side stream's own workspace
-    torch.cuda.current_stream().wait_stream(s)
-    with torch.cuda.graph(graph):
-        for _ in range(4):
-            out.copy_(torch.ops.sxe.skinny_gemm(x, w, None))
-    # an eager call with 4x the tiles (forced modes split it) grows the eager workspace
-    big = torch.randn(4 * N, K, device="cuda", dtype=torch.bfloat16, generator=g)
-    yb = torch.ops.sxe.skinny_gemm(x, big, None)
-    torch.cuda.synchronize()
-    for _ in range(3):
-        graph.replay()
-    torch.cuda.synchronize()
-    assert torch.equal(out, ys[0])
-    refb = x.float() @ big.float().t()
-    assert (yb.float() - refb).abs().max().item() <= 1e-2 * refb.abs().max().item() + 1e-2
-
-
-def test_split_k_concurrent_streams_do_not_share_counters(monkeypatch):
-    """Two streams running split-K GEMMs at the same time (each its own workspace + counters)."""
-    monkeypatch.setenv("SXE_SKINNY_SPLITK", "4")
-    g = torch.Generator(device="cuda").manual_seed(11)
-    x = torch.randn(2, 4096, device="cuda", dtype=torch.bfloat16, generator=g)
-    ws = [torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16, generator=g) for _ in range(2)]
-    refs = [x.float() @ w.float().t() for w in ws]
-    streams = [torch.cuda.Stream() for _ in range(2)]
-    for st in streams:
-        st.wait_stream(torch.cuda.current_stream())
-    outs = [[], []]
-    for _ in range(20):
-        for i, st in enumerate(streams):
-            with torch.cuda.stream(st):
-                outs[i].append(torch.ops.sxe.skinny_gemm(x, ws[i], None))
-    for st in streams:
-        torch.cuda.current_stream().wait_stream(st)
-    torch.cuda.synchronize()
-    for i in range(2):
-        for y in outs[i]:
-            assert torch.equal(y, outs[i][0])
-        assert (outs[i][0].float() - refs[i]).abs().max().item() <= 1e-2 * refs[i].abs().max().item() + 1e-2
-
-
 def test_linear_dispatches_skinny_under_no_grad():
     from shuffle_exchange_amd.ops.linear import linear
     w = torch.randn(256, 512, device="cuda", dtype=torch.bfloat16)
