@@ -14,10 +14,9 @@ without the pass, per-parameter grad hooks would all fire after the whole backwa
 The first execution of every graph runs through ``ProfilingInterpreter`` (per-node time and
 memory); the summary is logged and kept in ``engine.compile_plan["fx"]``.
 
-ZeRO-3 keeps the schedule compiler of compile/backend.py: its parameters are partitioned
-(zero-size between uses), which a shape-specialising tracer would have to be taught to see
-through; the ZeRO-3 gather / release / prefetch decisions are made on the recorded schedule
-instead.
+ZeRO-3 builds on this compiler (compile/fx_zero3.py: gather / release / prefetch nodes in the same
+graphs). The reduce nodes address parameters by identity, so a graph is compiled per parameter set
+(``ParamBoundGraph``).
 """
 import itertools
 
@@ -39,6 +38,33 @@ def reduce_grad(grad: torch.Tensor, compiler_id: int, param_id: int) -> None:
 @reduce_grad.register_fake
 def _reduce_grad_fake(grad, compiler_id, param_id):
     return None
+
+
+class ParamBoundGraph:
+    """A Dynamo graph compiled once PER PARAMETER SET. The in-graph reduce (and ZeRO-3 fetch) nodes
+    name parameters by the identities seen when the graph was traced, but Dynamo reuses one compiled
+    frame for every module instance of the same class (a graph break inside a repeated decoder
+    layer compiles the layer's frame once and runs it for each layer, the parameters then being
+    ordinary graph inputs): a graph bound to layer 0 would hand layer 5's gradients to layer 0.
+    Every call looks up the compiled graph of the parameters actually passed in and compiles a new
+    one for an unseen set."""
+
+    def __init__(self, build, example_inputs, pid_of):
+        self.build = build
+        self.slots = [i for i, t in enumerate(example_inputs) if torch.is_tensor(t) and id(t) in pid_of]
+        self.fns = {self._key(example_inputs): build(list(example_inputs))}
+        self._boxed_call = getattr(next(iter(self.fns.values())), "_boxed_call", False)
+
+    def _key(self, args):
+        return tuple(id(args[i]) for i in self.slots)
+
+    def __call__(self, *args):
+        flat = args[0] if len(args) == 1 and isinstance(args[0], list) else args
+        key = self._key(flat)
+        fn = self.fns.get(key)
+        if fn is None:
+            fn = self.fns[key] = self.build(list(flat))
+        return fn(*args)
 
 
 class FXCompiler:
@@ -67,6 +93,9 @@ class FXCompiler:
 
     # ---------------------------------------------------------------------------- the backend
     def backend(self, gm, example_inputs):
+        return ParamBoundGraph(lambda inputs: self.compile_graph(gm, inputs), example_inputs, self.pid_of)
+
+    def compile_graph(self, gm, example_inputs):
         from functorch.compile import make_boxed_func
         from torch._functorch.aot_autograd import aot_module_simplified
         from torch._functorch.partitioners import min_cut_rematerialization_partition
@@ -127,6 +156,8 @@ def compile_fx(engine, cfg, compile_kwargs=None):
             if hasattr(p, a):
                 delattr(p, a)
     if any(p.is_cuda for p in engine.module.parameters()):
+        from ..ops import native
+        native.require_hip()  # loaded before tracing: the dispatch predicates then stay lock-free
         from ..ops import fake_kernels  # noqa: F401  (shape functions of the HIP ops for tracing)
     fx = FXCompiler(engine, cfg)
     kw = {k: v for k, v in (compile_kwargs or {}).items() if k in ("dynamic", "fullgraph")}

@@ -27,6 +27,8 @@ eager, with the collectives at compiler-chosen points. The optimizer runs in gra
 full shapes over freed storage, which is what lets a shape-specialising tracer see them (the
 reference patches FakeTensor for the same reason, compile/patch_fake_tensor.py).
 """
+import logging
+
 import torch
 
 from ..utils.logging import log_dist
@@ -184,7 +186,7 @@ class FXZero3Compiler(FXCompiler):
         self.stats["release"] += 1
 
     # ---------------------------------------------------------------------------- the backend
-    def backend(self, gm, example_inputs):
+    def compile_graph(self, gm, example_inputs):
         from functorch.compile import make_boxed_func
         from torch._functorch.aot_autograd import aot_module_simplified
         from torch._functorch.partitioners import min_cut_rematerialization_partition
@@ -231,11 +233,19 @@ def compile_fx_zero3(engine, cfg, compile_kwargs=None):
             if hasattr(p, a):
                 delattr(p, a)
     if any(p.is_cuda for p in engine.module.parameters()):
+        from ..ops import native
+        native.require_hip()  # loaded before tracing: the dispatch predicates then stay lock-free
         from ..ops import fake_kernels  # noqa: F401
     opt.enter_graph_mode()
     fx = FXZero3Compiler(engine, cfg)
     kw = {k: v for k, v in (compile_kwargs or {}).items() if k in ("dynamic", "fullgraph")}
     kw.setdefault("dynamic", False)
+    # one graph for the whole forward: in graph mode the module hooks are gone, so a module that a
+    # graph break leaves to eager execution would read a released (zero-storage) parameter; Dynamo
+    # then names the break instead of the step failing somewhere inside it
+    if not kw.setdefault("fullgraph", True):
+        log_dist("compile: ZeRO-3 with fullgraph=False -- a graph break that leaves a module to eager "
+                 "execution reads released parameters", ranks=[0], level=logging.WARNING)
     compiled = torch.compile(engine.module, backend=fx.backend, **kw)
     log_dist(f"compile: FX graph compiler (ZeRO-3): {len(opt.fgroups)} fetch groups, gather/release/prefetch "
              f"(depth {fx.prefetch_depth}) and gradient reduce-scatter placed in the graphs", ranks=[0])

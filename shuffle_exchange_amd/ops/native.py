@@ -24,6 +24,11 @@ _state = {"hip": None, "cpu": None, "hip_err": None, "cpu_err": None}
 
 
 def _load(kind, path):
+    # lock-free once decided: the dispatch predicates run inside torch.compile'd regions, and Dynamo
+    # cannot enter a lock (a graph break there splits the model into per-layer frames)
+    done = _state[kind]
+    if done is not None:
+        return done
     with _lock:
         if _state[kind] is not None:
             return _state[kind]

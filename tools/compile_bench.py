@@ -36,6 +36,8 @@ def run(stage, compiled, a):
           "optimizer": {"type": "AdamW", "params": {"lr": 1e-5}},
           "zero_optimization": z, "compile": {"deepcompile": True, "fx_zero3": True}}
     eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    from torch._dynamo.utils import counters
+    counters.clear()
     if compiled:
         eng.compile()
     g = torch.Generator(device="cuda").manual_seed(1)
@@ -62,6 +64,7 @@ def run(stage, compiled, a):
         fx = eng.compile_plan["fx"]
         out["graph_reduces"] = sum(v.get("reduces", 0) for v in fx.graphs.values())
         out["graphs"] = len(fx.graphs)
+        out["graph_breaks"] = sum(counters["graph_break"].values())
     del eng, model
     gc.collect()
     torch.cuda.empty_cache()

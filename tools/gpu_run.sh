@@ -17,6 +17,7 @@
 #   attnprof          rocprofv3 kernel stats of tools/attn_bench.py 1
 #   pmc_attn          rocprofv3 counter passes over tools/pmc_attn.py
 #   pmc               rocprofv3 counter passes over tools/pmc_kernels.py
+#   pmcw=SCRIPT       the same kind of counter passes (plus stall counters) over tools/SCRIPT
 #   decode            tools/decode_bench.py ($DECODE_ARGS)
 #   decodeprof        rocprofv3 kernel trace of eager decode steps
 #   paged             tools/paged_attn_bench.py
@@ -71,6 +72,9 @@ run_step() {  # $1 = name, $2 = log file
     pmc)
       pmc_passes gpurun_out/pmc tools/pmc_kernels.py \
         "p1 SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES;p2 FETCH_SIZE GRBM_GUI_ACTIVE;p3 WRITE_SIZE TCC_HIT_sum" > "$log" 2>&1 ;;
+    pmcw)  # counter passes over an arbitrary workload script: pmcw=tools/pmc_mx.py
+      pmc_passes gpurun_out/pmcw tools/$(basename "$arg") \
+        "w1 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_INST_LDS;w2 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_MISC;w3 FETCH_SIZE GRBM_GUI_ACTIVE;w4 WRITE_SIZE TCC_HIT_sum" > "$log" 2>&1 ;;
     decode) timeout -k 10 700 python tools/decode_bench.py ${DECODE_ARGS:---batches 1,16,64 --modes graphs,graphs+fp8} > "$log" 2>&1 ;;
     decodeprof)
       mkdir -p gpurun_out/decprof
