@@ -3,6 +3,7 @@
 // (ds_read_b64_tr_b16)). See csrc/kernels/flash_attn.hip for the derivation of every map.
 #pragma once
 #include <hip/hip_runtime.h>
+#include "sxe_common.h"
 
 namespace sxe {
 namespace mf {
@@ -63,6 +64,20 @@ __device__ __forceinline__ f32x16 zero16() {
 
 // accumulator register i <-> row within a 32x32 tile for lane half h
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+// Epilogue of a TRANSPOSED accumulator (the weight was the MFMA's A operand, so the 32x32 tile is
+// Y^T): lane (l32, h) owns one output row and registers 4g .. 4g+3 are its columns 8g + 4h + 0..3.
+// `y` points at that row's column 4h of the tile; one 8-byte store per run, no per-element branch
+// or load (a per-element `if` + scale load makes hipcc wait vmcnt(0) -- i.e. for the previous
+// store -- before every element).
+__device__ __forceinline__ void store_acc_t(const f32x16& c, unsigned short* y, float s) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const unsigned lo = (unsigned)f32_to_bf16(c[4 * g] * s) | ((unsigned)f32_to_bf16(c[4 * g + 1] * s) << 16);
+    const unsigned hi = (unsigned)f32_to_bf16(c[4 * g + 2] * s) | ((unsigned)f32_to_bf16(c[4 * g + 3] * s) << 16);
+    *reinterpret_cast<unsigned long long*>(y + 8 * g) = (unsigned long long)lo | ((unsigned long long)hi << 32);
+  }
+}
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 

@@ -139,26 +139,19 @@ __global__ void __launch_bounds__(NTHR, 2) grouped_gemm_kernel(const unsigned sh
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma(b[j], a[i], acc[i][j]);  // Y^T tile: see store_acc_t
       __builtin_amdgcn_s_setprio(0);
     }
   }
-  // ---- epilogue: lane holds column n of 16 rows per accumulator --------------------------------
+  // ---- epilogue: lane holds token row m, 4 runs of 4 columns per accumulator ---------------------
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i) {
+    const int m = lo + wm * 64 + i * 32 + l32;  // lane's token row (transposed accumulators)
+    if (m >= hi) continue;
+    const float sm = scale ? (float)scale[m] : 1.f;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 64 + j * 32 + l32;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = lo + wm * 64 + i * 32 + acc_row(r, h);
-        if (m < hi) {
-          float v = acc[i][j][r];
-          if (scale) v *= (float)scale[m];
-          Y[(int64_t)m * N + n] = f32_to_bf16(v);
-        }
-      }
-    }
+    for (int j = 0; j < 2; ++j) store_acc_t(acc[i][j], Y + (int64_t)m * N + n0 + wn * 64 + j * 32 + 4 * h, sm);
+  }
 }
 
 
@@ -256,24 +249,18 @@ __global__ void __launch_bounds__(128 * WN, 1) grouped_gemm_dp_kernel(const unsi
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma(b[j], a[i], acc[i][j]);  // Y^T tile
       __builtin_amdgcn_s_setprio(0);
     }
   }
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int n = n0 + wn * (BN / WN) + j * 32 + l32;
+  for (int i = 0; i < 4; ++i) {
+    const int m = lo + wm * 128 + i * 32 + l32;
+    if (m >= hi) continue;
+    const float sm = scale ? (float)scale[m] : 1.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = lo + wm * 128 + i * 32 + acc_row(r, h);
-        if (m < hi) {
-          float v = acc[i][j][r];
-          if (scale) v *= (float)scale[m];
-          Y[(int64_t)m * N + n] = f32_to_bf16(v);
-        }
-      }
+    for (int j = 0; j < NJ; ++j)
+      store_acc_t(acc[i][j], Y + (int64_t)m * N + n0 + wn * (BN / WN) + j * 32 + 4 * h, sm);
   }
 }
 }  // namespace dp
@@ -341,25 +328,18 @@ __global__ void __launch_bounds__(NTHR, 2) grouped_gemm_q_kernel(const unsigned 
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma(b[j], a[i], acc[i][j]);  // Y^T tile: see store_acc_t
       __builtin_amdgcn_s_setprio(0);
     }
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i) {
+    const int m = lo + wm * 64 + i * 32 + l32;  // lane's token row (transposed accumulators)
+    if (m >= hi) continue;
+    const float sm = scale ? (float)scale[m] : 1.f;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 64 + j * 32 + l32;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = lo + wm * 64 + i * 32 + acc_row(r, h);
-        if (m < hi) {
-          float v = acc[i][j][r];
-          if (scale) v *= (float)scale[m];
-          Y[(int64_t)m * N + n] = f32_to_bf16(v);
-        }
-      }
-    }
+    for (int j = 0; j < 2; ++j) store_acc_t(acc[i][j], Y + (int64_t)m * N + n0 + wn * 64 + j * 32 + 4 * h, sm);
+  }
 }
 
 }  // namespace gg

@@ -48,14 +48,20 @@ HEAD_DIMS = (64, 128, 256)
 
 
 def _native_dim(D):
-    return next((d for d in HEAD_DIMS if d >= D), None)
+    for d in HEAD_DIMS:  # a plain loop: generator builtins are graph breaks under torch.compile
+        if d >= D:
+            return d
+    return None
 
 
 def _aligned(t):
-    # 16-byte aligned rows: base allocations are 512-B aligned, so the element offset decides (and
-    # unlike data_ptr() it is defined on the fake tensors a graph trace runs on)
-    return (t.stride(-1) == 1 and t.stride(0) % 8 == 0 and t.stride(1) % 8 == 0 and t.stride(2) % 8 == 0
-            and (t.storage_offset() * t.element_size()) % 16 == 0)
+    # 16-byte aligned rows: base allocations are 512-B aligned, so the element offset decides. Under
+    # torch.compile the offset is not traceable (storage_offset() is a graph break): the strides
+    # decide there and the kernel's own host check (flash_attn.hip) refuses a misaligned base loudly.
+    ok = t.stride(-1) == 1 and t.stride(0) % 8 == 0 and t.stride(1) % 8 == 0 and t.stride(2) % 8 == 0
+    if torch.compiler.is_compiling():
+        return ok
+    return ok and (t.storage_offset() * t.element_size()) % 16 == 0
 
 
 def hip_supported(q, k, v):
@@ -64,7 +70,7 @@ def hip_supported(q, k, v):
         return False
     return (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in HEAD_DIMS and q.shape[1] % TILE == 0
             and k.shape[1] % TILE == 0 and k.shape[-1] == q.shape[-1] and v.shape[-1] == q.shape[-1]
-            and q.shape[2] % k.shape[2] == 0 and all(_aligned(t) for t in (q, k, v)))
+            and q.shape[2] % k.shape[2] == 0 and _aligned(q) and _aligned(k) and _aligned(v))
 
 
 def hip_paddable(q, k, v):

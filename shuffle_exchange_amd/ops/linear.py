@@ -33,6 +33,8 @@ SKINNY_MAX_M = int(os.environ.get("SXE_SKINNY_MAX_M", 4))
 
 
 def _skinny(x, weight, bias):
+    if torch.compiler.is_compiling():  # data_ptr() is not traceable; graphs keep the library GEMM
+        return None
     K = x.shape[-1]
     if not (x.is_cuda and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and weight.dim() == 2
             and weight.is_contiguous() and K % 8 == 0 and weight.data_ptr() % 16 == 0):

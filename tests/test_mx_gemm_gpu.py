@@ -107,3 +107,41 @@ def test_skinny_dequant_decode(kind, M, N, K):
     ref = x.float() @ wd.t() + b.float()
     err = (y.float() - ref).abs().max().item()
     assert err <= 1e-2 * ref.abs().max().item() + 2e-3, err
+
+
+@pytest.mark.parametrize("tile", [1, 2, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("M,N,K", [(300, 256, 1024), (2048, 512, 384), (513, 768, 128), (256, 4096, 2048)])
+def test_mx_gemm_tile_variants(tile, M, N, K, monkeypatch):
+    """Every tile variant of the e4m3 path (SXE_MX_TILE, read per call) against the fp32 reference,
+    with a bias and a per-column scale: ragged M, one / two / many K stages (the phased tile's
+    prologue and tail), N not a multiple of 256 (variants needing 256 fall back)."""
+    monkeypatch.setenv("SXE_MX_TILE", str(tile))
+    torch.manual_seed(tile + M + N + K)
+    w = torch.randn(N, K, device="cuda") * 0.05
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    b = torch.randn(N, device="cuda").to(torch.bfloat16)
+    cs = torch.rand(N, device="cuda") + 0.5
+    W = mx.MXWeight(w, "mxfp8")
+    q, s = torch.ops.sxe.mx_quant_fp8(x)
+    y = torch.ops.sxe.mx_gemm(q, s, W.q, W.scale, mx.FORMATS["mxfp8"][0], b, cs)
+    ref = (mx.dequantize(q, s, "mxfp8", K) @ mx.dequantize(W.q, W.scale, "mxfp8", K).t()) * cs + b.float()
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item() + 1e-3, (tile, err)
+    y0 = torch.ops.sxe.mx_gemm(q, s, W.q, W.scale, mx.FORMATS["mxfp8"][0], None, None)
+    ref0 = mx.dequantize(q, s, "mxfp8", K) @ mx.dequantize(W.q, W.scale, "mxfp8", K).t()
+    assert (y0.float() - ref0).abs().max().item() <= 1e-2 * ref0.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("tile", [1, 2, 6, 7, 9])
+def test_mx_gemm_tile_identity(tile, monkeypatch):
+    """X = I (exact in e4m3), W asymmetric small integers: Y must equal W^T exactly for every tile
+    variant -- catches a transposed epilogue or a swapped operand / exponent map."""
+    monkeypatch.setenv("SXE_MX_TILE", str(tile))
+    K, N = 256, 512
+    x = torch.eye(K, device="cuda").to(torch.bfloat16)
+    w = (torch.arange(N * K, device="cuda").reshape(N, K) % 7 - 3).float()
+    w[:, 128:] *= 4  # a second exponent per row: blocks 4.. differ from blocks 0..3
+    W = mx.MXWeight(w, "mxfp8")
+    q, s = torch.ops.sxe.mx_quant_fp8(x)
+    y = torch.ops.sxe.mx_gemm(q, s, W.q, W.scale, mx.FORMATS["mxfp8"][0], None, None)
+    torch.testing.assert_close(y.float(), mx.dequantize(W.q, W.scale, "mxfp8", K).t(), rtol=0, atol=0)
