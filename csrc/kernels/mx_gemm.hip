@@ -522,145 +522,6 @@ __global__ void __launch_bounds__(64 * NWV, 1)
 }
 }  // namespace dp
 
-// ---------------------------------------------------------------------------------------------------
-// Phased variant (e4m3 weights): dp's 256 x 256 tile and 8 waves (2 x 4, 128 x 64 each), with the K
-// loop cut into 64-deep stages (one MFMA k-step) held in a 4-buffer LDS ring. Every stage's DMA is
-// issued 3 stages ahead and retired by a counted vmcnt that never drains to 0 inside the loop, and
-// each stage runs as two phases { ds_read the phase's operands || issue half of the stage-ahead DMA
-// -> lgkmcnt(0) + s_barrier -> 4 MFMAs -> s_barrier }: the reads of phase p + 1 run under the MFMAs
-// of phase p (cdna_hip_programming.md T3+T4). 64-byte LDS rows, 16-byte slot s of row r holding
-// chunk s ^ ((r >> 2) & 3); the exponents come as the aligned 4-byte word of the stage pair.
-namespace ph {
-constexpr int BM = 256, BN = 256, NWV = 8, KST = 64, NBUF = 4;
-constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, S_BYTES = (BM + BN) * 4;
-constexpr int STAGE = A_BYTES + B_BYTES + S_BYTES;
-__device__ __forceinline__ int f4(int r) { return (r >> 2) & 3; }
-
-// PART 0: the A codes (2 glds per wave) and the exponents (1); PART 1: the B codes (2)
-template <int PART>
-__device__ __forceinline__ void issue(char* buf, const uint8_t* Xq, const uint8_t* Xs, const uint8_t* Wq,
-                                      const uint8_t* Ws, int m0, int n0, int M, int K, int KS, int kb, int w,
-                                      int lane) {
-  if constexpr (PART == 0) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int g = w * 2 + j, row = 16 * g + (lane >> 2), ch = (lane & 3) ^ f4(row);
-      const int gr = min(m0 + row, M - 1);
-      dp::glds16(Xq + (int64_t)gr * K + (int64_t)kb * KST + 16 * ch, buf + g * 1024);
-    }
-    // exponents: the aligned 4-byte word of the stage's stage PAIR (blocks 4 (kb / 2) .. + 3; the
-    // stage uses bytes 2 (kb & 1) and 2 (kb & 1) + 1) -- waves 0-3 the A rows', 4-7 the B rows' (one
-    // select, no branch: a block boundary here lets the compiler move the MFMA clusters)
-    const int row = 64 * (w & 3) + lane;
-    const uint8_t* src = w < 4 ? Xs + (int64_t)min(m0 + row, M - 1) * KS : Ws + (int64_t)(n0 + row) * KS;
-    dp::glds4(src + 4 * (kb >> 1), buf + A_BYTES + B_BYTES + 256 * w);
-  } else {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int g = w * 2 + j, row = 16 * g + (lane >> 2), ch = (lane & 3) ^ f4(row);
-      dp::glds16(Wq + (int64_t)(n0 + row) * K + (int64_t)kb * KST + 16 * ch, buf + A_BYTES + g * 1024);
-    }
-  }
-}
-
-// the lane's 32 codes of a 64-K step: bytes [16 h, 16 h + 16) and [32 + 16 h, 48 + 16 h) of its row
-__device__ __forceinline__ i32x8 rd(const char* base, int row, int h) {
-  const char* rp = base + row * 64;
-  const u32x4 x0 = *reinterpret_cast<const u32x4*>(rp + 16 * (h ^ f4(row)));
-  const u32x4 x1 = *reinterpret_cast<const u32x4*>(rp + 16 * ((2 + h) ^ f4(row)));
-  return i32x8{(int)x0[0], (int)x0[1], (int)x0[2], (int)x0[3], (int)x1[0], (int)x1[1], (int)x1[2], (int)x1[3]};
-}
-
-// One MFMA cluster of a phase: rows i = I0, I0 + 1 of the wave tile against both column blocks. The
-// weight is the MFMA's A operand, so an accumulator holds Y^T: lane l32 owns token row m, and its 16
-// elements are 4 runs of 4 consecutive output columns (8-byte stores in the epilogue).
-template <int I0>
-__device__ __forceinline__ void cluster(f32x16 (&acc)[4][2], const i32x8 (&a)[4], const i32x8 (&b)[2],
-                                        const unsigned (&sa)[4], const unsigned (&sb)[2], int sh) {
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-  for (int i = I0; i < I0 + 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
-          b[j], a[i], acc[i][j], 0, 0, 0, (int)((sb[j] >> sh) & 0xff), 0, (int)((sa[i] >> sh) & 0xff));
-  __builtin_amdgcn_s_setprio(0);
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-// One 64-deep K stage in two phases; PRE: issue stage kb + 3's DMA, WAITN: the vmcnt that retires
-// stage kb + 1 (loads of later stages still in flight).
-template <bool PRE, int WAITN>
-__device__ __forceinline__ void stage(f32x16 (&acc)[4][2], char* smem, const uint8_t* Xq, const uint8_t* Xs,
-                                      const uint8_t* Wq, const uint8_t* Ws, int m0, int n0, int M, int K, int KS,
-                                      int kb, int w, int lane, int wm, int wn, int h, int l32) {
-  const int sh = 8 * (2 * (kb & 1) + h);  // the lane's exponent byte within the stage-pair word
-  const char* buf = smem + (kb & 3) * STAGE;
-  char* nbuf = smem + ((kb + 3) & 3) * STAGE;
-  // ---- phase 0: accumulator rows i = 0, 1 (the B operands and exponents are read here) -----------
-  const unsigned* sc = reinterpret_cast<const unsigned*>(buf + A_BYTES + B_BYTES);
-  unsigned sa[4], sb[2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) sa[i] = sc[wm * 128 + i * 32 + l32];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) sb[j] = sc[BM + wn * 64 + j * 32 + l32];
-  i32x8 a[4], b[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) b[j] = rd(buf + A_BYTES, wn * 64 + j * 32 + l32, h);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) a[i] = rd(buf, wm * 128 + i * 32 + l32, h);
-  if constexpr (PRE) issue<0>(nbuf, Xq, Xs, Wq, Ws, m0, n0, M, K, KS, kb + 3, w, lane);
-  dp::raw_barrier();
-  cluster<0>(acc, a, b, sa, sb, sh);
-  __builtin_amdgcn_s_barrier();
-  // ---- phase 1: rows i = 2, 3; the next stage is retired here (read after this phase's barriers) --
-#pragma unroll
-  for (int i = 2; i < 4; ++i) a[i] = rd(buf, wm * 128 + i * 32 + l32, h);
-  if constexpr (PRE) issue<1>(nbuf, Xq, Xs, Wq, Ws, m0, n0, M, K, KS, kb + 3, w, lane);
-  dp::vm_wait<WAITN>();
-  dp::raw_barrier();
-  cluster<2>(acc, a, b, sa, sb, sh);
-  __builtin_amdgcn_s_barrier();
-}
-
-__global__ void __launch_bounds__(64 * NWV, 1)
-    mx_gemm_ph_kernel(const uint8_t* __restrict__ Xq, const uint8_t* __restrict__ Xs, const uint8_t* __restrict__ Wq,
-                      const uint8_t* __restrict__ Ws, const unsigned short* __restrict__ bias,
-                      const float* __restrict__ col_scale, unsigned short* __restrict__ Y, int M, int N, int K) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tm = (M + BM - 1) / BM, tn = N / BN, nwg = tm * tn;
-  const int orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-  const int pid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  const int m0 = (pid % tm) * BM, n0 = (pid / tm) * BN;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int wm = w >> 2, wn = w & 3, h = lane >> 5, l32 = lane & 31;
-  const int KS = K / 32, nk = K / KST;
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  const int pro = min(nk, NBUF - 1);
-  for (int s = 0; s < pro; ++s) {
-    issue<0>(smem + s * STAGE, Xq, Xs, Wq, Ws, m0, n0, M, K, KS, s, w, lane);
-    issue<1>(smem + s * STAGE, Xq, Xs, Wq, Ws, m0, n0, M, K, KS, s, w, lane);
-  }
-  if (pro == 3) dp::vm_wait<10>(); else if (pro == 2) dp::vm_wait<5>(); else dp::vm_wait<0>();
-  dp::raw_barrier();
-
-  // steady state: straight-line stages (no branch inside, so the MFMA clusters stay between their
-  // barriers -- a block boundary lets the compiler sink them into the next phase)
-  int kb = 0;
-  for (; kb + 3 < nk; ++kb) stage<true, 10>(acc, smem, Xq, Xs, Wq, Ws, m0, n0, M, K, KS, kb, w, lane, wm, wn, h, l32);
-  for (; kb < nk; ++kb) stage<false, 0>(acc, smem, Xq, Xs, Wq, Ws, m0, n0, M, K, KS, kb, w, lane, wm, wn, h, l32);
-  store_t<4, 2>(acc, Y, col_scale, bias, m0 + wm * 128, n0 + wn * 64, M, N, h, l32);
-}
-}  // namespace ph
 
 template <int BM, int BN, int WM, int WN, int FB>
 void launch(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq, const at::Tensor& ws,
@@ -684,7 +545,8 @@ void launch(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq, co
 // tile variants: 0 auto, 1 = 128x128 / 4 waves, 2 = 256x128 / 4 waves, 3 = 256x256 / 4 waves
 // (128x128 per wave, accumulators in AGPRs), 4 = 256x256 / 8 waves, 5 = 256x128 / 8 waves,
 // 6 = 256x256 / 8 waves LDS-DMA pipelined (namespace dp), 7 = the same at 256x128 / 4 waves,
-// 8 = 256x256 / 4 waves, 9 = 256x256 / 8 waves phased (namespace ph, e4m3 weights)
+// 8 = 256x256 / 4 waves (a phased 64-deep-stage form of 6 measured slower on every shape:
+// profiles/r05/mx_gemm_phased_tile_ab.log)
 static int tile_override() {  // read per call: the kernel tests sweep every variant in one process
   const char* e = getenv("SXE_MX_TILE");
   return e ? atoi(e) : 0;
@@ -711,23 +573,6 @@ void launch_dp(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq,
                      cs ? cs->data_ptr<float>() : nullptr, reinterpret_cast<unsigned short*>(y.data_ptr()), M, N, K);
 }
 
-void launch_ph(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq, const at::Tensor& ws,
-               const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& cs, at::Tensor& y, int M, int N,
-               int K) {
-  const size_t lds = (size_t)ph::NBUF * ph::STAGE;
-  static bool attr = [&] {
-    SXE_HIP_CHECK(hipFuncSetAttribute((const void*)ph::mx_gemm_ph_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds));
-    return true;
-  }();
-  (void)attr;
-  const int G_ = ((M + ph::BM - 1) / ph::BM) * (N / ph::BN);
-  hipLaunchKernelGGL(ph::mx_gemm_ph_kernel, dim3(G_), dim3(64 * ph::NWV), lds, cur_stream(), xq.data_ptr<uint8_t>(),
-                     xs.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), ws.data_ptr<uint8_t>(),
-                     bias ? reinterpret_cast<const unsigned short*>(bias->data_ptr()) : nullptr,
-                     cs ? cs->data_ptr<float>() : nullptr, reinterpret_cast<unsigned short*>(y.data_ptr()), M, N, K);
-}
-
 template <int FB>
 void dispatch_tile(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq, const at::Tensor& ws,
                    const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& cs, at::Tensor& y, int M,
@@ -740,10 +585,8 @@ void dispatch_tile(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor&
     const int64_t g256 = (int64_t)((M + 255) / 256) * (N / 256), g2561 = (int64_t)((M + 255) / 256) * (N / 128);
     v = (N % 256 == 0 && M > 256 && g256 >= kNumCUs) ? 6 : (M > 256 && g2561 >= kNumCUs / 2) ? 7 : 1;
   }
-  if ((v == 3 || v == 4 || v == 6 || v == 8 || v == 9) && N % 256 != 0) v = 2;
-  if (v == 9 && FB != 0) v = 6;  // the phased tile reads e4m3 weights only
+  if ((v == 3 || v == 4 || v == 6 || v == 8) && N % 256 != 0) v = 2;
   switch (v) {
-    case 9: launch_ph(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
     case 6: launch_dp<FB, 256>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
     case 8: launch_dp<FB, 256, 4>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
     case 7: launch_dp<FB, 128>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;

@@ -31,7 +31,9 @@ __device__ __forceinline__ void load_w8(const typename WType<T, WF32>::type* w, 
 // WPR = waves per row: 1 (the default: one wave per row, no barrier) or 4 (the whole 256-thread
 // block on one row, block-level reductions) for launches with few rows -- decode's single-token
 // RMSNorm took 9 us as one wave sweeping 4096 elements in 8 dependent-latency chunks.
-template <DT T, bool WF32, bool LN, bool RES, int NCH, int WPR = 1>
+// EXACT: H == NCH * 8 * lanes per row, so no chunk needs its bounds check -- the loads of every
+// chunk then issue back to back (a per-chunk `if` makes hipcc wait for each chunk's loads in turn).
+template <DT T, bool WF32, bool LN, bool RES, int NCH, int WPR = 1, bool EXACT = false>
 __global__ void __launch_bounds__(256) norm_fwd_kernel(const typename dt_traits<T>::storage* __restrict__ x,
                                                        const typename dt_traits<T>::storage* __restrict__ res,
                                                        const typename WType<T, WF32>::type* __restrict__ w,
@@ -51,21 +53,37 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const typename dt_traits<
     const S* xr = x + r * H;
     float v[NCH][8];
     float s = 0.f;
+    // every chunk's loads first, then the residual stores: a store between two chunks' loads makes
+    // the next wait cover it (vmcnt counts stores too)
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = (c * LPR + lane) * 8;
-      if (col < H) {
-        load8<T>(xr + col, v[c]);
-        if constexpr (RES) {
-          float t[8];
-          load8<T>(res + r * H + col, t);
+      if (EXACT || col < H) load8<T>(xr + col, v[c]);
+    }
+    if constexpr (RES) {
+      float t[NCH][8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[c][j] += t[j];
+      for (int c = 0; c < NCH; ++c) {
+        const int col = (c * LPR + lane) * 8;
+        if (EXACT || col < H) load8<T>(res + r * H + col, t[c]);
+      }
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int col = (c * LPR + lane) * 8;
+        if (EXACT || col < H) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[c][j] += t[c][j];
           // the residual stream is kept in the activation dtype (as the unfused path would)
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[c][j] = to_f32<T>(from_f32<T>(v[c][j]));
           store8<T>(h_out + r * H + col, v[c]);
         }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = (c * LPR + lane) * 8;
+      if (EXACT || col < H) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += v[c][j];
       }
@@ -77,7 +95,7 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const typename dt_traits<
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         const int col = (c * LPR + lane) * 8;
-        if (col < H) {
+        if (EXACT || col < H) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) { float d = v[c][j] - mean; s += d * d; }
         }
@@ -87,7 +105,7 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const typename dt_traits<
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         const int col = (c * LPR + lane) * 8;
-        if (col < H) {
+        if (EXACT || col < H) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) s += v[c][j] * v[c][j];
         }
@@ -97,7 +115,7 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const typename dt_traits<
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = (c * LPR + lane) * 8;
-      if (col < H) {
+      if (EXACT || col < H) {
         float wv[8], o[8];
         load_w8<T, WF32>(w + col, wv);
         if constexpr (LN) {
@@ -124,7 +142,7 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(const typename dt_traits<
 }
 
 // ---------------------------------------------------------------------------------------------
-template <DT T, bool WF32, bool LN, bool DRES, int NCH>
+template <DT T, bool WF32, bool LN, bool DRES, int NCH, bool EXACT = false>
 __global__ void __launch_bounds__(256) norm_bwd_kernel(const typename dt_traits<T>::storage* __restrict__ dy,
                                                        const typename dt_traits<T>::storage* __restrict__ x,
                                                        const float* __restrict__ rstd_in, const float* __restrict__ mean_in,
@@ -151,7 +169,7 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const typename dt_traits<
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = (c * 64 + lane) * 8;
-      if (col < H) {
+      if (EXACT || col < H) {
         float dyv[8], wv[8];
         load8<T>(dy + r * H + col, dyv);
         load8<T>(x + r * H + col, xh[c]);
@@ -172,7 +190,7 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const typename dt_traits<
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = (c * 64 + lane) * 8;
-      if (col < H) {
+      if (EXACT || col < H) {
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -194,7 +212,7 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const typename dt_traits<
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int col = (c * 64 + lane) * 8;
-    if (col < H) {
+    if (EXACT || col < H) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) lds[wv_id * H + col + j] = dw_acc[c][j];
     }
@@ -208,7 +226,7 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const typename dt_traits<
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = (c * 64 + lane) * 8;
-      if (col < H) {
+      if (EXACT || col < H) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) lds[wv_id * H + col + j] = db_acc[c][j];
       }
@@ -218,6 +236,12 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const typename dt_traits<
       db_part[(int64_t)blockIdx.x * H + i] = lds[i] + lds[H + i] + lds[2 * H + i] + lds[3 * H + i];
     }
   }
+}
+
+// SXE_NORM_EXACT=0 keeps the bounds-checked variants (A/B of the exact-width kernels)
+static bool exact_ok(int H, int nch) {
+  const char* e = getenv("SXE_NORM_EXACT");
+  return H == nch * 512 && !(e && e[0] == '0');
 }
 
 static int pick_nch(int H) {
@@ -269,7 +293,8 @@ std::vector<at::Tensor> norm_fwd(at::Tensor x, c10::optional<at::Tensor> residua
   SXE_DISPATCH_DT(d, TT, SXE_DISPATCH_BOOL(wf32, WF, SXE_DISPATCH_BOOL(layernorm, LNB, SXE_DISPATCH_BOOL(has_res, RB, SXE_DISPATCH_NCH(nch, NC, {
     using S = typename dt_traits<TT>::storage;
     using W = typename WType<TT, WF>::type;
-    auto kern = block_rows ? norm_fwd_kernel<TT, WF, LNB, RB, NC, 4> : norm_fwd_kernel<TT, WF, LNB, RB, NC, 1>;
+    auto kern = block_rows ? norm_fwd_kernel<TT, WF, LNB, RB, NC, 4>
+                : (exact_ok(H, NC) ? norm_fwd_kernel<TT, WF, LNB, RB, NC, 1, true> : norm_fwd_kernel<TT, WF, LNB, RB, NC, 1>);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, cur_stream(),
                        reinterpret_cast<const S*>(x.data_ptr()), has_res ? reinterpret_cast<const S*>(residual->data_ptr()) : nullptr,
                        reinterpret_cast<const W*>(weight.data_ptr()), has_b ? reinterpret_cast<const W*>(bias->data_ptr()) : nullptr,
@@ -305,7 +330,8 @@ std::vector<at::Tensor> norm_bwd(at::Tensor dy, at::Tensor x, at::Tensor rstd, c
   SXE_DISPATCH_DT(d, TT, SXE_DISPATCH_BOOL(wf32, WF, SXE_DISPATCH_BOOL(layernorm, LNB, SXE_DISPATCH_BOOL(has_dres, DR, SXE_DISPATCH_NCH(nch, NC, {
     using S = typename dt_traits<TT>::storage;
     using W = typename WType<TT, WF>::type;
-    hipLaunchKernelGGL((norm_bwd_kernel<TT, WF, LNB, DR, NC>), dim3(grid), dim3(256), lds, cur_stream(),
+    auto kern = exact_ok(H, NC) ? norm_bwd_kernel<TT, WF, LNB, DR, NC, true> : norm_bwd_kernel<TT, WF, LNB, DR, NC>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, cur_stream(),
                        reinterpret_cast<const S*>(dy.data_ptr()), reinterpret_cast<const S*>(x.data_ptr()),
                        rstd.data_ptr<float>(), layernorm ? mean->data_ptr<float>() : nullptr,
                        reinterpret_cast<const W*>(weight.data_ptr()),
