@@ -79,7 +79,8 @@ def build(jobs=None, force=False, only=None, verbose=True):
     hip_flags = common + [f"--offload-arch={ARCH}", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
                           "-fno-gpu-rdc", "-munsafe-fp-atomics", "-Wno-unused-result",
                           "-Wno-return-type", "-ffp-contract=fast"]
-    cpu_flags = common + ["-fopenmp", "-Wall", "-Wno-unused-function", "-Wno-sign-compare"]
+    # -fno-math-errno: std::sqrt in the optimizer loops may not set errno, else GCC keeps them scalar
+    cpu_flags = common + ["-fopenmp", "-fno-math-errno", "-Wall", "-Wno-unused-function", "-Wno-sign-compare"]
     targets = []
     if only in (None, "hip"):
         hip_srcs = sorted(f for f in os.listdir(os.path.join(CSRC, "kernels")) if f.endswith(".hip"))

@@ -43,9 +43,21 @@ struct AdamArgs {
   int adamw;
 };
 
+// branch-free round-to-nearest-even bf16 (quiet NaN kept): vectorises inside the update loop
+static inline uint16_t f32_to_bf16_rne(float f) {
+  uint32_t x;
+  std::memcpy(&x, &f, 4);
+  const uint32_t r = (x + 0x7fffu + ((x >> 16) & 1u)) >> 16;
+  const uint32_t q = (x >> 16) | 0x40u;
+  return (uint16_t)(((x & 0x7fffffffu) > 0x7f800000u) ? q : r);
+}
+
+// The bit16 copy of the updated parameter is written in the same SIMD loop as the update (one pass
+// over the tile; the separate scalar conversion loop it replaces ran once more over every element).
+template <int LK>
 __attribute__((target_clones("avx512f", "avx2", "default")))
 static void adam_tile(float* __restrict p, const void* __restrict gv, int gk, float* __restrict m,
-                      float* __restrict v, void* __restrict lpv, int lk, int64_t n, AdamArgs a) {
+                      float* __restrict v, void* __restrict lpv, int64_t n, AdamArgs a) {
   float gbuf[4096];
   if (gk == G_F32) {
     const float* g = (const float*)gv;
@@ -56,6 +68,7 @@ static void adam_tile(float* __restrict p, const void* __restrict gv, int gk, fl
 #pragma omp simd
     for (int64_t i = 0; i < n; ++i) gbuf[i] = bf16_to_f32(g[i]) * a.gscale;
   }
+  uint16_t* lp = (uint16_t*)lpv;
 #pragma omp simd
   for (int64_t i = 0; i < n; ++i) {
     float gi = gbuf[i];
@@ -69,12 +82,9 @@ static void adam_tile(float* __restrict p, const void* __restrict gv, int gk, fl
     p[i] = pi;
     m[i] = mi;
     v[i] = vi;
+    if constexpr (LK == L_BF16) lp[i] = f32_to_bf16_rne(pi);
   }
-  if (lk == L_BF16) {
-    uint16_t* lp = (uint16_t*)lpv;
-    for (int64_t i = 0; i < n; ++i) lp[i] = f32_to_bf16(p[i]);
-  } else if (lk == L_F16) {
-    uint16_t* lp = (uint16_t*)lpv;
+  if constexpr (LK == L_F16) {
     for (int64_t i = 0; i < n; ++i) lp[i] = f32_to_f16(p[i]);
   }
 }
@@ -119,7 +129,10 @@ void adam_step_(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, c10::opt
   for (int64_t t = 0; t < tiles; ++t) {
     const int64_t o = t * T;
     const int64_t len = std::min(T, n - o);
-    adam_tile(pp + o, gp + o * gsz, gk, mp + o, vp + o, lpp ? lpp + o * 2 : nullptr, lk, len, a);
+    char* lo = lpp ? lpp + o * 2 : nullptr;
+    if (lk == L_BF16) adam_tile<L_BF16>(pp + o, gp + o * gsz, gk, mp + o, vp + o, lo, len, a);
+    else if (lk == L_F16) adam_tile<L_F16>(pp + o, gp + o * gsz, gk, mp + o, vp + o, lo, len, a);
+    else adam_tile<L_NONE>(pp + o, gp + o * gsz, gk, mp + o, vp + o, nullptr, len, a);
   }
 }
 
