@@ -53,7 +53,7 @@ def test_norm_fwd_bwd_vs_fp32(exact, H, ln, monkeypatch):
         out = (hr - mu) * torch.rsqrt(((hr - mu) ** 2).mean(-1, keepdim=True) + eps) * wr + br
     else:
         out = hr * torch.rsqrt((hr * hr).mean(-1, keepdim=True) + eps) * wr
-    gx, gw, gb = torch.autograd.grad(out, (hr, wr, br), dy.float())
+    gx, gw, gb = torch.autograd.grad(out, (hr, wr, br), dy.float(), allow_unused=True)
     torch.testing.assert_close(dx.float(), gx + dres.float(), rtol=2e-2, atol=3e-2)
     torch.testing.assert_close(dw, gw, rtol=1e-3, atol=1e-2)
     if ln:

@@ -37,9 +37,9 @@ def main():
     tb = t(lambda: torch.ops.sxe.norm_bwd(dy, h, rstd, None, w, dy, False))
     mb = R * H * 2 / 1e6
     print(json.dumps({"exact": os.environ.get("SXE_NORM_EXACT", "1"), "fwd_res_ms": round(tf, 4),
-                      "fwd_res_TBps": round(4 * mb / tf / 1e6, 2), "fwd_ms": round(tf0, 4),
-                      "fwd_TBps": round(2 * mb / tf0 / 1e6, 2), "bwd_dres_ms": round(tb, 4),
-                      "bwd_TBps": round(4 * mb / tb / 1e6, 2)}), flush=True)
+                      "fwd_res_TBps": round(4 * mb / tf / 1e3, 2), "fwd_ms": round(tf0, 4),
+                      "fwd_TBps": round(2 * mb / tf0 / 1e3, 2), "bwd_dres_ms": round(tb, 4),
+                      "bwd_TBps": round(4 * mb / tb / 1e3, 2)}), flush=True)
 
 
 if __name__ == "__main__":
