@@ -138,6 +138,7 @@ def fused_merge_linear(part_o, part_ml, weight, bias=None):
 # 1.59 ms vs 1.63 (transposes + hipBLASLt TN fp32-out), 4096x14336 0.84 vs 0.89, 4096x4096 0.24 vs
 # 0.25 (NT fp32-out), 6144x4096 0.43 vs 0.46 (1.5 waves of tiles); the LM head keeps the library path.
 SXE_WGRAD = os.environ.get("SXE_WGRAD", "1") == "1"
+WGRAD_MIN_TILES = int(os.environ.get("SXE_WGRAD_MIN_TILES", "384"))  # non-multiple-of-256 tile counts
 
 
 def _sxe_wgrad_ok(gy2, x2, buf):
@@ -150,7 +151,7 @@ def _sxe_wgrad_ok(gy2, x2, buf):
     tiles = (M // 256) * (N // 256)
     # 1.5 waves of tiles (the fused QKV projection, 6144 x 4096) still beat the NT library GEMM:
     # 0.431 vs 0.462 ms at 8192 tokens (profiles/r05/wgrad_attention_shapes.log)
-    return tiles % 256 == 0 or tiles >= 384
+    return tiles % 256 == 0 or tiles >= WGRAD_MIN_TILES
 
 
 def _tn_ok(gy2, x2):

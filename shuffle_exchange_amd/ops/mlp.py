@@ -18,7 +18,9 @@ write them:
 
 Each weight gradient is a bf16 TN GEMM (as autograd's own bf16 weight gradients are) added into
 the ZeRO fp32 accumulator, or written straight into a bf16 reduce-scatter slot. The measured
-alternatives (fp32-out TN with beta = 1; the k-major kernel) lose at these shapes.
+alternatives (fp32-out TN with beta = 1; the k-major kernel) lose at these shapes: the fp32-out
+GEMM cost the whole Llama-3-8B step 2.8 % (24,602 vs 25,302 tokens/s in one box session,
+profiles/r05/headline_wgrad_norm_ab.log) although it drops the cast / add passes.
 Reference counterpart: the MLP of deepspeed/model_implementations / the HF Llama MLP the reference
 trains through autograd (no fused MLP exists there); parity is autograd's result (tests/test_mlp_tn.py).
 """
@@ -52,11 +54,6 @@ def weight_grad_tn(w, gyT, xT):
     buf, accumulate = tgt(w)
     if buf.dtype == gyT.dtype and not accumulate and buf.is_contiguous():
         torch.mm(gyT, xT.t(), out=buf.view(w.shape))  # bf16 reduce-scatter slot of a multi-rank unit
-    elif buf.dtype == torch.float32 and gyT.is_cuda and buf.is_contiguous():
-        # fp32 accumulator: one fp32-output GEMM accumulating in its epilogue (beta = 1) -- no bf16 dW
-        # round trip and no separate cast-copy / fp32 add pass (those were 1.2 % of the Llama-3-8B step)
-        b2 = buf.view(w.shape)
-        torch.ops.aten.addmm.dtype_out(b2, gyT, xT.t(), torch.float32, beta=1 if accumulate else 0, alpha=1, out=b2)
     else:
         dw = torch.mm(gyT, xT.t()).view_as(buf)
         buf.add_(dw) if accumulate else buf.copy_(dw)

@@ -476,6 +476,20 @@ class HostOptimizerStep:
 
         self._worker = threading.Thread(target=work, name="sxe-host-adam", daemon=True)
         self._worker.start()
+        if not getattr(self, "_atexit_set", False):
+            # a process that ends while the worker is inside the C++ update (OpenMP team running)
+            # aborts in the runtime's teardown ("terminate called without an active exception"):
+            # join it first
+            import atexit
+            import weakref
+            ref = weakref.ref(self)
+            atexit.register(lambda: ref() is not None and ref()._join_worker())
+            self._atexit_set = True
+
+    def _join_worker(self):
+        w = self._worker
+        if w is not None:
+            w.join()
 
     def _raise(self):
         if self._error is not None:
