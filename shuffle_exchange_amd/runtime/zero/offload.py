@@ -134,6 +134,7 @@ class HostOptimizerStep:
             assert self.nvme_path, "offload_optimizer.device=nvme needs nvme_path"
         acc = get_accelerator()
         self.STAGE_SLOTS = max(2, int(os.environ.get("SXE_OFFLOAD_STAGE_SLOTS", 3)))
+        self.D2H_PIECE = max(4096, int(os.environ.get("SXE_OFFLOAD_D2H_PIECE", 64 << 20)))  # elements
         self.d2h = acc.named_stream("offload_d2h") if acc.gpu else None
         self.h2d = acc.named_stream("offload_h2d") if acc.gpu else None
         self._h2d_done = None
@@ -284,6 +285,10 @@ class HostOptimizerStep:
             return self._update_async(opt, cur, coef, flat)
         NS = len(self.gslots)
         d2h_ev = {}
+        # Each unit's gradient crosses in PIECE-element pieces with an event per piece, and the C++
+        # update walks the pieces as they land: the CPU no longer waits for a whole unit's copy (74 ms
+        # per step for the first, 1 G-element unit of Llama-3-70B) before it can start.
+        PIECE = self.D2H_PIECE
         import time as _time
         tr = {"t0": _time.perf_counter(), "d2h_wait": 0.0, "cpu": 0.0, "h2d_wait": 0.0, "units": len(flat),
               "elems": sum(x[2].chunk for x in flat)} if self.trace_on else None
@@ -294,11 +299,15 @@ class HostOptimizerStep:
             if cur is None:
                 dst.copy_(u.grad)
                 return
+            evs = []
             with get_accelerator().stream(self.d2h):
-                dst.copy_(u.grad, non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(self.d2h)
-                d2h_ev[k] = ev
+                for a in range(0, u.chunk, PIECE):
+                    b = min(u.chunk, a + PIECE)
+                    dst[a:b].copy_(u.grad[a:b], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self.d2h)
+                    evs.append((a, b, ev))
+            d2h_ev[k] = evs
 
         if cur is not None:
             self.d2h.wait_stream(cur)
@@ -320,12 +329,7 @@ class HostOptimizerStep:
             if nvme and k + 1 < len(flat):
                 gn, iN, un, _ = flat[k + 1]
                 pend[k + 1] = self.swapper.read((k + 1) % nslot, gn, iN, un.chunk)
-            if k in d2h_ev:
-                if tr is not None:
-                    t = _time.perf_counter()
-                d2h_ev.pop(k).synchronize()
-                if tr is not None:
-                    tr["d2h_wait"] += _time.perf_counter() - t
+            pieces = d2h_ev.pop(k, None) or [(0, u.chunk, None)]
             slot = k % NS
             grad = self.gslots[slot][:u.chunk]
             if nvme:
@@ -344,11 +348,21 @@ class HostOptimizerStep:
                 lp = self.lslots[slot][:u.chunk]
             else:
                 lp = u.shard_for_overwrite()  # pinned host shard, or an NVMe swap buffer
-            if tr is not None:
-                t = _time.perf_counter()
-            self._host_kernel(opt, pg, st, master, grad, states, lp, coef)
-            if tr is not None:
-                tr["cpu"] += _time.perf_counter() - t
+            for a, b, ev in pieces:
+                if ev is not None:
+                    if tr is not None:
+                        t = _time.perf_counter()
+                    ev.synchronize()
+                    if tr is not None:
+                        tr["d2h_wait"] += _time.perf_counter() - t
+                if tr is not None:
+                    t = _time.perf_counter()
+                if a == 0 and b == u.chunk:
+                    self._host_kernel(opt, pg, st, master, grad, states, lp, coef)
+                else:
+                    self._host_kernel(opt, pg, st, master[a:b], grad[a:b], [x[a:b] for x in states], lp[a:b], coef)
+                if tr is not None:
+                    tr["cpu"] += _time.perf_counter() - t
             if nvme:
                 self.swapper.write(k % nslot, g, i, u.chunk)
             if k + NS < len(flat):

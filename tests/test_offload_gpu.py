@@ -57,3 +57,17 @@ def test_offload_matches_hbm_adam(stage, offload):
         a, b = off[k].float(), v.float()
         rel = ((a - b).norm() / (b.norm() + 1e-12)).item()
         assert rel < 5e-3, (k, rel)
+
+
+@pytest.mark.parametrize("stage", [2, 3])
+def test_offload_piecewise_d2h_matches_hbm_adam(stage, monkeypatch):
+    """The host update walking a unit's gradient in D2H pieces as they land (SXE_OFFLOAD_D2H_PIECE,
+    here 4096 elements: dozens of pieces per unit) trains to the same parameters."""
+    monkeypatch.setenv("SXE_OFFLOAD_D2H_PIECE", "4096")
+    off = run_dist(_case, 1, stage, "cpu")[0]
+    monkeypatch.delenv("SXE_OFFLOAD_D2H_PIECE")
+    ref = run_dist(_case, 1, stage, "none")[0]
+    for k, v in ref.items():
+        a, b = off[k].float(), v.float()
+        rel = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert rel < 5e-3, (k, rel)
