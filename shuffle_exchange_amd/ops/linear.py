@@ -136,9 +136,15 @@ def fused_merge_linear(part_o, part_ml, weight, bias=None):
 # with ds_read_b64_tr_b16, fp32 accumulate in the epilogue): no transposed copies of dY / X at all.
 # Measured on MI355X at 8192 tokens (tools/wgrad_exp.py, profiles/wgrad_kernel.log): 28672x4096
 # 1.59 ms vs 1.63 (transposes + hipBLASLt TN fp32-out), 4096x14336 0.84 vs 0.89, 4096x4096 0.24 vs
-# 0.25 (NT fp32-out), 6144x4096 0.43 vs 0.46 (1.5 waves of tiles); the LM head keeps the library path.
+# 0.25 (NT fp32-out); it loses where its 256x256 tile grid leaves a partial last wave of blocks
+# (6144x4096: 1.5 waves over 256 CUs, see WGRAD_MIN_TILES) and on the LM head, which keep the
+# library paths.
 SXE_WGRAD = os.environ.get("SXE_WGRAD", "1") == "1"
-WGRAD_MIN_TILES = int(os.environ.get("SXE_WGRAD_MIN_TILES", "384"))  # non-multiple-of-256 tile counts
+# smallest non-multiple-of-256 tile count for the hand-written kernel: the fused QKV projection (384
+# tiles, 1.5 waves) wins in isolation at 8192 tokens (0.43 vs 0.46 ms) but not inside the
+# Llama-3-8B step at 16,384 tokens per micro-step (0.78 vs 0.74 ms per call,
+# profiles/r05/bench_llama3_8b_zero3_1gpu_step_final.md, headline_wgrad_norm_ab.log)
+WGRAD_MIN_TILES = int(os.environ.get("SXE_WGRAD_MIN_TILES", "768"))
 
 
 def _sxe_wgrad_ok(gy2, x2, buf):
@@ -149,8 +155,6 @@ def _sxe_wgrad_ok(gy2, x2, buf):
     if K % 128 or M % 256 or N % 256 or gy2.stride(0) % 8 or x2.stride(0) % 8 or M * N >= 2 ** 27:
         return False
     tiles = (M // 256) * (N // 256)
-    # 1.5 waves of tiles (the fused QKV projection, 6144 x 4096) still beat the NT library GEMM:
-    # 0.431 vs 0.462 ms at 8192 tokens (profiles/r05/wgrad_attention_shapes.log)
     return tiles % 256 == 0 or tiles >= WGRAD_MIN_TILES
 
 
