@@ -183,6 +183,9 @@ def main():
                     help="what activation checkpointing recomputes (default: the config's; auto = the "
                          "least recompute whose saved activations fit the HBM budget)")
     ap.add_argument("--layers", type=int, default=None, help="override layer count (a cut model: not the metric)")
+    ap.add_argument("--offload-ratio", type=float, default=None,
+                    help="offload configs: Twin-Flow offload_optimizer.ratio (share of the optimizer on the "
+                         "host; default 1.0 = the whole optimizer, the reference's ZeRO-Infinity setting)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = plumbing dry-run over gloo (tests only; invalid for the metric)")
     args = ap.parse_args()
@@ -242,6 +245,8 @@ def main():
     else:
         model = ctor(cfg)
     zero = zero_knobs(c, cfg, stage)
+    if args.offload_ratio is not None and "offload_optimizer" in zero:
+        zero["offload_optimizer"]["ratio"] = float(args.offload_ratio)
     ds_config = {
         "train_micro_batch_size_per_gpu": mbs,
         "gradient_accumulation_steps": gas,
