@@ -103,6 +103,9 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
             # expert and dense partitions are disjoint across the whole DP group: one norm reduce
             self.partition_group = dp_group
         self._init_master()
+        for units in self.units:  # fp32 accumulators start zeroed: every slot counts as written
+            for u in units:
+                u.acc_valid = [True] * len(u.params)
         self._register_hooks()
         self._module_units = None  # module -> units of its own params (set by attach_module)
         self._pending_events = {}  # unit -> HIP event of its post-step gather (consumed by forward)
@@ -136,8 +139,8 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         u = self.param_unit[p]
         i = u.param_index[id(p)]
         o, n = u.offsets[i], u.numels[i]
-        if u.topo.S == 1:
-            return u.grad[o:o + n].view(p.shape), True
+        if u.topo.S == 1:  # the step's first write of the slot overwrites (GEMM beta = 0)
+            return u.grad[o:o + n].view(p.shape), u.acc_valid[i]
         if u.staging is None:
             u.staging = torch.empty(u.padded, dtype=u.dtype, device=u.device)
             if u.padded > u.numel:
@@ -147,6 +150,8 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
     def _grad_done(self, p):
         u = self.param_unit[p]
         i = u.param_index[id(p)]
+        if u.topo.S == 1:
+            u.acc_valid[i] = True
         if not u.filled[i]:
             u.filled[i] = True
             u.pending -= 1
@@ -172,8 +177,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                 return
             if unit.topo.S == 1:
                 i = unit.param_index[id(p)]
-                o, n = unit.offsets[i], unit.numels[i]
-                unit.grad[o:o + n].add_(p.grad.reshape(-1), alpha=self._unit_scale(unit))
+                self._acc_write(unit, i, p.grad, self._unit_scale(unit))
                 unit.filled[i] = True
                 p.grad = None
                 return
@@ -183,11 +187,26 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                 self._reduce_unit(unit)
         return hook
 
+    def _acc_write(self, u, i, src, alpha):
+        """Add ``alpha * src`` into slot i of a single-rank unit's fp32 accumulator -- or overwrite
+        it, when the slot is stale (its first write of the step: zero_grad_buffers)."""
+        o, n = u.offsets[i], u.numels[i]
+        dst = u.grad[o:o + n]
+        src = src.reshape(-1)
+        if u.acc_valid[i]:
+            dst.add_(src, alpha=alpha)
+        else:
+            if src.dtype == dst.dtype:
+                torch.mul(src, alpha, out=dst)
+            else:
+                dst.copy_(src)
+                if alpha != 1.0:
+                    dst.mul_(alpha)
+            u.acc_valid[i] = True
+
     def _accumulate_fp32(self, unit, p):
         if unit.topo.S == 1:
-            i = unit.param_index[id(p)]
-            o, n = unit.offsets[i], unit.numels[i]
-            unit.grad[o:o + n].add_(p.grad.reshape(-1), alpha=self._unit_scale(unit))
+            self._acc_write(unit, unit.param_index[id(p)], p.grad, self._unit_scale(unit))
         else:
             unit.stage_grad(p, p.grad)  # fp32 staging (staging_dtype), no reduce before the boundary
         p.grad = None
@@ -253,8 +272,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                     # micro-batches) go straight into the fp32 accumulator
                     for i, p in enumerate(u.params):
                         if p.grad is not None:
-                            o, n = u.offsets[i], u.numels[i]
-                            u.grad[o:o + n].add_(p.grad.reshape(-1), alpha=self._unit_scale(u))
+                            self._acc_write(u, i, p.grad, self._unit_scale(u))
                             p.grad = None
                     continue
                 if u.pending > 0:
@@ -274,8 +292,42 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
             torch.cuda.current_stream().wait_stream(self.comm_stream)
 
     # ----------------------------------------------------------------------------------------- step
+    def zero_grad_buffers(self):
+        """Single-rank units (their accumulator is only ever written by this rank's backward) are
+        marked stale instead of zeroed -- an 11.9 B-parameter Mixtral step spent 7 ms in that
+        memset: each slot's first write of the next step overwrites and the slots no gradient
+        reached are zeroed right before the update (_zero_stale). Units that reduce-scatter into
+        their accumulator (add_) are zeroed as before."""
+        multi = [u for units in self.units for u in units if u.topo.S > 1]
+        if len(multi) == sum(len(us) for us in self.units):
+            return super().zero_grad_buffers()
+        for units in self.units:
+            for u in units:
+                if u.topo.S == 1:
+                    u.acc_valid = [False] * len(u.params)
+        if multi:
+            if self.__dict__.get("_step_inflight"):
+                from ...accelerator import get_accelerator
+                with get_accelerator().stream(self._step_stream):
+                    for u in multi:
+                        u.grad.zero_()
+            else:
+                for u in multi:
+                    u.grad.zero_()
+
+    def _zero_stale(self):
+        for units in self.units:
+            for u in units:
+                if u.topo.S == 1 and not all(u.acc_valid):
+                    for i, ok in enumerate(u.acc_valid):
+                        if not ok:
+                            o, n = u.offsets[i], u.numels[i]
+                            u.grad[o:o + n].zero_()
+                    u.acc_valid = [True] * len(u.params)
+
     def step(self, closure=None, lr_kwargs=None):
         self._wait_comm()
+        self._zero_stale()
         if self.se is not None and self.method == "Gossip":
             self.se.pre_step([u.shard for units in self.units for u in units])
         coef, skip = self._grad_norm_and_flags()

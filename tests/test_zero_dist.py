@@ -378,3 +378,54 @@ def test_zero3_reduce_scatter_has_its_own_communicator_and_one_refresh_gather():
         assert r["refresh"] == [1] * steps, r["refresh"]
     ref = C.reference_train({"type": "SGD", "params": {"lr": 0.1}}, steps, world, 1, 16)
     _close(r["params"], ref)
+
+
+class _Branchy(torch.nn.Module):
+    """Parameter `b` only gets a gradient on odd steps (a MoE expert that received no tokens)."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(8, 8)
+        self.b = torch.nn.Linear(8, 8)
+        self.use_b = False
+
+    def forward(self, x):
+        y = self.a(x)
+        return self.b(y) if self.use_b else y
+
+
+def _case_stale(rank, world, stage, gas):
+    import shuffle_exchange_amd as sxe
+    torch.manual_seed(0)
+    m = _Branchy()
+    ref = _Branchy()
+    ref.load_state_dict(m.state_dict())
+    ds = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": gas, "gradient_clipping": 1.0,
+          "zero_optimization": {"stage": stage}, "optimizer": ADAMW}
+    eng, _, _, _ = sxe.initialize(model=m, config=ds)
+    opt = torch.optim.AdamW(ref.parameters(), lr=1e-2, weight_decay=0.01)
+    for p in ref.parameters():  # a missing gradient is a zero gradient (flat ZeRO semantics)
+        p.grad = torch.zeros_like(p)
+    g = torch.Generator().manual_seed(5)
+    for step in range(4):
+        m.use_b = ref.use_b = step % 2 == 1
+        opt.zero_grad(set_to_none=False)
+        for _ in range(gas):
+            x = torch.randn(2, 8, generator=g)
+            loss = eng(x).pow(2).mean()
+            eng.backward(loss)
+            eng.step()
+            (ref(x).pow(2).mean() / gas).backward()
+        torch.nn.utils.clip_grad_norm_(ref.parameters(), 1.0)
+        opt.step()
+    return {k: v.detach().clone() for k, v in m.state_dict().items()}, {k: v.detach().clone() for k, v in ref.state_dict().items()}
+
+
+@pytest.mark.parametrize("stage,gas", [(1, 1), (1, 2), (2, 1), (2, 2)])
+def test_single_rank_stale_accumulators(stage, gas):
+    """ZeRO-1/2 on one rank mark the fp32 gradient accumulators stale after a step instead of
+    zeroing them: the first write of the next step overwrites, and a parameter without a gradient
+    in a step (here `b` on even steps) is zeroed before the update -- the trajectory equals torch
+    AdamW fed zero gradients for the unused parameter."""
+    got, ref = run_dist(_case_stale, 1, stage, gas)[0]
+    _close(got, ref, tol=1e-4)
