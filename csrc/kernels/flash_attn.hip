@@ -21,8 +21,9 @@
 //    both the row reads (ds_read_b128) and the transposed reads (guide T10, image (b));
 //  * K/V (or Q/dO) tiles are register-staged one tile ahead (T14 issue-early/write-late) into a
 //    double-buffered LDS ring: one barrier per tile;
-//  * backward = delta pre-pass + dK/dV kernel (keys on lanes, dK^T/dV^T accumulated in registers
-//    across all GQA query heads: no atomics) + dQ kernel (forward-shaped): deterministic.
+//  * backward = pre-pass (-delta = -rowsum(dO * O), lse * log2(e)) + dQ kernel (forward-shaped) +
+//    dK/dV kernel (keys on lanes, dK^T/dV^T accumulated in registers across the GQA query heads): no
+//    atomics, deterministic.
 //  * heavy-first block order for the causal triangle.
 #include "sxe_common.h"
 #include <torch/library.h>
@@ -197,19 +198,32 @@ __device__ __forceinline__ void map_block(int nblk, int BH, bool heavy_last_inde
 // writes 1 KiB = 1024 / (2 D) rows linearly, so the XOR swizzle goes on the per-lane SOURCE chunk
 // (the swizzle is an involution: position c' of row `row` holds logical chunk c' ^ f(row)).
 // =============================================================================================
+//
+// Issued from inline asm, not __builtin_amdgcn_global_load_lds: the compiler's wait-count pass
+// cannot tell a builtin DMA's LDS writes from the ring's LDS reads, so it put an `s_waitcnt
+// vmcnt(0)` before the first ds_read after every issue -- each dK/dV tile waited for the NEXT
+// tile's load before its first MFMA (no prefetch at all), and dQ before its dQ MFMAs. Completion is
+// tracked by hand instead: every consumer runs vm_wait_all() + a barrier before it reads a slot.
+extern __shared__ __attribute__((aligned(16))) char smem[];  // every kernel's dynamic LDS
+// M0 value of a wave-uniform pointer into smem: the symbol's LDS address plus the byte offset (a
+// generic-to-LDS cast of the pointer itself costs a 64-bit null check per DMA instruction)
+__device__ __forceinline__ unsigned lds_addr(const char* p) {
+  return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem +
+                                        (unsigned)(p - smem));
+}
 __device__ __forceinline__ void glds16(const void* gsrc, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_addr(lds_wave_base)), "v"(gsrc)
+               : "memory", "m0");
 }
 __device__ __forceinline__ void glds4(const void* gsrc, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 4, 0, 0);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(lds_addr(lds_wave_base)), "v"(gsrc)
+               : "memory", "m0");
 }
 template <int ROWS, int D, int NWV = NW>
 __device__ __forceinline__ void tile_glds(const unsigned short* base, int64_t row_stride, int row0, char* lds) {
   constexpr int CH = D / 8, RPK = 64 / CH;  // rows per 1 KiB wave-instruction
   static_assert(ROWS % (RPK * NWV) == 0, "tile rows must split evenly over the waves");
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
   for (int i = 0; i < ROWS / RPK / NWV; ++i) {
     const int n = i * NWV + w;
@@ -219,7 +233,12 @@ __device__ __forceinline__ void tile_glds(const unsigned short* base, int64_t ro
     glds16(base + (int64_t)(row0 + row) * row_stride + ch * 8, lds + n * 1024);
   }
 }
-__device__ __forceinline__ void vm_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// s_waitcnt vmcnt(0) through the builtin (expcnt / lgkmcnt fields left at their maxima), not inline
+// asm: the compiler's wait-count pass then knows every load it tracks has landed, so it does not
+// keep counting the operand loads issued before a tile loop as pending inside the loop (where its
+// counted waits would also wait for the hand-tracked LDS-DMA below)
+__device__ __forceinline__ void vm_wait_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 
 // =============================================================================================
 // Forward. Grid: (Sq / rows per workgroup) * B * H blocks. q: [B, Sq, *, D], k/v/o: [B, Sk, *, D]
@@ -423,12 +442,15 @@ __global__ void __launch_bounds__(NWF * 64, (fwd_min_waves<D, NWF>())) fwd_kerne
 }
 
 // =============================================================================================
-// Backward pre-pass: delta[b, h, s] = sum_d dO * O  (fp32); D/8 threads per row
+// Backward pre-pass, per (batch, head, query) row: -delta = -sum_d dO * O and lse * log2(e) (fp32),
+// D/8 threads per row. (Computing delta inside the dQ kernel instead -- it holds the dO rows --
+// measured neutral: the dQ prologue's extra O load cost what the launch saved.)
 // =============================================================================================
 template <int D>
 __global__ void __launch_bounds__(256) delta_kernel(const unsigned short* __restrict__ dout, Strides ds,
                                                     const unsigned short* __restrict__ o, Strides os,
-                                                    float* __restrict__ delta, int B, int H, int S) {
+                                                    const float* __restrict__ lse, float* __restrict__ ndelta,
+                                                    float* __restrict__ lse2, int B, int H, int S) {
   constexpr int TPR = D / 8, RPB = 256 / TPR;
   const int64_t row = (int64_t)blockIdx.x * RPB + (threadIdx.x / TPR);
   const int part = threadIdx.x % TPR;
@@ -444,7 +466,10 @@ __global__ void __launch_bounds__(256) delta_kernel(const unsigned short* __rest
   for (int e = 0; e < 8; ++e) acc += x[e] * y[e];
 #pragma unroll
   for (int off = TPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, TPR);
-  if (part == 0) delta[row] = acc;
+  if (part == 0) {
+    ndelta[row] = -acc;
+    lse2[row] = lse[row] * LOG2E;
+  }
 }
 
 template <int D>
@@ -457,7 +482,7 @@ constexpr int bwd_min_waves() { return D >= 256 ? 1 : 2; }
 template <bool MASK, int D>
 __device__ __forceinline__ void dq_tile(const char* kt, const char* vt, const bf16x8 (&qf)[D / 16],
                                         const bf16x8 (&df)[D / 16], f32x16 (&dqacc)[D / 32], float c, float lse2,
-                                        float dlt, int kbase, int qpos, int r, int h, int lane, bool diag, bool tail,
+                                        float ndlt, int kbase, int qpos, int r, int h, int lane, bool diag, bool tail,
                                         int kvlen, const uint8_t* lay_row, int blk) {
   int dd = kbase + 4 * h - qpos - r, dl = kbase + 4 * h - kvlen;  // see fwd_tile
   if (MASK) asm volatile("" : "+v"(dd), "+v"(dl));
@@ -484,7 +509,7 @@ __device__ __forceinline__ void dq_tile(const char* kt, const char* vt, const bf
         if (tail && dl + 32 * j + acc_row(i, 0) >= 0) p = 0.f;
         if (!(i < 8 ? b0 : b1)) p = 0.f;
       }
-      s[i] = p * (dp[i] - dlt);  // dS^T
+      s[i] = p * (dp[i] + ndlt);  // dS^T (ndlt = -delta)
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -500,7 +525,7 @@ template <bool SPARSE, int D>
 __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dq_kernel(
     const unsigned short* __restrict__ q, Strides qs, const unsigned short* __restrict__ k, Strides ks,
     const unsigned short* __restrict__ v, Strides vs, const unsigned short* __restrict__ dout, Strides dos,
-    const float* __restrict__ lse, const float* __restrict__ delta, unsigned short* __restrict__ dq, Strides dqs,
+    const float* __restrict__ lse, const float* __restrict__ ndelta, unsigned short* __restrict__ dq, Strides dqs,
     int B, int H, int Hk, int Sq, int Sk, float scale, int causal, Sparse sp, int kvlen, int qoff) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int ROWB = 2 * D;
@@ -531,13 +556,13 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dq_kernel(
   }
 
   const float lse2 = lse[lrow] * LOG2E;
-  const float dlt = delta[lrow];
   bf16x8 qf[D / 16], df[D / 16];
 #pragma unroll
   for (int t = 0; t < D / 16; ++t) {
     qf[t] = *reinterpret_cast<const bf16x8*>(qp + (int64_t)(q0 + r) * qs.s + 16 * t + 8 * h);
     df[t] = *reinterpret_cast<const bf16x8*>(dop + (int64_t)(q0 + r) * dos.s + 16 * t + 8 * h);
   }
+  const float ndlt = ndelta[lrow];
   f32x16 dqacc[D / 32];
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) dqacc[t] = zero16();
@@ -557,10 +582,10 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dq_kernel(
       const bool diag = causal && (kbase + KT - 1 > qpos);
       const bool tail = kbase + KT > kvlen;
       if (SPARSE || diag || tail)
-        dq_tile<true, D>(kt, vt, qf, df, dqacc, c, lse2, dlt, kbase, qpos, r, h, lane, diag, tail, kvlen, lay_row,
+        dq_tile<true, D>(kt, vt, qf, df, dqacc, c, lse2, ndlt, kbase, qpos, r, h, lane, diag, tail, kvlen, lay_row,
                          SPARSE ? sp.blk : 1);
       else
-        dq_tile<false, D>(kt, vt, qf, df, dqacc, c, lse2, dlt, kbase, qpos, r, h, lane, false, false, kvlen,
+        dq_tile<false, D>(kt, vt, qf, df, dqacc, c, lse2, ndlt, kbase, qpos, r, h, lane, false, false, kvlen,
                           nullptr, 1);
     }
     vm_wait_all();
@@ -617,16 +642,23 @@ __device__ __forceinline__ void dkdv_tile(const char* slot, const char* vblk, co
     b1 = sp.layout[((int64_t)hq0 * sp.nb + (qt0 + 16) / sp.blk) * sp.nb + kbl] != 0;
   }
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int qi = acc_row(i, h);
-    float p = fast_exp2(__builtin_fmaf(s[i], c, -l2[qi] * LOG2E));
-    if (MASK) {
-      if (diag && (k0 + r > qt0 + qi + qoff)) p = 0.f;
-      if (!(qi < 16 ? b0 : b1)) p = 0.f;
-    }
-    s[i] = p;                      // P
-    dp[i] = p * (dp[i] - dl[qi]);  // dS
+  for (int i = 0; i < 16; ++i) s[i] = fast_exp2(__builtin_fmaf(s[i], c, -l2[acc_row(i, h)]));  // P; l2 = lse log2(e)
+  // masks under wave-uniform (scalar) branches: interior tiles -- most of them -- run no per-score
+  // compares / selects (`diag` and the layout pointer are SGPR values; see the readfirstlane of w)
+  if (MASK && diag) {
+    int dd = k0 + r - 4 * h - qt0 - qoff;  // masked iff key > query + qoff, i.e. dd > row(i, 0)
+    asm volatile("" : "+v"(dd));            // keep the per-row compares against constants (see fwd_tile)
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (dd > acc_row(i, 0)) s[i] = 0.f;
   }
+  if (MASK && sp.layout) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (!(acc_row(i, h) < 16 ? b0 : b1)) s[i] = 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dp[i] = s[i] * (dp[i] + dl[acc_row(i, h)]);  // dS = P (dP - delta); dl = -delta
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
     const bf16x8 pb = acc_to_b(s, s2);
@@ -656,7 +688,10 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
   char* vblk = smem;
   char* ring = smem + G_::VBLK;
   int* tlist = reinterpret_cast<int*>(ring + 2 * G_::SLOT) + 1;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  // w via readfirstlane: the compiler then knows it (and k0, the causal `diag` test) is wave-uniform,
+  // so the diagonal mask is a scalar branch rather than per-lane selects on every tile
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), r = lane & 31,
+            h = lane >> 5;
   const int nkb = Sk / QB;
   int bh, kb;
   const int HB = SPLIT ? H : Hk;
@@ -711,18 +746,22 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
     dva[t] = zero16();
   }
   vm_wait_all();
+  // pin the K fragments as loaded before the loop: left to itself the compiler sinks their loads
+  // below the barrier, and its counted waits for them inside the loop then also wait on the
+  // hand-tracked LDS-DMA of the next tile
+#pragma unroll
+  for (int t = 0; t < D / 16; ++t) asm volatile("" ::"v"(kf[t]));
   __syncthreads();
   int cur = 0;
   for (int it = 0; it < total; ++it) {
-    if (it + 1 < total) issue(it + 1, ring + (cur ^ 1) * G_::SLOT);
     const int qt0 = sp.layout ? tlist[it] * QT : c_q;
     c_q = c_q + QT >= Sq ? qstart : c_q + QT;
     const bool active = !causal || (qt0 + QT - 1 + qoff >= k0);
-    if (active) {
-      const char* slot = ring + cur * G_::SLOT;
-      const bool diag = causal && (qt0 + qoff < k0 + QW);
-      dkdv_tile<true, D, PART>(slot, vblk, kf, dka, dva, c, qt0, k0, w, r, h, lane, diag, sp, hq0, kbl, qoff);
-    }
+    const bool diag = causal && (qt0 + qoff < k0 + QW);
+    if (it + 1 < total) issue(it + 1, ring + (cur ^ 1) * G_::SLOT);
+    if (active)
+      dkdv_tile<true, D, PART>(ring + cur * G_::SLOT, vblk, kf, dka, dva, c, qt0, k0, w, r, h, lane, diag, sp, hq0,
+                               kbl, qoff);
     vm_wait_all();
     __syncthreads();
     cur ^= 1;
@@ -909,13 +948,14 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
   const int B = q.size(0), Sq = q.size(1), H = q.size(2), Sk = k.size(1), Hk = k.size(2);
   constexpr int ROWB = 2 * D;
   using G_ = fa::KVL<D>;
-  auto delta = at::empty({B, H, Sq}, q.options().dtype(at::kFloat));
+  auto ndelta = at::empty({B, H, Sq}, q.options().dtype(at::kFloat));
+  auto lse2 = at::empty({B, H, Sq}, q.options().dtype(at::kFloat));
   const int64_t rows = (int64_t)B * H * Sq;
   constexpr int RPB = 256 / (D / 8);
   hipLaunchKernelGGL(fa::delta_kernel<D>, dim3((rows + RPB - 1) / RPB), dim3(256), 0, cur_stream(),
                      reinterpret_cast<const unsigned short*>(dout.data_ptr()), strides_of(dout),
-                     reinterpret_cast<const unsigned short*>(o.data_ptr()), strides_of(o), delta.data_ptr<float>(), B,
-                     H, Sq);
+                     reinterpret_cast<const unsigned short*>(o.data_ptr()), strides_of(o), lse.data_ptr<float>(),
+                     ndelta.data_ptr<float>(), lse2.data_ptr<float>(), B, H, Sq);
   SXE_LAUNCH_CHECK();
   const size_t lds_dq = 4 * fa::KT * ROWB + (sp.layout ? kListBytes : 0);
   const size_t lds_kv_max = G_::VBLK + 2 * G_::SLOT + kListBytes;
@@ -940,7 +980,7 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
                      reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
                      reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),
                      reinterpret_cast<const unsigned short*>(dout.data_ptr()), strides_of(dout),
-                     lse.data_ptr<float>(), delta.data_ptr<float>(),
+                     lse.data_ptr<float>(), ndelta.data_ptr<float>(),
                      reinterpret_cast<unsigned short*>(dq.data_ptr()), strides_of(dq), B, H, Hk, Sq, Sk, (float)scale,
                      causal ? 1 : 0, sp, kvlen, qoff);
   SXE_LAUNCH_CHECK();
@@ -960,7 +1000,7 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
                        reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
                        reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),
                        reinterpret_cast<const unsigned short*>(dout.data_ptr()), strides_of(dout),
-                       lse.data_ptr<float>(), delta.data_ptr<float>(),
+                       lse2.data_ptr<float>(), ndelta.data_ptr<float>(),
                        reinterpret_cast<unsigned short*>(dk.data_ptr()), strides_of(dk),
                        reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv),
                        partials ? pk.data_ptr<float>() : nullptr, partials ? pv.data_ptr<float>() : nullptr, B, H, Hk,
