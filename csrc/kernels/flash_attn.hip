@@ -333,7 +333,12 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const b
 template <int D, int NWF>
 constexpr int fwd_min_waves() { return D >= 256 ? 1 : 8 / NWF; }
 
-template <bool SPARSE, int NWF, int D>
+// DMA: K/V tiles go straight to LDS (global_load_lds from inline asm, see glds16) instead of through
+// the register Stager; head dim 256 always (staging registers would not fit next to its 128
+// accumulator + 64 Q-fragment registers), smaller head dims by default (SXE_FA_FWD_DMA=0 selects the
+// register Stager: 4-7 % slower at D 128, B4 S2048 to B1 S32k, equal at D 64 --
+// profiles/r05/attn_fwd_dma_ab.log)
+template <bool SPARSE, int NWF, int D, bool DMA = (D >= 256)>
 __global__ void __launch_bounds__(NWF * 64, (fwd_min_waves<D, NWF>())) fwd_kernel(
     const unsigned short* __restrict__ q, Strides qs, const unsigned short* __restrict__ k, Strides ks,
     const unsigned short* __restrict__ v, Strides vs, unsigned short* __restrict__ o, Strides os,
@@ -373,15 +378,12 @@ __global__ void __launch_bounds__(NWF * 64, (fwd_min_waves<D, NWF>())) fwd_kerne
   const int ntiles = SPARSE ? build_tile_list(sp, head, 0, nkt, KT, qb * QBF, qb * QBF + QBF, true, tlist) : nkt;
   auto tile_at = [&](int i) { return SPARSE ? tlist[i] : i; };
   const uint8_t* lrow = SPARSE ? sp.layout + ((int64_t)head * sp.nb + (q0 + r) / sp.blk) * sp.nb : nullptr;
-  // head dim 256: K/V tiles go straight to LDS (global_load_lds): register staging would not fit
-  // next to the 128 accumulator + 64 Q-fragment registers of a wave
-  constexpr bool DMA = D >= 256;
   Stager<KT, NWF, D> sk, sv;
   const int t0 = ntiles > 0 ? tile_at(0) : 0;
   if constexpr (DMA) {
     if (ntiles > 0) {
-      tile_glds<KT, D>(kp, ks.s, t0 * KT, smem);
-      tile_glds<KT, D>(vp, vs.s, t0 * KT, smem + KT * ROWB);
+      tile_glds<KT, D, NWF>(kp, ks.s, t0 * KT, smem);
+      tile_glds<KT, D, NWF>(vp, vs.s, t0 * KT, smem + KT * ROWB);
     }
     vm_wait_all();
   } else {
@@ -396,8 +398,8 @@ __global__ void __launch_bounds__(NWF * 64, (fwd_min_waves<D, NWF>())) fwd_kerne
     const bool more = (t + 1) < ntiles;
     if (more) {
       if constexpr (DMA) {
-        tile_glds<KT, D>(kp, ks.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF);
-        tile_glds<KT, D>(vp, vs.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF + KT * ROWB);
+        tile_glds<KT, D, NWF>(kp, ks.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF);
+        tile_glds<KT, D, NWF>(vp, vs.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF + KT * ROWB);
       } else {
         sk.load(kp, ks.s, tile_at(t + 1) * KT, Sk);
         sv.load(vp, vs.s, tile_at(t + 1) * KT, Sk);
@@ -671,18 +673,19 @@ __device__ __forceinline__ void dkdv_tile(const char* slot, const char* vblk, co
   }
 }
 
-// SPLIT (GQA): one workgroup per (batch, QUERY head, key block) instead of per KV head: under a
-// causal mask the KV-head form gives key block 0 G x (Sq/128) query tiles while the mean block has
-// half of that, and with B*Hk*Sk/128 ~ 2 workgroups per CU the whole launch waits for block 0
-// (measured 650 us at B4 S2048 H32/8). Splitting the G query heads cuts the longest job by G; the
-// per-head fp32 dK/dV partials [B, Sk, H, D] are summed over G by dkdv_reduce_kernel.
+// SPLIT (GQA): one workgroup per (batch, group of `hpw` QUERY heads, key block) instead of per KV
+// head: under a causal mask the KV-head form gives key block 0 G x (Sq/128) query tiles while the
+// mean block has half of that, and with B*Hk*Sk/128 ~ 2 workgroups per CU the whole launch waits for
+// block 0 (measured 650 us at B4 S2048 H32/8). Splitting the G query heads into G/hpw groups cuts the
+// longest job by G/hpw; the per-group fp32 dK/dV partials [B, Sk, H/hpw, D] are summed by
+// dkdv_reduce_kernel (hpw = 2 halves that partial traffic against hpw = 1).
 template <bool SPLIT, int D, int PART = 3>
 __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
     const unsigned short* __restrict__ q, Strides qs, const unsigned short* __restrict__ k, Strides ks,
     const unsigned short* __restrict__ v, Strides vs, const unsigned short* __restrict__ dout, Strides dos,
     const float* __restrict__ lse, const float* __restrict__ delta, unsigned short* __restrict__ dk, Strides dks,
     unsigned short* __restrict__ dv, Strides dvs, float* __restrict__ pk, float* __restrict__ pv, int B, int H,
-    int Hk, int Sq, int Sk, float scale, int causal, Sparse sp, int qoff) {
+    int Hk, int Sq, int Sk, float scale, int causal, Sparse sp, int qoff, int hpw) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using G_ = KVL<D>;
   char* vblk = smem;
@@ -694,12 +697,12 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
             h = lane >> 5;
   const int nkb = Sk / QB;
   int bh, kb;
-  const int HB = SPLIT ? H : Hk;
+  const int G = SPLIT ? hpw : H / Hk;  // query heads swept by this workgroup (sparse: 1)
+  const int HB = H / G;                 // workgroups along the head axis
   map_block(nkb, B * HB, false, bh, kb);  // key block 0 is the heaviest under causality
   const int b = bh / HB, hsel = bh - b * HB;
-  const int G = SPLIT ? 1 : H / Hk;
-  const int kh = SPLIT ? hsel / (H / Hk) : hsel;
-  const int hq0 = SPLIT ? hsel : kh * G;  // first query head swept by this workgroup
+  const int hq0 = hsel * G;             // first query head swept by this workgroup
+  const int kh = hq0 / (H / Hk);
   const int k0 = kb * QB + w * QW;  // this wave's first key
   const unsigned short* kp = k + b * ks.b + kh * ks.h;
   const unsigned short* vp = v + b * vs.b + kh * vs.h;
@@ -766,9 +769,9 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
     __syncthreads();
     cur ^= 1;
   }
-  if (SPLIT && pk != nullptr) {  // fp32 partials, layout [B, Sk, H, D] contiguous
-    float* kp32 = pk + (((int64_t)b * Sk + k0 + r) * H + hq0) * D;
-    float* vp32 = pv + (((int64_t)b * Sk + k0 + r) * H + hq0) * D;
+  if (SPLIT && pk != nullptr) {  // fp32 partials, layout [B, Sk, H / hpw, D] contiguous
+    float* kp32 = pk + (((int64_t)b * Sk + k0 + r) * HB + hsel) * D;
+    float* vp32 = pv + (((int64_t)b * Sk + k0 + r) * HB + hsel) * D;
 #pragma unroll
     for (int t = 0; t < D / 32; ++t)
 #pragma unroll
@@ -802,7 +805,8 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
 }
 
 
-// dk[b, s, kh, :] = sum_g pk[b, s, kh*G + g, :] (dv likewise); one thread per 8 output elements.
+// dk[b, s, kh, :] = sum_g pk[b, s, kh*G + g, :] (dv likewise) over the G = H / Hk partial groups of
+// each KV head (H here = the partial count, query heads / hpw); one thread per 8 output elements.
 template <int D>
 __global__ void __launch_bounds__(256) dkdv_reduce_kernel(const float* __restrict__ pk, const float* __restrict__ pv,
                                                           unsigned short* __restrict__ dk, Strides dks,
@@ -874,6 +878,7 @@ static int env_int(const char* name, int dflt) {
   return (e != nullptr && *e != 0) ? std::atoi(e) : dflt;
 }
 static bool fwd_narrow() { return env_int("SXE_FA_FWD_WAVES", 8) == 4; }
+static bool fwd_dma() { return env_int("SXE_FA_FWD_DMA", 1) != 0; }
 
 template <typename F>
 static void set_lds_limit(F* f, size_t bytes) {
@@ -899,6 +904,10 @@ static std::vector<at::Tensor> fwd_impl_d(at::Tensor q, at::Tensor k, at::Tensor
     if constexpr (D < 256) {
       set_lds_limit(&fa::fwd_kernel<false, 8, D>, mx);
       set_lds_limit(&fa::fwd_kernel<true, 8, D>, mx);
+      set_lds_limit(&fa::fwd_kernel<false, 4, D, true>, mx);
+      set_lds_limit(&fa::fwd_kernel<true, 4, D, true>, mx);
+      set_lds_limit(&fa::fwd_kernel<false, 8, D, true>, mx);
+      set_lds_limit(&fa::fwd_kernel<true, 8, D, true>, mx);
     }
     attr = true;
   }
@@ -914,6 +923,14 @@ static std::vector<at::Tensor> fwd_impl_d(at::Tensor q, at::Tensor k, at::Tensor
                        Sq, Sk, (float)scale, causal ? 1 : 0, sp, kvlen, qoff);
   };
   if constexpr (D < 256) {
+    if (fwd_dma()) {
+      if (wide)
+        sp.layout ? launch(fa::fwd_kernel<true, 8, D, true>, 8) : launch(fa::fwd_kernel<false, 8, D, true>, 8);
+      else
+        sp.layout ? launch(fa::fwd_kernel<true, 4, D, true>, 4) : launch(fa::fwd_kernel<false, 4, D, true>, 4);
+      SXE_LAUNCH_CHECK();
+      return {o, lse};
+    }
     if (wide) {
       sp.layout ? launch(fa::fwd_kernel<true, 8, D>, 8) : launch(fa::fwd_kernel<false, 8, D>, 8);
       SXE_LAUNCH_CHECK();
@@ -986,13 +1003,32 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
   SXE_LAUNCH_CHECK();
   // sparse: always one workgroup per query head (per-head tile lists); with GQA the per-head fp32
   // partials are reduced; causal GQA: split to remove the key-block-0 tail (see dkdv_kernel)
-  const bool split = sp.layout != nullptr || (causal && H > Hk);
-  const bool partials = split && H > Hk;
+  // query heads per dK/dV workgroup in the split form (a divisor of the GQA group; sparse: 1). Auto
+  // (SXE_FA_DKDV_HPW unset / 0): the largest divisor whose heaviest workgroup -- key block 0 sweeps
+  // hpw x Sq/32 query tiles under the causal mask -- still fits the mean load of the 2 x CUs
+  // workgroup slots (hpw <= B H nkb / (4 CUs)), and at most 2 from 8k keys on, where the partials'
+  // traffic no longer matters and the balance does. Measured fwd+bwd (H32/8 D128 causal; 1 / 2 / 4
+  // heads per workgroup): B8 S2048 1.88 / 1.76 / 1.69 ms, B4 S2048 0.84 / 0.76 / 0.88, B1 S32k
+  // 36.4 / 36.2 / 37.3; B1 S32k H4/1 4.75 / 6.14 / 9.15 (profiles/r05/attn_dkdv_hpw_sweep.log)
+  int hpw = sp.layout != nullptr ? 1 : env_int("SXE_FA_DKDV_HPW", 0);
+  if (hpw == 0) {
+    int64_t cap = (int64_t)B * H * (Sk / fa::QB) / (4 * kNumCUs);
+    if (Sk >= 8192 && cap > 2) cap = 2;
+    for (int d = H / Hk; d >= 1; --d)
+      if ((H / Hk) % d == 0 && d <= cap) {
+        hpw = d;
+        break;
+      }
+  }
+  if (hpw < 1 || (H / Hk) % hpw != 0) hpw = 1;
+  const bool split = sp.layout != nullptr || (causal && H / Hk > hpw);
+  const bool partials = split && H / hpw > Hk;
+  const int np = H / hpw;  // partial head groups
   const size_t lds_kv = G_::VBLK + 2 * G_::SLOT + (sp.layout ? kListBytes : 0);
   at::Tensor pk, pv;
   if (partials) {
-    pk = at::empty({B, Sk, H, D}, q.options().dtype(at::kFloat));
-    pv = at::empty({B, Sk, H, D}, q.options().dtype(at::kFloat));
+    pk = at::empty({B, Sk, np, D}, q.options().dtype(at::kFloat));
+    pv = at::empty({B, Sk, np, D}, q.options().dtype(at::kFloat));
   }
   auto launch = [&](auto kern, int heads) {
     hipLaunchKernelGGL(kern, dim3((Sk / fa::QB) * B * heads), dim3(256), lds_kv, cur_stream(),
@@ -1004,22 +1040,22 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
                        reinterpret_cast<unsigned short*>(dk.data_ptr()), strides_of(dk),
                        reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv),
                        partials ? pk.data_ptr<float>() : nullptr, partials ? pv.data_ptr<float>() : nullptr, B, H, Hk,
-                       Sq, Sk, (float)scale, causal ? 1 : 0, sp, qoff);
+                       Sq, Sk, (float)scale, causal ? 1 : 0, sp, qoff, hpw);
   };
   if (split) {
     if constexpr (D >= 256) {
-      launch(fa::dkdv_kernel<true, D, 1>, H);
+      launch(fa::dkdv_kernel<true, D, 1>, np);
       SXE_LAUNCH_CHECK();
-      launch(fa::dkdv_kernel<true, D, 2>, H);
+      launch(fa::dkdv_kernel<true, D, 2>, np);
     } else {
-      launch(fa::dkdv_kernel<true, D>, H);
+      launch(fa::dkdv_kernel<true, D>, np);
     }
     SXE_LAUNCH_CHECK();
     if (partials) {
       const int64_t n8 = (int64_t)B * Sk * Hk * (D / 8);
       hipLaunchKernelGGL(fa::dkdv_reduce_kernel<D>, dim3(stream_grid(n8, 256)), dim3(256), 0, cur_stream(),
                          pk.data_ptr<float>(), pv.data_ptr<float>(), reinterpret_cast<unsigned short*>(dk.data_ptr()),
-                         strides_of(dk), reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv), B, Sk, H,
+                         strides_of(dk), reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv), B, Sk, np,
                          Hk);
     }
   } else if constexpr (D >= 256) {

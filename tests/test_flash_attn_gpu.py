@@ -39,6 +39,30 @@ def test_flash_fwd_bwd(causal, B, S, H, Hk):
     assert _rel(v.grad, v2.grad) < 2e-2
 
 
+@pytest.mark.parametrize("hpw", ["1", "2", "4", "3"])
+@pytest.mark.parametrize("D", [64, 128, 256])
+@pytest.mark.parametrize("B,S,H,Hk", [(1, 384, 8, 2), (2, 256, 12, 3)])
+def test_flash_bwd_dkdv_head_groups(hpw, D, B, S, H, Hk, monkeypatch):
+    """Causal GQA backward with the dK/dV workgroups sweeping `hpw` query heads each
+    (SXE_FA_DKDV_HPW, read per call): 1 and 2 write fp32 partials summed by the reduce kernel, a
+    whole group (4 of G=4, 3 of G=3) writes dK/dV directly, a non-divisor falls back to 1."""
+    from shuffle_exchange_amd.ops.attention import attention, reference_attention
+    monkeypatch.setenv("SXE_FA_DKDV_HPW", hpw)
+    torch.manual_seed(H + D)
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    o = attention(q, k, v, causal=True)
+    q2, k2, v2 = (t.detach().float().requires_grad_() for t in (q, k, v))
+    o2 = reference_attention(q2, k2, v2, causal=True)
+    do = torch.randn_like(o2)
+    (o.float() * do).sum().backward()
+    (o2 * do).sum().backward()
+    assert _rel(q.grad, q2.grad) < 2e-2
+    assert _rel(k.grad, k2.grad) < 2e-2
+    assert _rel(v.grad, v2.grad) < 2e-2
+
+
 def test_flash_lse():
     from shuffle_exchange_amd.ops.attention import attention_with_lse, reference_attention
     q = torch.randn(1, 256, 2, 128, device="cuda", dtype=torch.bfloat16)
@@ -198,16 +222,19 @@ def test_flash_cross_and_prefix_lengths(causal, Sq, Sk, D, monkeypatch):
     assert (lse - lse2).abs().max().item() < 2e-2
 
 
+@pytest.mark.parametrize("dma", ["0", "1"])
 @pytest.mark.parametrize("waves", [4, 8])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("B,Sq,Sk,H,Hk,D", [(2, 256, 256, 4, 4, 128), (1, 512, 512, 8, 2, 128),
                                             (2, 256, 256, 4, 2, 64), (1, 256, 768, 4, 1, 128),
                                             (1, 512, 1024, 4, 2, 64), (1, 1024, 1024, 2, 2, 128)])
-def test_flash_fwd_variants(waves, causal, B, Sq, Sk, H, Hk, D, monkeypatch):
-    """Both forward variants (4 and 8 waves per workgroup, SXE_FA_FWD_WAVES, read per call) against
-    the fp32 oracle: head dims 64 / 128, causal / full, q_len != kv_len, GQA."""
+def test_flash_fwd_variants(dma, waves, causal, B, Sq, Sk, H, Hk, D, monkeypatch):
+    """Every forward variant (4 and 8 waves per workgroup, SXE_FA_FWD_WAVES; K/V through registers
+    or by LDS-DMA, SXE_FA_FWD_DMA; both read per call) against the fp32 oracle: head dims 64 / 128,
+    causal / full, q_len != kv_len, GQA."""
     A = _no_sdpa(monkeypatch)
     monkeypatch.setenv("SXE_FA_FWD_WAVES", str(waves))
+    monkeypatch.setenv("SXE_FA_FWD_DMA", dma)
     torch.manual_seed(2)
     q = torch.randn(B, Sq, H, D, device="cuda", dtype=torch.bfloat16)
     k = torch.randn(B, Sk, Hk, D, device="cuda", dtype=torch.bfloat16)
