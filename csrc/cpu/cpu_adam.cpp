@@ -125,7 +125,10 @@ void adam_step_(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, c10::opt
   const int64_t gsz = g.element_size();
   const int64_t T = 4096;
   const int64_t tiles = (n + T - 1) / T;
-#pragma omp parallel for schedule(static)
+  // dynamic chunks of 16 tiles (256 KB of each array): the asynchronous host tier runs this team
+  // beside the training thread, and under a static split one preempted thread stalls the whole
+  // update by its share
+#pragma omp parallel for schedule(dynamic, 16)
   for (int64_t t = 0; t < tiles; ++t) {
     const int64_t o = t * T;
     const int64_t len = std::min(T, n - o);
@@ -197,6 +200,10 @@ double sumsq(at::Tensor x) {
 
 int64_t num_threads() { return omp_get_max_threads(); }
 
+// OpenMP team size of the CALLING thread's later updates (a per-thread setting): the asynchronous
+// host-optimizer worker leaves one CPU to the thread that keeps launching GPU work
+void set_num_threads(int64_t n) { omp_set_num_threads((int)std::max<int64_t>(1, n)); }
+
 }  // namespace sxe_cpu
 
 TORCH_LIBRARY(sxe_cpu, m) {
@@ -206,6 +213,7 @@ TORCH_LIBRARY(sxe_cpu, m) {
   m.def("adagrad_step_(Tensor(a!) p, Tensor g, Tensor(b!) s, float lr, float eps, float wd) -> ()");
   m.def("sumsq(Tensor x) -> float");
   m.def("num_threads() -> int", &sxe_cpu::num_threads);
+  m.def("set_num_threads(int n) -> ()", &sxe_cpu::set_num_threads);
 }
 TORCH_LIBRARY_IMPL(sxe_cpu, CPU, m) {
   m.impl("adam_step_", &sxe_cpu::adam_step_);

@@ -456,6 +456,11 @@ class HostOptimizerStep:
             try:
                 if dev is not None:
                     torch.cuda.set_device(dev)
+                cops = getattr(torch.ops, "sxe_cpu", None)
+                if cops is not None and hasattr(cops, "set_num_threads"):
+                    # one CPU stays with the training thread, which keeps launching the next
+                    # forward's kernels while this team updates (per-thread OpenMP setting)
+                    cops.set_num_threads(max(1, int(cops.num_threads()) - 1))
                 NS = len(self.gslots)
                 for k, ((g, i, u, off), (grad, ev)) in enumerate(zip(flat, d2h)):
                     ta = _time.perf_counter()
