@@ -27,6 +27,27 @@ def test_skinny_gemm_matches_fp32(M, N, K, with_bias):
     assert err <= 1e-2 * ref.abs().max().item() + 1e-2, err
 
 
+@pytest.mark.parametrize("M", [1, 4])
+@pytest.mark.parametrize("N,K", [(100, 264), (4104, 4096)])
+def test_skinny_gemm_nontemporal_loads_match(M, N, K, monkeypatch):
+    """SXE_SKINNY_NT=1 (non-temporal weight loads: separate kernel instantiations) gives the same
+    bits as the default loads, for the plain GEMM and the fused RMSNorm / SwiGLU prologues."""
+    g = torch.Generator(device="cuda").manual_seed(N + K)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    gw = torch.rand(K, device="cuda", generator=g).bfloat16()
+    x2 = torch.randn(M, 2 * K, device="cuda", dtype=torch.bfloat16, generator=g)
+    outs = []
+    for nt in ("0", "1"):
+        monkeypatch.setenv("SXE_SKINNY_NT", nt)
+        y = torch.ops.sxe.skinny_gemm(x, w, None)
+        yr = torch.ops.sxe.skinny_gemm_pro(x, None, gw, 1e-5, w, None, None, 1)[0]
+        ys = torch.ops.sxe.skinny_gemm_pro(x2, None, None, 0.0, w, None, None, 2)[0]
+        outs.append((y, yr, ys))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_linear_dispatches_skinny_under_no_grad():
     from shuffle_exchange_amd.ops.linear import linear
     w = torch.randn(256, 512, device="cuda", dtype=torch.bfloat16)
