@@ -82,6 +82,39 @@ __device__ __forceinline__ bf16x8 lds_trA(const char* base, int row0, int dt, in
   return __builtin_bit_cast(bf16x8, c);
 }
 
+// Per-lane byte offsets of the two LDS read forms above, computed once per kernel: the swizzle only
+// looks at the low 4 row bits, so for a tile row base row0 that is a multiple of 16
+//   lds_row16(base, row0 + r, 2 t2 + h)  = base + 2D row0 + row[t2]
+//   lds_trA(base, row0, dt, lane)        = tr_read(base + 2D row0, tr[dt][0], tr[dt][1])
+// and every read in a tile loop is a hoisted VGPR plus an instruction immediate (recomputed per read,
+// the XOR'd offsets cost ~40 VALU adds per forward tile).
+template <int D>
+struct LaneOffs {
+  int row[D / 16];
+  int tr[D / 32][2];
+  __device__ __forceinline__ void init(int lane) {
+    const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int t2 = 0; t2 < D / 16; ++t2) row[t2] = soff<D>(r, 2 * t2 + h);
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, hh = g >> 1;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) {
+      const int ch = 4 * dt + 2 * (g & 1) + (p >> 1);
+      tr[dt][0] = soff<D>(4 * hh + q, ch) + 8 * (p & 1);
+      tr[dt][1] = soff<D>(4 * hh + q + 8, ch) + 8 * (p & 1);
+    }
+  }
+};
+__device__ __forceinline__ bf16x8 lds_row_at(const char* base, int off) {
+  return *reinterpret_cast<const bf16x8*>(base + off);
+}
+__device__ __forceinline__ bf16x8 lds_tr_at(const char* base, const int (&o)[2]) {
+  i16x4 lo = lds_tr(base, o[0]);
+  i16x4 hi = lds_tr(base, o[1]);
+  const i16x8 c = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, c);
+}
+
 // Accumulator registers 8s..8s+7 -> bf16 B operand (k-step s of the accumulator-as-operand trick).
 __device__ __forceinline__ bf16x8 acc_to_b(const f32x16& a, int s) {
   bf16x8 r;
@@ -249,7 +282,7 @@ __device__ __forceinline__ void vm_wait_all() { __builtin_amdgcn_s_waitcnt(0x0F7
 // the Llama-3 shape ~90 % of the tiles take it; the masked body handles the diagonal, the kv_len
 // tail and block-sparse layouts.
 template <bool MASK, int D>
-__device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const bf16x8 (&qf)[D / 16],
+__device__ __forceinline__ void fwd_tile(const LaneOffs<D>& lo, const char* kt, const char* vt, const bf16x8 (&qf)[D / 16],
                                          f32x16 (&oacc)[D / 32], float& m, float& l, float c, int kbase, int qpos,
                                          int r, int h, int lane, bool diag, bool tail, int kvlen, const uint8_t* lrow,
                                          int blk) {
@@ -262,7 +295,7 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const b
     s[j] = zero16();
     if (j == 1 && skip1) break;
 #pragma unroll
-    for (int t2 = 0; t2 < D / 16; ++t2) s[j] = mfma(lds_row16<D>(kt, 32 * j + r, 2 * t2 + h), qf[t2], s[j]);
+    for (int t2 = 0; t2 < D / 16; ++t2) s[j] = mfma(lds_row_at(kt + 32 * j * 2 * D, lo.row[t2]), qf[t2], s[j]);
   }
   // raw scores: the max is taken before scaling (c > 0) and the scale folds into the exp's FMA
   float mx = -INFINITY;
@@ -321,7 +354,8 @@ __device__ __forceinline__ void fwd_tile(const char* kt, const char* vt, const b
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 pb = acc_to_b(s[j], s2);
 #pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt) oacc[dt] = mfma(lds_trA<D>(vt, 32 * j + 16 * s2, dt, lane), pb, oacc[dt]);
+      for (int dt = 0; dt < D / 32; ++dt)
+        oacc[dt] = mfma(lds_tr_at(vt + (32 * j + 16 * s2) * 2 * D, lo.tr[dt]), pb, oacc[dt]);
     }
   }
 }
@@ -393,13 +427,18 @@ __global__ void __launch_bounds__(NWF * 64, (fwd_min_waves<D, NWF>())) fwd_kerne
     sv.store(smem + KT * ROWB);
   }
   __syncthreads();
-  int cur = 0;
-  for (int t = 0; t < ntiles; ++t) {
+  LaneOffs<D> lo;
+  lo.init(lane);
+  // the tile loop runs unrolled by two so the ring slot is a compile-time constant in each copy: every
+  // LDS address is then a hoisted per-lane offset plus an instruction immediate (with a runtime slot
+  // each K / V read paid a VALU add per tile -- ~50 of the interior tile's ~200 VALU instructions)
+  auto step = [&](const int t, auto slot) {
+    constexpr int CUR = decltype(slot)::value;
     const bool more = (t + 1) < ntiles;
     if (more) {
       if constexpr (DMA) {
-        tile_glds<KT, D, NWF>(kp, ks.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF);
-        tile_glds<KT, D, NWF>(vp, vs.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF + KT * ROWB);
+        tile_glds<KT, D, NWF>(kp, ks.s, tile_at(t + 1) * KT, smem + (CUR ^ 1) * BUF);
+        tile_glds<KT, D, NWF>(vp, vs.s, tile_at(t + 1) * KT, smem + (CUR ^ 1) * BUF + KT * ROWB);
       } else {
         sk.load(kp, ks.s, tile_at(t + 1) * KT, Sk);
         sv.load(vp, vs.s, tile_at(t + 1) * KT, Sk);
@@ -409,24 +448,27 @@ __global__ void __launch_bounds__(NWF * 64, (fwd_min_waves<D, NWF>())) fwd_kerne
     // a wave whose queries all precede this tile has nothing to add (causal)
     const bool active = !causal || kbase <= qpos + QW - 1;
     if (active) {
-      const char* kt = smem + cur * BUF;
+      const char* kt = smem + CUR * BUF;
       const char* vt = kt + KT * ROWB;
       const bool diag = causal && (kbase + KT - 1 > qpos);
       const bool tail = kbase + KT > kvlen;  // keys past the valid length (padded key axis)
       if (SPARSE || diag || tail)
-        fwd_tile<true, D>(kt, vt, qf, oacc, m, l, c, kbase, qpos, r, h, lane, diag, tail, kvlen, lrow,
+        fwd_tile<true, D>(lo, kt, vt, qf, oacc, m, l, c, kbase, qpos, r, h, lane, diag, tail, kvlen, lrow,
                           SPARSE ? sp.blk : 1);
       else
-        fwd_tile<false, D>(kt, vt, qf, oacc, m, l, c, kbase, qpos, r, h, lane, false, false, kvlen, nullptr, 1);
+        fwd_tile<false, D>(lo, kt, vt, qf, oacc, m, l, c, kbase, qpos, r, h, lane, false, false, kvlen, nullptr, 1);
     }
     if constexpr (DMA) {
       vm_wait_all();
     } else if (more) {
-      sk.store(smem + (cur ^ 1) * BUF);
-      sv.store(smem + (cur ^ 1) * BUF + KT * ROWB);
+      sk.store(smem + (CUR ^ 1) * BUF);
+      sv.store(smem + (CUR ^ 1) * BUF + KT * ROWB);
     }
     __syncthreads();
-    cur ^= 1;
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    step(t, std::integral_constant<int, 0>{});
+    if (t + 1 < ntiles) step(t + 1, std::integral_constant<int, 1>{});
   }
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;  // a fully masked row outputs zeros
@@ -482,7 +524,7 @@ constexpr int bwd_min_waves() { return D >= 256 ? 1 : 2; }
 // dS^T = P^T (dP^T - delta), dQ^T += K^T dS^T.
 // =============================================================================================
 template <bool MASK, int D>
-__device__ __forceinline__ void dq_tile(const char* kt, const char* vt, const bf16x8 (&qf)[D / 16],
+__device__ __forceinline__ void dq_tile(const LaneOffs<D>& lo, const char* kt, const char* vt, const bf16x8 (&qf)[D / 16],
                                         const bf16x8 (&df)[D / 16], f32x16 (&dqacc)[D / 32], float c, float lse2,
                                         float ndlt, int kbase, int qpos, int r, int h, int lane, bool diag, bool tail,
                                         int kvlen, const uint8_t* lay_row, int blk) {
@@ -495,8 +537,8 @@ __device__ __forceinline__ void dq_tile(const char* kt, const char* vt, const bf
     f32x16 s = zero16(), dp = zero16();
 #pragma unroll
     for (int t2 = 0; t2 < D / 16; ++t2) {
-      s = mfma(lds_row16<D>(kt, 32 * j + r, 2 * t2 + h), qf[t2], s);
-      dp = mfma(lds_row16<D>(vt, 32 * j + r, 2 * t2 + h), df[t2], dp);
+      s = mfma(lds_row_at(kt + 32 * j * 2 * D, lo.row[t2]), qf[t2], s);
+      dp = mfma(lds_row_at(vt + 32 * j * 2 * D, lo.row[t2]), df[t2], dp);
     }
     bool b0 = true, b1 = true;
     if (MASK && lay_row) {
@@ -518,7 +560,7 @@ __device__ __forceinline__ void dq_tile(const char* kt, const char* vt, const bf
       const bf16x8 db = acc_to_b(s, s2);
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt)
-        dqacc[dt] = mfma(lds_trA<D>(kt, 32 * j + 16 * s2, dt, lane), db, dqacc[dt]);
+        dqacc[dt] = mfma(lds_tr_at(kt + (32 * j + 16 * s2) * 2 * D, lo.tr[dt]), db, dqacc[dt]);
     }
   }
 }
@@ -569,30 +611,40 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dq_kernel(
 #pragma unroll
   for (int t = 0; t < D / 32; ++t) dqacc[t] = zero16();
   vm_wait_all();
+  // pin the Q / dO fragments and row constants as loaded before the loop (see dkdv_kernel)
+#pragma unroll
+  for (int t = 0; t < D / 16; ++t) asm volatile("" ::"v"(qf[t]), "v"(df[t]));
+  asm volatile("" ::"v"(lse2), "v"(ndlt));
   __syncthreads();
-  int cur = 0;
-  for (int t = 0; t < ntiles; ++t) {
+  LaneOffs<D> lo;
+  lo.init(lane);
+  // unrolled by two: compile-time ring slot, hoisted LDS offsets (see fwd_kernel)
+  auto step = [&](const int t, auto slot) {
+    constexpr int CUR = decltype(slot)::value;
     if (t + 1 < ntiles) {
-      tile_glds<KT, D>(kp, ks.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF);
-      tile_glds<KT, D>(vp, vs.s, tile_at(t + 1) * KT, smem + (cur ^ 1) * BUF + KT * ROWB);
+      tile_glds<KT, D>(kp, ks.s, tile_at(t + 1) * KT, smem + (CUR ^ 1) * BUF);
+      tile_glds<KT, D>(vp, vs.s, tile_at(t + 1) * KT, smem + (CUR ^ 1) * BUF + KT * ROWB);
     }
     const int kbase = tile_at(t) * KT;
     const bool active = !causal || kbase <= qpos + QW - 1;
     if (active) {
-      const char* kt = smem + cur * BUF;
-      const char* vt = smem + cur * BUF + KT * ROWB;
+      const char* kt = smem + CUR * BUF;
+      const char* vt = smem + CUR * BUF + KT * ROWB;
       const bool diag = causal && (kbase + KT - 1 > qpos);
       const bool tail = kbase + KT > kvlen;
       if (SPARSE || diag || tail)
-        dq_tile<true, D>(kt, vt, qf, df, dqacc, c, lse2, ndlt, kbase, qpos, r, h, lane, diag, tail, kvlen, lay_row,
-                         SPARSE ? sp.blk : 1);
+        dq_tile<true, D>(lo, kt, vt, qf, df, dqacc, c, lse2, ndlt, kbase, qpos, r, h, lane, diag, tail, kvlen,
+                         lay_row, SPARSE ? sp.blk : 1);
       else
-        dq_tile<false, D>(kt, vt, qf, df, dqacc, c, lse2, ndlt, kbase, qpos, r, h, lane, false, false, kvlen,
+        dq_tile<false, D>(lo, kt, vt, qf, df, dqacc, c, lse2, ndlt, kbase, qpos, r, h, lane, false, false, kvlen,
                           nullptr, 1);
     }
     vm_wait_all();
     __syncthreads();
-    cur ^= 1;
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    step(t, std::integral_constant<int, 0>{});
+    if (t + 1 < ntiles) step(t + 1, std::integral_constant<int, 1>{});
   }
   unsigned short* op = dq + b * dqs.b + head * dqs.h + (int64_t)(q0 + r) * dqs.s;
 #pragma unroll
@@ -623,7 +675,8 @@ template <int D> struct KVL {
 // PART: 3 = dK and dV in one sweep; 1 = dV only; 2 = dK only (head dim 256: the two 128-register
 // accumulators of one sweep would spill, so two sweeps each recompute S = Q K^T)
 template <bool MASK, int D, int PART>
-__device__ __forceinline__ void dkdv_tile(const char* slot, const char* vblk, const bf16x8 (&kf)[D / 16],
+__device__ __forceinline__ void dkdv_tile(const LaneOffs<D>& lo, const char* slot, const char* vblk,
+                                          const bf16x8 (&kf)[D / 16],
                                           f32x16 (&dka)[D / 32], f32x16 (&dva)[D / 32], float c, int qt0, int k0,
                                           int w, int r, int h, int lane, bool diag, const Sparse& sp, int hq0,
                                           int kbl, int qoff) {
@@ -634,9 +687,9 @@ __device__ __forceinline__ void dkdv_tile(const char* slot, const char* vblk, co
   f32x16 s = zero16(), dp = zero16();
 #pragma unroll
   for (int t2 = 0; t2 < D / 16; ++t2) {
-    s = mfma(lds_row16<D>(qt, r, 2 * t2 + h), kf[t2], s);  // S  [query][key]
+    s = mfma(lds_row_at(qt, lo.row[t2]), kf[t2], s);  // S  [query][key]
     if constexpr ((PART & 2) != 0)
-      dp = mfma(lds_row16<D>(dt_, r, 2 * t2 + h), lds_row16<D>(vblk, w * QW + r, 2 * t2 + h), dp);  // dP
+      dp = mfma(lds_row_at(dt_, lo.row[t2]), lds_row_at(vblk + w * QW * 2 * D, lo.row[t2]), dp);  // dP
   }
   bool b0 = true, b1 = true;  // layout bits of query rows qt0+[0,16) and qt0+[16,32) vs this key
   if (MASK && sp.layout) {
@@ -667,8 +720,8 @@ __device__ __forceinline__ void dkdv_tile(const char* slot, const char* vblk, co
     const bf16x8 db = acc_to_b(dp, s2);
 #pragma unroll
     for (int t = 0; t < D / 32; ++t) {
-      if constexpr ((PART & 1) != 0) dva[t] = mfma(lds_trA<D>(dt_, 16 * s2, t, lane), pb, dva[t]);  // dV^T += dO^T P
-      if constexpr ((PART & 2) != 0) dka[t] = mfma(lds_trA<D>(qt, 16 * s2, t, lane), db, dka[t]);   // dK^T += Q^T dS
+      if constexpr ((PART & 1) != 0) dva[t] = mfma(lds_tr_at(dt_ + 16 * s2 * 2 * D, lo.tr[t]), pb, dva[t]);  // dV^T
+      if constexpr ((PART & 2) != 0) dka[t] = mfma(lds_tr_at(qt + 16 * s2 * 2 * D, lo.tr[t]), db, dka[t]);   // dK^T
     }
   }
 }
@@ -755,19 +808,25 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
 #pragma unroll
   for (int t = 0; t < D / 16; ++t) asm volatile("" ::"v"(kf[t]));
   __syncthreads();
-  int cur = 0;
-  for (int it = 0; it < total; ++it) {
+  LaneOffs<D> lo;
+  lo.init(lane);
+  // unrolled by two: compile-time ring slot, hoisted LDS offsets (see fwd_kernel)
+  auto step = [&](const int it, auto slotc) {
+    constexpr int CUR = decltype(slotc)::value;
     const int qt0 = sp.layout ? tlist[it] * QT : c_q;
     c_q = c_q + QT >= Sq ? qstart : c_q + QT;
     const bool active = !causal || (qt0 + QT - 1 + qoff >= k0);
     const bool diag = causal && (qt0 + qoff < k0 + QW);
-    if (it + 1 < total) issue(it + 1, ring + (cur ^ 1) * G_::SLOT);
+    if (it + 1 < total) issue(it + 1, ring + (CUR ^ 1) * G_::SLOT);
     if (active)
-      dkdv_tile<true, D, PART>(ring + cur * G_::SLOT, vblk, kf, dka, dva, c, qt0, k0, w, r, h, lane, diag, sp, hq0,
-                               kbl, qoff);
+      dkdv_tile<true, D, PART>(lo, ring + CUR * G_::SLOT, vblk, kf, dka, dva, c, qt0, k0, w, r, h, lane, diag, sp,
+                               hq0, kbl, qoff);
     vm_wait_all();
     __syncthreads();
-    cur ^= 1;
+  };
+  for (int it = 0; it < total; it += 2) {
+    step(it, std::integral_constant<int, 0>{});
+    if (it + 1 < total) step(it + 1, std::integral_constant<int, 1>{});
   }
   if (SPLIT && pk != nullptr) {  // fp32 partials, layout [B, Sk, H / hpw, D] contiguous
     float* kp32 = pk + (((int64_t)b * Sk + k0 + r) * HB + hsel) * D;
