@@ -1083,6 +1083,9 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
   const bool split = sp.layout != nullptr || (causal && H / Hk > hpw);
   const bool partials = split && H / hpw > Hk;
   const int np = H / hpw;  // partial head groups
+  // head dim 256: dV and dK in two sweeps (PART 1 / 2: each recomputes S, 128 accumulator registers
+  // apiece) or one (SXE_FA_DKDV_ONE_SWEEP=1: S once, 256 accumulators, a few spilled registers)
+  const bool one_sweep = D >= 256 && env_int("SXE_FA_DKDV_ONE_SWEEP", 0) != 0;
   const size_t lds_kv = G_::VBLK + 2 * G_::SLOT + (sp.layout ? kListBytes : 0);
   at::Tensor pk, pv;
   if (partials) {
@@ -1102,7 +1105,7 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
                        Sq, Sk, (float)scale, causal ? 1 : 0, sp, qoff, hpw);
   };
   if (split) {
-    if constexpr (D >= 256) {
+    if (D >= 256 && !one_sweep) {
       launch(fa::dkdv_kernel<true, D, 1>, np);
       SXE_LAUNCH_CHECK();
       launch(fa::dkdv_kernel<true, D, 2>, np);
@@ -1117,7 +1120,7 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
                          strides_of(dk), reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv), B, Sk, np,
                          Hk);
     }
-  } else if constexpr (D >= 256) {
+  } else if (D >= 256 && !one_sweep) {
     launch(fa::dkdv_kernel<false, D, 1>, Hk);
     SXE_LAUNCH_CHECK();
     launch(fa::dkdv_kernel<false, D, 2>, Hk);

@@ -63,6 +63,30 @@ def test_flash_bwd_dkdv_head_groups(hpw, D, B, S, H, Hk, monkeypatch):
     assert _rel(v.grad, v2.grad) < 2e-2
 
 
+@pytest.mark.parametrize("one_sweep", ["0", "1"])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("B,S,H,Hk", [(1, 256, 4, 4), (1, 384, 8, 2)])
+def test_flash_bwd_d256_sweeps(one_sweep, causal, B, S, H, Hk, monkeypatch):
+    """Head dim 256 backward with dV and dK in two sweeps (default) or one (SXE_FA_DKDV_ONE_SWEEP=1,
+    read per call), MHA and causal GQA (split + reduce), against the fp32 oracle."""
+    from shuffle_exchange_amd.ops.attention import attention, reference_attention
+    monkeypatch.setenv("SXE_FA_DKDV_ONE_SWEEP", one_sweep)
+    torch.manual_seed(S + H)
+    D = 256
+    q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    o = attention(q, k, v, causal=causal)
+    q2, k2, v2 = (t.detach().float().requires_grad_() for t in (q, k, v))
+    o2 = reference_attention(q2, k2, v2, causal=causal)
+    do = torch.randn_like(o2)
+    (o.float() * do).sum().backward()
+    (o2 * do).sum().backward()
+    assert _rel(q.grad, q2.grad) < 2e-2
+    assert _rel(k.grad, k2.grad) < 2e-2
+    assert _rel(v.grad, v2.grad) < 2e-2
+
+
 def test_flash_lse():
     from shuffle_exchange_amd.ops.attention import attention_with_lse, reference_attention
     q = torch.randn(1, 256, 2, 128, device="cuda", dtype=torch.bfloat16)
