@@ -1083,9 +1083,10 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
   const bool split = sp.layout != nullptr || (causal && H / Hk > hpw);
   const bool partials = split && H / hpw > Hk;
   const int np = H / hpw;  // partial head groups
-  // head dim 256: dV and dK in two sweeps (PART 1 / 2: each recomputes S, 128 accumulator registers
-  // apiece) or one (SXE_FA_DKDV_ONE_SWEEP=1: S once, 256 accumulators, a few spilled registers)
-  const bool one_sweep = D >= 256 && env_int("SXE_FA_DKDV_ONE_SWEEP", 0) != 0;
+  // head dim 256: dV and dK in one sweep (S once, 256 accumulators, a few spilled registers; default)
+  // or two (SXE_FA_DKDV_ONE_SWEEP=0: PART 1 / 2, each recomputes S): one sweep is 1-9 % faster
+  // fwd+bwd (profiles/r05/attn_d256_one_sweep_ab.log)
+  const bool one_sweep = D >= 256 && env_int("SXE_FA_DKDV_ONE_SWEEP", 1) != 0;
   const size_t lds_kv = G_::VBLK + 2 * G_::SLOT + (sp.layout ? kListBytes : 0);
   at::Tensor pk, pv;
   if (partials) {
