@@ -522,151 +522,6 @@ __global__ void __launch_bounds__(64 * NWV, 1)
 }
 }  // namespace dp
 
-// =============================================================================================
-// 64-deep half stages of the dp tile (e4m3 weights; tile variant 9). The dp kernel's 68 KB stages
-// fit twice in LDS, so one stage is in flight while the other is read, and its counters show the
-// waves waiting on that DMA (profiles/r05/pmc_mx_dp_tile.md: MFMA busy 37 %, mxfp4 no faster than
-// mxfp8). Here a stage is K = 64: A and B as 64-byte rows (16 rows per 1 KiB wave instruction,
-// slot s of row r holds chunk s ^ ((r >> 2) & 3), the fp4 image's conflict-free swizzle) plus each
-// row's exponent word of the enclosing 128-K block; four 34 KB buffers keep three half stages in
-// flight. The DMA is issued from inline asm (the compiler's wait-count pass cannot tell its LDS
-// writes from the reads of another buffer) and tracked with counted vmcnt + a raw barrier.
-// =============================================================================================
-namespace dph {
-constexpr int BM = 256, BN = 256, NWV = 8, WNW = NWV / 2, TNW = BN / WNW, NJ = TNW / 32;
-constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, S_BYTES = (BM + BN) * 4;
-constexpr int STAGE = A_BYTES + B_BYTES + S_BYTES;  // 34 KiB
-constexpr int NBUF = 4;
-constexpr int A_INSTR = BM / 16 / NWV, B_INSTR = BN / 16 / NWV, S_INSTR = (BM + BN) / 64 / NWV;
-constexpr int LOADS = A_INSTR + B_INSTR + S_INSTR;  // DMA instructions per wave per half stage
-static_assert(S_INSTR == 1 && A_INSTR * NWV * 16 == BM && B_INSTR * NWV * 16 == BN, "half-stage DMA plan");
-__device__ __forceinline__ int f4(int r) { return (r >> 2) & 3; }
-
-extern __shared__ __attribute__((aligned(16))) char smem[];
-__device__ __forceinline__ unsigned lds_u32(const char* p) {
-  return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem +
-                                        (unsigned)(p - smem));
-}
-__device__ __forceinline__ void adma16(const void* g, const char* l) {
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_u32(l)), "v"(g) : "memory", "m0");
-}
-__device__ __forceinline__ void adma4(const void* g, const char* l) {
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(lds_u32(l)), "v"(g) : "memory", "m0");
-}
-
-__device__ __forceinline__ void issue_half(char* buf, const uint8_t* Xq, const uint8_t* Xs, const uint8_t* Wq,
-                                           const uint8_t* Ws, int wks, int m0, int n0, int M, int K, int KS,
-                                           int kh, int w, int lane) {
-  const int slot = lane & 3, r16 = lane >> 2;
-#pragma unroll
-  for (int j = 0; j < A_INSTR; ++j) {
-    const int g = w * A_INSTR + j, row = 16 * g + r16, gr = min(m0 + row, M - 1);
-    adma16(Xq + (int64_t)gr * K + (int64_t)kh * 64 + 16 * (slot ^ f4(row)), buf + g * 1024);
-  }
-#pragma unroll
-  for (int j = 0; j < B_INSTR; ++j) {
-    const int g = w * B_INSTR + j, row = 16 * g + r16;
-    adma16(Wq + (int64_t)(n0 + row) * K + (int64_t)kh * 64 + 16 * (slot ^ f4(row)), buf + A_BYTES + g * 1024);
-  }
-  // exponent words (4 E8M0 bytes of the 128-K block kh / 2): wave w moves rows 64 w .. 64 w + 63 of
-  // [A rows | B rows]
-  char* sb = buf + A_BYTES + B_BYTES;
-  if (w < BM / 64) {
-    const int gr = min(m0 + 64 * w + lane, M - 1);
-    adma4(Xs + (int64_t)gr * KS + 4 * (kh >> 1), sb + 64 * w * 4);
-  } else {
-    const int row = 64 * (w - BM / 64) + lane;
-    adma4(Ws + (int64_t)(n0 + row) * wks + 4 * (kh >> 1), sb + 64 * w * 4);
-  }
-}
-
-template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-
-template <int FB>
-__global__ void __launch_bounds__(64 * NWV, 1)
-    mx_gemm_h64_kernel(const uint8_t* __restrict__ Xq, const uint8_t* __restrict__ Xs, const uint8_t* __restrict__ Wq,
-                       const uint8_t* __restrict__ Ws, int wks, const unsigned short* __restrict__ bias,
-                       const float* __restrict__ col_scale, unsigned short* __restrict__ Y, int M, int N, int K) {
-  constexpr int MF = mfma_fmt(FB);
-  // bijective XCD-major remap (8 XCDs, round-robin dispatch), as the dp kernel
-  const int tm = (M + BM - 1) / BM, tn = N / BN, nwg = tm * tn;
-  const int orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-  const int pid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  const int m0 = (pid % tm) * BM, n0 = (pid / tm) * BN;
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = w / WNW, wn = w % WNW, h = lane >> 5, l32 = lane & 31;
-  const int KS = K / 32;
-  const int nh = K / 64;  // half stages (K % 128 == 0: even)
-
-  f32x16 acc[4][NJ];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  // per-lane LDS offsets of the A / B fragment rows (64-byte rows, two 16-byte chunks each)
-  int oa[4][2], ob[NJ][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = wm * 128 + i * 32 + l32;
-    oa[i][0] = row * 64 + 16 * (h ^ f4(row));
-    oa[i][1] = row * 64 + 16 * ((2 + h) ^ f4(row));
-  }
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int row = wn * TNW + j * 32 + l32;
-    ob[j][0] = A_BYTES + row * 64 + 16 * (h ^ f4(row));
-    ob[j][1] = A_BYTES + row * 64 + 16 * ((2 + h) ^ f4(row));
-  }
-  const int osa = A_BYTES + B_BYTES + 4 * (wm * 128 + l32), osb = A_BYTES + B_BYTES + 4 * (BM + wn * TNW + l32);
-
-#pragma unroll
-  for (int p = 0; p < NBUF - 1; ++p)
-    if (p < nh) issue_half(smem + p * STAGE, Xq, Xs, Wq, Ws, wks, m0, n0, M, K, KS, p, w, lane);
-  for (int kh = 0; kh < nh; ++kh) {
-    // half stage kh has landed once at most the half stages issued after it are outstanding
-    if (kh + 2 < nh) vm_wait<2 * LOADS>();
-    else if (kh + 1 < nh) vm_wait<LOADS>();
-    else vm_wait<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's part of half stage kh landed; kh - 1 is read by all
-    if (kh + NBUF - 1 < nh)
-      issue_half(smem + ((kh + NBUF - 1) % NBUF) * STAGE, Xq, Xs, Wq, Ws, wks, m0, n0, M, K, KS, kh + NBUF - 1, w,
-                 lane);
-    const char* buf = smem + (kh % NBUF) * STAGE;
-    const int sh = 8 * (2 * (kh & 1) + h);
-    unsigned sa[4], sbw[NJ];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) sa[i] = *reinterpret_cast<const unsigned*>(buf + osa + 128 * i);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) sbw[j] = *reinterpret_cast<const unsigned*>(buf + osb + 128 * j);
-    i32x8 a[4], b[NJ];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const u32x4 x0 = *reinterpret_cast<const u32x4*>(buf + oa[i][0]);
-      const u32x4 x1 = *reinterpret_cast<const u32x4*>(buf + oa[i][1]);
-      a[i] = i32x8{(int)x0[0], (int)x0[1], (int)x0[2], (int)x0[3], (int)x1[0], (int)x1[1], (int)x1[2], (int)x1[3]};
-    }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const u32x4 x0 = *reinterpret_cast<const u32x4*>(buf + ob[j][0]);
-      const u32x4 x1 = *reinterpret_cast<const u32x4*>(buf + ob[j][1]);
-      b[j] = i32x8{(int)x0[0], (int)x0[1], (int)x0[2], (int)x0[3], (int)x1[0], (int)x1[1], (int)x1[2], (int)x1[3]};
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(  // Y^T tile: see store_t
-            b[j], a[i], acc[i][j], MF, 0, 0, (int)((sbw[j] >> sh) & 0xff), 0, (int)((sa[i] >> sh) & 0xff));
-    __builtin_amdgcn_s_setprio(0);
-  }
-  store_t<4, NJ>(acc, Y, col_scale, bias, m0 + wm * 128, n0 + wn * TNW, M, N, h, l32);
-}
-}  // namespace dph
 
 
 template <int BM, int BN, int WM, int WN, int FB>
@@ -692,7 +547,8 @@ void launch(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq, co
 // (128x128 per wave, accumulators in AGPRs), 4 = 256x256 / 8 waves, 5 = 256x128 / 8 waves,
 // 6 = 256x256 / 8 waves LDS-DMA pipelined (namespace dp), 7 = the same at 256x128 / 4 waves,
 // 8 = 256x256 / 4 waves (a phased 64-deep-stage form of 6 measured slower on every shape:
-// profiles/r05/mx_gemm_phased_tile_ab.log), 9 = 6 with 64-deep half stages, four in LDS (e4m3)
+// profiles/r05/mx_gemm_phased_tile_ab.log; 6 with 64-deep half stages, four in LDS, was slower
+// too: profiles/r05/mx_half_stage_tile_ab.log)
 static int tile_override() {  // read per call: the kernel tests sweep every variant in one process
   const char* e = getenv("SXE_MX_TILE");
   return e ? atoi(e) : 0;
@@ -720,25 +576,6 @@ void launch_dp(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq,
 }
 
 template <int FB>
-void launch_h64(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq, const at::Tensor& ws,
-                const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& cs, at::Tensor& y, int M,
-                int N, int K) {
-  constexpr size_t lds = (size_t)dph::NBUF * dph::STAGE;
-  static bool attr = [&] {
-    SXE_HIP_CHECK(hipFuncSetAttribute((const void*)dph::mx_gemm_h64_kernel<FB>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    return true;
-  }();
-  (void)attr;
-  const int G_ = ((M + dph::BM - 1) / dph::BM) * (N / dph::BN);
-  const int wks = ws.size(0) == 1 ? 0 : (int)ws.size(1);
-  hipLaunchKernelGGL((dph::mx_gemm_h64_kernel<FB>), dim3(G_), dim3(64 * dph::NWV), lds, cur_stream(),
-                     xq.data_ptr<uint8_t>(), xs.data_ptr<uint8_t>(), wq.data_ptr<uint8_t>(), ws.data_ptr<uint8_t>(),
-                     wks, bias ? reinterpret_cast<const unsigned short*>(bias->data_ptr()) : nullptr,
-                     cs ? cs->data_ptr<float>() : nullptr, reinterpret_cast<unsigned short*>(y.data_ptr()), M, N, K);
-}
-
-template <int FB>
 void dispatch_tile(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq, const at::Tensor& ws,
                    const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& cs, at::Tensor& y, int M,
                    int N, int K) {
@@ -750,12 +587,8 @@ void dispatch_tile(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor&
     const int64_t g256 = (int64_t)((M + 255) / 256) * (N / 256), g2561 = (int64_t)((M + 255) / 256) * (N / 128);
     v = (N % 256 == 0 && M > 256 && g256 >= kNumCUs) ? 6 : (M > 256 && g2561 >= kNumCUs / 2) ? 7 : 1;
   }
-  if (v == 9 && (fmt_bits(FB) != 8 || is_planes(FB))) v = 6;  // the half-stage tile is e4m3-only
-  if ((v == 3 || v == 4 || v == 6 || v == 8 || v == 9) && N % 256 != 0) v = 2;
+  if ((v == 3 || v == 4 || v == 6 || v == 8) && N % 256 != 0) v = 2;
   switch (v) {
-    case 9:
-      if constexpr (fmt_bits(FB) == 8 && !is_planes(FB)) launch_h64<FB>(xq, xs, wq, ws, bias, cs, y, M, N, K);
-      break;
     case 6: launch_dp<FB, 256>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
     case 8: launch_dp<FB, 256, 4>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
     case 7: launch_dp<FB, 128>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
