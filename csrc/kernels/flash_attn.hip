@@ -565,8 +565,11 @@ __device__ __forceinline__ void dq_tile(const LaneOffs<D>& lo, const char* kt, c
   }
 }
 
-template <bool SPARSE, int D>
-__global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dq_kernel(
+// NWF waves per workgroup, 32 queries each: 8 (256 queries) shares every staged K/V tile among twice
+// the queries of 4 -- half the L2-to-LDS tile traffic per query, at one workgroup per CU
+// (SXE_FA_DQ_WAVES, read per call; Sq a multiple of 256, head dims 64 / 128)
+template <bool SPARSE, int D, int NWF = 4>
+__global__ void __launch_bounds__(NWF * 64, (NWF == 8 ? 1 : bwd_min_waves<D>())) dq_kernel(
     const unsigned short* __restrict__ q, Strides qs, const unsigned short* __restrict__ k, Strides ks,
     const unsigned short* __restrict__ v, Strides vs, const unsigned short* __restrict__ dout, Strides dos,
     const float* __restrict__ lse, const float* __restrict__ ndelta, unsigned short* __restrict__ dq, Strides dqs,
@@ -576,12 +579,13 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dq_kernel(
   constexpr int BUF = 2 * KT * ROWB;
   int* tlist = reinterpret_cast<int*>(smem + 4 * KT * ROWB) + 1;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-  const int nqb = Sq / QB;
+  constexpr int QBF = NWF * QW;
+  const int nqb = Sq / QBF;
   int bh, qb;
   map_block(nqb, B * H, causal != 0, bh, qb);
   const int b = bh / H, head = bh - b * H;
   const int kh = head / (H / Hk);
-  const int q0 = qb * QB + w * QW;
+  const int q0 = qb * QBF + w * QW;
   const int qpos = q0 + qoff;
   const unsigned short* qp = q + b * qs.b + head * qs.h;
   const unsigned short* dop = dout + b * dos.b + head * dos.h;
@@ -589,14 +593,14 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dq_kernel(
   const unsigned short* vp = v + b * vs.b + kh * vs.h;
   const float c = scale * LOG2E;
   const int64_t lrow = ((int64_t)b * H + head) * Sq + q0 + r;
-  const int kend = causal ? min(Sk, (qb + 1) * QB + qoff) : Sk;
+  const int kend = causal ? min(Sk, (qb + 1) * QBF + qoff) : Sk;
   const int nkt = (max(kend, 0) + KT - 1) / KT;
-  const int ntiles = SPARSE ? build_tile_list(sp, head, 0, nkt, KT, qb * QB, qb * QB + QB, true, tlist) : nkt;
+  const int ntiles = SPARSE ? build_tile_list(sp, head, 0, nkt, KT, qb * QBF, qb * QBF + QBF, true, tlist) : nkt;
   auto tile_at = [&](int i) { return SPARSE ? tlist[i] : i; };
   const uint8_t* lay_row = SPARSE ? sp.layout + ((int64_t)head * sp.nb + (q0 + r) / sp.blk) * sp.nb : nullptr;
   if (ntiles > 0) {
-    tile_glds<KT, D>(kp, ks.s, tile_at(0) * KT, smem);
-    tile_glds<KT, D>(vp, vs.s, tile_at(0) * KT, smem + KT * ROWB);
+    tile_glds<KT, D, NWF>(kp, ks.s, tile_at(0) * KT, smem);
+    tile_glds<KT, D, NWF>(vp, vs.s, tile_at(0) * KT, smem + KT * ROWB);
   }
 
   const float lse2 = lse[lrow] * LOG2E;
@@ -622,8 +626,8 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dq_kernel(
   auto step = [&](const int t, auto slot) {
     constexpr int CUR = decltype(slot)::value;
     if (t + 1 < ntiles) {
-      tile_glds<KT, D>(kp, ks.s, tile_at(t + 1) * KT, smem + (CUR ^ 1) * BUF);
-      tile_glds<KT, D>(vp, vs.s, tile_at(t + 1) * KT, smem + (CUR ^ 1) * BUF + KT * ROWB);
+      tile_glds<KT, D, NWF>(kp, ks.s, tile_at(t + 1) * KT, smem + (CUR ^ 1) * BUF);
+      tile_glds<KT, D, NWF>(vp, vs.s, tile_at(t + 1) * KT, smem + (CUR ^ 1) * BUF + KT * ROWB);
     }
     const int kbase = tile_at(t) * KT;
     const bool active = !causal || kbase <= qpos + QW - 1;
@@ -1039,6 +1043,10 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
   if (!attr_set) {  // > 64 KiB of dynamic LDS must be opted into (gfx950 has 160 KiB per CU)
     set_lds_limit(&fa::dq_kernel<false, D>, 4 * fa::KT * ROWB + kListBytes);
     set_lds_limit(&fa::dq_kernel<true, D>, 4 * fa::KT * ROWB + kListBytes);
+    if constexpr (D < 256) {
+      set_lds_limit(&fa::dq_kernel<false, D, 8>, 4 * fa::KT * ROWB + kListBytes);
+      set_lds_limit(&fa::dq_kernel<true, D, 8>, 4 * fa::KT * ROWB + kListBytes);
+    }
     set_lds_limit(&fa::dkdv_kernel<false, D>, lds_kv_max);
     set_lds_limit(&fa::dkdv_kernel<true, D>, lds_kv_max);
     if constexpr (D >= 256) {
@@ -1049,9 +1057,13 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
     }
     attr_set = true;
   }
+  const bool dq8 = D < 256 && Sq % 256 == 0 && env_int("SXE_FA_DQ_WAVES", 4) == 8;
   auto* dqk = sp.layout ? fa::dq_kernel<true, D> : fa::dq_kernel<false, D>;
-  hipLaunchKernelGGL(dqk, dim3((Sq / fa::QB) * B * H),
-                     dim3(256), lds_dq, cur_stream(),
+  if constexpr (D < 256) {
+    if (dq8) dqk = sp.layout ? fa::dq_kernel<true, D, 8> : fa::dq_kernel<false, D, 8>;
+  }
+  hipLaunchKernelGGL(dqk, dim3((Sq / (dq8 ? 2 * fa::QB : fa::QB)) * B * H),
+                     dim3(dq8 ? 512 : 256), lds_dq, cur_stream(),
                      reinterpret_cast<const unsigned short*>(q.data_ptr()), strides_of(q),
                      reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
                      reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),

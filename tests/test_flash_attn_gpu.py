@@ -87,6 +87,30 @@ def test_flash_bwd_d256_sweeps(one_sweep, causal, B, S, H, Hk, monkeypatch):
     assert _rel(v.grad, v2.grad) < 2e-2
 
 
+@pytest.mark.parametrize("waves", ["4", "8"])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("B,Sq,Sk,H,Hk,D", [(1, 512, 512, 8, 2, 128), (2, 256, 768, 4, 1, 128),
+                                            (1, 512, 512, 4, 4, 64), (1, 384, 384, 4, 2, 128)])
+def test_flash_bwd_dq_waves(waves, causal, B, Sq, Sk, H, Hk, D, monkeypatch):
+    """dQ kernel with 4 or 8 waves per workgroup (SXE_FA_DQ_WAVES, read per call; 8 needs Sq a
+    multiple of 256, else 4 runs) against the fp32 oracle, incl. q_len != kv_len and GQA."""
+    from shuffle_exchange_amd.ops.attention import attention, reference_attention
+    monkeypatch.setenv("SXE_FA_DQ_WAVES", waves)
+    torch.manual_seed(Sq + Sk + D)
+    q = torch.randn(B, Sq, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, Sk, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, Sk, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    o = attention(q, k, v, causal=causal)
+    q2, k2, v2 = (t.detach().float().requires_grad_() for t in (q, k, v))
+    o2 = reference_attention(q2, k2, v2, causal=causal)
+    do = torch.randn_like(o2)
+    (o.float() * do).sum().backward()
+    (o2 * do).sum().backward()
+    assert _rel(q.grad, q2.grad) < 2e-2
+    assert _rel(k.grad, k2.grad) < 2e-2
+    assert _rel(v.grad, v2.grad) < 2e-2
+
+
 def test_flash_lse():
     from shuffle_exchange_amd.ops.attention import attention_with_lse, reference_attention
     q = torch.randn(1, 256, 2, 128, device="cuda", dtype=torch.bfloat16)
