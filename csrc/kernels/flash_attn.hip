@@ -670,10 +670,10 @@ __global__ void __launch_bounds__(NWF * 64, (NWF == 8 ? 1 : bwd_min_waves<D>()))
 // registers.
 // =============================================================================================
 constexpr int QT = 32;  // queries per tile in the dK/dV sweep
-template <int D> struct KVL {
+template <int D, int KB = QB> struct KVL {
   static constexpr int TILE = QT * 2 * D;              // one Q (or dO) tile
   static constexpr int SLOT = 2 * TILE + 2 * QT * 4;   // Q, dO, lse[32], delta[32]
-  static constexpr int VBLK = QB * 2 * D;              // the V block
+  static constexpr int VBLK = KB * 2 * D;              // the V block of KB keys
 };
 
 // PART: 3 = dK and dV in one sweep; 1 = dV only; 2 = dK only (head dim 256: the two 128-register
@@ -736,15 +736,19 @@ __device__ __forceinline__ void dkdv_tile(const LaneOffs<D>& lo, const char* slo
 // block 0 (measured 650 us at B4 S2048 H32/8). Splitting the G query heads into G/hpw groups cuts the
 // longest job by G/hpw; the per-group fp32 dK/dV partials [B, Sk, H/hpw, D] are summed by
 // dkdv_reduce_kernel (hpw = 2 halves that partial traffic against hpw = 1).
-template <bool SPLIT, int D, int PART = 3>
-__global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
+// NWK waves per workgroup, 32 keys each: 8 (256 keys, head dim 128; SXE_FA_DKDV_WAVES, read per
+// call) shares every staged Q / dO tile among twice the keys of 4 -- half the L2-to-LDS traffic per
+// key, at one workgroup per CU
+template <bool SPLIT, int D, int PART = 3, int NWK = 4>
+__global__ void __launch_bounds__(NWK * 64, (NWK == 8 ? 1 : bwd_min_waves<D>())) dkdv_kernel(
     const unsigned short* __restrict__ q, Strides qs, const unsigned short* __restrict__ k, Strides ks,
     const unsigned short* __restrict__ v, Strides vs, const unsigned short* __restrict__ dout, Strides dos,
     const float* __restrict__ lse, const float* __restrict__ delta, unsigned short* __restrict__ dk, Strides dks,
     unsigned short* __restrict__ dv, Strides dvs, float* __restrict__ pk, float* __restrict__ pv, int B, int H,
     int Hk, int Sq, int Sk, float scale, int causal, Sparse sp, int qoff, int hpw) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  using G_ = KVL<D>;
+  constexpr int KB = NWK * QW;  // keys per workgroup
+  using G_ = KVL<D, KB>;
   char* vblk = smem;
   char* ring = smem + G_::VBLK;
   int* tlist = reinterpret_cast<int*>(ring + 2 * G_::SLOT) + 1;
@@ -752,7 +756,7 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
   // so the diagonal mask is a scalar branch rather than per-lane selects on every tile
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), r = lane & 31,
             h = lane >> 5;
-  const int nkb = Sk / QB;
+  const int nkb = Sk / KB;
   int bh, kb;
   const int G = SPLIT ? hpw : H / Hk;  // query heads swept by this workgroup (sparse: 1)
   const int HB = H / G;                 // workgroups along the head axis
@@ -760,15 +764,15 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
   const int b = bh / HB, hsel = bh - b * HB;
   const int hq0 = hsel * G;             // first query head swept by this workgroup
   const int kh = hq0 / (H / Hk);
-  const int k0 = kb * QB + w * QW;  // this wave's first key
+  const int k0 = kb * KB + w * QW;  // this wave's first key
   const unsigned short* kp = k + b * ks.b + kh * ks.h;
   const unsigned short* vp = v + b * vs.b + kh * vs.h;
   const float c = scale * LOG2E;
   // causal: the first query that sees key block kb (query i sees keys <= i + qoff)
-  const int qstart = causal ? min(Sq, max(0, kb * QB - qoff) / QT * QT) : 0;
+  const int qstart = causal ? min(Sq, max(0, kb * KB - qoff) / QT * QT) : 0;
   const int ntq = (Sq - qstart) / QT;
   // sparse: SPLIT mode (G == 1), list of the active 32-query tiles of this key block
-  const int total = sp.layout ? build_tile_list(sp, hq0, qstart / QT, Sq / QT, QT, kb * QB, kb * QB + QB, false, tlist)
+  const int total = sp.layout ? build_tile_list(sp, hq0, qstart / QT, Sq / QT, QT, kb * KB, kb * KB + KB, false, tlist)
                               : ntq * G;
   const int kbl = sp.layout ? (k0 + r) / sp.blk : 0;
   // dense tile order: the query tiles qstart .. Sq of head hq0, then of hq0 + 1, ... -- walked by
@@ -786,14 +790,14 @@ __global__ void __launch_bounds__(256, (bwd_min_waves<D>())) dkdv_kernel(
         ++is_h;
       }
     }
-    tile_glds<QT, D>(q + b * qs.b + hq * qs.h, qs.s, qt0, slot);
-    tile_glds<QT, D>(dout + b * dos.b + hq * dos.h, dos.s, qt0, slot + G_::TILE);
+    tile_glds<QT, D, NWK>(q + b * qs.b + hq * qs.h, qs.s, qt0, slot);
+    tile_glds<QT, D, NWK>(dout + b * dos.b + hq * dos.h, dos.s, qt0, slot + G_::TILE);
     if (w == 0) {  // 64 lanes x 4 B: lse[32] then delta[32]
       const int64_t lr = ((int64_t)b * H + hq) * Sq + qt0 + (lane & 31);
       glds4(lane < 32 ? (const void*)(lse + lr) : (const void*)(delta + lr), slot + 2 * G_::TILE);
     }
   };
-  if constexpr ((PART & 2) != 0) tile_glds<QB, D>(vp, vs.s, kb * QB, vblk);
+  if constexpr ((PART & 2) != 0) tile_glds<KB, D, NWK>(vp, vs.s, kb * KB, vblk);
   if (total > 0) issue(0, ring);
   bf16x8 kf[D / 16];
 #pragma unroll
@@ -1049,6 +1053,11 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
     }
     set_lds_limit(&fa::dkdv_kernel<false, D>, lds_kv_max);
     set_lds_limit(&fa::dkdv_kernel<true, D>, lds_kv_max);
+    if constexpr (D == 128) {
+      const size_t mx8 = fa::KVL<D, 256>::VBLK + 2 * G_::SLOT + kListBytes;
+      set_lds_limit(&fa::dkdv_kernel<false, D, 3, 8>, mx8);
+      set_lds_limit(&fa::dkdv_kernel<true, D, 3, 8>, mx8);
+    }
     if constexpr (D >= 256) {
       set_lds_limit(&fa::dkdv_kernel<false, D, 1>, lds_kv_max);
       set_lds_limit(&fa::dkdv_kernel<true, D, 1>, lds_kv_max);
@@ -1099,14 +1108,16 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
   // or two (SXE_FA_DKDV_ONE_SWEEP=0: PART 1 / 2, each recomputes S): one sweep is 1-9 % faster
   // fwd+bwd (profiles/r05/attn_d256_one_sweep_ab.log)
   const bool one_sweep = D >= 256 && env_int("SXE_FA_DKDV_ONE_SWEEP", 1) != 0;
-  const size_t lds_kv = G_::VBLK + 2 * G_::SLOT + (sp.layout ? kListBytes : 0);
+  // head dim 128: 8-wave dK/dV workgroups of 256 keys (SXE_FA_DKDV_WAVES=8, read per call)
+  const bool kv8 = D == 128 && Sk % 256 == 0 && env_int("SXE_FA_DKDV_WAVES", 4) == 8;
+  const size_t lds_kv = (kv8 ? fa::KVL<D, 256>::VBLK : G_::VBLK) + 2 * G_::SLOT + (sp.layout ? kListBytes : 0);
   at::Tensor pk, pv;
   if (partials) {
     pk = at::empty({B, Sk, np, D}, q.options().dtype(at::kFloat));
     pv = at::empty({B, Sk, np, D}, q.options().dtype(at::kFloat));
   }
-  auto launch = [&](auto kern, int heads) {
-    hipLaunchKernelGGL(kern, dim3((Sk / fa::QB) * B * heads), dim3(256), lds_kv, cur_stream(),
+  auto launch = [&](auto kern, int heads, int nwk = 4) {
+    hipLaunchKernelGGL(kern, dim3((Sk / (nwk * fa::QW)) * B * heads), dim3(nwk * 64), lds_kv, cur_stream(),
                        reinterpret_cast<const unsigned short*>(q.data_ptr()), strides_of(q),
                        reinterpret_cast<const unsigned short*>(k.data_ptr()), strides_of(k),
                        reinterpret_cast<const unsigned short*>(v.data_ptr()), strides_of(v),
@@ -1117,14 +1128,27 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
                        partials ? pk.data_ptr<float>() : nullptr, partials ? pv.data_ptr<float>() : nullptr, B, H, Hk,
                        Sq, Sk, (float)scale, causal ? 1 : 0, sp, qoff, hpw);
   };
-  if (split) {
-    if (D >= 256 && !one_sweep) {
-      launch(fa::dkdv_kernel<true, D, 1>, np);
-      SXE_LAUNCH_CHECK();
-      launch(fa::dkdv_kernel<true, D, 2>, np);
-    } else {
-      launch(fa::dkdv_kernel<true, D>, np);
+  // the dK/dV launch(es) of one form: SPLIT = one workgroup per query-head group (partials / direct)
+  auto run_dkdv = [&](auto splitc, int heads) {
+    constexpr bool SP = decltype(splitc)::value;
+    if constexpr (D >= 256) {
+      if (!one_sweep) {
+        launch(fa::dkdv_kernel<SP, D, 1>, heads);
+        SXE_LAUNCH_CHECK();
+        launch(fa::dkdv_kernel<SP, D, 2>, heads);
+        return;
+      }
     }
+    if constexpr (D == 128) {
+      if (kv8) {
+        launch(fa::dkdv_kernel<SP, D, 3, 8>, heads, 8);
+        return;
+      }
+    }
+    launch(fa::dkdv_kernel<SP, D>, heads);
+  };
+  if (split) {
+    run_dkdv(std::true_type{}, np);
     SXE_LAUNCH_CHECK();
     if (partials) {
       const int64_t n8 = (int64_t)B * Sk * Hk * (D / 8);
@@ -1133,12 +1157,8 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
                          strides_of(dk), reinterpret_cast<unsigned short*>(dv.data_ptr()), strides_of(dv), B, Sk, np,
                          Hk);
     }
-  } else if (D >= 256 && !one_sweep) {
-    launch(fa::dkdv_kernel<false, D, 1>, Hk);
-    SXE_LAUNCH_CHECK();
-    launch(fa::dkdv_kernel<false, D, 2>, Hk);
   } else {
-    launch(fa::dkdv_kernel<false, D>, Hk);
+    run_dkdv(std::false_type{}, Hk);
   }
   SXE_LAUNCH_CHECK();
 }

@@ -90,12 +90,15 @@ def test_flash_bwd_d256_sweeps(one_sweep, causal, B, S, H, Hk, monkeypatch):
 @pytest.mark.parametrize("waves", ["4", "8"])
 @pytest.mark.parametrize("causal", [True, False])
 @pytest.mark.parametrize("B,Sq,Sk,H,Hk,D", [(1, 512, 512, 8, 2, 128), (2, 256, 768, 4, 1, 128),
-                                            (1, 512, 512, 4, 4, 64), (1, 384, 384, 4, 2, 128)])
+                                            (1, 512, 512, 4, 4, 64), (1, 384, 384, 4, 2, 128),
+                                            (2, 512, 512, 8, 8, 128)])
 def test_flash_bwd_dq_waves(waves, causal, B, Sq, Sk, H, Hk, D, monkeypatch):
-    """dQ kernel with 4 or 8 waves per workgroup (SXE_FA_DQ_WAVES, read per call; 8 needs Sq a
-    multiple of 256, else 4 runs) against the fp32 oracle, incl. q_len != kv_len and GQA."""
+    """dQ and dK/dV kernels with 4 or 8 waves per workgroup (SXE_FA_DQ_WAVES / SXE_FA_DKDV_WAVES,
+    read per call; 8 needs the axis a multiple of 256 -- and head dim 128 for dK/dV -- else 4 runs)
+    against the fp32 oracle, incl. q_len != kv_len and GQA (split + partials under the mask)."""
     from shuffle_exchange_amd.ops.attention import attention, reference_attention
     monkeypatch.setenv("SXE_FA_DQ_WAVES", waves)
+    monkeypatch.setenv("SXE_FA_DKDV_WAVES", waves)
     torch.manual_seed(Sq + Sk + D)
     q = torch.randn(B, Sq, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     k = torch.randn(B, Sk, Hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
