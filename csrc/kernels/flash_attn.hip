@@ -1066,7 +1066,10 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
     }
     attr_set = true;
   }
-  const bool dq8 = D < 256 && Sq % 256 == 0 && env_int("SXE_FA_DQ_WAVES", 4) == 8;
+  // 8-wave dQ workgroups from 8k queries on (auto; SXE_FA_DQ_WAVES=4 / 8 forces): 1.5-2 % faster
+  // fwd+bwd at S8k / S32k, neutral at 2k (profiles/r05/attn_bwd_waves_ab.log)
+  const int dqw = env_int("SXE_FA_DQ_WAVES", 0);
+  const bool dq8 = D < 256 && Sq % 256 == 0 && (dqw == 8 || (dqw == 0 && Sq >= 8192));
   auto* dqk = sp.layout ? fa::dq_kernel<true, D> : fa::dq_kernel<false, D>;
   if constexpr (D < 256) {
     if (dq8) dqk = sp.layout ? fa::dq_kernel<true, D, 8> : fa::dq_kernel<false, D, 8>;
@@ -1109,7 +1112,9 @@ static void bwd_impl_d(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v
   // fwd+bwd (profiles/r05/attn_d256_one_sweep_ab.log)
   const bool one_sweep = D >= 256 && env_int("SXE_FA_DKDV_ONE_SWEEP", 1) != 0;
   // head dim 128: 8-wave dK/dV workgroups of 256 keys (SXE_FA_DKDV_WAVES=8, read per call)
-  const bool kv8 = D == 128 && Sk % 256 == 0 && env_int("SXE_FA_DKDV_WAVES", 4) == 8;
+  // (auto from 8k keys on, as the dQ kernel; SXE_FA_DKDV_WAVES=4 / 8 forces)
+  const int kvw = env_int("SXE_FA_DKDV_WAVES", 0);
+  const bool kv8 = D == 128 && Sk % 256 == 0 && (kvw == 8 || (kvw == 0 && Sk >= 8192));
   const size_t lds_kv = (kv8 ? fa::KVL<D, 256>::VBLK : G_::VBLK) + 2 * G_::SLOT + (sp.layout ? kListBytes : 0);
   at::Tensor pk, pv;
   if (partials) {
