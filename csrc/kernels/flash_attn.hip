@@ -944,7 +944,13 @@ static int env_int(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return (e != nullptr && *e != 0) ? std::atoi(e) : dflt;
 }
-static bool fwd_narrow() { return env_int("SXE_FA_FWD_WAVES", 8) == 4; }
+// 4-wave forward workgroups: forced by SXE_FA_FWD_WAVES=4, and the auto choice (unset / 0) at head
+// dim 64, where they ran 6 % faster (0.102 vs 0.108 ms at B4 S2048 H32/8 causal); 8 waves elsewhere
+// (equal causal at head dim 128, 7 % faster non-causal: profiles/r05/attn_fwd_waves_ab.log)
+static bool fwd_narrow(int D) {
+  const int w = env_int("SXE_FA_FWD_WAVES", 0);
+  return w == 4 || (w == 0 && D == 64);
+}
 static bool fwd_dma() { return env_int("SXE_FA_FWD_DMA", 1) != 0; }
 
 template <typename F>
@@ -979,7 +985,7 @@ static std::vector<at::Tensor> fwd_impl_d(at::Tensor q, at::Tensor k, at::Tensor
     attr = true;
   }
   // 8 waves share each staged K/V tile when the query axis allows; head dim 256 runs 4 (register budget)
-  const bool wide = D < 256 && Sq % 256 == 0 && !fwd_narrow();
+  const bool wide = D < 256 && Sq % 256 == 0 && !fwd_narrow(D);
   const int grid = (Sq / fa::QB) * B * H;
   auto launch = [&](auto kern, int nwf) {
     hipLaunchKernelGGL(kern, dim3(nwf == 8 ? grid / 2 : grid), dim3(nwf * 64), lds, cur_stream(),
