@@ -944,12 +944,13 @@ static int env_int(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return (e != nullptr && *e != 0) ? std::atoi(e) : dflt;
 }
-// 4-wave forward workgroups: forced by SXE_FA_FWD_WAVES=4, and the auto choice (unset / 0) at head
-// dim 64, where they ran 6 % faster (0.102 vs 0.108 ms at B4 S2048 H32/8 causal); 8 waves elsewhere
-// (equal causal at head dim 128, 7 % faster non-causal: profiles/r05/attn_fwd_waves_ab.log)
+// 4-wave forward workgroups only when forced (SXE_FA_FWD_WAVES=4): 8 waves are equal or faster on
+// every measured shape -- causal equal at head dims 64 / 128, non-causal 3-7 % faster
+// (profiles/r05/attn_fwd_waves_ab.log, attn_fwd_waves_d64_ab.log; one earlier box showed 4 waves
+// 6 % ahead at D64 causal, which a second box did not reproduce)
 static bool fwd_narrow(int D) {
-  const int w = env_int("SXE_FA_FWD_WAVES", 0);
-  return w == 4 || (w == 0 && D == 64);
+  (void)D;
+  return env_int("SXE_FA_FWD_WAVES", 8) == 4;
 }
 static bool fwd_dma() { return env_int("SXE_FA_FWD_DMA", 1) != 0; }
 
