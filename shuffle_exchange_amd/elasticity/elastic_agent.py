@@ -62,7 +62,12 @@ def _rdzv_view(handler, now=None):
     beats = getattr(st, "last_heartbeats", {}) or {}
     dead = 0
     if settings is not None and beats:
-        now = now or datetime.datetime.utcnow()
+        if now is None:
+            # torch's dynamic rendezvous stores aware UTC heartbeats (datetime.now(timezone.utc)); match
+            # whatever the stored values are so the comparison never mixes naive and aware times
+            sample = next(iter(beats.values()))
+            now = (datetime.datetime.now(datetime.timezone.utc) if getattr(sample, "tzinfo", None) is not None
+                   else datetime.datetime.utcnow())
         window = settings.keep_alive_interval * settings.keep_alive_max_attempt
         dead = sum(1 for t in beats.values() if t < now - window)
     return parts, dead
@@ -113,7 +118,8 @@ class SXEElasticAgent(LocalElasticAgent):
                 self._restart_workers(self._worker_group)
                 start_parts, _ = _rdzv_view(handler)
             elif act == FAIL:
+                # a shrunk-but-HEALTHY group must still report FAILED, or elastic_launch exits 0 on a job it
+                # just killed; like torch's own loop, a failure skips the exit barrier
                 self._stop_workers(self._worker_group)
                 self._worker_group.state = WorkerState.FAILED
-                self._exit_barrier()
-                return run_result
+                return RunResult(state=WorkerState.FAILED, failures=dict(run_result.failures or {}))

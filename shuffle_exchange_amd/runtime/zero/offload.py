@@ -440,6 +440,11 @@ class HostOptimizerStep:
                 ev = torch.cuda.Event()
                 ev.record(self.d2h)
             d2h.append((dst, ev))
+        # Invariant: nothing may write u.grad on the compute stream until these copies have read it.
+        # The compute stream is NOT made to wait here (that would serialise the next forward behind the
+        # mirror); every writer of the accumulators calls wait_grad_mirror() first instead -- the
+        # backward via before_backward(), ZeRO-3's _zero_stale()/zero-fill via the same hook.
+        self._d2h_done = d2h[-1][1] if d2h else None
         for g in self.groups:
             st = opt.optimizer.state[opt.master[g]]
             if opt.kind in ("adam", "adagrad"):
@@ -558,6 +563,14 @@ class HostOptimizerStep:
         asynchronous update must have read them."""
         if self.d2h is not None and torch.cuda.is_available():
             torch.cuda.current_stream().wait_stream(self.d2h)
+
+    def wait_grad_mirror(self):
+        """Order the current stream after the last gradient-mirror D2H copy of the pending asynchronous
+        update (a no-op once it has been waited for). Call before any eager write of ``u.grad``."""
+        ev = getattr(self, "_d2h_done", None)
+        if ev is not None and torch.cuda.is_available():
+            torch.cuda.current_stream().wait_event(ev)
+            self._d2h_done = None
 
     def _log_async_trace(self, tr):
         self.trace.append(tr)

@@ -316,6 +316,8 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                     u.grad.zero_()
 
     def _zero_stale(self):
+        if self.host_step is not None:
+            self.host_step.wait_grad_mirror()  # the async host update's D2H may still read u.grad
         for units in self.units:
             for u in units:
                 if u.topo.S == 1 and not all(u.acc_valid):

@@ -746,6 +746,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 u.rs_valid = False
 
     def _zero_stale(self):
+        if self.host_step is not None:
+            self.host_step.wait_grad_mirror()  # the async host update's D2H may still read u.grad
         for units in self.units:
             for u in units:
                 if u.persistent and self.S == 1:

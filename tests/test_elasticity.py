@@ -103,3 +103,60 @@ def test_elastic_agent_rdzv_view_counts_dead_heartbeats():
                                                               keep_alive_max_attempt=3))
     assert _rdzv_view(h, now) == (2, 1)
     assert _rdzv_view(types.SimpleNamespace()) == (None, 0)
+
+
+def test_elastic_agent_rdzv_view_aware_heartbeats_default_now():
+    """torch's DynamicRendezvousHandler stores aware UTC heartbeats; the default ``now`` must compare
+    against them without a naive/aware TypeError."""
+    import datetime
+    import types
+    from shuffle_exchange_amd.elasticity.elastic_agent import _rdzv_view
+    now = datetime.datetime.now(datetime.timezone.utc)
+    st = types.SimpleNamespace(participants={"a": 0, "b": 1, "c": 2},
+                               last_heartbeats={"a": now, "b": now - datetime.timedelta(seconds=100),
+                                                "c": now - datetime.timedelta(seconds=1)})
+    h = types.SimpleNamespace(_state_holder=types.SimpleNamespace(state=st),
+                              _settings=types.SimpleNamespace(keep_alive_interval=datetime.timedelta(seconds=5),
+                                                              keep_alive_max_attempt=3))
+    assert _rdzv_view(h) == (3, 1)
+
+
+def test_elastic_agent_fail_on_shrunk_healthy_group_reports_failed():
+    """Membership shrank, the local group is still HEALTHY, no restarts left: the agent stops the
+    workers and returns a FAILED result (so elastic_launch exits non-zero) without the exit barrier."""
+    import datetime
+    import types
+    from torch.distributed.elastic.agent.server.api import RunResult, WorkerState
+    from shuffle_exchange_amd.elasticity.elastic_agent import SXEElasticAgent
+    now = datetime.datetime.now(datetime.timezone.utc)
+    beats = {"a": now, "b": now}
+    st = types.SimpleNamespace(participants={"a": 0, "b": 1}, last_heartbeats=beats)
+    handler = types.SimpleNamespace(_state_holder=types.SimpleNamespace(state=st),
+                                    _settings=types.SimpleNamespace(keep_alive_interval=datetime.timedelta(seconds=5),
+                                                                    keep_alive_max_attempt=3),
+                                    num_nodes_waiting=lambda: 0)
+    calls = []
+
+    class Fake:
+        _remaining_restarts = 0
+        _worker_group = types.SimpleNamespace(spec=types.SimpleNamespace(role="default", rdzv_handler=handler,
+                                                                         monitor_interval=0, max_restarts=0),
+                                              state=None)
+
+        def _initialize_workers(self, wg):
+            calls.append("init")
+
+        def _monitor_workers(self, wg):
+            beats["b"] = now - datetime.timedelta(seconds=100)       # node b stops heart-beating
+            return RunResult(state=WorkerState.HEALTHY)
+
+        def _stop_workers(self, wg):
+            calls.append("stop")
+
+        def _exit_barrier(self):
+            calls.append("barrier")
+
+    res = SXEElasticAgent._invoke_run(Fake())
+    assert res.state == WorkerState.FAILED and res.is_failed()
+    assert calls == ["init", "stop"]
+    assert Fake._worker_group.state == WorkerState.FAILED
