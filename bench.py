@@ -283,8 +283,26 @@ def main():
             engine.step()
         return loss
 
-    for _ in range(args.warmup):
+    diag = None
+    for i in range(args.warmup):
+        if i == 0 and world > 1:  # collective fingerprint of the first step: every rank issued the same
+            dist.reset_fingerprint()   # sequence of (op, group, size, dtype) or the run stops here
+            dist.enable_fingerprint(True)
         loss = train_step()
+        if i == 0 and world > 1:
+            dist.enable_fingerprint(False)
+            digest, count = dist.fingerprint_digest()
+            dist.verify_fingerprints()
+            it = dist.get_init_times()
+            diag = {"fingerprint_first_step": {"sha1": digest[:16], "collectives": count, "ranks_agree": True},
+                    "init_process_group_ms": round(it["init_process_group_ms"] or 0.0, 1),
+                    "communicators": len(it["groups"]),
+                    "communicator_init_ms": round(sum(ms for _, ms in it["groups"]), 1),
+                    "communicator_init_max_ms": round(max([ms for _, ms in it["groups"]] or [0.0]), 1)}
+            if rank == 0:
+                print(f"[bench] first step: {count} collectives, fingerprints agree on all {world} ranks; "
+                      f"init_process_group {diag['init_process_group_ms']} ms, {diag['communicators']} "
+                      f"communicators in {diag['communicator_init_ms']} ms", file=sys.stderr, flush=True)
     sync()
     dist.barrier()
     sync()
@@ -352,6 +370,8 @@ def main():
             "comm_model": comm_model(engine.optimizer, world, stage, c["knobs"], gas),
             "valid_for_metric": valid,
         }
+        if diag is not None:
+            out["diagnostics"] = diag
         print(json.dumps(out), flush=True)
     dist.barrier()
     if dist.is_initialized():

@@ -55,6 +55,8 @@ class _State:
     comms = defaultdict(lambda: defaultdict(list))  # op -> msg_size -> [latency_ms...]
     op_counts = defaultdict(int)  # log_name -> collectives issued (always counted, no sync)
     volume = defaultdict(lambda: [0, 0])  # op -> [calls, payload bytes] (always counted, no sync)
+    group_init = []  # (cache key, ms) per communicator created by new_group
+    init_ms = None  # init_process_group wall time
     defer = os.environ.get("SXE_COMM_DEFER", "0") == "1"
     defer_cycles = int(os.environ.get("SXE_COMM_DEFER_CYCLES", 2_000_000))
 
@@ -109,8 +111,10 @@ def init_distributed(dist_backend=None, auto_mpi_discovery=True, distributed_por
         kw["store"] = tdist.HashStore()
     else:
         kw["init_method"] = init_method
+    t0 = time.perf_counter()
     tdist.init_process_group(backend=backend, timeout=timeout, rank=int(env["RANK"]),
                              world_size=int(env["WORLD_SIZE"]), **kw)
+    _State.init_ms = (time.perf_counter() - t0) * 1000.0
     _State.initialized = True
     _State.backend = backend
     if verbose:
@@ -167,7 +171,9 @@ def new_group(ranks, cache=True, tag=None):
         return _State.group_cache[key]
     if not is_initialized():
         return None
+    t0 = time.perf_counter()
     g = tdist.new_group(list(ranks_key))
+    _State.group_init.append((key, (time.perf_counter() - t0) * 1000.0))
     if cache:
         _State.group_cache[key] = g
     return g
@@ -369,6 +375,13 @@ def reset_comms_stats():
     _State.comms.clear()
     _State.op_counts.clear()
     _State.volume.clear()
+
+
+def get_init_times():
+    """Wall time of ``init_process_group`` and of every ``new_group`` (RCCL comm split / init) so far:
+    ``{"init_process_group_ms": ms, "groups": [(ranks, ms), ...]}``."""
+    return {"init_process_group_ms": _State.init_ms,
+            "groups": [(list(k), round(ms, 3)) for k, ms in _State.group_init]}
 
 
 def get_op_counts():

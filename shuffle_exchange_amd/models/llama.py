@@ -98,6 +98,9 @@ PRESETS = {
                       max_position_embeddings=4096),
     "llama-tiny": dict(vocab_size=512, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
                        num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=256),
+    # 8-rank rehearsals: 16 query / 8 KV heads so Ulysses SP=8 is legal (Llama-3-8B's 32/8 ratio halved)
+    "llama-tiny8": dict(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                        num_attention_heads=16, num_key_value_heads=8, max_position_embeddings=256),
 }
 
 

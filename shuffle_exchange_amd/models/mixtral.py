@@ -49,6 +49,10 @@ PRESETS = {
     "mixtral-tiny": dict(vocab_size=512, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
                          num_attention_heads=4, num_key_value_heads=2, max_position_embeddings=256,
                          num_local_experts=4),
+    # 8-rank rehearsals: 8 experts (EP=8 legal, one expert per rank, like Mixtral-8x7B at N=8)
+    "mixtral-tiny8": dict(vocab_size=512, hidden_size=128, intermediate_size=256, num_hidden_layers=2,
+                          num_attention_heads=8, num_key_value_heads=8, max_position_embeddings=256,
+                          num_local_experts=8),
 }
 
 

@@ -174,6 +174,7 @@ class HostOptimizerStep:
         if opt.kind not in HOST_KINDS and self.device == "nvme":
             raise ValueError("NVMe optimizer offload supports Adam/AdamW/Lion/Adagrad")
         self.groups = self.host_groups(opt)
+        self._preflight(opt)
         G = len(opt.units)
         opt.grad_host, opt.lp_host = [None] * G, [None] * G
         # Host staging of gradients (fp32, D2H) and updated bit16 params (H2D): a ring of
@@ -230,6 +231,26 @@ class HostOptimizerStep:
                 self.swapper.write(0, g, i, u.chunk)
                 self.swapper.drain()
         log_dist(f"ZeRO-Infinity: optimizer state on NVMe under {self.swapper.dir}", ranks=[0])
+
+    def _preflight(self, opt):
+        """Host bytes this rank's tier allocates, checked against the node's MemAvailable for every
+        local rank before the first allocation (a 70B model offloaded by 8 ranks needs ~1 TB)."""
+        from ...utils.host_resources import configure_host_threads, preflight_host_memory
+        self.threads = configure_host_threads()
+        units = [u for g in sorted(self.groups) for u in opt.units[g]]
+        if not units:
+            return
+        total = sum(u.chunk for u in units)
+        maxc = max(u.chunk for u in units)
+        streamed = opt.kind in HOST_KINDS
+        per_elem = (4 * self._kinds(opt)) if self.device == "cpu" else 0  # master + optimizer states
+        if not streamed:
+            per_elem += 4 + 2  # full-group gradient and bit16 mirrors
+        slots = self.STAGE_SLOTS * maxc * 6 if streamed else 0
+        if self.device == "nvme":
+            slots += self.buffer_count * maxc * 4 * self._kinds(opt)
+        preflight_host_memory(total * per_elem + slots,
+                              f"ZeRO-Offload optimizer tier ({self.device}, {total / 1e9:.2f} G elements)")
 
     # ------------------------------------------------------------------------------------ update
     def _host_kernel(self, opt, pg, st, master, grad, states, lp, coef):
@@ -384,7 +405,7 @@ class HostOptimizerStep:
             if cur is not None:
                 torch.cuda.synchronize()
             tr["wall"] = _time.perf_counter() - tr["t0"]
-            tr["threads"] = torch.get_num_threads()
+            tr["threads"] = int(torch.ops.sxe_cpu.num_threads())
             self.trace.append(tr)
             gb = tr["elems"] * 4 / 1e9
             log_dist(f"offload step: wall {tr['wall'] * 1e3:.0f} ms | C++ update {tr['cpu'] * 1e3:.0f} ms "
@@ -464,8 +485,10 @@ class HostOptimizerStep:
                 cops = getattr(torch.ops, "sxe_cpu", None)
                 if cops is not None and hasattr(cops, "set_num_threads"):
                     # one CPU stays with the training thread, which keeps launching the next
-                    # forward's kernels while this team updates (per-thread OpenMP setting)
-                    cops.set_num_threads(max(1, int(cops.num_threads()) - 1))
+                    # forward's kernels while this team updates (per-thread OpenMP setting: a new
+                    # thread starts from the env default, so pass the rank's share explicitly)
+                    n = getattr(self, "threads", None) or int(cops.num_threads())
+                    cops.set_num_threads(max(1, int(n) - 1))
                 NS = len(self.gslots)
                 for k, ((g, i, u, off), (grad, ev)) in enumerate(zip(flat, d2h)):
                     ta = _time.perf_counter()

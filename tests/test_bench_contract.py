@@ -91,3 +91,46 @@ def test_bench_tuned_zero3_comm_model_matches_measured(tmp_path):
     # tuned: ONE gather of the model per step and ONE deferred reduce-scatter per step
     for op in ("all_gather_into_tensor", "reduce_scatter_tensor"):
         assert meas[op]["bytes_per_step"] == model_[op], (op, meas[op], model_[op])
+
+
+CONFIGS = ["llama8b-z3", "llama8b-z3-default", "mixtral-ep", "llama70b-infinity", "llama8b-sp32k"]
+
+
+@pytest.mark.parametrize("world", [4, 8])
+@pytest.mark.parametrize("config", CONFIGS)
+def test_bench_configs_wide_cpu(tmp_path, config, world):
+    """Every BASELINE config at the driver's W=4 and W=8 over gloo, with models whose head/expert
+    counts make SP=8 / EP=8 legal (llama-tiny8: 16 q / 8 kv heads, mixtral-tiny8: 8 experts): one
+    JSON line, the config's parallelism degree equal to W where it scales with W, the measured
+    ZeRO collective bytes equal to the analytic model, and the first step's collective fingerprint
+    identical on every rank (bench.py raises otherwise)."""
+    model = "mixtral-tiny8" if config == "mixtral-ep" else "llama-tiny8"
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    port = 29700 + 2 * CONFIGS.index(config) + (0 if world == 4 else 20)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus",
+           str(world), "--steps", "2", "--warmup", "1", "--config", config, "--model", model, "--device", "cpu",
+           "--mbs", "1", "--gas", "2", "--seq", "128"]
+    if config == "llama70b-infinity":
+        cmd += ["--layers", "2"]
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=900)
+    assert r.returncode == 0, r.stdout[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-4000:]
+    out = json.loads(lines[0])
+    cfg = out["config"]
+    assert out["n_gpus"] == world and cfg["name"] == config and out["valid_for_metric"] is False
+    diag = out["diagnostics"]
+    assert diag["fingerprint_first_step"]["ranks_agree"] and diag["fingerprint_first_step"]["collectives"] > 0
+    assert diag["communicators"] >= 1
+    if config == "mixtral-ep":
+        assert cfg["expert_parallel_size"] == world and f"ep{world}" in cfg["parallelism"]
+    elif config == "llama8b-sp32k":
+        assert cfg["sequence_parallel_size"] == world and cfg["global_batch"] == 2
+    else:
+        assert f"dp{world}" in cfg["parallelism"] and cfg["global_batch"] == world * 2
+    meas, model_ = out["comm_measured"], out["comm_model"]
+    assert model_, out
+    for op, b in model_.items():
+        assert meas[op]["bytes_per_step"] == b, (op, meas[op], b)
