@@ -122,7 +122,11 @@ def comm_model(opt, world, stage, knobs, gas, elem_bytes=2):
             return {}
         # the gather policy of runtime/zero/stage3.py replayed on the recorded forward trace
         size = {fg.idx: sum(u.padded for u in fg.units if not u.persistent) for fg in opt.fgroups}
-        persistent = sum(u.padded for fg in opt.fgroups for u in fg.units if u.persistent)
+        # frozen units are gathered but never reduced, nor refreshed after the step
+        rs_size = sum(u.padded for fg in opt.fgroups for u in fg.units
+                      if not u.persistent and not getattr(u, "frozen", False))
+        persistent = sum(u.padded for fg in opt.fgroups for u in fg.units
+                         if u.persistent and not getattr(u, "frozen", False))
         trace = list(opt.trace)
         if getattr(opt, "retain_params", False):
             gathered = sum(size[i] for i in trace)  # once per step: retained until the boundary backward
@@ -138,7 +142,7 @@ def comm_model(opt, world, stage, knobs, gas, elem_bytes=2):
             gathered = gas * (sum(size[i] for i in trace) + sum(size[i] for i in trace if i not in kept))
         n_rs = 1 if getattr(opt, "defer_reduce", False) else gas
         out["all_gather_into_tensor"] = (gathered + persistent) * elem_bytes  # persistent: refreshed after the step
-        out["reduce_scatter_tensor"] = n_rs * (sum(size.values()) + persistent) * elem_bytes
+        out["reduce_scatter_tensor"] = n_rs * (rs_size + persistent) * elem_bytes
     elif stage in (1, 2) and hasattr(opt, "units"):
         total = sum(u.padded for units in opt.units for u in units if u.topo.S > 1) * elem_bytes
         out["reduce_scatter_tensor"] = total * (gas if stage == 2 else 1)

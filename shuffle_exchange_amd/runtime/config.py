@@ -467,7 +467,6 @@ class SXEConfig:
         "round_robin_gradients": "gradient partitions are flat units reduce-scattered straight into their owner",
         "mics_hierarchical_params_gather": "single-node xGMI: the MiCS shard group is gathered in one step",
         "allgather_bucket_size": "ZeRO-1/2 all-gather one flat unit at a time (units are sized by reduce_bucket_size)",
-        "zero_quantized_nontrainable_weights": "frozen weights are not partitioned by ZeRO-3 here (kept resident)",
         "contiguous_gradients": "gradients always land in contiguous flat units",
         "use_multi_rank_bucket_allreduce": "ZeRO-1/2 always use a true reduce-scatter",
         "legacy_stage1": "one ZeRO-1/2 implementation",

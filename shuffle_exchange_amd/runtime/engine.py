@@ -541,7 +541,8 @@ class SXEEngine(nn.Module):
                 defer_reduce=zc.defer_reduce, retain_params=zc.retain_params, loco_param=zc.zeropp_loco_param,
                 prefetch_bucket_size=(zc.prefetch_bucket_size if "prefetch_bucket_size" in zc.model_fields_set
                                       and "prefetch_depth" not in zc.model_fields_set else None),
-                model_persistence_threshold=zc.model_persistence_threshold, param_swap=param_swap)
+                model_persistence_threshold=zc.model_persistence_threshold, param_swap=param_swap,
+                quantized_nontrainable=zc.zero_quantized_nontrainable_weights)
         elif stage == 1 and dtype == torch.bfloat16 and cfg.grad_accum_dtype == "fp32" and host_step is None:
             # reference engine.py:1384-1386: bf16 + ZeRO-1 + fp32 gradient accumulation -> BF16_Optimizer
             from .bf16_optimizer import BF16_Optimizer
@@ -1408,13 +1409,30 @@ class SXEEngine(nn.Module):
 
     def _frozen_param_fragments(self):
         """Frozen (requires_grad=False) parameters by name, on the host (reference
-        ``_get_zero_frozen_param_attributes(_get_param_fragment_func)``): ZeRO keeps them out of its
-        flat units, so each is whole on every rank."""
+        ``_get_zero_frozen_param_attributes(_get_param_fragment_func)``). ZeRO-1/2 keep them whole on
+        every rank. ZeRO-3 partitions them in gather-only units: every rank takes part in the gathers
+        (a collective), the first rank keeps the whole tensors (zero_to_fp32 reads its file)."""
         out = {}
+        opt = self.optimizer
+        if self.zero_optimization_stage() == 3 and getattr(opt, "frozen_units", None):
+            keep = dist.get_rank() == 0
+            full = opt.frozen_state_dict(keep=keep)
+            if not keep:
+                return {}
+            for n, p in self.module.named_parameters():
+                if not p.requires_grad and p in full:
+                    out[n] = full[p]
+            return out
         for n, p in self.module.named_parameters():
             if not p.requires_grad and p.numel() > 0:
                 out[n] = p.detach().cpu().clone()
         return out
+
+    def quantize_nontrainable_params(self):
+        """ZeRO-3 with ``zero_quantized_nontrainable_weights``: store every frozen unit int8 (reference
+        engine/stage3 ``quantize_nontrainable_params``; call it after freezing parameters)."""
+        fn = getattr(self.optimizer, "quantize_nontrainable_params", None)
+        return fn() if fn is not None else 0
 
     def _copy_recovery_script(self, tag_dir):
         """Copy the offline consolidation script into the tag directory (reference engine.py:3767
@@ -1486,7 +1504,8 @@ class SXEEngine(nn.Module):
                 optimizer=None,
                 param_shapes=[{names[p]: tuple(getattr(p, "ds_shape", p.shape)) for p in pg["params_orig"]}
                               for pg in self._orig_param_groups()],
-                frozen_param_shapes={n: tuple(p.shape) for n, p in self.module.named_parameters() if not p.requires_grad},
+                frozen_param_shapes={n: tuple(getattr(p, "ds_shape", p.shape))
+                                     for n, p in self.module.named_parameters() if not p.requires_grad},
                 shared_params=self._shared_params(),
                 frozen_param_fragments=self._frozen_param_fragments() if (stage >= 2 and not exclude_frozen_parameters)
                 else None,

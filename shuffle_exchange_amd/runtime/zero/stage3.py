@@ -112,7 +112,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                  quantized_gradients=False, hpz_partition_size=1, quant_group_size=128, grad_quant_bits=8,
                  max_reuse_distance=1_000_000_000, max_live_parameters=1_000_000_000, defer_reduce=False,
                  retain_params=False, loco_param=None, prefetch_bucket_size=None,
-                 model_persistence_threshold=2**63 - 1, param_swap=None):
+                 model_persistence_threshold=2**63 - 1, param_swap=None, quantized_nontrainable=False):
         acc = get_accelerator()
         device = torch.device(acc.current_device_name())
         self.module = module
@@ -161,6 +161,9 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         self._loco_idx = 0
         self.qgroup = int(quant_group_size)
         self.gbits = int(grad_quant_bits)
+        # zero_quantized_nontrainable_weights: frozen shards stored int8 + group scales (quant.hip),
+        # dequantized by the gather (reference stage3.py:1558, partition_parameters.py:1685,1769)
+        self.quant_frozen = bool(quantized_nontrainable)
         self.hpz = int(hpz_partition_size or 1)
         self.hpz_group = None
         if self.hpz > 1 and self.S > self.hpz:
@@ -204,6 +207,11 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         self._hooks = []
         self.fgroups = []
         self.param_unit = {}
+        # frozen (requires_grad=False) parameters: gather-only units -- partitioned bit16 (or int8)
+        # shard, fetched and released with their module, no gradient / master / optimizer state
+        self.frozen_unit = {}
+        self.frozen_units = []
+        self._bwd_frozen = []
         self._build(unit_classes)
         self._init_master()
         self._register()
@@ -240,9 +248,15 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         self.units = [[] for _ in self.optimizer.param_groups]
         for fi, (name, mod) in enumerate(discover_units(self.module, unit_classes)):
             own_only = name.endswith("#own") or name == "#root"
-            params = list(mod.parameters(recurse=not own_only))
-            params = [p for p in params if p.requires_grad and id(p) in group_of and p not in self.param_unit]
-            if not params:
+            allp = list(mod.parameters(recurse=not own_only))
+            params = [p for p in allp if p.requires_grad and id(p) in group_of and p not in self.param_unit]
+            # frozen weights (a LoRA base model, frozen embeddings) are owned by ZeRO-3 too: without
+            # this a zero.Init-partitioned frozen parameter has no data at all, and one built whole
+            # would stay whole on every rank (reference partitioned_param_coordinator.py:300,437,544
+            # fetches every parameter of a submodule, trainable or not)
+            frozen = [p for p in allp if not p.requires_grad and p not in self.frozen_unit
+                      and getattr(p, "allreduce", True) is not False]
+            if not params and not frozen:
                 continue
             fg = _FetchGroup(len(self.fgroups), name, mod, own_only)
             by_group = {}
@@ -254,21 +268,29 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 fg.units.append(u)
                 for p in plist:
                     self.param_unit[p] = u
+            if frozen:
+                u = self._make_unit(frozen, f"{name}/frozen", fg, frozen=True)
+                fg.units.append(u)
+                self.frozen_units.append(u)
+                for p in frozen:
+                    self.frozen_unit[p] = u
             self.fgroups.append(fg)
         # external parameters: a module that uses a parameter owned by another unit (tied
         # embeddings / LM head, or register_external_parameter) fetches that unit too (reference
         # partition_parameters.py register_external_parameter, parameter_offload.py external params)
         fg_of = {id(fg.module): fg for fg in self.fgroups}
+        owner = dict(self.frozen_unit)
+        owner.update(self.param_unit)
 
         def scan(mod, name, cover):
             fg = fg_of.get(id(mod))
             here = fg if fg is not None else cover  # the fetch group whose hook runs around mod
             ext = list(getattr(mod, "_sxe_external_params", []))
             ext += [p for p in mod.parameters(recurse=False)
-                    if p in self.param_unit and self.param_unit[p].fg is not here]
+                    if p in owner and owner[p].fg is not here]
             ext_units = []
             for p in ext:
-                u = self.param_unit.get(p)
+                u = owner.get(p)
                 if u is not None and u not in ext_units and (here is None or u not in here.units):
                     ext_units.append(u)
             if ext_units:
@@ -293,12 +315,14 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 self.param_unit[p] = u
             self.fgroups.append(fg)
 
-    def _make_unit(self, params, name, fg):
+    def _make_unit(self, params, name, fg, frozen=False):
         dtype = params[0].dtype
         u = FlatUnit(params, self.S, self.topo.offset, dtype, self.device, name=name, materialize_full=False)
         u.comm_dtype = unit_comm_dtype(params)  # torch_autocast: bf16 reduce-scatter when every param is marked
         u.fg = fg
         u.owner = self
+        u.frozen = frozen
+        u.frozen_q = False
         u.persistent = (self.S == 1 and not self.offload_param) or (
             u.numel < self.persist_thr and self._persist_total + u.numel <= self.model_persist_thr)
         if u.persistent:
@@ -319,7 +343,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             u.shard = flat[u.lo:u.hi]
             u.state = AVAILABLE
         else:
-            if self.pswap is not None:
+            if self.pswap is not None and not frozen:
                 self.pswap.register(u, flat[u.lo:u.hi].cpu())
                 u.shard = None
                 u.swap = self.pswap
@@ -341,7 +365,47 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         u.sec_shard, u.sec_valid = None, False
         for p in params:
             p.ds_unit = u
+        if frozen and self.quant_frozen:
+            self._quantize_frozen(u)
         return u
+
+    def _quantize_frozen(self, u):
+        """Store a frozen unit's shard as int8 + fp32 group scales (half the bytes of bf16); the
+        gather all-gathers the int8 shards and dequantizes into the unit buffer. Resident units
+        (one rank, small units, host-resident shards) keep bit16."""
+        if u.persistent or u.frozen_q or self.S == 1 or u.swap is not None or u.shard.device != self.device:
+            return False
+        self._quantize_shard(u)
+        u.shard = None
+        u.frozen_q = True
+        return True
+
+    def quantize_nontrainable_params(self):
+        """Quantize every frozen unit that is still stored in bit16 (reference stage3.py:1558: after
+        ``zero_quantized_nontrainable_weights`` was switched on, or frozen units were added).
+        Returns the number of units quantized."""
+        if not self.quant_frozen:
+            log_dist("quantize_nontrainable_params(): zero_quantized_nontrainable_weights is off, nothing to do",
+                     ranks=[0])
+            return 0
+        self.wait_params()
+        return sum(1 for u in self.frozen_units if self._quantize_frozen(u))
+
+    def frozen_state_dict(self, keep=True):
+        """{param: full host tensor} of every frozen parameter (a collective: gathers each frozen
+        unit in turn, then releases it). Ranks with ``keep=False`` take part without a copy."""
+        out = {}
+        self.wait_params()
+        for u in self.frozen_units:
+            was = u.state
+            if not u.persistent:
+                self._fetch_unit(u)
+            if keep:
+                for p in u.params:
+                    out[p] = p.detach().cpu().clone()
+            if not u.persistent and was == RELEASED:
+                self._release_unit(u)
+        return out
 
     # -------------------------------------------------------------------------------------- hooks
     def _register(self):
@@ -458,7 +522,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         def post(mod, args, out):
             if self.tracer is not None and not self._in_bwd:
                 self.tracer.on_fwd_end(fg)
-            if torch.is_grad_enabled() and any(u.params[0].requires_grad for u in fg.units):
+            if torch.is_grad_enabled():  # frozen-only groups too: their backward reads the weights
                 out = self._wrap_outputs(fg, out)
             if not self._in_bwd and not (torch.is_grad_enabled() and self._keep_for_backward(fg)):
                 self._release(fg)
@@ -566,7 +630,9 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 u.graph_unlinked = False
             swapped = u.swap is not None
             src = u.swap.acquire(u) if swapped else u.shard
-            if src.device != u.flat.device:
+            if src is None:  # int8 frozen shard: the quantized gather below reads u.qshard
+                src = u.flat
+            elif src.device != u.flat.device:
                 src = src.to(u.flat.device, non_blocking=True)
                 if st is not None:
                     src.record_stream(st)
@@ -582,7 +648,7 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             elif self.hpz > 1 and self._in_bwd and u.sec_valid:
                 # hpZ: backward re-gather inside the intra-node group from the secondary shards
                 dist.all_gather_into_tensor(u.flat, u.sec_shard, group=self.hpz_group)
-            elif self.qwz:
+            elif self.qwz or u.frozen_q:
                 self._quantized_gather(u, st)
             else:
                 dist.all_gather_into_tensor(u.flat, src, group=self.topo.slice_group)
@@ -615,6 +681,16 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         if st is not None:
             qa.record_stream(st)
             sa.record_stream(st)
+
+    def _fetch_unit(self, u):
+        if u.state == RELEASED:
+            self._launch_gather(u)
+        if u.state == INFLIGHT:
+            if u.event is not None:
+                cur = torch.cuda.current_stream()
+                cur.wait_event(u.event)
+                u.flat.record_stream(cur)
+            u.state = AVAILABLE
 
     def _fetch(self, fg, wait=True):
         for u in fg.units:
@@ -685,7 +761,16 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
 
     def _pre_backward(self, fg):
         self._in_bwd = True
+        if self._bwd_frozen:
+            # frozen units get no gradient hook to release them: the previous group's backward has
+            # run once the next group's output gradient exists
+            keep = [u for u in self._bwd_frozen if u in fg.units]
+            for u in self._bwd_frozen:
+                if u not in keep:
+                    self._release_unit(u)
+            self._bwd_frozen = keep
         self._fetch(fg, wait=True)
+        self._bwd_frozen.extend(u for u in fg.units if u.frozen and not u.persistent and u not in self._bwd_frozen)
         self._prefetch_after(fg, backward=True)
         if self.tracer is not None:
             self.tracer.on_bwd_begin(fg)
@@ -821,6 +906,10 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                     self._reduce_unit(u)
                 if not u.persistent:
                     self._release_unit(u)
+        for u in self.frozen_units:
+            if not u.persistent:
+                self._release_unit(u)
+        self._bwd_frozen = []
         if self._observed and self._observed != self.trace:
             # trace changed (data-dependent control flow): adopt the new order
             seen, order = set(), []
@@ -855,8 +944,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         seen, out = set(), []
         rest = [fg for fg in self.fgroups if fg.name == "#rest"]
         groups = rest + [self.fgroups[j] for j in self.trace] + list(self.fgroups)
-        resident = [u for fg in groups for u in fg.units if u.persistent or u.keep]  # _refresh_persistent's
-        for u in (resident if self.S > 1 else []) + [u for fg in groups for u in fg.units]:
+        resident = [u for fg in groups for u in fg.units if (u.persistent or u.keep) and not u.frozen]
+        for u in (resident if self.S > 1 else []) + [u for fg in groups for u in fg.units if not u.frozen]:
             if id(u) not in seen:
                 seen.add(id(u))
                 out.append(u)
@@ -972,7 +1061,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
 
     def gather_params(self, params):
         self.wait_params()
-        units = {id(self.param_unit[p]): self.param_unit[p] for p in params if p in self.param_unit}
+        owner = lambda p: self.param_unit.get(p) or self.frozen_unit.get(p)  # noqa: E731
+        units = {id(owner(p)): owner(p) for p in params if owner(p) is not None}
         for u in units.values():
             if not u.persistent and u.state == RELEASED:
                 self._launch_gather(u)
@@ -989,6 +1079,13 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         for u in units:
             if src_rank is not None:
                 dist.broadcast(u.flat, src=src_rank, group=group)
+            if getattr(u, "frozen", False):  # no master: the shard (or its int8 form) is the state
+                if u.frozen_q:
+                    from ...ops.quantizer import quantize
+                    u.qshard = quantize(u.flat[u.lo:u.hi], self._qgroup(u), 8)
+                elif not u.persistent:
+                    u.shard.copy_(u.flat[u.lo:u.hi])
+                continue
             if not u.persistent:
                 u.shard.copy_(u.flat[u.lo:u.hi])
             if self.host_step is not None:

@@ -418,3 +418,79 @@ def case_zero3_comm_design(rank, world, steps):
     return {"same_group": opt.reduce_group is opt.topo.slice_group,
             "rs_ranks": comm.group_ranks(opt.reduce_group), "ag_ranks": comm.group_ranks(opt.topo.slice_group),
             "n_persist": n_persist, "refresh": refresh, "params": full_params(eng)}
+
+
+def _freeze_lora_style(model):
+    """Freeze every MLP projection and the token embedding (a LoRA-style frozen base); attention
+    projections, norms and the LM head stay trainable."""
+    names = []
+    for n, p in model.named_parameters():
+        if ".mlp." in n or n.startswith("embed_tokens"):
+            p.requires_grad_(False)
+            names.append(n)
+    return names
+
+
+def case_zero3_frozen(rank, world, steps, quant, tmpdir):
+    """zero.Init + ZeRO-3 with frozen base weights: the frozen parameters become gather-only units
+    (1/W shard per rank, optionally int8), the forward/backward read them, the trainable ones update."""
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+    torch.manual_seed(5)
+    cfg = llama_config("llama-tiny")
+    with sxe.zero.Init(dtype=torch.float32):
+        model = LlamaForCausalLM(cfg)
+    frozen_names = _freeze_lora_style(model)
+    ds = {"train_micro_batch_size_per_gpu": 1,
+          "zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 0,
+                                "stage3_gather_16bit_weights_on_model_save": True,
+                                "zero_quantized_nontrainable_weights": bool(quant)},
+          "optimizer": {"type": "AdamW", "params": {"lr": 1e-2, "weight_decay": 0.0}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    opt = eng.optimizer
+    frozen_total = sum(p.ds_numel for n, p in model.named_parameters() if n in frozen_names)
+    frozen_shard = sum((u.qshard[0].numel() if u.frozen_q else u.shard.numel()) for u in opt.frozen_units)
+    frozen_bytes = sum((u.qshard[0].numel() * u.qshard[0].element_size() + u.qshard[1].numel() * 4)
+                       if u.frozen_q else u.shard.numel() * u.shard.element_size() for u in opt.frozen_units)
+    n_quant = sum(1 for u in opt.frozen_units if u.frozen_q)
+    released = all(p.data.numel() == 0 for n, p in model.named_parameters() if n in frozen_names)
+    before = full_params(eng)
+    g = torch.Generator().manual_seed(11)
+    losses = []
+    for _ in range(steps):
+        b = torch.randint(0, cfg.vocab_size, (world, 16), generator=g)[rank:rank + 1]
+        loss = eng(b, labels=b)
+        eng.backward(loss)
+        eng.step()
+        losses.append(float(loss.detach()))
+    after = full_params(eng)
+    eng.save_16bit_model(tmpdir, "frozen16.bin")
+    saved = torch.load(os.path.join(tmpdir, "frozen16.bin"), weights_only=True) if rank == 0 else None
+    frags = eng._frozen_param_fragments()
+    return {"frozen_names": frozen_names, "frozen_total": frozen_total, "frozen_shard": frozen_shard,
+            "frozen_bytes": frozen_bytes, "n_quant": n_quant, "n_frozen_units": len(opt.frozen_units),
+            "released": released, "before": before, "after": after, "losses": losses,
+            "saved_keys": sorted(saved) if saved is not None else None,
+            "saved_frozen": {k: saved[k].float() for k in frozen_names} if saved is not None else None,
+            "frag_keys": sorted(frags)}
+
+
+def frozen_reference(before, frozen_names, steps, world, lr=1e-2):
+    """Single-process reference of case_zero3_frozen from its initial weights, on the global batch."""
+    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+    cfg = llama_config("llama-tiny")
+    model = LlamaForCausalLM(cfg).float()
+    model.load_state_dict({k: v.float() for k, v in before.items()}, strict=False)
+    for n, p in model.named_parameters():
+        p.requires_grad_(n not in frozen_names)
+    opt = torch.optim.AdamW([p for p in model.parameters() if p.requires_grad], lr=lr, weight_decay=0.0)
+    g = torch.Generator().manual_seed(11)
+    losses = []
+    for _ in range(steps):
+        b = torch.randint(0, cfg.vocab_size, (world, 16), generator=g)
+        loss = model(b, labels=b)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(float(loss.detach()))
+    return {n: q.detach().float().clone() for n, q in model.named_parameters()}, losses
