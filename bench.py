@@ -171,6 +171,35 @@ def effective_zero(opt):
     return {"optimizer": type(opt).__name__}
 
 
+def _attribute_step(train_step, out_dir):
+    """Profile one step with torch.profiler and write, per GPU kernel, the op and Python call sites
+    that launched it (what a rocprofv3 kernel table cannot say): ``attrib_kernels.txt``."""
+    from torch.profiler import ProfilerActivity, profile
+    os.makedirs(out_dir, exist_ok=True)
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+        train_step()
+        torch.cuda.synchronize()
+    with open(os.path.join(out_dir, "attrib_ops.txt"), "w") as f:
+        f.write(prof.key_averages(group_by_stack_n=6).table(sort_by="self_cuda_time_total", row_limit=80,
+                                                             max_name_column_width=90, max_src_column_width=200))
+    ev = [e for e in prof.events() if e.device_type.name == "CUDA"] if hasattr(prof, "events") else []
+    agg = {}
+    for e in ev:
+        p = e.cpu_parent
+        chain = []
+        while p is not None and len(chain) < 4:
+            chain.append(p.name)
+            p = p.cpu_parent
+        stack = [s for s in (getattr(e.cpu_parent, "stack", None) or []) if "shuffle_exchange_amd" in s or "bench.py" in s]
+        key = (e.name[:90], " < ".join(chain), " | ".join(stack[:3]))
+        a = agg.setdefault(key, [0, 0.0])
+        a[0] += 1
+        a[1] += e.device_time_total / 1000.0 if hasattr(e, "device_time_total") else e.cuda_time_total / 1000.0
+    with open(os.path.join(out_dir, "attrib_kernels.txt"), "w") as f:
+        for (k, chain, stack), (n, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:120]:
+            f.write(f"{ms:9.2f} ms {n:5d}x  {k}\n      ops: {chain}\n      at: {stack}\n")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -319,6 +348,10 @@ def main():
     sync()
     elapsed = time.perf_counter() - t0
     vol = dist.get_comm_volume()
+    prof_dir = os.environ.get("SXE_BENCH_TORCH_PROFILE")
+    if prof_dir and rank == 0 and on_gpu:  # one extra step AFTER the timed loop: kernel -> op -> Python stack
+        _attribute_step(train_step, prof_dir)
+    dist.barrier()
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())

@@ -164,22 +164,36 @@ class ZeroOptimizerBase:
     def _grad_norm_and_flags(self):
         """Device-side: global grad norm (unscaled), the clip/unscale coefficient and the skip
         (non-finite) flag, with ONE small all-reduce for all step metadata. No host sync."""
-        sq = None
+        # Shuffle-exchange + MoE (stage12): expert groups are partitioned over expert-DP groups that
+        # span the slices, so their sum of squares is summed world-wide in a slot of its own
+        split = bool(getattr(self, "_split_expert_norm", False))
+        sq = sq_e = None
         for g, gr in enumerate(self.grads):
             s = fused.sumsq(gr)
-            w = self.optimizer.param_groups[g].get("norm_weight", 1.0) if g < len(self.optimizer.param_groups) else 1.0
+            pg = self.optimizer.param_groups[g] if g < len(self.optimizer.param_groups) else {}
+            w = pg.get("norm_weight", 1.0)
             if w != 1.0:
                 s = s * w
-            sq = s if sq is None else sq + s
-        sq = sq.reshape(1).float()
+            if split and pg.get("moe", False):
+                sq_e = s if sq_e is None else sq_e + s
+            else:
+                sq = s if sq is None else sq + s
+        sq = sq.reshape(1).float() if sq is not None else torch.zeros(1, dtype=torch.float32, device=self.device)
         domain, D = self._norm_domains()
         if D > 1 or dist.get_world_size() > 1:
-            meta = torch.zeros(D + 1, dtype=torch.float32, device=sq.device)
+            E = 1 if split else 0
+            meta = torch.zeros(D + E + 1, dtype=torch.float32, device=sq.device)
             meta[domain:domain + 1] = torch.nan_to_num(sq, nan=0.0, posinf=0.0)
-            meta[D:] = (~torch.isfinite(sq)).float()
+            bad = (~torch.isfinite(sq)).float()
+            if split:
+                sq_e = sq_e.reshape(1).float() if sq_e is not None else torch.zeros_like(sq)
+                meta[D:D + 1] = torch.nan_to_num(sq_e, nan=0.0, posinf=0.0)
+                bad = bad + (~torch.isfinite(sq_e)).float()
+            meta[D + E:] = bad
             dist.all_reduce(meta, group=None, log_name="step_meta")
+            tot = meta[domain:domain + 1] + (meta[D:D + 1] if split else 0.0)
             # a non-finite gradient anywhere in the world -> inf norm -> every rank skips the step
-            sq = torch.where(meta[D:] > 0, torch.full_like(sq, float("inf")), meta[domain:domain + 1])
+            sq = torch.where(meta[D + E:] > 0, torch.full_like(sq, float("inf")), tot)
         ls = float(self.loss_scaler.loss_scale)
         norm = sq.sqrt() / ls
         skip = (~torch.isfinite(norm)).float()

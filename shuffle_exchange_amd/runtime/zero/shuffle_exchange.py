@@ -161,19 +161,27 @@ class ShuffleExchange:
             dist.all_reduce(f, group=group)
             t.copy_(f)
 
-    @staticmethod
-    def _packed(tensors, fn):
+    def _packed(self, tensors, fn):
         """Run ``fn(flat)`` once per dtype over all ``tensors`` packed back to back: one collective per
         step instead of one per chunk (every RCCL call pays its launch + ring-setup latency over the
-        xGMI links; the pack / unpack copies run at HBM speed). A lone tensor goes in place."""
+        xGMI links; the pack / unpack copies run at HBM speed). A lone tensor goes in place. The pack
+        buffer is persistent per (dtype, device): no allocation per step (the chunks themselves cannot
+        alias one buffer -- each unit's flat buffer must stay contiguous for its all-gather)."""
         by_dt = {}
         for t in tensors:
             by_dt.setdefault(t.dtype, []).append(t)
+        bufs = self.__dict__.setdefault("_pack_bufs", {})
         for ts in by_dt.values():
             if len(ts) == 1 and ts[0].is_contiguous():
                 fn(ts[0])
                 continue
-            flat = torch.cat([t.reshape(-1) for t in ts])
+            total = sum(t.numel() for t in ts)
+            key = (ts[0].dtype, ts[0].device)
+            buf = bufs.get(key)
+            if buf is None or buf.numel() < total:
+                buf = bufs[key] = torch.empty(total, dtype=ts[0].dtype, device=ts[0].device)
+            flat = buf[:total]
+            torch.cat([t.reshape(-1) for t in ts], out=flat)
             fn(flat)
             o = 0
             for t in ts:

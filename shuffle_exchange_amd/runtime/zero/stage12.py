@@ -99,9 +99,15 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         self.bit16_dtype = dtype
         if self._moe_topos:
             if self.shuffle_exchange_enabled:
-                raise NotImplementedError("Shuffle-exchange slices with MoE expert groups are not supported")
-            # expert and dense partitions are disjoint across the whole DP group: one norm reduce
-            self.partition_group = dp_group
+                # Shuffle-exchange + MoE (reference stage_1_and_2.py:810-821): expert groups keep their
+                # expert-data-parallel ZeRO partitioning across the slices (their gradient is the
+                # global one, reduced over the expert-DP group and divided by the dense DP size), only
+                # the dense groups are sliced and averaged between slices. The norm domain of the
+                # dense part stays the slice; the expert sum of squares is summed world-wide.
+                self._split_expert_norm = True
+            else:
+                # expert and dense partitions are disjoint across the whole DP group: one norm reduce
+                self.partition_group = dp_group
         self._init_master()
         for units in self.units:  # fp32 accumulators start zeroed: every slot counts as written
             for u in units:
@@ -226,7 +232,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         the dense data-parallel size, so the expert gradients do not depend on ep_size (reference
         stage_1_and_2.py:1316 divides the whole bucket by the dp group size; engine.py:2713-2716) --
         an EDP group of one rank (ep == dp) still averages over the dp ranks whose tokens it saw."""
-        return self.sp_scale / (self.topo.S if getattr(u, "moe", False) else u.topo.S)
+        return self.sp_scale / (self.topo.W if getattr(u, "moe", False) else u.topo.S)
 
     def _reduce_unit(self, u):
         st = u.staging
@@ -331,7 +337,7 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         self._wait_comm()
         self._zero_stale()
         if self.se is not None and self.method == "Gossip":
-            self.se.pre_step([u.shard for units in self.units for u in units])
+            self.se.pre_step([u.shard for u in self._dense_units()])
         coef, skip = self._grad_norm_and_flags()
         if getattr(self.loss_scaler, "dynamic", False):
             if self._handle_overflow_host():
@@ -387,8 +393,12 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
             evs = {}
         with get_accelerator().stream(stream):
             if self.se is not None:
-                # one packed inter-slice collective per step for all chunks (Gossip: one plan)
-                self.se.sync([u.shard for u in units], masters)
+                # one packed inter-slice collective per step for all dense chunks (Gossip: one plan);
+                # expert chunks are already identical across their expert-DP group
+                dense = self._dense_units()
+                if masters is not None:
+                    masters = [u.master for u in dense]
+                self.se.sync([u.shard for u in dense], masters)
             for i, u in enumerate(units):
                 ev = evs.pop(u, None)  # this unit's overlapped update (zero/base.py)
                 if ev is not None and u.topo.S > 1:
@@ -428,12 +438,15 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
             p.grad = None
 
     # ---------------------------------------------------------------------- Shuffle-exchange hooks
+    def _dense_units(self):
+        return [u for units in self.units for u in units if not getattr(u, "moe", False)]
+
     def shuffle_exchange(self):
         if self.se is not None:
             self.se.shuffle_exchange()
 
     def synchronization(self):
-        if self.se is not None and self.se.synchronization([u.shard for units in self.units for u in units]):
+        if self.se is not None and self.se.synchronization([u.shard for u in self._dense_units()]):
             self._allgather_params()
 
     def reset_rings(self, rings):

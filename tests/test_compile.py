@@ -153,3 +153,13 @@ def test_prefetch_pass_respects_budget_and_covers_gather_time():
     plan2 = prefetch(g, zero3_schedule(g, {}, 0), budget=1000 + 10_000, slack=1.0)
     trig2 = {j: t for t, js in plan2["prefetch"]["fwd"].items() for j in js}
     assert trig2[5] == 2 and trig2[4] == 1  # 3 nodes of 1 ms cover 2.5 ms
+
+
+def test_compile_config_warns_on_no_effect_keys():
+    """compile keys with no effect here (sync_*, symmetric_memory, keep_*) and unknown keys warn
+    instead of being accepted silently."""
+    from shuffle_exchange_amd.compile.config import CompileConfig
+    c = CompileConfig.from_dict({"deepcompile": True, "symmetric_memory": True, "sync_after_reduce": True,
+                                 "keep_all_input_tensors": True, "bogus_key": 1})
+    assert set(c.ignored) == {"symmetric_memory", "sync_after_reduce", "keep_all_input_tensors", "bogus_key"}
+    assert CompileConfig.from_dict({"deepcompile": True, "keep_int_input_tensors": True}).ignored == []

@@ -234,3 +234,52 @@ def test_moe_checkpoint_round_trip(tmp_path, world, tp, ep, expert_tp, stage):
                  weights_only=False)
     assert not any(".deepspeed_moe.experts." in k for k in sd["module"])
     assert sd["num_experts"] == [E] * n_layers
+
+
+# ------------------------------------------------------------------- Shuffle-exchange with MoE
+def _case_train_se(rank, world, ep, stage, steps, method, slice_count, clip=0.0):
+    import shuffle_exchange_amd as sxe
+    ref, cfg = _mixtral(1)
+    model, _ = _mixtral(ep, seed=11)
+    _load_from_reference(model, ref, ep, 1, False)
+    eng, _, _, _ = sxe.initialize(model=model, config=_ds(1, stage, clip), method=method, slice_count=slice_count)
+    opt = eng.optimizer
+    info = {"se": bool(getattr(opt, "shuffle_exchange_enabled", False)),
+            "moe_units": sum(1 for us in opt.units for u in us if u.moe),
+            "moe_partition": max((u.topo.S for us in opt.units for u in us if u.moe), default=0),
+            "dense_partition": max((u.topo.S for us in opt.units for u in us if not u.moe), default=0)}
+    batches = _batches(world, steps, cfg.vocab_size)
+    losses = _run(eng, _local(batches))
+    norm = eng.get_global_grad_norm()
+    return {"losses": losses, "sd": _full_state(eng, model, 1, False), "info": info,
+            "norm": float(norm) if norm is not None else None}
+
+
+@pytest.mark.parametrize("method,stage", [("RR", 2), ("RR", 1), ("H-RR", 2)])
+def test_shuffle_exchange_with_moe_equals_dp_sgd(method, stage):
+    """Shuffle-exchange on an expert-parallel model (reference stage_1_and_2.py:810-821): W=4, EP=2,
+    slices of 2. Dense groups are partitioned inside a slice and averaged across slices; expert groups
+    keep their expert-DP partitioning (which spans the slices) and the global gradient. With SGD the
+    run equals single-process DP-SGD on the global batch."""
+    world, ep, steps = 4, 2, 2
+    res = run_dist(_case_train_se, world, ep, stage, steps, method, 2)
+    ref_losses, ref_sd, _ = _reference(world, steps, 0.0)
+    for r in res:
+        assert r["info"]["se"] and r["info"]["moe_units"] > 0
+        assert r["info"]["dense_partition"] == 2 and r["info"]["moe_partition"] == world // ep
+    mean = [sum(r["losses"][t] for r in res) / len(res) for t in range(steps)]
+    for a, b in zip(mean, ref_losses):
+        assert a == pytest.approx(b, rel=1e-5, abs=1e-6)
+    for r in res:
+        for k, v in ref_sd.items():
+            d = (r["sd"][k] - v).abs().max().item()
+            assert d <= 2e-5 * max(1.0, v.abs().max().item()), f"{k}: {d}"
+
+
+def test_shuffle_exchange_with_moe_clip_norm():
+    """With clipping the dense part of the norm is the slice's, the expert part the world's: every
+    rank of a slice agrees, and the run is finite."""
+    res = run_dist(_case_train_se, 4, 2, 2, 2, "RR", 2, 1.0)
+    n = [r["norm"] for r in res]
+    assert n[0] == pytest.approx(n[1], rel=1e-6) and n[2] == pytest.approx(n[3], rel=1e-6)
+    assert all(x == x and x > 0 for x in n)
