@@ -6,10 +6,12 @@ Parity: reference inference/engine.py -- ``InferenceEngine`` :40 (``_create_mode
 ``_generate``), config inference/config.py ``DeepSpeedInferenceConfig``.
 The framework's own models always run the gfx950 kernels. ``replace_with_kernel_inject`` (default
 False, as in the reference) swaps Hugging Face layers that have an injection policy for fused gfx950
-layers (module_inject/replace_module.py); it is skipped -- with a log line -- under AutoTP
-(tp_size > 1) and post-init weight quantization, whose sharded / quantized weights the fused
-layers cannot take. ``generate`` uses the ragged KV-cached engine whenever the architecture has a
-v2 implementation, independent of injection.
+layers (module_inject/replace_module.py); under ``tp_size > 1`` the fused layers are sliced per rank
+(heads of the packed QKV, MLP columns; row-parallel outputs all-reduce), and with post-init weight
+quantization their GEMM weights are stored int8 / int4. ``checkpoint`` takes a file, a JSON
+descriptor or an ``mp_rank_*`` directory, merged / split to the running TP degree
+(runtime/state_dict_factory.py) and loaded strictly. ``generate`` uses the ragged KV-cached engine
+whenever the architecture has a v2 implementation (TP 1), independent of injection.
 """
 from dataclasses import dataclass, field
 from typing import Optional
@@ -36,6 +38,7 @@ class InferenceConfig:
     kv_block_size: int = 64
     kv_cache_fraction: float = 0.5
     weight_quantization: Optional[dict] = None  # {"post_init_quant": {name-key: {num_bits, group_size, ...}}}
+    load_strict: bool = True  # checkpoint keys must match the model exactly (missing / unexpected raise)
 
     def __post_init__(self):
         if isinstance(self.dtype, str):
@@ -88,37 +91,60 @@ class InferenceEngine(torch.nn.Module):
         self._config = config
         self.module = model
         dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+        tp_group = None
         if config.tp_size > 1:
             dist.init_distributed()
-            from ..module_inject.auto_tp import tp_model_init
             from ..parallel import groups
             groups.initialize(tensor_parallel_size=config.tp_size)
-            tp_model_init(model, config.tp_size, tp_group=groups.get_tensor_model_parallel_group())
+            tp_group = groups.get_tensor_model_parallel_group()
         if config.checkpoint:
-            sd = torch.load(config.checkpoint, map_location="cpu", weights_only=True)
-            model.load_state_dict(sd.get("module", sd), strict=False)
-        model.to(device=dev, dtype=config.dtype).eval()
-        if config.weight_quantization:
-            from .quantization import _init_group_wise_weight_quantization
-            _init_group_wise_weight_quantization(model, {"weight_quantization": config.weight_quantization})
+            # one file, a JSON descriptor or an mp_rank_* checkpoint directory, merged to the whole model
+            # (runtime/state_dict_factory.py) BEFORE any sharding: the TP split below cuts it to this
+            # job's degree whatever degree it was saved at; strict unless load_strict=False
+            from ..runtime.state_dict_factory import load_state_dict_source
+            load_state_dict_source(model, config.checkpoint, strict=config.load_strict)
         self.injected_layers = 0
         self.injection_skipped = None
+        self.tp_sharded_layers = 0
+        quant = (config.weight_quantization or {}).get("post_init_quant") if config.weight_quantization else None
         if config.replace_with_kernel_inject:
-            if config.tp_size > 1 or config.weight_quantization:
-                self.injection_skipped = "tp_size > 1" if config.tp_size > 1 else "weight_quantization"
-                log_dist(f"kernel injection skipped ({self.injection_skipped}): fused layers need whole, dense "
-                         f"weights", ranks=[0])
-            else:
-                # Hugging Face layers with an injection policy -> fused gfx950 layers (replace_module.py).
-                # The fused layers re-pack their weights, so the KV-cached ragged decoder (built on the
-                # first generate) reads the HF tensors as they were before injection.
-                self._ragged_src = _HFWeights.of(model)
-                from ..module_inject.replace_module import replace_transformer_layer
-                from ..module_inject.diffusers import generic_injection
-                self.injected_layers = replace_transformer_layer(model)
-                # diffusers-style attention (UNet / VAE / transformer blocks; reference
-                # generic_injection): fused packed-projection attention modules
-                self.injected_layers += generic_injection(model)
+            model.to(device=dev, dtype=config.dtype).eval()
+            # Hugging Face layers with an injection policy -> fused gfx950 layers (replace_module.py).
+            # The fused layers re-pack their weights, so the KV-cached ragged decoder (built on the
+            # first generate) reads the HF tensors as they were before injection.
+            self._ragged_src = _HFWeights.of(model) if config.tp_size == 1 and not quant else None
+            from ..module_inject.replace_module import (replace_transformer_layer, shard_fused_layers,
+                                                        quantize_fused_layer, _Fused)
+            from ..module_inject.diffusers import generic_injection
+            self.injected_layers = replace_transformer_layer(model)
+            # diffusers-style attention (UNet / VAE / transformer blocks; reference
+            # generic_injection): fused packed-projection attention modules
+            self.injected_layers += generic_injection(model)
+            if config.tp_size > 1:
+                # reference replace_module.py:207-231: the injected layers' q|k|v heads and MLP columns
+                # are sliced per rank, attention-out / MLP-out all-reduce over the TP group
+                self.tp_sharded_layers = shard_fused_layers(model, dist.get_rank(tp_group), config.tp_size, tp_group)
+                if self.tp_sharded_layers == 0:  # nothing injectable: AutoTP shards the model's linears
+                    from ..module_inject.auto_tp import tp_model_init
+                    tp_model_init(model, config.tp_size, tp_group=tp_group)
+            if quant:
+                for name, m in model.named_modules():
+                    if isinstance(m, _Fused):
+                        names = [name] + [f"{name}.{n}" for n, _ in m.orig.named_modules()] if m.orig is not None \
+                            else [name]
+                        key = next((k for k in quant if any(k in n for n in names)), None)
+                        if key is not None:
+                            quantize_fused_layer(m, quant[key])
+                from .quantization import _init_group_wise_weight_quantization
+                _init_group_wise_weight_quantization(model, {"weight_quantization": config.weight_quantization})
+        else:
+            if config.tp_size > 1:
+                from ..module_inject.auto_tp import tp_model_init
+                tp_model_init(model, config.tp_size, tp_group=tp_group)
+            model.to(device=dev, dtype=config.dtype).eval()
+            if config.weight_quantization:
+                from .quantization import _init_group_wise_weight_quantization
+                _init_group_wise_weight_quantization(model, {"weight_quantization": config.weight_quantization})
         self.device = dev
         self._graphs = {}
         self._ragged = None
@@ -166,7 +192,10 @@ class InferenceEngine(torch.nn.Module):
                 state_manager=StateManagerConfig(memory_config=MemoryConfig(fraction=self._config.kv_cache_fraction)))
             if self.device.type != "cuda":
                 cfg.num_kv_blocks = 1024
-            self._ragged = build_engine(self._ragged_src or self.module, cfg)
+            try:
+                self._ragged = build_engine(self._ragged_src or self.module, cfg)
+            except (KeyError, ValueError) as e:  # an architecture the ragged decoder does not describe
+                raise NotImplementedError(f"no ragged KV-cache implementation: {e}") from e
             self._ragged_src = None  # the ragged decoder holds its own packed copy now
         return self._ragged
 
@@ -191,6 +220,7 @@ class InferenceEngine(torch.nn.Module):
                 gen = []
                 for _ in range(max_new):
                     logits = self.module(ids)
+                    logits = getattr(logits, "logits", logits)  # Hugging Face ModelOutput
                     logits = logits[0] if isinstance(logits, tuple) else logits
                     nxt = int(logits[0, -1].argmax())
                     gen.append(nxt)

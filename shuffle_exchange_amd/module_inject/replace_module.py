@@ -71,19 +71,52 @@ class _Fused(nn.Module):
         """(orig parameter, view of a fused tensor) pairs; see the module docstring."""
         return []
 
-    def _link(self):
-        if self.__dict__.get("orig") is None:
-            return
-        for param, view in self._links():
-            param.data = view
-
     def _apply(self, fn, *args, **kwargs):
         out = super()._apply(fn, *args, **kwargs)
+        for q in self.__dict__.get("_qweights", {}).values():  # int8 / int4 weights (quantize_fused_layer)
+            q.to(fn(torch.empty(0, device=q.q.device)).device)
         self._link()
         return out
 
     def _delegate(self, *args, **kwargs):
+        if self.__dict__.get("_unlinked"):
+            raise NotImplementedError(f"{type(self).__name__}: this call needs the original Hugging Face layer, which "
+                                      f"was released when the fused layer was tensor-parallel sharded or quantized")
         return self.orig(*args, **kwargs)
+
+    # ---------------------------------------------------------------- tensor parallelism
+    _tp = None  # (rank, size, group) once shard_fused_layer ran
+
+    def _row(self, x, w, b=None):
+        """Row-parallel projection: the rank's partial product, summed over the TP group (the
+        bias is held by TP rank 0 only, so the sum adds it once)."""
+        y = linear(x, w, b)
+        if self._tp is not None:
+            from .. import comm as dist
+            dist.inference_all_reduce(y, group=self._tp[2])
+        return y
+
+    def _alibi_heads(self, alibi, B):
+        """This rank's heads of an ALiBi bias built for every head ([B * heads, 1, kv])."""
+        if self._tp is None:
+            return alibi.view(B, self.nh, 1, -1).float()
+        r, n, _ = self._tp
+        return alibi.view(B, self.nh * n, 1, -1)[:, r * self.nh:(r + 1) * self.nh].float()
+
+    def _unlink_orig(self):
+        """Free the original layer's parameters (their views no longer match the sharded / quantized
+        fused tensors) and stop re-linking them."""
+        orig = self.__dict__.get("orig")
+        if orig is not None:
+            for p in orig.parameters():
+                p.data = p.data.new_empty(0)
+        self.__dict__["_unlinked"] = True
+
+    def _link(self):
+        if self.__dict__.get("orig") is None or self.__dict__.get("_unlinked"):
+            return
+        for param, view in self._links():
+            param.data = view
 
 
 class FusedEncoderLayer(_Fused):
@@ -126,9 +159,9 @@ class FusedEncoderLayer(_Fused):
         B, S, H = x.shape
         qkv = linear(x, self.w_qkv, self.b_qkv).view(B, S, 3, self.nh, self.hd)
         o = _attend(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], attention_mask, False, 1.0 / math.sqrt(self.hd))
-        a = linear(o.reshape(B, S, H), self.w_o, self.b_o)
+        a = self._row(o.reshape(B, S, -1), self.w_o, self.b_o)
         h, _ = layer_norm(a, self.ln1_w, self.ln1_b, self.eps1, residual=x)
-        m = linear(bias_act(linear(h, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
+        m = self._row(bias_act(linear(h, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
         y, _ = layer_norm(m, self.ln2_w, self.ln2_b, self.eps2, residual=h)
         return y
 
@@ -179,9 +212,9 @@ class FusedGPT2Block(_Fused):
             kt, vt = past_key_values.update(k.transpose(1, 2), v.transpose(1, 2), self.layer_idx)
             k, v = kt.transpose(1, 2), vt.transpose(1, 2)
         o = _attend(q, k, v, attention_mask, attention_mask is None, self.scale)
-        a = linear(o.reshape(B, S, H), self.w_o, self.b_o)
+        a = self._row(o.reshape(B, S, -1), self.w_o, self.b_o)
         h2, h = layer_norm(a, self.ln2_w, self.ln2_b, self.eps2, residual=x)
-        m = linear(bias_act(linear(h2, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
+        m = self._row(bias_act(linear(h2, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
         return h + m
 
 
@@ -242,7 +275,7 @@ class FusedGPTNeoXLayer(_Fused):
             self._link()
 
     def _mlp(self, y):
-        return linear(bias_act(linear(y, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
+        return self._row(bias_act(linear(y, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
 
     def forward(self, hidden_states, attention_mask=None, position_ids=None, use_cache=False, layer_past=None,
                 position_embeddings=None, **kwargs):
@@ -260,7 +293,7 @@ class FusedGPTNeoXLayer(_Fused):
             kt, vt = layer_past.update(k.transpose(1, 2), v.transpose(1, 2), self.layer_idx)
             k, v = kt.transpose(1, 2), vt.transpose(1, 2)
         o = _attend(q, k, v, attention_mask, attention_mask is None, self.scale)
-        a = linear(o.reshape(B, S, H), self.w_o, self.b_o)
+        a = self._row(o.reshape(B, S, -1), self.w_o, self.b_o)
         if self.parallel:
             return self._mlp(layer_norm(x, self.ln2_w, self.ln2_b, self.eps2)) + a + x
         y2, h = layer_norm(a, self.ln2_w, self.ln2_b, self.eps2, residual=x)
@@ -344,9 +377,9 @@ class FusedLlamaLayer(_Fused):
             kt, vt = past_key_values.update(k.transpose(1, 2), v.transpose(1, 2), self.layer_idx)
             k, v = kt.transpose(1, 2), vt.transpose(1, 2)
         o = _attend_gqa(q, k, v, attention_mask, attention_mask is None, self.scale)
-        a = linear(o.reshape(B, S, self.nq * self.hd), self.w_o)
+        a = self._row(o.reshape(B, S, self.nq * self.hd), self.w_o)
         y2, h = rms_norm(a, self.ln2_w, self.eps2, residual=x)
-        return h + linear(swiglu(linear(y2, self.w_gu)), self.w_down)
+        return h + self._row(swiglu(linear(y2, self.w_gu)), self.w_down)
 
 
 class FusedOPTLayer(_Fused):
@@ -397,9 +430,9 @@ class FusedOPTLayer(_Fused):
             kt, vt = past_key_values.update(k.transpose(1, 2), v.transpose(1, 2), self.layer_idx)
             k, v = kt.transpose(1, 2), vt.transpose(1, 2)
         o = _attend(q, k, v, attention_mask, attention_mask is None, 1.0)
-        a = linear(o.reshape(B, S, H), self.w_o, self.b_o)
+        a = self._row(o.reshape(B, S, -1), self.w_o, self.b_o)
         y2, h = layer_norm(a, self.ln2_w, self.ln2_b, self.eps2, residual=x)
-        return h + linear(bias_act(linear(y2, self.w_fc1), self.b_fc1, _act_name(self.act)), self.w_fc2, self.b_fc2)
+        return h + self._row(bias_act(linear(y2, self.w_fc1), self.b_fc1, _act_name(self.act)), self.w_fc2, self.b_fc2)
 
 
 class FusedGPTJBlock(_Fused):
@@ -455,8 +488,8 @@ class FusedGPTJBlock(_Fused):
             k, v = kt.transpose(1, 2), vt.transpose(1, 2)
         o = _attend(q.float(), k.float(), v.float(), attention_mask, attention_mask is None,
                     1.0 / math.sqrt(self.hd)).to(x.dtype)  # GPT-J attends in fp32
-        a = linear(o.reshape(B, S, H), self.w_o)
-        m = linear(bias_act(linear(y, self.w_in), self.b_in, _act_name(self.act)), self.w_out, self.b_out)
+        a = self._row(o.reshape(B, S, -1), self.w_o)
+        m = self._row(bias_act(linear(y, self.w_in), self.b_in, _act_name(self.act)), self.w_out, self.b_out)
         return a + m + x, None
 
 
@@ -498,9 +531,9 @@ class FusedDistilBertBlock(_Fused):
         B, S, H = x.shape
         qkv = linear(x, self.w_qkv, self.b_qkv).view(B, S, 3, self.nh, self.hd)
         o = _attend(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], attention_mask, False, 1.0 / math.sqrt(self.hd))
-        a = linear(o.reshape(B, S, H), self.w_o, self.b_o)
+        a = self._row(o.reshape(B, S, -1), self.w_o, self.b_o)
         h, _ = layer_norm(a, self.ln1_w, self.ln1_b, self.eps1, residual=x)
-        f = linear(bias_act(linear(h, self.w1), self.b1, self.act), self.w2, self.b2)
+        f = self._row(bias_act(linear(h, self.w1), self.b1, self.act), self.w2, self.b2)
         y, _ = layer_norm(f, self.ln2_w, self.ln2_b, self.eps2, residual=h)
         return y
 
@@ -562,13 +595,13 @@ class FusedBloomBlock(_Fused):
         if layer_past is not None:
             k, v = layer_past.update(k, v, self.layer_idx)
         scores = torch.matmul(q, k.transpose(-1, -2)).float()
-        ab = alibi.view(B, self.nh, 1, -1).float()  # HF builds [B*nh, 1, kv]
+        ab = self._alibi_heads(alibi, B)  # HF builds [B*nh, 1, kv]
         o = _probs_context(scores, v, attention_mask, ab, attention_mask is None, 0, self.inv_norm)
         res = y if self.post_ln_residual else x
-        a = linear(o.transpose(1, 2).reshape(B, S, H), self.w_o, self.b_o)
+        a = self._row(o.transpose(1, 2).reshape(B, S, -1), self.w_o, self.b_o)
         h2, h = layer_norm(a, self.ln2_w, self.ln2_b, self.eps2, residual=res)
         res2 = h2 if self.post_ln_residual else h
-        m = linear(bias_act(linear(h2, self.w_fc), self.b_fc, "gelu"), self.w_out, self.b_out)
+        m = self._row(bias_act(linear(h2, self.w_fc), self.b_fc, "gelu"), self.w_out, self.b_out)
         return res2 + m, None
 
 
@@ -617,9 +650,9 @@ class FusedGPTNeoBlock(_Fused):
             k, v = layer_past.update(k, v, self.layer_idx)
         scores = torch.matmul(q.float(), k.float().transpose(-1, -2))
         o = _probs_context(scores, v, attention_mask, None, True, self.window, 1.0)
-        a = linear(o.transpose(1, 2).reshape(B, S, H), self.w_o, self.b_o)
+        a = self._row(o.transpose(1, 2).reshape(B, S, -1), self.w_o, self.b_o)
         h2, h = layer_norm(a, self.ln2_w, self.ln2_b, self.eps2, residual=x)
-        m = linear(bias_act(linear(h2, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
+        m = self._row(bias_act(linear(h2, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
         return h + m, None
 
 
@@ -665,9 +698,9 @@ class FusedCLIPEncoderLayer(_Fused):
         qkv = linear(y, self.w_qkv, self.b_qkv).view(B, S, 3, self.nh, self.hd)
         causal = bool(kwargs.get("is_causal", False)) and attention_mask is None
         o = _attend(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], attention_mask, causal, self.scale)
-        a = linear(o.reshape(B, S, H), self.w_o, self.b_o)
+        a = self._row(o.reshape(B, S, -1), self.w_o, self.b_o)
         h2, h = layer_norm(a, self.ln2_w, self.ln2_b, self.eps2, residual=x)
-        m = linear(bias_act(linear(h2, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
+        m = self._row(bias_act(linear(h2, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
         return h + m
 
 
@@ -744,10 +777,10 @@ class FusedMegatronLayer(_Fused):
         ln1 = layer_norm(x, self.ln1_w, self.ln1_b, self.eps1)
         qkv = linear(ln1, self.w_qkv, self.b_qkv).view(B, S, 3, self.nh, self.hd)
         o = _attend(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], None, True, 1.0 / math.sqrt(self.hd))
-        a = linear(o.reshape(B, S, self.nh * self.hd), self.w_o, self.b_o)
+        a = self._row(o.reshape(B, S, self.nh * self.hd), self.w_o, self.b_o)
         ln2, h = layer_norm(a, self.ln2_w, self.ln2_b, self.eps2, residual=ln1 if self.post_ln_residual else x)
         if self.dense_mlp:
-            m = linear(bias_act(linear(ln2, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
+            m = self._row(bias_act(linear(ln2, self.w_fc), self.b_fc, self.act), self.w_out, self.b_out)
         else:
             m = self.mlp(ln2)
             m = m[0] if isinstance(m, tuple) else m
@@ -832,9 +865,9 @@ class FusedInternLMLayer(_Fused):
             present = (k.transpose(1, 2), v.transpose(1, 2))
         causal_only = _is_causal_additive(attention_mask, S, k.shape[1])
         o = _attend(q, k, v, None if causal_only else attention_mask, causal_only, 1.0 / math.sqrt(self.hd))
-        a = linear(o.reshape(B, S, H), self.w_o, self.b_o)
+        a = self._row(o.reshape(B, S, -1), self.w_o, self.b_o)
         y2, h = rms_norm(a, self.ln2_w, self.eps2, residual=x)
-        out = (h + linear(swiglu(linear(y2, self.w_gu)), self.w_down),)
+        out = (h + self._row(swiglu(linear(y2, self.w_gu)), self.w_down),)
         return out + ((present,) if use_cache else ())
 
 
@@ -881,4 +914,158 @@ def replace_transformer_layer(model, config=None):
             if ctor is not None:
                 setattr(parent, name, ctor(child, config))
                 n += 1
+    return n
+
+
+# ------------------------------------------------------------------------------------------------
+# Tensor parallelism of injected layers (reference replace_module.py:207-231: the containers' qkv /
+# mlp tensors are sliced per rank by ReplaceWithTensorSlicing and the attention-out / MLP-out
+# GEMMs all-reduce). Per fused class: the head counts divided by the TP degree, the packed QKV
+# layout ("3": [q|k|v] x heads x hd rows, "h3": Bloom's [head][q|k|v][hd], "gqa": [nq | nkv | nkv]
+# heads), the column-parallel (output-row) projections, the packed gate|up projections and the
+# row-parallel (input-column) projections whose products ``_row`` sums over the TP group.
+_ENC = dict(heads=("nh",), qkv=("w_qkv", "b_qkv", "3"), col=[("w_fc", "b_fc")], gu=[],
+            row=[("w_o", "b_o"), ("w_out", "b_out")])
+TP_SPECS = {
+    FusedEncoderLayer: _ENC, FusedGPT2Block: _ENC, FusedGPTNeoXLayer: _ENC, FusedCLIPEncoderLayer: _ENC,
+    FusedMegatronLayer: _ENC,
+    FusedLlamaLayer: dict(heads=("nq", "nkv"), qkv=("w_qkv", "b_qkv", "gqa"), col=[], gu=["w_gu"],
+                          row=[("w_o", None), ("w_down", None)]),
+    FusedInternLMLayer: dict(heads=("nh",), qkv=("w_qkv", "b_qkv", "3"), col=[], gu=["w_gu"],
+                             row=[("w_o", "b_o"), ("w_down", None)]),
+    FusedOPTLayer: dict(heads=("nh",), qkv=("w_qkv", "b_qkv", "3"), col=[("w_fc1", "b_fc1")], gu=[],
+                        row=[("w_o", "b_o"), ("w_fc2", "b_fc2")]),
+    FusedGPTJBlock: dict(heads=("nh",), qkv=("w_qkv", None, "3"), col=[("w_in", "b_in")], gu=[],
+                         row=[("w_o", None), ("w_out", "b_out")]),
+    FusedDistilBertBlock: dict(heads=("nh",), qkv=("w_qkv", "b_qkv", "3"), col=[("w1", "b1")], gu=[],
+                               row=[("w_o", "b_o"), ("w2", "b2")]),
+    FusedBloomBlock: dict(heads=("nh",), qkv=("w_qkv", "b_qkv", "h3"), col=[("w_fc", "b_fc")], gu=[],
+                          row=[("w_o", "b_o"), ("w_out", "b_out")]),
+    FusedGPTNeoBlock: dict(heads=("nh",), qkv=("w_qkv", None, "3"), col=[("w_fc", "b_fc")], gu=[],
+                           row=[("w_o", "b_o"), ("w_out", "b_out")]),
+}
+
+
+def _rows(t, r, n):
+    k = t.shape[0] // n
+    return t[r * k:(r + 1) * k]
+
+
+def _cut_qkv(t, kind, heads, hd, r, n):
+    tail = tuple(t.shape[1:])
+    if kind == "3":
+        nh = heads[0]
+        return t.reshape(3, nh, hd, *tail)[:, r * nh // n:(r + 1) * nh // n].reshape(-1, *tail)
+    if kind == "h3":
+        nh = heads[0]
+        return t.reshape(nh, 3 * hd, *tail)[r * nh // n:(r + 1) * nh // n].reshape(-1, *tail)
+    nq, nkv = heads
+    q = t[:nq * hd].reshape(nq, hd, *tail)[r * nq // n:(r + 1) * nq // n]
+    k = t[nq * hd:(nq + nkv) * hd].reshape(nkv, hd, *tail)[r * nkv // n:(r + 1) * nkv // n]
+    v = t[(nq + nkv) * hd:].reshape(nkv, hd, *tail)[r * nkv // n:(r + 1) * nkv // n]
+    return torch.cat([q.reshape(-1, *tail), k.reshape(-1, *tail), v.reshape(-1, *tail)])
+
+
+def shard_fused_layer(layer, rank, size, group):
+    """Slice one injected layer to TP rank ``rank`` of ``size`` (in place)."""
+    spec = TP_SPECS.get(type(layer))
+    if spec is None:
+        raise NotImplementedError(f"no tensor-parallel layout for {type(layer).__name__}")
+    if isinstance(layer, FusedMegatronLayer) and not layer.dense_mlp:
+        raise NotImplementedError("Megatron MoE layers under tensor parallelism: shard the experts with expert "
+                                  "parallelism instead")
+    heads = [int(getattr(layer, h)) for h in spec["heads"]]
+    if any(h % size for h in heads):
+        raise ValueError(f"{type(layer).__name__}: {dict(zip(spec['heads'], heads))} heads are not divisible by "
+                         f"tp_size={size}")
+
+    def put(name, t):
+        setattr(layer, name, nn.Parameter(t.contiguous().clone(), requires_grad=False))
+
+    wq, bq, kind = spec["qkv"]
+    put(wq, _cut_qkv(getattr(layer, wq), kind, heads, layer.hd, rank, size))
+    if bq is not None and getattr(layer, bq, None) is not None:
+        put(bq, _cut_qkv(getattr(layer, bq), kind, heads, layer.hd, rank, size))
+    for w, b in spec["col"]:
+        put(w, _rows(getattr(layer, w), rank, size))
+        if b is not None and getattr(layer, b, None) is not None:
+            put(b, _rows(getattr(layer, b), rank, size))
+    for w in spec["gu"]:
+        t = getattr(layer, w)
+        half = t.shape[0] // 2
+        put(w, torch.cat([_rows(t[:half], rank, size), _rows(t[half:], rank, size)]))
+    for w, b in spec["row"]:
+        t = getattr(layer, w)
+        k = t.shape[1] // size
+        put(w, t[:, rank * k:(rank + 1) * k])
+        if b is not None and getattr(layer, b, None) is not None and rank != 0:
+            put(b, torch.zeros_like(getattr(layer, b)))  # added once: by TP rank 0
+    for h, v in zip(spec["heads"], heads):
+        setattr(layer, h, v // size)
+    layer._unlink_orig()
+    layer._tp = (rank, size, group)
+    return layer
+
+
+def shard_fused_layers(model, rank, size, group):
+    """Slice every injected layer of ``model`` for TP rank ``rank``; the rest of the model (embeddings,
+    final norm, LM head) stays replicated. Returns the number of sharded layers."""
+    n = 0
+    for m in model.modules():
+        if isinstance(m, _Fused):
+            shard_fused_layer(m, rank, size, group)
+            n += 1
+    return n
+
+
+class _FusedQWeight:
+    """A quantized GEMM weight of an injected layer: ``ops.linear`` calls ``.linear(x, bias)`` for
+    non-tensor weights; int8 / int4 groups are dequantized right before the GEMM
+    (inference/quantization.py)."""
+
+    def __init__(self, w, cfg):
+        from ..inference.quantization import _QuantizedWeight
+        self.qw = _QuantizedWeight(w.detach(), **cfg)
+        self.shape, self.dtype = tuple(w.shape), w.dtype
+
+    @property
+    def q(self):
+        return self.qw.q
+
+    def to(self, device):
+        self.qw.to(device)
+        return self
+
+    def linear(self, x, bias=None):
+        return F.linear(x, self.qw.dequantize().to(x.dtype), bias)
+
+    def nbytes(self):
+        return self.qw.nbytes()
+
+
+def quantize_fused_layer(layer, cfg):
+    """Store every GEMM weight of an injected layer group-quantized (``cfg``: num_bits, group_size,
+    group_dim, symmetric -- the weight_quantization.post_init_quant entry). Returns the count."""
+    spec = TP_SPECS.get(type(layer))
+    if spec is None:
+        return 0
+    names = [spec["qkv"][0]] + [w for w, _ in spec["col"]] + list(spec["gu"]) + [w for w, _ in spec["row"]]
+    c = dict(cfg)
+    c.setdefault("num_bits", 8)
+    c.setdefault("group_size", 64)
+    c.setdefault("group_dim", 1)
+    c.setdefault("symmetric", False)
+    qs = layer.__dict__.setdefault("_qweights", {})
+    n = 0
+    for name in names:
+        w = layer._parameters.get(name)
+        if w is None or w.shape[c["group_dim"]] % int(c["group_size"]):
+            continue
+        q = _FusedQWeight(w, c)
+        del layer._parameters[name]
+        layer.__dict__[name] = q
+        qs[name] = q.qw
+        n += 1
+    if n:
+        layer._unlink_orig()
     return n

@@ -166,17 +166,24 @@ def test_gpt2_left_padded_batched_generate():
     assert torch.equal(got, ref)
 
 
-def test_init_inference_skips_injection_under_quantization():
+def test_init_inference_injects_and_quantizes():
+    """Kernel injection with post-init weight quantization: the injected layers' GEMM weights are
+    stored int8 (a key matching one of the layer's HF submodules selects it), logits stay close."""
     import shuffle_exchange_amd as sxe
     model = _gpt2()
     ids = torch.randint(0, 300, (1, 8))
+    with torch.no_grad():
+        ref = model(ids, use_cache=False).logits
     eng = sxe.init_inference(model, dtype=torch.float32, replace_with_kernel_inject=True,
                              weight_quantization={"post_init_quant": {"c_fc": {"num_bits": 8, "group_size": 64}}})
-    assert eng.injected_layers == 0 and eng.injection_skipped == "weight_quantization"
-    assert not any(isinstance(m, rm._Fused) for m in model.modules())
+    assert eng.injected_layers == 2 and eng.injection_skipped is None
+    fused = [m for m in model.modules() if isinstance(m, rm._Fused)]
+    assert len(fused) == 2 and all(isinstance(m.w_qkv, rm._FusedQWeight) for m in fused)
+    assert all(isinstance(m.w_out, rm._FusedQWeight) for m in fused)
     with torch.no_grad():
         out = eng(ids.to(eng.device), use_cache=False).logits
-    assert torch.isfinite(out).all()
+    rel = ((out.cpu() - ref).norm() / ref.norm()).item()
+    assert rel < 2e-2, rel
 
 
 @pytest.mark.gpu
