@@ -25,3 +25,10 @@ def build_hf_engine(path_or_model, engine_config: RaggedInferenceEngineConfig = 
     model = load_hf_decoder(path_or_model, dtype=dtype, device=device, weight_quant=weight_quant, tp_group=tp_group,
                             tp_size=tp)
     return InferenceEngineV2(model, engine_config)
+
+
+def build_engine_from_ds_checkpoint(path, engine_config: RaggedInferenceEngineConfig = None, debug_level=None):
+    """Rebuild an engine from ``InferenceEngineV2.serialize`` output (reference engine_factory.py:32-66);
+    see serialization.py."""
+    from .serialization import build_engine_from_ds_checkpoint as _build
+    return _build(path, engine_config, debug_level)

@@ -222,10 +222,11 @@ class InferenceEngineV2:
         return s.cur_allocated_blocks * self._kv.block_size - s.seen_tokens
 
     def serialize(self, save_path):
-        import os
-        os.makedirs(save_path, exist_ok=True)
-        torch.save({k: v.detach().cpu() for k, v in self._model.model.state_dict().items()},
-                   os.path.join(save_path, "params.pt"))
+        """Write this rank's model (weights as served: TP shard, quantized form) plus the metadata
+        ``build_engine_from_ds_checkpoint`` rebuilds it from (reference engine_v2.py:251;
+        serialization.py). Every tensor-parallel rank calls it."""
+        from .serialization import serialize_engine
+        return serialize_engine(self, save_path)
 
     # ----------------------------------------------------------------------------- generation
     @torch.no_grad()
