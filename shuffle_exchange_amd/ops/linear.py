@@ -23,6 +23,10 @@ import torch.nn.functional as F
 # (tools/wgrad_layout_exp.py, tools/wgrad_tn_exp.py: -0.13 ms per 28672x4096 / 4096x14336 call,
 # -0.47 ms for the 128256x4096 LM head, at K = 8192 tokens). Smaller weights keep the fused path.
 TN_MIN_ELEMS = int(os.environ.get("SXE_WGRAD_TN_MIN_ELEMS", 32 * 2**20))
+# TN weight gradient into an fp32 accumulator: one fp32-output GEMM with beta = 1 (hipBLASLt "BSS"
+# kernels), or (SXE_WGRAD_TN_FP32OUT=0) the bf16-output TN GEMM -- the faster kernel family -- plus
+# an fp32 accumulate pass (what ops/mlp.py's weight_grad_tn does for the MLP weights)
+TN_FP32_OUT = os.environ.get("SXE_WGRAD_TN_FP32OUT", "1") == "1"
 
 # Decode-shaped products (<= 4 rows, no autograd) stream the weight through the MFMA skinny-GEMM
 # kernel (csrc/kernels/skinny_gemm.hip) instead of hipBLASLt's general tiles. Measured on MI355X
@@ -266,12 +270,12 @@ def write_weight_grad(w, gy2, x2):
         a, b = torch.ops.sxe.transpose16(gy2), torch.ops.sxe.transpose16(x2).t()
         if buf.dtype == gy2.dtype and not accumulate:
             torch.mm(a, b, out=buf)  # the reduce-scatter staging slot of a multi-rank unit
-        elif buf.dtype == torch.float32:
+        elif buf.dtype == torch.float32 and TN_FP32_OUT:
             # fp32-out TN GEMM accumulating in its epilogue (beta = 1): no bf16 dW round trip and no
             # separate fp32 add pass (28672x4096 at 8192 tokens: 1.62 vs 1.74 ms, wgrad_tn_fp32_exp)
             torch.ops.aten.addmm.dtype_out(buf, a, b, torch.float32, beta=1 if accumulate else 0, alpha=1, out=buf)
         else:
-            dw = torch.mm(a, b)
+            dw = torch.mm(a, b).view_as(buf)
             buf.add_(dw) if accumulate else buf.copy_(dw)
     elif buf.dtype == torch.float32 and gy2.dtype != torch.float32:
         if gy2.is_cuda:

@@ -6,11 +6,15 @@ and softmax.py:224 ``Softmax`` (scale, rpe, key-padding and attention masks in a
 Sparse tensors use the reference format: ``[B, nnz, block, block]``, the non-zero blocks of the
 layout ``[H, M, N]`` in ``layout.nonzero()`` (head, block-row, block-column) order.
 
-MI355X path: no Triton. Each product is ONE batched GEMM over the non-zero blocks (hipBLASLt's
-strided-batched bf16 MFMA GEMM): ``sdd`` gathers the block rows of A and block columns of B per
-non-zero and multiplies [nnz] (block x K) x (K x block) pairs; ``dsd`` / ``dds`` multiply each
-non-zero block by its dense panel and sum the partial products per output block row / column with
-one ``index_add``. Softmax works on the compact blocks only: per-row max and sum are segment
+MI355X path: no Triton. bf16 / fp16 GPU inputs run the HIP block-sparse kernels
+(csrc/kernels/bsmm.hip: MFMA 16x16x32 tiles that read the dense operands in place through their
+strides -- transposes and broadcast heads included -- and, for ``dsd`` / ``dds``, sum a block row's /
+column's products in registers over the layout's CSR / CSC lists); their backward runs the same
+three kernels with the reference's mode / transpose algebra (matmul.py:628 ``_sparse_matmul``).
+Other dtypes and devices take the batched-GEMM form: ``sdd`` gathers the block rows of A and block
+columns of B per non-zero and multiplies [nnz] (block x K) x (K x block) pairs; ``dsd`` / ``dds``
+multiply each non-zero block by its dense panel and sum the partial products per output block row /
+column with one ``index_add``. Softmax works on the compact blocks only: per-row max and sum are segment
 reductions over the blocks of one (head, block-row) group (``scatter_reduce`` / ``index_add``), so
 memory stays O(nnz block^2) -- the dense S x S score matrix is never formed. Gradients flow through
 the same ops (autograd). Block-sparse attention itself does not use these: it runs fused in the
@@ -50,7 +54,66 @@ class MatMul:
             self._idx[device] = tuple(t.to(device) for t in self._hij)
         return self._idx[device]
 
+    # ---------------------------------------------------------------- HIP kernels (bsmm.hip)
+    def _hip_ok(self, a, b):
+        from . import native
+        if not (a.is_cuda and b.is_cuda and a.dtype == b.dtype and a.dtype in (torch.bfloat16, torch.float16)
+                and self.block in (16, 32, 64, 128) and native.use_hip(a)):
+            return False
+        dense = b if self.mode == "dsd" else a
+        if self.mode == "sdd":  # the reduction dim is the backward's dense width
+            A = _pad4(a)
+            return (A.shape[-2] if self.trans_a else A.shape[-1]) % 16 == 0
+        d = _pad4(dense)
+        d = d.transpose(-1, -2) if (self.trans_b if self.mode == "dsd" else self.trans_a) else d
+        return (d.shape[-1] if self.mode == "dsd" else d.shape[-2]) % 16 == 0
+
+    def _lists(self, device, kind, trans):
+        """CSR (kind 'row', dsd) / CSC (kind 'col', dds) lists of the output blocks: ptr [H*R + 1],
+        ent [nnz, 2] = (non-zero index, reduction block) -- built once per device."""
+        key = (device, kind, bool(trans))
+        if key not in self._idx:
+            h, i, j = self._index(device)
+            H, M, N = self.spdims
+            if (kind == "row") != bool(trans):
+                out, red, R = i, j, M
+            else:
+                out, red, R = j, i, N
+            g = h * R + out
+            order = torch.argsort(g, stable=True)
+            cnt = torch.bincount(g, minlength=H * R)
+            ptr = torch.zeros(H * R + 1, dtype=torch.int32, device=device)
+            ptr[1:] = cnt.cumsum(0).to(torch.int32)
+            nzid = torch.arange(h.numel(), device=device)
+            ent = torch.stack([nzid[order], red[order]], 1).to(torch.int32).contiguous()
+            self._idx[key] = (ptr, ent, R)
+        return self._idx[key]
+
+    def _hij32(self, device):
+        key = (device, "hij")
+        if key not in self._idx:
+            h, i, j = self._index(device)
+            self._idx[key] = torch.stack([h, i, j], 1).to(torch.int32).contiguous()
+        return self._idx[key]
+
+    def _k_sdd(self, A, B):
+        return torch.ops.sxe.bsmm_sdd(A, B, self._hij32(A.device), self.block)
+
+    def _k_dsd(self, S, trans, D):
+        ptr, ent, R = self._lists(S.device, "row", trans)
+        return torch.ops.sxe.bsmm_dsd(_pad4(S).contiguous(), bool(trans), D, ptr, ent, self.spdims[0], R, self.block)
+
+    def _k_dds(self, D, S, trans):
+        ptr, ent, R = self._lists(S.device, "col", trans)
+        return torch.ops.sxe.bsmm_dds(D, _pad4(S).contiguous(), bool(trans), ptr, ent, self.spdims[0], R, self.block)
+
     def __call__(self, a, b):
+        if self._hip_ok(a, b):
+            nd = max(a.dim(), b.dim()) if self.mode == "sdd" else (b if self.mode == "dsd" else a).dim()
+            c = _BSMM.apply(self, a, b)
+            while c.dim() > nd and c.shape[0] == 1:
+                c = c.squeeze(0)
+            return c
         nd = max(a.dim(), b.dim())
         if self.mode != "sdd":
             nd = (b if self.mode == "dsd" else a).dim()
@@ -96,6 +159,68 @@ class MatMul:
         while c.dim() > nd and c.shape[0] == 1:
             c = c.squeeze(0)
         return c
+
+
+def _t(x):
+    return x.transpose(-1, -2)
+
+
+def _fit(g, like):
+    """Sum a gradient over the dims its (padded 4-D) input broadcast, then give it the input's shape."""
+    ref = _pad4(like)
+    for d in range(g.dim()):
+        if ref.shape[d] == 1 and g.shape[d] != 1:
+            g = g.sum(d, keepdim=True)
+    return g.reshape(like.shape).to(like.dtype)
+
+
+class _BSMM(torch.autograd.Function):
+    """The HIP block-sparse products with their backward (reference matmul.py ``_sparse_matmul``
+    backward: the gradient of each mode is two products of the other modes)."""
+
+    @staticmethod
+    def forward(ctx, mm, a, b):
+        ctx.mm = mm
+        ctx.save_for_backward(a, b)
+        A, B = _pad4(a), _pad4(b)
+        if mm.mode == "sdd":
+            return mm._k_sdd(_t(A) if mm.trans_a else A, _t(B) if mm.trans_b else B)
+        if mm.mode == "dsd":
+            return mm._k_dsd(A, mm.trans_a, _t(B) if mm.trans_b else B)
+        return mm._k_dds(_t(A) if mm.trans_a else A, B, mm.trans_b)
+
+    @staticmethod
+    def backward(ctx, g):
+        mm = ctx.mm
+        a, b = ctx.saved_tensors
+        A, B = _pad4(a), _pad4(b)
+        g = _pad4(g).contiguous()
+        da = db = None
+        if mm.mode == "sdd":  # C = A' B' (sparse)
+            Ap, Bp = (_t(A) if mm.trans_a else A), (_t(B) if mm.trans_b else B)
+            if ctx.needs_input_grad[1]:
+                dA = mm._k_dsd(g, False, _t(Bp))
+                da = _fit(_t(dA) if mm.trans_a else dA, a)
+            if ctx.needs_input_grad[2]:
+                dB = mm._k_dds(_t(Ap), g, False)
+                db = _fit(_t(dB) if mm.trans_b else dB, b)
+        elif mm.mode == "dsd":  # C = S' D'
+            Dp = _t(B) if mm.trans_b else B
+            if ctx.needs_input_grad[1]:
+                dS = mm._k_sdd(Dp, _t(g)) if mm.trans_a else mm._k_sdd(g, _t(Dp))
+                da = _fit(dS, a)
+            if ctx.needs_input_grad[2]:
+                dD = mm._k_dsd(A, not mm.trans_a, g)
+                db = _fit(_t(dD) if mm.trans_b else dD, b)
+        else:  # dds: C = D' S'
+            Dp = _t(A) if mm.trans_a else A
+            if ctx.needs_input_grad[1]:
+                dD = mm._k_dds(g, B, not mm.trans_b)
+                da = _fit(_t(dD) if mm.trans_a else dD, a)
+            if ctx.needs_input_grad[2]:
+                dS = mm._k_sdd(_t(g), Dp) if mm.trans_b else mm._k_sdd(_t(Dp), g)
+                db = _fit(dS, b)
+        return None, da, db
 
 
 class Softmax:

@@ -1,0 +1,80 @@
+"""HIP block-sparse MatMul kernels (csrc/kernels/bsmm.hip) vs the fp32 PyTorch batched-GEMM path of
+the same class on the same layout: sdd / dsd / dds, every transpose combination, block 16 / 32 / 64,
+broadcast heads, forward and backward (reference ops/sparse_attention/matmul.py:628 ``MatMul``)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    from shuffle_exchange_amd.ops import native
+    native.require_hip()
+
+
+def _layout(H, M, N, seed):
+    g = torch.Generator().manual_seed(seed)
+    lay = (torch.rand(H, M, N, generator=g) < 0.4).long()
+    lay[:, 0, 0] = 1
+    lay[:, M - 1, N - 1] = 1
+    return lay
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _shapes(mode, ta, tb, Bsz, H, M, N, blk, K, head_b):
+    hb = 1 if head_b else H
+    if mode == "sdd":
+        A = (Bsz, H, M * blk, K)
+        Bm = (Bsz, hb, K, N * blk)
+    elif mode == "dsd":
+        A = None
+        rows_dense = (M if ta else N) * blk  # the dense operand's rows = the sparse operand's columns
+        Bm = (Bsz, hb, rows_dense, K)
+    else:
+        cols_dense = (N if tb else M) * blk
+        A = (Bsz, hb, K, cols_dense)
+        Bm = None
+    if A is not None and ta and mode != "dsd":
+        A = A[:2] + (A[3], A[2])
+    if Bm is not None and tb and mode != "dds":
+        Bm = Bm[:2] + (Bm[3], Bm[2])
+    return A, Bm
+
+
+@pytest.mark.parametrize("blk", [16, 32, 64])
+@pytest.mark.parametrize("mode", ["sdd", "dsd", "dds"])
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
+def test_bsmm_matches_fp32(mode, ta, tb, blk):
+    from shuffle_exchange_amd.ops.sparse_ops import MatMul
+    torch.manual_seed(blk + 7 * ta + 3 * tb)
+    Bsz, H, M, N, K = 2, 2, 3, 4, 48
+    lay = _layout(H, M, N, blk)
+    nnz = int(lay.sum())
+    As, Bs = _shapes(mode, ta, tb, Bsz, H, M, N, blk, K, head_b=(mode == "sdd"))
+    dev = "cuda"
+    if mode == "dsd":
+        a = torch.randn(Bsz, nnz, blk, blk, device=dev)
+        b = torch.randn(*Bs, device=dev)
+    elif mode == "dds":
+        a = torch.randn(*As, device=dev)
+        b = torch.randn(Bsz, nnz, blk, blk, device=dev)
+    else:
+        a = torch.randn(*As, device=dev)
+        b = torch.randn(*Bs, device=dev)
+    mm = MatMul(lay, blk, mode, trans_a=ta, trans_b=tb)
+    a16, b16 = (t.bfloat16().requires_grad_() for t in (a, b))
+    a32, b32 = (t.float().requires_grad_() for t in (a, b))
+    assert mm._hip_ok(a16, b16)
+    c16 = mm(a16, b16)
+    c32 = mm(a32, b32)  # fp32: the batched-GEMM path
+    assert c16.shape == c32.shape
+    assert _rel(c16, c32) < 1e-2, _rel(c16, c32)
+    g = torch.randn_like(c32)
+    (c16.float() * g).sum().backward()
+    (c32 * g).sum().backward()
+    assert _rel(a16.grad, a32.grad) < 2e-2
+    assert _rel(b16.grad, b32.grad) < 2e-2
