@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round-6 measurement batch: headline A/B of the weight-gradient paths, decode kernel trace, GEMM table.
+set -o pipefail
+O=gpurun_out/r06
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 900 tools/ab_bench.sh $O/ab_wgrad 2 "" "SXE_WGRAD_TN_MIN_ELEMS=20000000 SXE_WGRAD_TN_FP32OUT=0" --steps 6 --warmup 2 || exit 1
+timeout -k 10 300 python tools/gemm_step_table.py > $O/gemm_step_table.md 2> $O/gemm_step_table.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/decode_prof -o run -- python tools/decode_bench.py --batches 1 --modes graphs --steps 64 > $O/decode_prof.log 2>&1 || exit 1
