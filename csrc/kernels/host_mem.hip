@@ -21,6 +21,47 @@ at::Tensor pinned_empty(int64_t numel, at::ScalarType dtype) {
       at::TensorOptions().dtype(dtype).device(at::kCPU));
 }
 
+// Host -> device copy by a kernel that reads the pinned buffer over the link itself (hipHostMalloc
+// memory is mapped into the GPU's address space), instead of a DMA on a copy engine: the ZeRO-Infinity
+// asynchronous tier moves each updated bit16 shard back while the gradient mirror's device -> host
+// copies of later units still occupy the copy engine, where a DMA would queue behind all of them.
+// A small grid (<= 128 workgroups) keeps the compute stream's kernels on the rest of the CUs; every
+// lane keeps 4 x 16-byte reads in flight to cover the link latency.
+__global__ void __launch_bounds__(256) host_read_kernel(const u16x8* __restrict__ src, u16x8* __restrict__ dst,
+                                                        int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const u16x8 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+void h2d_copy_(at::Tensor dst, at::Tensor src) {
+  SXE_CHECK(dst.is_cuda() && !src.is_cuda(), "h2d_copy_: device destination, host source");
+  SXE_CHECK(dst.is_contiguous() && src.is_contiguous() && dst.nbytes() == src.nbytes(), "h2d_copy_: same-size contiguous");
+  const int64_t bytes = (int64_t)src.nbytes();
+  SXE_CHECK(bytes % 16 == 0 && (reinterpret_cast<uintptr_t>(src.data_ptr()) & 15) == 0 &&
+                (reinterpret_cast<uintptr_t>(dst.data_ptr()) & 15) == 0, "h2d_copy_: 16-byte aligned sizes");
+  if (bytes == 0) return;
+  void* dsrc = nullptr;
+  SXE_HIP_CHECK(hipHostGetDevicePointer(&dsrc, src.data_ptr(), 0));  // fails unless src is pinned host memory
+  c10::DeviceGuard guard(dst.device());
+  const int64_t n16 = bytes / 16;
+  const int blocks = (int)std::min<int64_t>(128, (n16 + 1023) / 1024);
+  hipLaunchKernelGGL(host_read_kernel, dim3(blocks), dim3(256), 0, cur_stream(), reinterpret_cast<const u16x8*>(dsrc),
+                     reinterpret_cast<u16x8*>(dst.data_ptr()), n16);
+  SXE_LAUNCH_CHECK();
+}
+
 }  // namespace sxe
 
-TORCH_LIBRARY_FRAGMENT(sxe, m) { m.def("pinned_empty(int numel, ScalarType dtype) -> Tensor", &sxe::pinned_empty); }
+TORCH_LIBRARY_FRAGMENT(sxe, m) {
+  m.def("pinned_empty(int numel, ScalarType dtype) -> Tensor", &sxe::pinned_empty);
+  m.def("h2d_copy_(Tensor(a!) dst, Tensor src) -> ()");
+}
+TORCH_LIBRARY_IMPL(sxe, CUDA, m) { m.impl("h2d_copy_", &sxe::h2d_copy_); }

@@ -155,6 +155,13 @@ class HostOptimizerStep:
         # (profiles/r05/llama70b-infinity_async_{on,off}.log, timeline
         # llama70b-infinity_async_trace.jsonl).
         self.async_update = os.environ.get("SXE_OFFLOAD_ASYNC", "0") == "1" and self.device == "cpu"
+        # asynchronous tier, copy scheduling: SXE_OFFLOAD_ASYNC_WINDOW=W > 0 keeps only W units' gradient
+        # D2H copies queued ahead of the host update (the worker issues unit k + W's when unit k is done)
+        # instead of the whole mirror at step() -- an updated shard's H2D then queues behind at most W
+        # D2H pieces on the copy engine; SXE_OFFLOAD_H2D_KERNEL=1 moves the updated shards with a kernel
+        # that reads the pinned buffer over the link (host_mem.hip h2d_copy_), off the copy engines
+        self.async_window = int(os.environ.get("SXE_OFFLOAD_ASYNC_WINDOW", "0"))
+        self.h2d_kernel = os.environ.get("SXE_OFFLOAD_H2D_KERNEL", "0") == "1"
         self._worker = None
         self._ready = {}
         self._h2d_ev = {}
@@ -448,24 +455,34 @@ class HostOptimizerStep:
         t0 = _time.perf_counter()
         if cur is not None:
             self.d2h.wait_stream(cur)
+            self._grads_ready = torch.cuda.Event()  # the backward that wrote u.grad (windowed issue)
+            self._grads_ready.record(cur)
         d2h, o = [], 0
         for g, i, u, off in flat:
-            dst = self.ghost[o:o + u.chunk]
+            d2h.append([self.ghost[o:o + u.chunk], None])
             o += u.chunk
+        window = self.async_window if (self.async_window > 0 and cur is not None) else len(flat)
+
+        def issue(k):
+            dst, u = d2h[k][0], flat[k][2]
             if cur is None:
                 dst.copy_(u.grad)
-                d2h.append((dst, None))
-                continue
+                return
             with get_accelerator().stream(self.d2h):
                 dst.copy_(u.grad, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self.d2h)
-            d2h.append((dst, ev))
+            d2h[k][1] = ev
+        self._issued_all = threading.Event()
+        for k in range(min(window, len(flat))):
+            issue(k)
+        if window >= len(flat):
+            self._issued_all.set()
         # Invariant: nothing may write u.grad on the compute stream until these copies have read it.
         # The compute stream is NOT made to wait here (that would serialise the next forward behind the
-        # mirror); every writer of the accumulators calls wait_grad_mirror() first instead -- the
-        # backward via before_backward(), ZeRO-3's _zero_stale()/zero-fill via the same hook.
-        self._d2h_done = d2h[-1][1] if d2h else None
+        # mirror); every writer of the accumulators calls wait_grad_mirror() / before_backward() first
+        # -- which, with a windowed issue, also wait until the worker has issued every copy.
+        self._d2h_last = (d2h, len(flat) - 1) if flat else None
         for g in self.groups:
             st = opt.optimizer.state[opt.master[g]]
             if opt.kind in ("adam", "adagrad"):
@@ -490,7 +507,8 @@ class HostOptimizerStep:
                     n = getattr(self, "threads", None) or int(cops.num_threads())
                     cops.set_num_threads(max(1, int(n) - 1))
                 NS = len(self.gslots)
-                for k, ((g, i, u, off), (grad, ev)) in enumerate(zip(flat, d2h)):
+                for k, (g, i, u, off) in enumerate(flat):
+                    grad, ev = d2h[k]
                     ta = _time.perf_counter()
                     if ev is not None:
                         ev.synchronize()
@@ -508,11 +526,20 @@ class HostOptimizerStep:
                     tc = _time.perf_counter()
                     if u.shard_is_cuda():
                         with get_accelerator().stream(self.h2d):
-                            u.shard.copy_(lp, non_blocking=True)
+                            if self.h2d_kernel and (u.chunk * lp.element_size()) % 16 == 0:
+                                torch.ops.sxe.h2d_copy_(u.shard, lp)
+                            else:
+                                u.shard.copy_(lp, non_blocking=True)
                             hev = torch.cuda.Event()
                             hev.record(self.h2d)
                         self._lslot_ev[slot] = hev
                         self._h2d_ev[id(u)] = hev
+                    if k + window < len(flat):
+                        if k == 0 and cur is not None:
+                            self.d2h.wait_event(self._grads_ready)
+                        issue(k + window)
+                        if k + window == len(flat) - 1:
+                            self._issued_all.set()
                     if tr is not None:
                         tr["units"].append((u.name, u.chunk, ta - t0, tb - t0, tc - t0))
                     self._ready[id(u)].set()
@@ -520,6 +547,7 @@ class HostOptimizerStep:
                 self._error = e
                 for e2 in self._ready.values():
                     e2.set()
+                self._issued_all.set()
 
         self._worker = threading.Thread(target=work, name="sxe-host-adam", daemon=True)
         self._worker.start()
@@ -583,17 +611,32 @@ class HostOptimizerStep:
 
     def before_backward(self):
         """The backward rewrites the fp32 gradient accumulators: the D2H copies of the previous
-        asynchronous update must have read them."""
+        asynchronous update must have read them (all of them issued first, with a windowed issue)."""
+        ia = getattr(self, "_issued_all", None)
+        if ia is not None:
+            ia.wait()
+        self._raise_if_failed()
         if self.d2h is not None and torch.cuda.is_available():
             torch.cuda.current_stream().wait_stream(self.d2h)
+
+    def _raise_if_failed(self):
+        if getattr(self, "_error", None) is not None:
+            self.wait_all()
 
     def wait_grad_mirror(self):
         """Order the current stream after the last gradient-mirror D2H copy of the pending asynchronous
         update (a no-op once it has been waited for). Call before any eager write of ``u.grad``."""
-        ev = getattr(self, "_d2h_done", None)
+        last = getattr(self, "_d2h_last", None)
+        if last is None:
+            return
+        ia = getattr(self, "_issued_all", None)
+        if ia is not None:
+            ia.wait()
+        d2h, k = last
+        ev = d2h[k][1]
         if ev is not None and torch.cuda.is_available():
             torch.cuda.current_stream().wait_event(ev)
-            self._d2h_done = None
+        self._d2h_last = None
 
     def _log_async_trace(self, tr):
         self.trace.append(tr)

@@ -23,9 +23,9 @@ def _case(rank, world, stage, offload, nvme_dir=None):
     with sxe.zero.Init(dtype=torch.bfloat16):
         model = LlamaForCausalLM(cfg)
     zc = {"stage": stage, "stage3_param_persistence_threshold": 0}
-    if offload in ("cpu", "twin_flow"):
+    if offload in ("cpu", "twin_flow", "cpu_opt"):
         zc["offload_optimizer"] = {"device": "cpu", "pin_memory": True, "ratio": 0.5 if offload == "twin_flow" else 1.0}
-        if stage == 3:
+        if stage == 3 and offload != "cpu_opt":
             zc["offload_param"] = {"device": "cpu", "pin_memory": True}
     elif offload == "nvme":
         zc["offload_optimizer"] = {"device": "nvme", "nvme_path": nvme_dir}
@@ -71,3 +71,30 @@ def test_offload_piecewise_d2h_matches_hbm_adam(stage, monkeypatch):
         a, b = off[k].float(), v.float()
         rel = ((a - b).norm() / (b.norm() + 1e-12)).item()
         assert rel < 5e-3, (k, rel)
+
+
+@pytest.mark.parametrize("window,kernel", [("0", "0"), ("2", "0"), ("2", "1"), ("0", "1")])
+def test_offload_async_copy_schedules_match_sync(window, kernel, monkeypatch):
+    """The asynchronous host tier (SXE_OFFLOAD_ASYNC) with a windowed gradient-D2H issue
+    (SXE_OFFLOAD_ASYNC_WINDOW) and / or kernel-driven H2D of the updated shards
+    (SXE_OFFLOAD_H2D_KERNEL, host_mem.hip h2d_copy_) trains to bit-identical parameters as the
+    synchronous tier: same kernels, same order, only the copy scheduling differs."""
+    ref = run_dist(_case, 1, 3, "cpu_opt")[0]
+    monkeypatch.setenv("SXE_OFFLOAD_ASYNC", "1")
+    monkeypatch.setenv("SXE_OFFLOAD_ASYNC_WINDOW", window)
+    monkeypatch.setenv("SXE_OFFLOAD_H2D_KERNEL", kernel)
+    got = run_dist(_case, 1, 3, "cpu_opt")[0]
+    for k, v in ref.items():
+        assert torch.equal(got[k], v), k
+
+
+def test_h2d_copy_kernel():
+    from shuffle_exchange_amd.ops import native
+    from shuffle_exchange_amd.runtime.zero.offload import pinned_empty
+    native.require_hip()
+    src = pinned_empty(3 * 2**20 + 8, torch.bfloat16)
+    src.copy_(torch.randn(src.numel()).bfloat16())
+    dst = torch.empty(src.numel(), dtype=torch.bfloat16, device="cuda")
+    torch.ops.sxe.h2d_copy_(dst, src)
+    torch.cuda.synchronize()
+    assert torch.equal(dst.cpu(), src)
