@@ -268,11 +268,14 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
                 fg.units.append(u)
                 for p in plist:
                     self.param_unit[p] = u
-            if frozen:
-                u = self._make_unit(frozen, f"{name}/frozen", fg, frozen=True)
+            by_dt = {}
+            for p in frozen:  # one flat buffer per dtype (e.g. an fp8-coded LoRA base next to a bf16 bias)
+                by_dt.setdefault(p.dtype, []).append(p)
+            for dt, plist in by_dt.items():
+                u = self._make_unit(plist, f"{name}/frozen" + ("" if len(by_dt) == 1 else f"/{dt}"), fg, frozen=True)
                 fg.units.append(u)
                 self.frozen_units.append(u)
-                for p in frozen:
+                for p in plist:
                     self.frozen_unit[p] = u
             self.fgroups.append(fg)
         # external parameters: a module that uses a parameter owned by another unit (tied
@@ -373,7 +376,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         """Store a frozen unit's shard as int8 + fp32 group scales (half the bytes of bf16); the
         gather all-gathers the int8 shards and dequantizes into the unit buffer. Resident units
         (one rank, small units, host-resident shards) keep bit16."""
-        if u.persistent or u.frozen_q or self.S == 1 or u.swap is not None or u.shard.device != self.device:
+        if (u.persistent or u.frozen_q or self.S == 1 or u.swap is not None or u.shard.device != self.device
+                or u.dtype not in (torch.bfloat16, torch.float16, torch.float32)):
             return False
         self._quantize_shard(u)
         u.shard = None

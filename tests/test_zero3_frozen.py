@@ -43,3 +43,45 @@ def test_zero3_frozen_params_zero_init_w2(tmp_path, quant):
     for k in names:
         torch.testing.assert_close(r0["saved_frozen"][k], r0["after"][k])
     assert set(r0["frag_keys"]) == set(names) and r1["frag_keys"] == []
+
+
+def _case_lora(rank, world, tmpdir):
+    """OptimizedLinear LoRA layers (frozen bf16 base + trainable A / B) built under zero.Init and
+    trained with ZeRO-3: the base weights are gather-only units."""
+    import torch.nn as nn
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd.linear.optimized_linear import LoRAConfig, OptimizedLinear
+    torch.manual_seed(3)
+
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = OptimizedLinear(64, 128, lora_config=LoRAConfig(lora_r=8), dtype=torch.float32)
+            self.b = OptimizedLinear(128, 32, lora_config=LoRAConfig(lora_r=8), dtype=torch.float32)
+
+        def forward(self, x):
+            return self.b(torch.relu(self.a(x))).square().mean()
+
+    with sxe.zero.Init(dtype=torch.float32):
+        net = Net()
+    ds = {"train_micro_batch_size_per_gpu": 1, "zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 0},
+          "optimizer": {"type": "SGD", "params": {"lr": 0.1}}}
+    eng, _, _, _ = sxe.initialize(model=net, config=ds)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(world, 16, 64, generator=g)[rank]  # one batch, stepped on repeatedly
+    losses = []
+    for _ in range(3):
+        loss = eng(x)
+        eng.backward(loss)
+        eng.step()
+        losses.append(float(loss.detach()))
+    return {"losses": losses, "nf": len(eng.optimizer.frozen_units),
+            "shard": sum(u.shard.numel() for u in eng.optimizer.frozen_units)}
+
+
+def test_zero3_lora_optimized_linear_zero_init_w2(tmp_path):
+    res = run_dist(_case_lora, 2, str(tmp_path))
+    for r in res:
+        assert r["nf"] == 2 and all(l == l for l in r["losses"])
+        assert r["losses"][-1] < r["losses"][0]
+    assert res[0]["shard"] <= (64 * 128 + 128 * 32) // 2 + 2 * 128

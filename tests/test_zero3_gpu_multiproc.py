@@ -97,3 +97,51 @@ def test_zero_init_gpu_memory_two_ranks():
         assert r["held"] <= r["full"] / 2 + (4 << 20), r
         assert r["peak"] <= r["full"] / 2 + 2 * max(r["layer"], 8192 * 1024 * 2) + (16 << 20), r
         assert r["peak"] < 0.75 * r["full"], r
+
+
+def _case_frozen(rank, world, quant):
+    os.environ["LOCAL_RANK"] = "0"
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+    torch.cuda.set_device(0)
+    torch.manual_seed(0)
+    cfg = llama_config("llama-tiny", hidden_size=256, intermediate_size=512, num_attention_heads=2,
+                       num_key_value_heads=1, vocab_size=1024, num_hidden_layers=2)
+    with sxe.zero.Init(dtype=torch.bfloat16):
+        model = LlamaForCausalLM(cfg)
+    frozen = C._freeze_lora_style(model)
+    ds = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": 2, "bf16": {"enabled": True},
+          "zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 0,
+                                "zero_quantized_nontrainable_weights": quant},
+          "optimizer": {"type": "SGD", "params": {"lr": 0.05}}}
+    eng, _, _, _ = sxe.initialize(model=model, config=ds)
+    before = C.full_params(eng)
+    g = torch.Generator().manual_seed(7)
+    for _ in range(2):
+        for _ in range(2):
+            ids = torch.randint(0, cfg.vocab_size, (2 * world, 128), generator=g)
+            local = ids[rank * 2:(rank + 1) * 2].cuda()
+            loss = eng(local, labels=local)
+            eng.backward(loss)
+            eng.step()
+    torch.cuda.synchronize()
+    opt = eng.optimizer
+    return {"params": C.full_params(eng), "before": before, "frozen": frozen,
+            "nq": sum(1 for u in opt.frozen_units if u.frozen_q), "nf": len(opt.frozen_units)}
+
+
+@pytest.mark.parametrize("quant", [False, True])
+def test_zero3_frozen_two_ranks_one_gpu(quant):
+    """ZeRO-3 gather-only units for frozen weights on the GPU path (side-stream gathers, int8 shards
+    dequantized by the HIP kernel), 2 ranks on one GPU vs the single-rank run."""
+    two = run_dist(_case_frozen, 2, quant)
+    one = run_dist(_case_frozen, 1, quant)[0]
+    assert two[0]["nf"] >= 2 and two[0]["nq"] == (two[0]["nf"] if quant else 0) and one["nq"] == 0
+    for k, v in one["params"].items():
+        a, b = two[0]["params"][k].float(), v.float()
+        rel = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert rel < (3e-2 if quant else 2e-2), (k, rel)
+        assert torch.equal(two[0]["params"][k], two[1]["params"][k]), k
+    for k in two[0]["frozen"]:
+        a, b = two[0]["params"][k].float(), two[0]["before"][k].float()
+        assert ((a - b).norm() / (b.norm() + 1e-12)).item() < (1e-2 if quant else 1e-6), k

@@ -27,12 +27,15 @@ def main():
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true", help="two shapes, MX formats only (tile sweeps)")
+    ap.add_argument("--shapes", default=None, help="M,N,K[;M,N,K...] instead of the default list")
     args = ap.parse_args()
     native.require_hip()
     shapes = [(2048, 6144, 4096), (2048, 4096, 4096), (2048, 28672, 4096), (2048, 4096, 14336), (8192, 4096, 4096),
               (512, 4096, 4096), (128, 14336, 4096)]
     if args.quick:
         shapes = [(2048, 28672, 4096), (8192, 4096, 4096), (2048, 4096, 4096)]
+    if args.shapes:
+        shapes = [tuple(int(v) for v in sh.split(",")) for sh in args.shapes.split(";")]
     import os
     print(f"SXE_MX_TILE={os.environ.get('SXE_MX_TILE', '0')}", flush=True)
     for M, N, K in shapes:
