@@ -1338,6 +1338,7 @@ class SXEEngine(nn.Module):
         result loads strictly into the unwrapped module (reference engine.py:3830-3905). Ranks called
         with ``keep=False`` take part in the gathers but keep no host copy (returns None)."""
         opt = self.optimizer
+        opt.wait_params()  # an asynchronous host update (offload.py) may still be writing shards
         by_param = {}
         for fg in opt.fgroups:
             opt._fetch(fg, wait=True)
