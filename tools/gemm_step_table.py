@@ -34,6 +34,8 @@ def main():
     a = ap.parse_args()
     from shuffle_exchange_amd.runtime.gemm_tuning import load_tuned_gemms
     from shuffle_exchange_amd.ops import linear as L
+    from shuffle_exchange_amd.ops import native
+    native.require_hip()
     from shuffle_exchange_amd.ops.mlp import weight_grad_tn
     load_tuned_gemms()
     T = a.tokens
