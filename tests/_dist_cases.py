@@ -431,7 +431,7 @@ def _freeze_lora_style(model):
     return names
 
 
-def case_zero3_frozen(rank, world, steps, quant, tmpdir):
+def case_zero3_frozen(rank, world, steps, quant, tmpdir, offload=False):
     """zero.Init + ZeRO-3 with frozen base weights: the frozen parameters become gather-only units
     (1/W shard per rank, optionally int8), the forward/backward read them, the trainable ones update."""
     import shuffle_exchange_amd as sxe
@@ -446,6 +446,9 @@ def case_zero3_frozen(rank, world, steps, quant, tmpdir):
                                 "stage3_gather_16bit_weights_on_model_save": True,
                                 "zero_quantized_nontrainable_weights": bool(quant)},
           "optimizer": {"type": "AdamW", "params": {"lr": 1e-2, "weight_decay": 0.0}}}
+    if offload:  # ZeRO-Infinity: host optimizer + host-resident parameter shards (frozen ones too)
+        ds["zero_optimization"]["offload_optimizer"] = {"device": "cpu"}
+        ds["zero_optimization"]["offload_param"] = {"device": "cpu"}
     eng, _, _, _ = sxe.initialize(model=model, config=ds)
     opt = eng.optimizer
     frozen_total = sum(p.ds_numel for n, p in model.named_parameters() if n in frozen_names)

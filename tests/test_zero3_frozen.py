@@ -9,10 +9,10 @@ from . import _dist_cases as C
 from .dist_utils import run_dist
 
 
-@pytest.mark.parametrize("quant", [False, True])
-def test_zero3_frozen_params_zero_init_w2(tmp_path, quant):
+@pytest.mark.parametrize("quant,offload", [(False, False), (True, False), (False, True)])
+def test_zero3_frozen_params_zero_init_w2(tmp_path, quant, offload):
     world, steps = 2, 3
-    res = run_dist(C.case_zero3_frozen, world, steps, quant, str(tmp_path))
+    res = run_dist(C.case_zero3_frozen, world, steps, quant, str(tmp_path), offload)
     r0, r1 = res[0], res[1]
     names = r0["frozen_names"]
     assert names and r0["n_frozen_units"] >= 2 and r0["released"]
