@@ -463,16 +463,25 @@ class HostOptimizerStep:
             o += u.chunk
         window = self.async_window if (self.async_window > 0 and cur is not None) else len(flat)
 
+        PIECE = self.D2H_PIECE
+
         def issue(k):
+            # the unit's gradient crosses in PIECE-element pieces with an event per piece; the worker's
+            # C++ update walks the pieces as they land (as the synchronous tier does) instead of
+            # waiting for the whole unit's copy
             dst, u = d2h[k][0], flat[k][2]
             if cur is None:
                 dst.copy_(u.grad)
                 return
+            evs = []
             with get_accelerator().stream(self.d2h):
-                dst.copy_(u.grad, non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(self.d2h)
-            d2h[k][1] = ev
+                for a in range(0, u.chunk, PIECE):
+                    b = min(u.chunk, a + PIECE)
+                    dst[a:b].copy_(u.grad[a:b], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self.d2h)
+                    evs.append((a, b, ev))
+            d2h[k][1] = evs
         self._issued_all = threading.Event()
         for k in range(min(window, len(flat))):
             issue(k)
@@ -508,11 +517,8 @@ class HostOptimizerStep:
                     cops.set_num_threads(max(1, int(n) - 1))
                 NS = len(self.gslots)
                 for k, (g, i, u, off) in enumerate(flat):
-                    grad, ev = d2h[k]
+                    grad, evs = d2h[k]
                     ta = _time.perf_counter()
-                    if ev is not None:
-                        ev.synchronize()
-                    tb = _time.perf_counter()
                     pg = opt.optimizer.param_groups[g]
                     st = opt.optimizer.state[opt.master[g]]
                     slot = k % NS
@@ -522,7 +528,19 @@ class HostOptimizerStep:
                         lp = self.lslots[slot][:u.chunk]
                     else:
                         lp = u.shard_for_overwrite()
-                    self._host_kernel(opt, pg, st, u.master, grad, self._state_views(opt, g, off, u.chunk), lp, coef)
+                    states = self._state_views(opt, g, off, u.chunk)
+                    wait = 0.0
+                    for a, b, ev in (evs if evs is not None else [(0, u.chunk, None)]):
+                        tw = _time.perf_counter()
+                        if ev is not None:
+                            ev.synchronize()
+                        wait += _time.perf_counter() - tw
+                        if a == 0 and b == u.chunk:
+                            self._host_kernel(opt, pg, st, u.master, grad, states, lp, coef)
+                        else:
+                            self._host_kernel(opt, pg, st, u.master[a:b], grad[a:b], [x[a:b] for x in states],
+                                              lp[a:b], coef)
+                    tb = ta + wait
                     tc = _time.perf_counter()
                     if u.shard_is_cuda():
                         with get_accelerator().stream(self.h2d):
@@ -633,7 +651,8 @@ class HostOptimizerStep:
         if ia is not None:
             ia.wait()
         d2h, k = last
-        ev = d2h[k][1]
+        evs = d2h[k][1]
+        ev = evs[-1][2] if evs else None
         if ev is not None and torch.cuda.is_available():
             torch.cuda.current_stream().wait_event(ev)
         self._d2h_last = None
