@@ -548,7 +548,8 @@ void launch(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor& wq, co
 // 6 = 256x256 / 8 waves LDS-DMA pipelined (namespace dp), 7 = the same at 256x128 / 4 waves,
 // 8 = 256x256 / 4 waves (a phased 64-deep-stage form of 6 measured slower on every shape:
 // profiles/r05/mx_gemm_phased_tile_ab.log; 6 with 64-deep half stages, four in LDS, was slower
-// too: profiles/r05/mx_half_stage_tile_ab.log)
+// too: profiles/r05/mx_half_stage_tile_ab.log), 9 = 64x128 / 4 waves (32x64 per wave) and
+// 10 = 64x64 / 4 waves (32x32 per wave) for problems whose 128x128 grid leaves CUs idle
 static int tile_override() {  // read per call: the kernel tests sweep every variant in one process
   const char* e = getenv("SXE_MX_TILE");
   return e ? atoi(e) : 0;
@@ -596,6 +597,8 @@ void dispatch_tile(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor&
     case 3: launch<256, 256, 2, 2, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
     case 4: launch<256, 256, 2, 4, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
     case 5: launch<256, 128, 2, 4, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
+    case 9: launch<64, 128, 2, 2, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
+    case 10: launch<64, 64, 2, 2, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
     default: launch<128, 128, 2, 2, FB>(xq, xs, wq, ws, bias, cs, y, M, N, K); break;
   }
 }

@@ -85,10 +85,14 @@ def paged_attention_reference(q, cache, block_table, q_start, q_len, kv_len, sca
 PA_MIN_KEYS = int(os.environ.get("SXE_PA_MIN_KEYS", 64))
 
 
-def choose_splits(num_seqs, nkv, max_kv_len, target_wgs=512):
+PA_TARGET_WGS = int(os.environ.get("SXE_PA_TARGET_WGS", 512))
+
+
+def choose_splits(num_seqs, nkv, max_kv_len, target_wgs=None):
     """KV splits so (seqs x kv heads x splits) fills the 256 CUs, never below PA_MIN_KEYS keys per
     split: at batch 1 the kernel is a latency chain (block table -> K/V loads -> MFMA -> merge), so
     more, shorter splits shorten it; at large batch one split per (seq, kv head) streams best."""
+    target_wgs = PA_TARGET_WGS if target_wgs is None else target_wgs
     base = max(1, num_seqs * nkv)
     want = max(1, math.ceil(target_wgs / base))
     return max(1, min(want, math.ceil(max(max_kv_len, 1) / PA_MIN_KEYS)))

@@ -96,6 +96,7 @@ class ShuffleExchange:
     def __init__(self, topo: SliceTopology, method="RR", rings=8, shuffle_step=50, seed=1234, gossip_p=1.0,
                  average_master=False):
         self.topo = topo
+        self.comm_device = None  # set by ZeRO-3 so host-resident shards are reduced on the device
         self.method = method
         self.shuffle_step = max(1, int(shuffle_step))
         self.seed = int(seed)
@@ -171,17 +172,26 @@ class ShuffleExchange:
         for t in tensors:
             by_dt.setdefault(t.dtype, []).append(t)
         bufs = self.__dict__.setdefault("_pack_bufs", {})
+        cdev = self.comm_device
         for ts in by_dt.values():
-            if len(ts) == 1 and ts[0].is_contiguous():
+            dev = ts[0].device if cdev is None else cdev
+            on_dev = all(t.device == dev for t in ts)
+            if len(ts) == 1 and ts[0].is_contiguous() and on_dev:
                 fn(ts[0])
                 continue
             total = sum(t.numel() for t in ts)
-            key = (ts[0].dtype, ts[0].device)
+            key = (ts[0].dtype, dev)
             buf = bufs.get(key)
             if buf is None or buf.numel() < total:
-                buf = bufs[key] = torch.empty(total, dtype=ts[0].dtype, device=ts[0].device)
+                buf = bufs[key] = torch.empty(total, dtype=ts[0].dtype, device=dev)
             flat = buf[:total]
-            torch.cat([t.reshape(-1) for t in ts], out=flat)
+            if on_dev:
+                torch.cat([t.reshape(-1) for t in ts], out=flat)
+            else:  # host-resident shards (ZeRO-3 offload_param): H2D into the pack buffer, D2H back
+                o = 0
+                for t in ts:
+                    flat[o:o + t.numel()].copy_(t.reshape(-1), non_blocking=True)
+                    o += t.numel()
             fn(flat)
             o = 0
             for t in ts:
@@ -228,7 +238,7 @@ class ShuffleExchange:
             a = float(self.alpha)
             am = float(alpha_m)
             for t, c in zip(shards, chunks):
-                t.mul_(a / (a + am)).add_(c.to(t.dtype), alpha=am / (a + am))
+                t.mul_(a / (a + am)).add_(c.to(t.device, t.dtype), alpha=am / (a + am))
             self.alpha += am
         self.queue = []
 
@@ -264,7 +274,7 @@ class ShuffleExchange:
         dests = torch.randint(0, n, (n,), generator=self.gen).tolist()
         me = self.topo.slice_id
         ops, recv = [], []
-        dev = shards[0].device
+        dev = shards[0].device if self.comm_device is None else self.comm_device
         for sid in range(n):
             dest = int(dests[sid])
             if senders[sid] != 1 or dest == sid:
@@ -275,10 +285,10 @@ class ShuffleExchange:
                 peer = self.topo.real(dest)
                 ops.append(dist.P2POp(tdist.isend, a, peer))
                 for t in shards:
-                    ops.append(dist.P2POp(tdist.isend, t.contiguous(), peer))
+                    ops.append(dist.P2POp(tdist.isend, t.to(dev).contiguous(), peer))
             if dest == me:
                 a = torch.empty(1, dtype=torch.float32, device=dev)
-                bufs = [torch.empty_like(t) for t in shards]
+                bufs = [torch.empty(t.shape, dtype=t.dtype, device=dev) for t in shards]
                 peer = self.topo.real(sid)
                 ops.append(dist.P2POp(tdist.irecv, a, peer))
                 for b in bufs:

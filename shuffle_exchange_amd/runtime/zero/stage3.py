@@ -139,8 +139,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         # ZeRO-Infinity parameter offload: partitioned bit16 shards live in pinned host memory and
         # are DMA'd in on the all-gather stream at fetch time
         self.offload_param = bool(offload_param)
-        if self.offload_param and self.se is not None:
-            raise NotImplementedError("offload_param with shuffle-exchange slices is not supported")
+        if self.se is not None:  # host-resident (offload_param) shards are averaged through device buffers
+            self.se.comm_device = device
         # offload_param.device = nvme: non-persistent shards live in a swap file (ZeRO-Infinity),
         # cached in a few pinned buffers (runtime/swap_tensor/partitioned_param_swapper.py)
         self.pswap = None

@@ -109,7 +109,7 @@ def test_skinny_dequant_decode(kind, M, N, K):
     assert err <= 1e-2 * ref.abs().max().item() + 2e-3, err
 
 
-@pytest.mark.parametrize("tile", [1, 2, 5, 6, 7, 8])
+@pytest.mark.parametrize("tile", [1, 2, 5, 6, 7, 8, 9, 10])
 @pytest.mark.parametrize("M,N,K", [(300, 256, 1024), (2048, 512, 384), (513, 768, 128), (256, 4096, 2048)])
 def test_mx_gemm_tile_variants(tile, M, N, K, monkeypatch):
     """Every tile variant of the e4m3 path (SXE_MX_TILE, read per call) against the fp32 reference,
@@ -132,7 +132,7 @@ def test_mx_gemm_tile_variants(tile, M, N, K, monkeypatch):
     assert (y0.float() - ref0).abs().max().item() <= 1e-2 * ref0.abs().max().item() + 1e-3
 
 
-@pytest.mark.parametrize("tile", [1, 2, 6, 7, 8])
+@pytest.mark.parametrize("tile", [1, 2, 6, 7, 8, 9, 10])
 def test_mx_gemm_tile_identity(tile, monkeypatch):
     """X = I (exact in e4m3), W asymmetric small integers: Y must equal W^T exactly for every tile
     variant -- catches a transposed epilogue or a swapped operand / exponent map."""

@@ -14,7 +14,7 @@ from .dist_utils import run_dist
 pytestmark = pytest.mark.gpu
 
 
-def _case(rank, world, reuse, stage=3, se=None, defer=False):
+def _case(rank, world, reuse, stage=3, se=None, defer=False, offload_param=False):
     os.environ["LOCAL_RANK"] = "0"  # both ranks on GPU 0
     import shuffle_exchange_amd as sxe
     from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
@@ -29,6 +29,8 @@ def _case(rank, world, reuse, stage=3, se=None, defer=False):
                                 "stage3_max_reuse_distance": reuse, "stage3_defer_reduce": defer,
                                 "stage3_retain_params_in_step": defer},
           "optimizer": {"type": "SGD", "params": {"lr": 0.05}}}
+    if offload_param:
+        ds["zero_optimization"]["offload_param"] = {"device": "cpu", "pin_memory": True}
     eng, _, _, _ = sxe.initialize(model=model, config=ds, **(se or {}))
     g = torch.Generator().manual_seed(7)
     for _ in range(2):
@@ -69,6 +71,20 @@ def test_shuffle_exchange_rr_four_ranks_one_gpu(stage):
     for k in four[0]["params"]:
         for r in range(1, 4):
             assert torch.equal(four[0]["params"][k], four[r]["params"][k]), (k, r)
+
+
+def test_shuffle_exchange_rr_with_offload_param_one_gpu():
+    """Shuffle-exchange RR with ZeRO-3 offload_param: the bit16 shards live in pinned host memory
+    and are averaged across slices through a device pack buffer (H2D, collective, D2H); every rank
+    ends identical and equal to the same run without the offload."""
+    se = {"method": "RR", "slice_count": 2}
+    off = run_dist(_case, 4, 0, 3, se, False, True)
+    dev = run_dist(_case, 4, 0, 3, se, False, False)
+    for k in off[0]["params"]:
+        for r in range(1, 4):
+            assert torch.equal(off[0]["params"][k], off[r]["params"][k]), (k, r)
+        a, b = off[0]["params"][k].float(), dev[0]["params"][k].float()
+        assert ((a - b).norm() / (b.norm() + 1e-12)).item() < 1e-2, k
 
 
 def _case_init_mem(rank, world):

@@ -58,6 +58,20 @@ def test_shuffle_exchange_rr_equals_dp_sgd(method, stage):
         _close(r["params"], ref, tol=1e-5)
 
 
+@pytest.mark.parametrize("method", ["RR", "H-RR"])
+def test_shuffle_exchange_with_offload_param_equals_dp_sgd(method):
+    """ZeRO-3 offload_param keeps the bit16 shards in (pinned) host memory: the inter-slice average
+    runs on them through the pack buffer and still equals DP-SGD over all ranks."""
+    world, mbs, seq, steps = 4, 1, 16, 3
+    ds = {"train_micro_batch_size_per_gpu": mbs, "optimizer": SGD,
+          "zero_optimization": {"stage": 3, "stage3_param_persistence_threshold": 0,
+                                "offload_param": {"device": "cpu"}}}
+    res = run_dist(C.case_train, world, ds, steps, mbs, seq, {"method": method, "slice_count": 2})
+    ref = C.reference_train(SGD, steps, world, mbs, seq)
+    for r in res:
+        _close(r["params"], ref, tol=1e-5)
+
+
 def test_shuffle_groups_consistent_and_reshuffle():
     world = 4
     res = run_dist(C.case_shuffle_groups, world, 1, 2, 2, 6)
