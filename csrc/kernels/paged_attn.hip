@@ -120,6 +120,7 @@ struct Args {
   float* part_ml;  // [splits, T, nq, 2]
   int T;
   int window;      // sliding window (Mistral / Qwen2): keys older than `window` positions are masked; 0 = off
+  int* counters;   // [S * nkv] zeroed split-arrival counters: the last split of a (seq, kv head) merges; or null
 };
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -349,6 +350,58 @@ __global__ __launch_bounds__(256) void paged_attn_kernel(Args a) {
     }
     __syncthreads();
   }
+  if (a.counters != nullptr) {
+    // In-kernel split merge: the last of the `splits` workgroups of this (sequence, kv head) to
+    // finish combines every split's partials (merge_kernel's math) and writes the bf16 output --
+    // no second launch. Release: each split's partials are made visible device-wide (across the
+    // XCDs' L2s) before its arrival is counted; acquire: the last one fences again before reading.
+    __shared__ int is_last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int prev = atomicAdd(a.counters + blockIdx.x, 1);
+      is_last = prev == a.splits - 1;
+      if (is_last) atomicExch(a.counters + blockIdx.x, 0);  // self-resetting: ready for the next launch / replay
+    }
+    __syncthreads();
+    if (!is_last) return;
+    __threadfence();
+    constexpr int U = 8;
+    const int64_t sstride = (int64_t)a.T * a.nq;
+    for (int idx = threadIdx.x; idx < nrows_total * D; idx += 256) {
+      const int r = idx / D, d = idx - r * D, tok = r / G, gh = r - tok * G;
+      const int t = qs + tok, h = kvh * G + gh;
+      const int64_t th = (int64_t)t * a.nq + h;
+      float M = -INFINITY, acc = 0.f, L = 0.f;
+      for (int s0 = 0; s0 < a.splits; s0 += U) {
+        float ms[U], ls[U], os[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t i2 = (int64_t)min(s0 + u, a.splits - 1) * sstride + th;
+          ms[u] = a.part_ml[i2 * 2];
+          ls[u] = a.part_ml[i2 * 2 + 1];
+          os[u] = a.part_o[i2 * D + d];
+        }
+        float Mc = M;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (s0 + u < a.splits) Mc = fmaxf(Mc, ms[u]);
+        const float rs = (M == -INFINITY) ? 0.f : exp2f(M - Mc);
+        acc *= rs;
+        L *= rs;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (s0 + u < a.splits && ms[u] != -INFINITY) {
+            const float f = exp2f(ms[u] - Mc);
+            acc += f * os[u];
+            L += f * ls[u];
+          }
+        }
+        M = Mc;
+      }
+      a.out[(int64_t)t * a.out_tok_stride + (int64_t)h * D + d] = f32_to_bf16(L > 0.f ? acc / L : 0.f);
+    }
+  }
 }
 
 // Combine the splits' fp32 partials of one (token, head): every load of a group of up to 16 splits is
@@ -462,7 +515,7 @@ void kv_cache_append(const at::Tensor& qkv, at::Tensor cache, const at::Tensor& 
 static at::Tensor paged_attention_impl(const at::Tensor& q, const at::Tensor& cache, const at::Tensor& block_table,
                                        const at::Tensor& q_start, const at::Tensor& q_len, const at::Tensor& kv_len,
                                        double scale, int64_t max_kv_len, int64_t splits, int64_t window,
-                                       std::vector<at::Tensor>* parts) {
+                                       std::vector<at::Tensor>* parts, const c10::optional<at::Tensor>& counters = {}) {
   SXE_CHECK_CUDA(q);
   SXE_CHECK(q.scalar_type() == at::kBFloat16 && cache.scalar_type() == at::kBFloat16, "bf16 only");
   SXE_CHECK(q.dim() == 3 && q.stride(2) == 1 && q.stride(1) == q.size(2), "q must be [T, nq, D] with head stride D");
@@ -505,6 +558,13 @@ static at::Tensor paged_attention_impl(const at::Tensor& q, const at::Tensor& ca
   a.part_o = nullptr;
   a.part_ml = nullptr;
   a.window = (int)std::max<int64_t>(0, window);
+  a.counters = nullptr;
+  if (splits > 1 && parts == nullptr && counters.has_value()) {
+    SXE_CHECK(counters->is_cuda() && counters->scalar_type() == at::kInt && counters->is_contiguous() &&
+                  counters->numel() >= (int64_t)S * nkv,
+              "paged_attention: counters int32 [>= S * nkv] on the device, zeroed");
+    a.counters = counters->data_ptr<int>();
+  }
   if (splits > 1) {
     part_o = at::empty({splits, T, nq, D}, q.options().dtype(at::kFloat));
     part_ml = at::empty({splits, T, nq, 2}, q.options().dtype(at::kFloat));
@@ -530,7 +590,7 @@ static at::Tensor paged_attention_impl(const at::Tensor& q, const at::Tensor& ca
     *parts = {part_o, part_ml};
     return out;
   }
-  if (splits > 1) {
+  if (splits > 1 && a.counters == nullptr) {
     if (D == 128)
       hipLaunchKernelGGL(pa::merge_kernel<128>, dim3(T * nq), dim3(128), 0, cur_stream(), a.part_o, a.part_ml,
                          (int)splits, T, nq, a.out, a.out_tok_stride);
@@ -547,8 +607,9 @@ static at::Tensor paged_attention_impl(const at::Tensor& q, const at::Tensor& ca
 
 at::Tensor paged_attention(const at::Tensor& q, const at::Tensor& cache, const at::Tensor& block_table,
                            const at::Tensor& q_start, const at::Tensor& q_len, const at::Tensor& kv_len, double scale,
-                           int64_t max_kv_len, int64_t splits, int64_t window) {
-  return paged_attention_impl(q, cache, block_table, q_start, q_len, kv_len, scale, max_kv_len, splits, window, nullptr);
+                           int64_t max_kv_len, int64_t splits, int64_t window, const c10::optional<at::Tensor>& counters) {
+  return paged_attention_impl(q, cache, block_table, q_start, q_len, kv_len, scale, max_kv_len, splits, window, nullptr,
+                              counters);
 }
 
 // [out, part_o, part_ml]: with one split `out` is the attention output and the partials are empty;
@@ -574,7 +635,7 @@ TORCH_LIBRARY_FRAGMENT(sxe, m) {
   m.def("rope_kv_cache_append(Tensor(a!) qkv, Tensor cos, Tensor sin, Tensor pos, Tensor(b!) cache, Tensor slots, "
         "int nq, int nkv) -> ()");
   m.def("paged_attention(Tensor q, Tensor cache, Tensor block_table, Tensor q_start, Tensor q_len, Tensor kv_len, "
-        "float scale, int max_kv_len, int splits, int window=0) -> Tensor");
+        "float scale, int max_kv_len, int splits, int window=0, Tensor(a!)? counters=None) -> Tensor");
   m.def("paged_attention_parts(Tensor q, Tensor cache, Tensor block_table, Tensor q_start, Tensor q_len, "
         "Tensor kv_len, float scale, int max_kv_len, int splits, int window=0) -> Tensor[]");
 }

@@ -123,6 +123,22 @@ def merge_attention_parts(part_o, part_ml, dtype):
     return torch.where(den.unsqueeze(-1) > 0, num / den.clamp_min(1e-30).unsqueeze(-1), 0.).to(dtype)
 
 
+# decode (T <= 4 tokens per sequence) with several KV splits: the last split workgroup of each
+# (sequence, kv head) merges the partials inside the attention launch (paged_attn.hip, arrival
+# counters) instead of a second merge launch
+PA_LAST_MERGE = os.environ.get("SXE_PA_LAST_MERGE", "1") == "1"
+_COUNTERS = {}
+
+
+def _split_counters(device, n):
+    """Zeroed int32 split-arrival counters (self-resetting in the kernel), one buffer per device,
+    grown outside any graph capture in the normal flow (the decode engine runs eagerly first)."""
+    c = _COUNTERS.get(device)
+    if c is None or c.numel() < n:
+        c = _COUNTERS[device] = torch.zeros(max(n, 4096), dtype=torch.int32, device=device)
+    return c
+
+
 def paged_attention(q, cache, block_table, q_start, q_len, kv_len, scale, max_kv_len, splits=None, window=None):
     """q: [T, nq, D] (head stride D); metadata int32 [S]; returns [T, nq, D]. ``window``: sliding
     window length (keys older than ``window`` positions are masked, Mistral / Qwen2). The HIP kernel
@@ -133,8 +149,11 @@ def paged_attention(q, cache, block_table, q_start, q_len, kv_len, scale, max_kv
     if native.use_hip(q) and q.shape[-1] in (64, 128, 256):
         if splits is None:
             splits = choose_splits(block_table.shape[0], cache.shape[2], max_kv_len)
+        S = block_table.shape[0]
+        cnt = (_split_counters(q.device, S * cache.shape[2])
+               if PA_LAST_MERGE and splits > 1 and q.shape[0] <= 4 * S else None)
         return torch.ops.sxe.paged_attention(q, cache, block_table, q_start, q_len, kv_len, float(scale),
-                                             int(max_kv_len), int(splits), int(window or 0))
+                                             int(max_kv_len), int(splits), int(window or 0), cnt)
     if q.is_cuda:
         from ..utils.logging import warning_once
         warning_once(f"paged_attention: head_dim={q.shape[-1]} window={window} not covered by the HIP kernel; "

@@ -123,3 +123,36 @@ def test_merge_attention_parts_matches_fused_kernel(splits):
     ref = paged_attention_reference(q.float(), cache.float(), bt, qs, ql, kl, scale)
     torch.testing.assert_close(merged.float(), fused.float(), atol=2e-2, rtol=2e-2)
     assert ((merged.float() - ref).norm() / ref.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("splits", [2, 5, 16])
+def test_in_kernel_split_merge_matches_merge_launch(splits, monkeypatch):
+    """Decode with the last split workgroup merging in-kernel (arrival counters) == the separate
+    merge launch, over repeated launches and HIP-graph replays (the counters must self-reset)."""
+    from shuffle_exchange_amd.ops import paged_attention as PA
+    qkv, cache, bt, qs, ql, kl, slots, maxkv = _setup([(700, 1), (1500, 1), (37, 1), (3000, 1)], 32, 8, 128, 16)
+    q = qkv[:, :32]
+    scale = 128 ** -0.5
+    monkeypatch.setattr(PA, "PA_LAST_MERGE", False)
+    sep = PA.paged_attention(q, cache, bt, qs, ql, kl, scale, maxkv, splits)
+    monkeypatch.setattr(PA, "PA_LAST_MERGE", True)
+    ref = PA.paged_attention_reference(q.float(), cache.float(), bt, qs, ql, kl, scale)
+    for _ in range(3):
+        last = PA.paged_attention(q, cache, bt, qs, ql, kl, scale, maxkv, splits)
+        torch.testing.assert_close(last.float(), sep.float(), atol=1e-2, rtol=1e-2)
+    assert ((last.float() - ref).norm() / ref.norm()).item() < 1e-2
+    assert int(PA._COUNTERS[q.device].abs().sum()) == 0
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        PA.paged_attention(q, cache, bt, qs, ql, kl, scale, maxkv, splits)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = PA.paged_attention(q, cache, bt, qs, ql, kl, scale, maxkv, splits)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(out.float(), sep.float(), atol=1e-2, rtol=1e-2)
+    assert int(PA._COUNTERS[q.device].abs().sum()) == 0
