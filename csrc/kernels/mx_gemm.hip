@@ -582,11 +582,16 @@ void dispatch_tile(const at::Tensor& xq, const at::Tensor& xs, const at::Tensor&
                    int N, int K) {
   int v = tile_override();
   if (v == 0) {
-    // measured on MI355X (profiles/mx_gemm_bench.log): the LDS-DMA pipelined 256 x 256 tile once it
-    // fills the chip, its 256 x 128 form when that still gives >= half a workgroup per CU, the
-    // register-staged 128 x 128 tile for small problems
+    // measured on MI355X (profiles/mx_gemm_bench.log, profiles/r06/mx/mx_small_tiles.log): the LDS-DMA
+    // pipelined 256 x 256 tile once it fills the chip, its 256 x 128 form when that still gives >= half
+    // a workgroup per CU, the 64 x 64 tile while a 128 x 128 grid would leave CUs idle (M <= 512 at
+    // N 4096 / 6144, M 128 at N 14336: 1.2-1.7x faster than 128 x 128 there), else 128 x 128
     const int64_t g256 = (int64_t)((M + 255) / 256) * (N / 256), g2561 = (int64_t)((M + 255) / 256) * (N / 128);
-    v = (N % 256 == 0 && M > 256 && g256 >= kNumCUs) ? 6 : (M > 256 && g2561 >= kNumCUs / 2) ? 7 : 1;
+    const int64_t g128 = (int64_t)((M + 127) / 128) * (N / 128);
+    v = (N % 256 == 0 && M > 256 && g256 >= kNumCUs) ? 6
+        : (M > 256 && g2561 >= kNumCUs / 2)          ? 7
+        : g128 < kNumCUs                             ? 10
+                                                     : 1;
   }
   if ((v == 3 || v == 4 || v == 6 || v == 8) && N % 256 != 0) v = 2;
   switch (v) {

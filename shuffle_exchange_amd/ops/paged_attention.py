@@ -123,10 +123,12 @@ def merge_attention_parts(part_o, part_ml, dtype):
     return torch.where(den.unsqueeze(-1) > 0, num / den.clamp_min(1e-30).unsqueeze(-1), 0.).to(dtype)
 
 
-# decode (T <= 4 tokens per sequence) with several KV splits: the last split workgroup of each
-# (sequence, kv head) merges the partials inside the attention launch (paged_attn.hip, arrival
-# counters) instead of a second merge launch
-PA_LAST_MERGE = os.environ.get("SXE_PA_LAST_MERGE", "1") == "1"
+# SXE_PA_LAST_MERGE=1: with several KV splits the last split workgroup of each (sequence, kv head)
+# merges the partials inside the attention launch (paged_attn.hip, arrival counters) instead of a
+# second merge launch. Off: its device-scope fences write back / invalidate the L2 the K/V stream
+# lives in -- Llama-3-8B ctx 1024 decode 4.50 vs 3.73 ms/token at batch 1, 6.60 vs 4.91 at batch 8
+# (profiles/r06/decode_split_merge_ab.log)
+PA_LAST_MERGE = os.environ.get("SXE_PA_LAST_MERGE", "0") == "1"
 _COUNTERS = {}
 
 
