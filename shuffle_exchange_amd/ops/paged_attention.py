@@ -81,8 +81,10 @@ def paged_attention_reference(q, cache, block_table, q_start, q_len, kv_len, sca
     return out
 
 
-# keys per split floor (A/B knob; see choose_splits): one 64-key wave chunk
-PA_MIN_KEYS = int(os.environ.get("SXE_PA_MIN_KEYS", 64))
+# keys per split floor (see choose_splits): 256 = four 64-key wave chunks per split. Llama-3-8B decode,
+# HIP graphs, fused merge: batch 1 ctx 1024 3.571 / 3.604 / 3.700 ms per token at 256 / 128 / 64,
+# ctx 4096 3.745 / 3.927 / 3.926; batch 8 and 32 within 1 % (profiles/r06/decode_split_floor_ab.log)
+PA_MIN_KEYS = int(os.environ.get("SXE_PA_MIN_KEYS", 256))
 
 
 PA_TARGET_WGS = int(os.environ.get("SXE_PA_TARGET_WGS", 512))

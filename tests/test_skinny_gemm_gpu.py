@@ -208,6 +208,7 @@ def test_decode_merge_fused_o_proj_matches_unfused(monkeypatch):
                        num_key_value_heads=2, vocab_size=1000, num_hidden_layers=2)
     model = LlamaForCausalLM(cfg).cuda().bfloat16().eval()
     prompt = torch.randint(0, cfg.vocab_size, (200,)).tolist()  # < max_position_embeddings (256)
+    monkeypatch.setattr(pa, "PA_MIN_KEYS", 64)  # several KV splits at this short context
     assert pa.choose_splits(1, 2, 206) > 1
     import shuffle_exchange_amd.ops.linear as lin
     calls = {"n": 0}
