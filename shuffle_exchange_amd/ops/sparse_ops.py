@@ -14,10 +14,11 @@ three kernels with the reference's mode / transpose algebra (matmul.py:628 ``_sp
 Other dtypes and devices take the batched-GEMM form: ``sdd`` gathers the block rows of A and block
 columns of B per non-zero and multiplies [nnz] (block x K) x (K x block) pairs; ``dsd`` / ``dds``
 multiply each non-zero block by its dense panel and sum the partial products per output block row /
-column with one ``index_add``. Softmax works on the compact blocks only: per-row max and sum are segment
-reductions over the blocks of one (head, block-row) group (``scatter_reduce`` / ``index_add``), so
-memory stays O(nnz block^2) -- the dense S x S score matrix is never formed. Gradients flow through
-the same ops (autograd). Block-sparse attention itself does not use these: it runs fused in the
+column with one ``index_add``. Softmax works on the compact blocks only: on the GPU one HIP kernel
+(csrc/kernels/bsoftmax.hip) walks each block row's CSR list per query row (forward and backward);
+elsewhere per-row max and sum are segment reductions over the blocks of one (head, block-row) group
+(``scatter_reduce`` / ``index_add``), so memory stays O(nnz block^2) -- the dense S x S score matrix
+is never formed. Gradients flow through the same ops (autograd). Block-sparse attention itself does not use these: it runs fused in the
 flash kernels (ops/sparse_attention.py ``block_sparse_attention``), which never write the scores.
 """
 import torch
@@ -252,12 +253,37 @@ class Softmax:
             return x[:, h if x.shape[1] > 1 else 0 * h, i, j]
         return x[h if x.shape[0] > 1 else 0 * h, i, j]
 
+    def _csr(self, device):
+        """Block-row pointer [H M + 1] and block column [nnz] (int32) of the layout on ``device``."""
+        key = ("csr", device)
+        if key not in self._idx:
+            h, i, j = self._hij
+            H, M, _ = self.spdims
+            cnt = torch.bincount(h * M + i, minlength=H * M)
+            ptr = torch.zeros(H * M + 1, dtype=torch.int64)
+            ptr[1:] = torch.cumsum(cnt, 0)
+            self._idx[key] = (ptr.int().to(device), j.int().to(device))
+        return self._idx[key]
+
+    def _hip_ok(self, x):
+        from . import native
+        return (x.is_cuda and x.dtype in (torch.float32, torch.bfloat16, torch.float16) and self.block % 8 == 0
+                and x.dim() == 4 and x.shape[1] == self.num_blocks and native.use_hip(x))
+
     def __call__(self, x, scale=1.0, rpe=None, key_padding_mask=None, attn_mask=None, key_padding_mask_mode="add",
                  attn_mask_mode="add"):
         for name, t in (("relative position embedding", rpe), ("Attention mask", attn_mask),
                         ("Key padding mask", key_padding_mask)):
             if t is not None and t.dtype != x.dtype:
                 raise ValueError(f"{name} must be {x.dtype}")
+        if self._hip_ok(x):  # csrc/kernels/bsoftmax.hip (gradient w.r.t. x only, as the reference)
+            f32 = lambda t: None if t is None else t.detach().float().contiguous()  # noqa: E731
+            r = f32(rpe)
+            if r is not None and r.dim() == 2:
+                r = r.unsqueeze(0)
+            kp = f32(key_padding_mask)
+            return _BSoftmax.apply(x.contiguous(), self, float(scale), r, f32(attn_mask), attn_mask_mode == "mul",
+                                   None if kp is None else kp.reshape(x.shape[0], -1), key_padding_mask_mode == "mul")
         h, i, j = self._index(x.device)
         H, M, N = self.spdims
         blk = self.block
@@ -300,3 +326,25 @@ def block_sparse_to_dense(xs, layout, block, fill=0.0):
     out = torch.full((xs.shape[0], H, M, N, block, block), fill, dtype=xs.dtype, device=xs.device)
     out[:, h, i, j] = xs
     return out.transpose(3, 4).reshape(xs.shape[0], H, M * block, N * block)
+
+
+class _BSoftmax(torch.autograd.Function):
+    """HIP block-sparse softmax (bsoftmax.hip); backward dx = y (dy - rowsum(dy y)) * ds/dx."""
+
+    @staticmethod
+    def forward(ctx, x, sm, scale, rpe, am, am_mul, kpm, kpm_mul):
+        ptr, col = sm._csr(x.device)
+        H, M, N = sm.spdims
+        y = torch.ops.sxe.bsparse_softmax_fwd(x, ptr, col, H, M, N, scale, rpe, am, am_mul, kpm, kpm_mul)
+        ctx.save_for_backward(y)
+        ctx.meta = (sm, scale, am, am_mul, kpm, kpm_mul)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        sm, scale, am, am_mul, kpm, kpm_mul = ctx.meta
+        ptr, col = sm._csr(y.device)
+        H, M, N = sm.spdims
+        dx = torch.ops.sxe.bsparse_softmax_bwd(y, dy.contiguous(), ptr, col, H, M, N, scale, am, am_mul, kpm, kpm_mul)
+        return dx, None, None, None, None, None, None, None

@@ -78,3 +78,41 @@ def test_bsmm_matches_fp32(mode, ta, tb, blk):
     (c32 * g).sum().backward()
     assert _rel(a16.grad, a32.grad) < 2e-2
     assert _rel(b16.grad, b32.grad) < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("blk", [16, 32, 64])
+@pytest.mark.parametrize("mode", ["add", "mul"])
+def test_block_sparse_softmax_hip_matches_fp32(dtype, blk, mode):
+    """HIP block-sparse softmax (bsoftmax.hip) forward and x-gradient == the fp32 PyTorch segment
+    reductions of the same class, with scale, rpe, attention mask and key-padding mask, a block row
+    with no blocks and a fully masked (-inf) key set (reference ops/sparse_attention/softmax.py)."""
+    from shuffle_exchange_amd.ops import sparse_ops as so
+    torch.manual_seed(blk)
+    H, M, B = 3, 5, 2
+    lay = _layout(H, M, M, blk)
+    lay[1, 2] = 0  # an empty block row
+    S = M * blk
+    sm = so.Softmax(lay, blk)
+    nnz = int(lay.sum())
+    x = torch.randn(B, nnz, blk, blk, device="cuda").to(dtype)
+    rpe = torch.randn(H, S, S, device="cuda").to(dtype)
+    if mode == "add":
+        kpm = torch.where(torch.rand(B, S, device="cuda") < 0.2, -1e4, 0.0).to(dtype)
+        am = (torch.randn(S, S, device="cuda") * 0.5).to(dtype)
+    else:
+        kpm = (torch.rand(B, S, device="cuda") > 0.2).to(dtype)
+        am = (torch.rand(S, S, device="cuda") > 0.1).to(dtype)
+    kw = dict(scale=0.3, rpe=rpe, key_padding_mask=kpm, attn_mask=am, key_padding_mask_mode=mode, attn_mask_mode=mode)
+    xh = x.clone().requires_grad_()
+    y = sm(xh, **kw)
+    assert sm._hip_ok(xh)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = x.float().clone().requires_grad_()
+    kwr = {k: (v.float() if torch.is_tensor(v) else v) for k, v in kw.items()}
+    yr = so.Softmax(lay, blk)(xr.cpu(), **{k: (v.cpu() if torch.is_tensor(v) else v) for k, v in kwr.items()})
+    yr.backward(g.float().cpu())
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert _rel(y.cpu(), yr) < tol
+    assert _rel(xh.grad.cpu(), xr.grad) < tol * 2
