@@ -20,7 +20,8 @@ run sync SXE_OFFLOAD_ASYNC=0 && \
 run async_w0_k0 SXE_OFFLOAD_ASYNC=1 && \
 run async_w2_k1 SXE_OFFLOAD_ASYNC=1 SXE_OFFLOAD_ASYNC_WINDOW=2 SXE_OFFLOAD_H2D_KERNEL=1 && \
 dec fused SXE_DECODE_FUSE_ATTN=1 && \
-dec separate SXE_DECODE_FUSE_ATTN=0 && \
-dec fused_t256 SXE_DECODE_FUSE_ATTN=1 SXE_PA_TARGET_WGS=256 && \
-dec fused_t128 SXE_DECODE_FUSE_ATTN=1 SXE_PA_TARGET_WGS=128 && \
-dec separate_t256 SXE_DECODE_FUSE_ATTN=0 SXE_PA_TARGET_WGS=256
+dec separate_mergelaunch SXE_DECODE_FUSE_ATTN=0 SXE_PA_LAST_MERGE=0 && \
+dec separate_lastmerge SXE_DECODE_FUSE_ATTN=0 SXE_PA_LAST_MERGE=1 && \
+dec lastmerge_t256 SXE_DECODE_FUSE_ATTN=0 SXE_PA_LAST_MERGE=1 SXE_PA_TARGET_WGS=256 && \
+dec lastmerge_k128 SXE_DECODE_FUSE_ATTN=0 SXE_PA_LAST_MERGE=1 SXE_PA_MIN_KEYS=128 && \
+dec fused_k128 SXE_DECODE_FUSE_ATTN=1 SXE_PA_MIN_KEYS=128

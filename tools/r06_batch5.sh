@@ -19,7 +19,3 @@ dec() {  # name, env...
       || { echo "decode $name failed"; tail -30 $O/decode_$name.log; exit 1; }
   echo "decode $name $(grep '^{' $O/decode_$name.log | tail -1)"
 }
-dec fused_k128 SXE_PA_MIN_KEYS=128 && \
-dec fused_k256 SXE_PA_MIN_KEYS=256 && \
-dec separate_k128 SXE_DECODE_FUSE_ATTN=0 SXE_PA_MIN_KEYS=128 && \
-dec separate_k256 SXE_DECODE_FUSE_ATTN=0 SXE_PA_MIN_KEYS=256
