@@ -10,10 +10,15 @@ so the ZeRO optimizers reduce its gradient over the expert-data-parallel group o
 """
 import copy
 
+import os
+
 import torch
 import torch.nn as nn
 
 from ..ops.activation import swiglu
+
+# SXE_MOE_DEFER_WGRAD=0: write the expert weight gradients every micro-step (see _GroupedMM)
+DEFER_WGRAD = os.environ.get("SXE_MOE_DEFER_WGRAD", "1") == "1"
 
 
 class Experts(nn.Module):
@@ -115,6 +120,17 @@ class _GroupedMM(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             from ..ops.linear import grad_target
             tgt = grad_target(w)
+            defer = getattr(w, "_sxe_grad_defer", None)
+            if tgt is not None and DEFER_WGRAD and defer is not None and defer(w):
+                # before the accumulation boundary: keep (x, dy) and write the weight gradient once, at
+                # the boundary, over all micro-steps' tokens -- one fp32 write of the expert's gradient
+                # per step instead of a write plus a read-modify-write per micro-step
+                w.__dict__.setdefault("_sxe_wstash", []).append((x, dy))
+                return dx, None
+            stash = w.__dict__.pop("_sxe_wstash", None)
+            if stash:
+                x = torch.cat([a for a, _ in stash] + [x], dim=1)
+                dy = torch.cat([g for _, g in stash] + [dy], dim=1)
             if tgt is not None:
                 from ..ops.linear import _sxe_wgrad_ok
                 buf, acc = tgt(w)
@@ -141,3 +157,25 @@ class _GroupedMM(torch.autograd.Function):
 
 def grouped_mm(x, w):
     return _GroupedMM.apply(x, w)
+
+
+def flush_deferred_wgrad(w):
+    """Write a weight gradient still held as (x, dy) pairs (no backward reached ``w`` at the
+    accumulation boundary): the same GEMMs as _GroupedMM's boundary pass."""
+    stash = w.__dict__.pop("_sxe_wstash", None)
+    if not stash:
+        return
+    x = torch.cat([a for a, _ in stash], dim=1)
+    dy = torch.cat([g for _, g in stash], dim=1)
+    defer, w._sxe_grad_defer = w._sxe_grad_defer, None
+    try:
+        _GroupedMM.backward(_FlushCtx(x, w), dy)
+    finally:
+        w._sxe_grad_defer = defer
+
+
+class _FlushCtx:
+    needs_input_grad = (False, True)
+
+    def __init__(self, x, w):
+        self.saved_tensors = (x, w)

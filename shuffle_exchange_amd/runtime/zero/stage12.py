@@ -140,6 +140,8 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
                 # bf16 reduce-scatter staging slot (S > 1) directly
                 p._sxe_grad_target = self._grad_target
                 p._sxe_grad_done = self._grad_done
+                if u.topo.S == 1:  # only this rank ever writes the accumulator: safe to write it late
+                    p._sxe_grad_defer = self._grad_defer
 
     def _grad_target(self, p):
         u = self.param_unit[p]
@@ -163,6 +165,12 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
             u.pending -= 1
         if u.topo.S > 1 and u.pending == 0:
             self._reduce_unit(u)
+
+    def _grad_defer(self, p):
+        """May a weight-gradient producer hold this micro-step's contribution and write it at the
+        accumulation boundary instead (moe/experts.py)? Yes before the boundary: a single-rank
+        unit's accumulator is read by nothing until the step."""
+        return not self.micro_step_boundary
 
     def grad_ready(self, p):
         """A gradient delivered outside autograd's AccumulateGrad (the FX graph compiler's in-graph
@@ -256,6 +264,11 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
     def reduce_gradients(self, pipeline_parallel=False):
         """Backward epilogue: reduce units whose params did not all produce grads (unused params)
         and, for ZeRO-1 at the boundary, everything still pending."""
+        if self.micro_step_boundary:
+            from ...moe.experts import flush_deferred_wgrad
+            for p in self.param_unit:
+                if p.__dict__.get("_sxe_wstash"):  # deferred weight grads no boundary backward consumed
+                    flush_deferred_wgrad(p)
         if self.stage == 1 and not self.micro_step_boundary:
             if self.fp32_accum:  # the fp32 staging sums carry into the next micro-step
                 for units in self.units:
