@@ -110,11 +110,16 @@ __device__ __forceinline__ void load_slab(const DmaPlan& d, int64_t lda, int64_t
 
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
+// Two K segments (A, B) rows [0, 16 ns1) then (A2, B2) rows [0, K - 16 ns1), same leading dims: the
+// product over the concatenated token axis without materialising the concatenation (the deferred
+// expert weight gradients of moe/experts.py: the stashed micro-step, then the boundary one).
+// ns1 = K / 16 (and A2 = A, B2 = B) for one segment.
 template <bool ACCUM, int R, bool STAGGER, bool NODMA = false>
 __global__ void __launch_bounds__(NTHR, 1) wgrad_kernel(const unsigned short* __restrict__ A, int64_t lda,
                                                         const unsigned short* __restrict__ B, int64_t ldb,
                                                         float* __restrict__ C, int64_t ldc, int M, int N, int K,
-                                                        float alpha, int group_m) {
+                                                        float alpha, int group_m, const unsigned short* A2,
+                                                        const unsigned short* B2, int ns1) {
   static_assert(R == 8, "fragment bases assume slots 0-3 / 4-7");
   constexpr int D = STAGGER ? R - 3 : R - 2;              // prefetch distance in slabs
   constexpr int WAIT = STAGGER ? 2 * (D - 2) : 2 * (D - 1);  // DMA left in flight at each wait
@@ -172,9 +177,16 @@ __global__ void __launch_bounds__(NTHR, 1) wgrad_kernel(const unsigned short* __
   };
   const unsigned lds_base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   const DmaPlan dp = dma_plan(A, lda, B, ldb, m0, n0, lds_base);
+  const DmaPlan dp2 = dma_plan(A2, lda, B2, ldb, m0, n0, lds_base);
+  auto load_any = [&](int slab, int slot) {  // slab in the first or the second K segment (wave-uniform)
+    if (slab < ns1)
+      load_slab(dp, lda, ldb, slab, slot);
+    else
+      load_slab(dp2, lda, ldb, slab - ns1, slot);
+  };
   // prologue: slabs 0 .. D-1, then the first phase's fragments
 #pragma unroll
-  for (int j = 0; j < D; ++j) load_slab(dp, lda, ldb, j, j);
+  for (int j = 0; j < D; ++j) load_any(j, j);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WAIT) : "memory");
   __builtin_amdgcn_s_barrier();
   read_frags(0, fa[0], fb[0]);
@@ -183,7 +195,7 @@ __global__ void __launch_bounds__(NTHR, 1) wgrad_kernel(const unsigned short* __
 #pragma unroll
     for (int j = 0; j < R; ++j) {  // phase s = s0 + j, slab s in slot j
       // the surplus DMA of the last D phases (clamped to the last slab) lands in consumed slots
-      if (!NODMA) load_slab(dp, lda, ldb, min(s0 + j + D, ns - 1), (j + D) % R);
+      if (!NODMA) load_any(min(s0 + j + D, ns - 1), (j + D) % R);
       if (NODMA)  // ablation (variant 3): the ring is never refilled -- MFMA + LDS + barrier ceiling
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else
@@ -246,7 +258,8 @@ template <bool ACCUM>
 __global__ void __launch_bounds__(NTHR, 1) kernel(const unsigned short* __restrict__ A, int64_t lda,
                                                   const unsigned short* __restrict__ B, int64_t ldb,
                                                   float* __restrict__ C, int64_t ldc, int M, int N, int K,
-                                                  float alpha, int group_m) {
+                                                  float alpha, int group_m, const unsigned short* A2,
+                                                  const unsigned short* B2, int ns1) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wr = w >> 1, wc = w & 1;
@@ -272,20 +285,27 @@ __global__ void __launch_bounds__(NTHR, 1) kernel(const unsigned short* __restri
 
   // DMA: slab rows 4*rq + (lane>>4), rq = 0..7; the 32 wave-instructions of a slab are
   // (op, half, rq) = (it>>2, (it>>1)&1, (it&1)*4 + w) for it = 0..7
-  Plan pl;
+  Plan pl, pl2;
   {
     const int row = lane >> 4;  // row & 3 == (lane >> 4) & 3 for every rq
     const int ch = (lane & 15) ^ swz(row);
     pl.a = A + (int64_t)row * lda + m0 + ch * 8;
     pl.b = B + (int64_t)row * ldb + n0 + ch * 8;
     pl.lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+    pl2 = pl;
+    pl2.a = A2 + (int64_t)row * lda + m0 + ch * 8;
+    pl2.b = B2 + (int64_t)row * ldb + n0 + ch * 8;
   }
-  auto load_slab = [&](int slab, int slot) {
+  const int ns1_32 = ns1 / 2;  // 16-row slabs of the first segment -> 32-row slabs (host: ns1 even)
+  auto load_slab = [&](int slab_any, int slot) {
+    const bool second = slab_any >= ns1_32;
+    const Plan& P = second ? pl2 : pl;
+    const int slab = second ? slab_any - ns1_32 : slab_any;
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
       const int op = it >> 2, half = (it >> 1) & 1, rq = (it & 1) * 4 + w;
       const int64_t rows = (int64_t)SLAB * slab + 4 * rq;
-      const unsigned short* src = op == 0 ? pl.a + rows * lda + half * 128 : pl.b + rows * ldb + half * 128;
+      const unsigned short* src = op == 0 ? P.a + rows * lda + half * 128 : P.b + rows * ldb + half * 128;
       const unsigned dst = __builtin_amdgcn_readfirstlane(pl.lds + slot * SLOT + (op * 2 + half) * HALF + 4 * rq * ROWB);
       glds16(src, dst);
     }
@@ -376,15 +396,14 @@ bool wgrad_supported(const at::Tensor& a, const at::Tensor& b, const at::Tensor&
 
 // c (+)= alpha * a^T @ b ; a: [K, M] bf16, b: [K, N] bf16, c: [M, N] fp32.
 // variant: 0 = 8 lock-step waves, 1 = 8 staggered waves, 2 = 4 waves of 128 x 128, for in-process A/B.
-void wgrad_gemm_variant_(const at::Tensor& a, const at::Tensor& b, at::Tensor c, double alpha, bool accumulate,
-                         int64_t variant) {
-  SXE_CHECK(wgrad_supported(a, b, c), "wgrad_gemm_: unsupported shapes/dtypes/strides");
+static void wgrad_launch(const at::Tensor& a, const at::Tensor& b, const at::Tensor& a2, const at::Tensor& b2, int K,
+                         int ns1, at::Tensor c, double alpha, bool accumulate, int64_t variant) {
   c10::DeviceGuard g(a.device());
-  const int K = a.size(0), M = a.size(1), N = b.size(1);
+  const int M = a.size(1), N = b.size(1);
   const int nwg = (M / wg::BM) * (N / wg::BN);
   const size_t lds = 8 * wg::SLOT;
   using Kern = void (*)(const unsigned short*, int64_t, const unsigned short*, int64_t, float*, int64_t, int, int,
-                        int, float, int);
+                        int, float, int, const unsigned short*, const unsigned short*, int);
   const int group_m = variant >= 16 ? (int)(variant >> 4) : wg::GROUP_M;  // A/B knob: variant + 16 * group_m
   variant &= 15;
   static const Kern kerns[4][2] = {{wg::wgrad_kernel<false, 8, false>, wg::wgrad_kernel<true, 8, false>},
@@ -403,14 +422,53 @@ void wgrad_gemm_variant_(const at::Tensor& a, const at::Tensor& b, at::Tensor c,
   hipLaunchKernelGGL(kerns[variant][accumulate ? 1 : 0], dim3(nwg), dim3(nthr), lds, cur_stream(),
                      reinterpret_cast<const unsigned short*>(a.data_ptr()), a.stride(0),
                      reinterpret_cast<const unsigned short*>(b.data_ptr()), b.stride(0), c.data_ptr<float>(),
-                     c.stride(0), M, N, K, (float)alpha, group_m);
+                     c.stride(0), M, N, K, (float)alpha, group_m, reinterpret_cast<const unsigned short*>(a2.data_ptr()),
+                     reinterpret_cast<const unsigned short*>(b2.data_ptr()), ns1);
   SXE_LAUNCH_CHECK();
 }
 
-void wgrad_gemm_(const at::Tensor& a, const at::Tensor& b, at::Tensor c, double alpha, bool accumulate) {
+void wgrad_gemm_variant_(const at::Tensor& a, const at::Tensor& b, at::Tensor c, double alpha, bool accumulate,
+                         int64_t variant) {
+  SXE_CHECK(wgrad_supported(a, b, c), "wgrad_gemm_: unsupported shapes/dtypes/strides");
+  const int K = a.size(0);
+  wgrad_launch(a, b, a, b, K, K / wg::SLAB, c, alpha, accumulate, variant);
+}
+
+static int64_t default_variant(const at::Tensor& a, const at::Tensor& b) {
   // 8 lock-step waves; super-rows of 4 M-tiles for tall outputs, 8 otherwise (tools/wgrad_exp.py)
   const int64_t tm = a.size(1) / wg::BM, tn = b.size(1) / wg::BN;
-  wgrad_gemm_variant_(a, b, c, alpha, accumulate, 0 + 16 * (tm >= 4 * tn ? 4 : 8));
+  return 0 + 16 * (tm >= 4 * tn ? 4 : 8);
+}
+
+void wgrad_gemm_(const at::Tensor& a, const at::Tensor& b, at::Tensor c, double alpha, bool accumulate) {
+  wgrad_gemm_variant_(a, b, c, alpha, accumulate, default_variant(a, b));
+}
+
+// c (+)= alpha * [a; a2]^T @ [b; b2] (concatenated along K = rows) without the concatenation:
+// a, a2 [K1 | K2, M], b, b2 [K1 | K2, N], equal leading dims, K1 % 32 == 0, (K1 + K2) % 128 == 0
+bool wgrad2_supported(const at::Tensor& a, const at::Tensor& b, const at::Tensor& a2, const at::Tensor& b2,
+                      const at::Tensor& c) {
+  if (a2.dim() != 2 || b2.dim() != 2 || a2.scalar_type() != a.scalar_type() || b2.scalar_type() != b.scalar_type() ||
+      a2.size(1) != a.size(1) || b2.size(1) != b.size(1) || a2.size(0) != b2.size(0) || a2.stride(1) != 1 ||
+      b2.stride(1) != 1 || a2.stride(0) != a.stride(0) || b2.stride(0) != b.stride(0) || a.size(0) % 32 != 0 ||
+      (reinterpret_cast<uintptr_t>(a2.data_ptr()) % 16) != 0 || (reinterpret_cast<uintptr_t>(b2.data_ptr()) % 16) != 0)
+    return false;
+  const int64_t K = a.size(0) + a2.size(0);
+  if (K % (8 * wg::SLAB) != 0) return false;
+  // the one-segment shape checks, with K = K1 + K2
+  return a.is_cuda() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
+         c.scalar_type() == at::kFloat && a.dim() == 2 && b.dim() == 2 && c.dim() == 2 && a.stride(1) == 1 &&
+         b.stride(1) == 1 && c.stride(1) == 1 && a.size(0) == b.size(0) && c.size(0) == a.size(1) &&
+         c.size(1) == b.size(1) && a.size(1) % wg::BM == 0 && b.size(1) % wg::BN == 0 &&
+         (reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0) && (reinterpret_cast<uintptr_t>(b.data_ptr()) % 16 == 0) &&
+         a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0;
+}
+
+void wgrad_gemm2_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& a2, const at::Tensor& b2, at::Tensor c,
+                  double alpha, bool accumulate) {
+  SXE_CHECK(wgrad2_supported(a, b, a2, b2, c), "wgrad_gemm2_: unsupported shapes/dtypes/strides");
+  const int K = (int)(a.size(0) + a2.size(0));
+  wgrad_launch(a, b, a2, b2, K, (int)(a.size(0) / wg::SLAB), c, alpha, accumulate, default_variant(a, b));
 }
 
 }  // namespace sxe
@@ -418,8 +476,10 @@ void wgrad_gemm_(const at::Tensor& a, const at::Tensor& b, at::Tensor c, double 
 TORCH_LIBRARY_FRAGMENT(sxe, m) {
   m.def("wgrad_gemm_(Tensor a, Tensor b, Tensor(a!) c, float alpha, bool accumulate) -> ()");
   m.def("wgrad_gemm_variant_(Tensor a, Tensor b, Tensor(a!) c, float alpha, bool accumulate, int variant) -> ()");
+  m.def("wgrad_gemm2_(Tensor a, Tensor b, Tensor a2, Tensor b2, Tensor(a!) c, float alpha, bool accumulate) -> ()");
 }
 TORCH_LIBRARY_IMPL(sxe, CUDA, m) {
   m.impl("wgrad_gemm_", &sxe::wgrad_gemm_);
   m.impl("wgrad_gemm_variant_", &sxe::wgrad_gemm_variant_);
+  m.impl("wgrad_gemm2_", &sxe::wgrad_gemm2_);
 }

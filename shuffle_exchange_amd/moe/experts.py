@@ -128,31 +128,54 @@ class _GroupedMM(torch.autograd.Function):
                 w.__dict__.setdefault("_sxe_wstash", []).append((x, dy))
                 return dx, None
             stash = w.__dict__.pop("_sxe_wstash", None)
-            if stash:
+            prev = None  # one stashed micro-step: its (x, dy) are the first K segment of the product
+            if stash and len(stash) == 1:
+                prev = stash[0]
+            elif stash:
                 x = torch.cat([a for a, _ in stash] + [x], dim=1)
                 dy = torch.cat([g for _, g in stash] + [dy], dim=1)
             if tgt is not None:
-                from ..ops.linear import _sxe_wgrad_ok
                 buf, acc = tgt(w)
                 for e in range(E):
-                    if _sxe_wgrad_ok(x[e], dy[e], buf[e]):  # hand-written k-major wgrad GEMM (gemm_wgrad.hip)
-                        torch.ops.sxe.wgrad_gemm_(x[e], dy[e], buf[e], 1.0, bool(acc))
-                    elif buf.dtype == torch.float32 and dy.dtype != torch.float32 and dy.is_cuda:
-                        torch.ops.aten.addmm.dtype_out(buf[e], x[e].t(), dy[e], torch.float32, beta=1 if acc else 0,
-                                                       alpha=1, out=buf[e])
-                    elif buf.dtype != dy.dtype:
-                        d = (x[e].t() @ dy[e]).to(buf.dtype)
-                        buf[e].add_(d) if acc else buf[e].copy_(d)
-                    elif acc:
-                        buf[e].addmm_(x[e].t(), dy[e])
-                    else:
-                        torch.mm(x[e].t(), dy[e], out=buf[e])
+                    if prev is not None:
+                        x1, g1 = prev[0][e], prev[1][e]
+                        if _wgrad2_ok(x1, g1, x[e], dy[e], buf[e]):
+                            torch.ops.sxe.wgrad_gemm2_(x1, g1, x[e], dy[e], buf[e], 1.0, bool(acc))
+                            continue
+                        _expert_wgrad(x1, g1, buf[e], acc)
+                        _expert_wgrad(x[e], dy[e], buf[e], True)
+                        continue
+                    _expert_wgrad(x[e], dy[e], buf[e], acc)
                 w._sxe_grad_done(w)
             else:
                 dw = torch.empty_like(w)
                 for e in range(E):
                     torch.mm(x[e].t(), dy[e], out=dw[e])
         return dx, dw
+
+
+def _expert_wgrad(xe, ge, be, acc):
+    """be (+)= xe^T ge for one expert: the hand-written k-major wgrad GEMM (gemm_wgrad.hip) where its
+    shapes allow, else an fp32-out library GEMM accumulating in its epilogue."""
+    from ..ops.linear import _sxe_wgrad_ok
+    if _sxe_wgrad_ok(xe, ge, be):
+        torch.ops.sxe.wgrad_gemm_(xe, ge, be, 1.0, bool(acc))
+    elif be.dtype == torch.float32 and ge.dtype != torch.float32 and ge.is_cuda:
+        torch.ops.aten.addmm.dtype_out(be, xe.t(), ge, torch.float32, beta=1 if acc else 0, alpha=1, out=be)
+    elif be.dtype != ge.dtype:
+        d = (xe.t() @ ge).to(be.dtype)
+        be.add_(d) if acc else be.copy_(d)
+    elif acc:
+        be.addmm_(xe.t(), ge)
+    else:
+        torch.mm(xe.t(), ge, out=be)
+
+
+def _wgrad2_ok(x1, g1, x2, g2, be):
+    """The two-segment wgrad kernel covers [x1; x2]^T [g1; g2] (no concatenated copy)."""
+    from ..ops.linear import _sxe_wgrad_ok
+    return (_sxe_wgrad_ok(x1, g1, be) and _sxe_wgrad_ok(x2, g2, be) and x1.stride(0) == x2.stride(0)
+            and g1.stride(0) == g2.stride(0))
 
 
 def grouped_mm(x, w):

@@ -285,6 +285,45 @@ def test_wgrad_gemm_vs_fp32_reference(variant, K, M, N, accumulate):
     assert _rel(c, ref) < 1e-5
 
 
+@pytest.mark.parametrize("K1,K2", [(128, 128), (256, 1024), (32, 96), (1024, 0)])
+@pytest.mark.parametrize("accumulate", [True, False])
+def test_wgrad_gemm_two_segments_vs_fp32_reference(K1, K2, accumulate):
+    """wgrad_gemm2_: C (+)= alpha [A1; A2]^T [B1; B2] read from two K segments in place (the deferred
+    expert weight gradients) == fp32 reference of the concatenated product; segments are slices of
+    larger row-major buffers (equal leading dims)."""
+    M, N = 512, 768
+    g = torch.Generator(device="cuda").manual_seed(K1 + 7 * K2)
+    big_a = torch.randn(K1 + K2 + 64, M, device="cuda", generator=g).bfloat16()
+    big_b = torch.randn(K1 + K2 + 64, N, device="cuda", generator=g).bfloat16()
+    a1, a2 = big_a[:K1], big_a[K1 + 64:]
+    b1, b2 = big_b[:K1], big_b[K1 + 64:]
+    c = torch.randn(M, N, device="cuda", generator=g)
+    ref = (c if accumulate else torch.zeros_like(c)) + 0.5 * (torch.cat([a1, a2]).float().t() @ torch.cat([b1, b2]).float())
+    torch.ops.sxe.wgrad_gemm2_(a1, b1, a2, b2, c, 0.5, accumulate)
+    assert _rel(c, ref) < 1e-5
+
+
+def test_grouped_mm_deferred_wgrad_two_segment_kernel_matches():
+    """moe/experts.py: a weight gradient deferred over two micro-steps goes through wgrad_gemm2_ at the
+    boundary (no concatenation) and equals the fp32 sum of both micro-steps."""
+    from shuffle_exchange_amd.moe import experts as E
+    w = torch.nn.Parameter(torch.randn(2, 512, 768, device="cuda", dtype=torch.bfloat16) * 0.02)
+    buf = torch.full((2, 512, 768), float("nan"), device="cuda")
+    st = {"valid": False, "boundary": False, "done": 0}
+    w._sxe_grad_target = lambda p: (buf, st["valid"])
+    w._sxe_grad_done = lambda p: st.update(valid=True, done=st["done"] + 1)
+    w._sxe_grad_defer = lambda p: not st["boundary"]
+    ref = torch.zeros(2, 512, 768, device="cuda")
+    for k in range(2):
+        st["boundary"] = k == 1
+        x = torch.randn(2, 256, 512, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+        gy = torch.randn(2, 256, 768, device="cuda", dtype=torch.bfloat16)
+        ref += torch.einsum("eck,ecn->ekn", x.detach().float(), gy.float())
+        E.grouped_mm(x, w).backward(gy)
+    assert st["done"] == 1 and E._wgrad2_ok(x.detach()[0], gy[0], x.detach()[0], gy[0], buf[0])
+    assert _rel(buf, ref) < 1e-5
+
+
 def test_linear_weight_grad_uses_wgrad_kernel_and_matches():
     """ops/linear routes a (4096 x 4096)-class fp32-accumulated weight gradient through the HIP kernel;
     result == fp32 reference accumulated over two micro-steps."""
