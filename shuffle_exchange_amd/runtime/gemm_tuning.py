@@ -30,7 +30,13 @@ def load_tuned_gemms(path=None):
         return True
     tun = torch.cuda.tunable
     tun.enable(True)
-    tun.tuning_enable(False)
+    # SXE_GEMM_TUNE_OUT=<csv>: tune the shapes this run meets that the table lacks (bounded search per
+    # shape) and write the table there -- merge it into the packaged file with tools/merge_tunableop.py
+    out = os.environ.get("SXE_GEMM_TUNE_OUT")
+    tun.tuning_enable(bool(out))
+    if out:
+        tun.set_filename(out)
+        tun.set_max_tuning_duration(int(os.environ.get("SXE_GEMM_TUNE_MS", "200")))
     # the table must have LF line endings: with CRLF the last validator's value carries a '\r'
     # and TunableOp rejects the whole file ("Failed validator: ROCBLAS_VERSION")
     ok = tun.read_file(path)
