@@ -303,24 +303,31 @@ def test_wgrad_gemm_two_segments_vs_fp32_reference(K1, K2, accumulate):
     assert _rel(c, ref) < 1e-5
 
 
-def test_grouped_mm_deferred_wgrad_two_segment_kernel_matches():
+def test_grouped_mm_deferred_wgrad_two_segment_kernel_matches(monkeypatch):
     """moe/experts.py: a weight gradient deferred over two micro-steps goes through wgrad_gemm2_ at the
     boundary (no concatenation) and equals the fp32 sum of both micro-steps."""
     from shuffle_exchange_amd.moe import experts as E
-    w = torch.nn.Parameter(torch.randn(2, 512, 768, device="cuda", dtype=torch.bfloat16) * 0.02)
-    buf = torch.full((2, 512, 768), float("nan"), device="cuda")
-    st = {"valid": False, "boundary": False, "done": 0}
+    w = torch.nn.Parameter(torch.randn(1, 4096, 4096, device="cuda", dtype=torch.bfloat16) * 0.02)
+    buf = torch.full((1, 4096, 4096), float("nan"), device="cuda")
+    st = {"valid": False, "boundary": False, "done": 0, "two": 0}
     w._sxe_grad_target = lambda p: (buf, st["valid"])
     w._sxe_grad_done = lambda p: st.update(valid=True, done=st["done"] + 1)
     w._sxe_grad_defer = lambda p: not st["boundary"]
-    ref = torch.zeros(2, 512, 768, device="cuda")
+    real = E._wgrad2_ok
+
+    def counted(*a):
+        ok = real(*a)
+        st["two"] += ok
+        return ok
+    monkeypatch.setattr(E, "_wgrad2_ok", counted)
+    ref = torch.zeros(1, 4096, 4096, device="cuda")
     for k in range(2):
         st["boundary"] = k == 1
-        x = torch.randn(2, 256, 512, device="cuda", dtype=torch.bfloat16, requires_grad=True)
-        gy = torch.randn(2, 256, 768, device="cuda", dtype=torch.bfloat16)
+        x = torch.randn(1, 256, 4096, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+        gy = torch.randn(1, 256, 4096, device="cuda", dtype=torch.bfloat16)
         ref += torch.einsum("eck,ecn->ekn", x.detach().float(), gy.float())
         E.grouped_mm(x, w).backward(gy)
-    assert st["done"] == 1 and E._wgrad2_ok(x.detach()[0], gy[0], x.detach()[0], gy[0], buf[0])
+    assert st["done"] == 1 and st["two"] == 1
     assert _rel(buf, ref) < 1e-5
 
 
