@@ -114,7 +114,7 @@ __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >
 // product over the concatenated token axis without materialising the concatenation (the deferred
 // expert weight gradients of moe/experts.py: the stashed micro-step, then the boundary one).
 // ns1 = K / 16 (and A2 = A, B2 = B) for one segment.
-template <bool ACCUM, int R, bool STAGGER, bool NODMA = false>
+template <bool ACCUM, int R, bool STAGGER, bool NODMA = false, bool SEG2 = false>
 __global__ void __launch_bounds__(NTHR, 1) wgrad_kernel(const unsigned short* __restrict__ A, int64_t lda,
                                                         const unsigned short* __restrict__ B, int64_t ldb,
                                                         float* __restrict__ C, int64_t ldc, int M, int N, int K,
@@ -177,9 +177,11 @@ __global__ void __launch_bounds__(NTHR, 1) wgrad_kernel(const unsigned short* __
   };
   const unsigned lds_base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   const DmaPlan dp = dma_plan(A, lda, B, ldb, m0, n0, lds_base);
-  const DmaPlan dp2 = dma_plan(A2, lda, B2, ldb, m0, n0, lds_base);
+  // one-segment instantiations keep the original single DMA plan (SEG2 = false: no second plan's
+  // registers, no per-slab segment test)
+  const DmaPlan dp2 = SEG2 ? dma_plan(A2, lda, B2, ldb, m0, n0, lds_base) : dp;
   auto load_any = [&](int slab, int slot) {  // slab in the first or the second K segment (wave-uniform)
-    if (slab < ns1)
+    if (!SEG2 || slab < ns1)
       load_slab(dp, lda, ldb, slab, slot);
     else
       load_slab(dp2, lda, ldb, slab - ns1, slot);
@@ -397,7 +399,7 @@ bool wgrad_supported(const at::Tensor& a, const at::Tensor& b, const at::Tensor&
 // c (+)= alpha * a^T @ b ; a: [K, M] bf16, b: [K, N] bf16, c: [M, N] fp32.
 // variant: 0 = 8 lock-step waves, 1 = 8 staggered waves, 2 = 4 waves of 128 x 128, for in-process A/B.
 static void wgrad_launch(const at::Tensor& a, const at::Tensor& b, const at::Tensor& a2, const at::Tensor& b2, int K,
-                         int ns1, at::Tensor c, double alpha, bool accumulate, int64_t variant) {
+                         int ns1, at::Tensor c, double alpha, bool accumulate, int64_t variant, bool seg2 = false) {
   c10::DeviceGuard g(a.device());
   const int M = a.size(1), N = b.size(1);
   const int nwg = (M / wg::BM) * (N / wg::BN);
@@ -406,10 +408,12 @@ static void wgrad_launch(const at::Tensor& a, const at::Tensor& b, const at::Ten
                         int, float, int, const unsigned short*, const unsigned short*, int);
   const int group_m = variant >= 16 ? (int)(variant >> 4) : wg::GROUP_M;  // A/B knob: variant + 16 * group_m
   variant &= 15;
-  static const Kern kerns[4][2] = {{wg::wgrad_kernel<false, 8, false>, wg::wgrad_kernel<true, 8, false>},
+  static const Kern kerns[5][2] = {{wg::wgrad_kernel<false, 8, false>, wg::wgrad_kernel<true, 8, false>},
                                    {wg::wgrad_kernel<false, 8, true>, wg::wgrad_kernel<true, 8, true>},
                                    {wg::w4::kernel<false>, wg::w4::kernel<true>},
-                                   {wg::wgrad_kernel<false, 8, false, true>, wg::wgrad_kernel<true, 8, false, true>}};
+                                   {wg::wgrad_kernel<false, 8, false, true>, wg::wgrad_kernel<true, 8, false, true>},
+                                   {wg::wgrad_kernel<false, 8, false, false, true>,
+                                    wg::wgrad_kernel<true, 8, false, false, true>}};
   static bool attr_set = [&] {
     for (auto& row : kerns)
       for (Kern k : row)
@@ -418,8 +422,9 @@ static void wgrad_launch(const at::Tensor& a, const at::Tensor& b, const at::Ten
   }();
   (void)attr_set;
   SXE_CHECK(variant >= 0 && variant <= 3, "wgrad_gemm_: variant must be 0..3");
+  SXE_CHECK(!seg2 || variant == 0, "wgrad_gemm2_: the 8-wave lock-step schedule only");
   const int nthr = variant == 2 ? wg::w4::NTHR : wg::NTHR;
-  hipLaunchKernelGGL(kerns[variant][accumulate ? 1 : 0], dim3(nwg), dim3(nthr), lds, cur_stream(),
+  hipLaunchKernelGGL(kerns[seg2 ? 4 : variant][accumulate ? 1 : 0], dim3(nwg), dim3(nthr), lds, cur_stream(),
                      reinterpret_cast<const unsigned short*>(a.data_ptr()), a.stride(0),
                      reinterpret_cast<const unsigned short*>(b.data_ptr()), b.stride(0), c.data_ptr<float>(),
                      c.stride(0), M, N, K, (float)alpha, group_m, reinterpret_cast<const unsigned short*>(a2.data_ptr()),
@@ -468,7 +473,7 @@ void wgrad_gemm2_(const at::Tensor& a, const at::Tensor& b, const at::Tensor& a2
                   double alpha, bool accumulate) {
   SXE_CHECK(wgrad2_supported(a, b, a2, b2, c), "wgrad_gemm2_: unsupported shapes/dtypes/strides");
   const int K = (int)(a.size(0) + a2.size(0));
-  wgrad_launch(a, b, a2, b2, K, (int)(a.size(0) / wg::SLAB), c, alpha, accumulate, default_variant(a, b));
+  wgrad_launch(a, b, a2, b2, K, (int)(a.size(0) / wg::SLAB), c, alpha, accumulate, default_variant(a, b), true);
 }
 
 }  // namespace sxe
