@@ -3,6 +3,9 @@
 set -o pipefail
 O=gpurun_out/r06/final
 mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "wgrad" \
+    > $O/wgrad_tests.log 2>&1 || { tail -30 $O/wgrad_tests.log; exit 1; }
+tail -1 $O/wgrad_tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -30 $O/smoke.log; exit 1; }
 echo "smoke ok"
 for cfg in llama8b-z3 mixtral-ep llama8b-sp32k llama70b-infinity; do
