@@ -9,7 +9,6 @@ Every expert parameter is tagged ``allreduce = False`` and ``group_name`` (refer
 so the ZeRO optimizers reduce its gradient over the expert-data-parallel group only.
 """
 import copy
-
 import os
 
 import torch
@@ -19,39 +18,6 @@ from ..ops.activation import swiglu
 
 # SXE_MOE_DEFER_WGRAD=0: write the expert weight gradients every micro-step (see _GroupedMM)
 DEFER_WGRAD = os.environ.get("SXE_MOE_DEFER_WGRAD", "1") == "1"
-# SXE_MOE_STREAMS=n: issue the per-expert GEMMs round-robin on n HIP streams so one expert's partial
-# last wave of tiles overlaps the next expert's GEMM (a [1280, 4096] x [4096, 28672] product is 2.2
-# waves of 256 x 256 tiles over the 256 CUs); 1 = all on the current stream
-MOE_STREAMS = int(os.environ.get("SXE_MOE_STREAMS", "1"))
-_streams = {}
-
-
-def _expert_streams(device):
-    """n side streams for the per-expert GEMM loop (None on CPU / n = 1)."""
-    if MOE_STREAMS <= 1 or device.type != "cuda":
-        return None
-    key = (device, MOE_STREAMS)
-    if key not in _streams:
-        _streams[key] = [torch.cuda.Stream(device=device) for _ in range(MOE_STREAMS)]
-    return _streams[key]
-
-
-def _per_expert(E, device, fn):
-    """Run fn(e) for every expert, round-robin over the side streams when enabled: every stream first
-    waits for the current stream's work, and the current stream waits for all of them at the end."""
-    ss = _expert_streams(device)
-    if ss is None:
-        for e in range(E):
-            fn(e)
-        return
-    cur = torch.cuda.current_stream(device)
-    for st in ss:
-        st.wait_stream(cur)
-    for e in range(E):
-        with torch.cuda.stream(ss[e % len(ss)]):
-            fn(e)
-    for st in ss:
-        cur.wait_stream(st)
 
 
 class Experts(nn.Module):
@@ -135,7 +101,8 @@ class _GroupedMM(torch.autograd.Function):
         E, C, _ = x.shape
         x = x.contiguous()
         y = x.new_empty(E, C, w.shape[2])
-        _per_expert(E, x.device, lambda e: torch.mm(x[e], w[e], out=y[e]))
+        for e in range(E):
+            torch.mm(x[e], w[e], out=y[e])
         ctx.save_for_backward(x, w)
         return y
 
@@ -147,7 +114,8 @@ class _GroupedMM(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            _per_expert(E, x.device, lambda e: torch.mm(dy[e], w[e].t(), out=dx[e]))
+            for e in range(E):
+                torch.mm(dy[e], w[e].t(), out=dx[e])
         if ctx.needs_input_grad[1]:
             from ..ops.linear import grad_target
             tgt = grad_target(w)
