@@ -25,7 +25,7 @@ import torch.nn.functional as F
 from ..ops.mlp import swiglu_mlp
 from ..runtime.activation_checkpointing.checkpointing import checkpoint
 from ..runtime.zero.partition_parameters import local_shard
-from ..ops.attention import attention_qkv_rope
+from ..ops.attention import attention_qkv_rope, qkv_proj_attention
 from ..ops.cross_entropy import fused_linear_cross_entropy
 from ..ops.linear import Embedding, Linear, linear
 from ..ops.norm import RMSNorm
@@ -124,8 +124,13 @@ class LlamaAttention(nn.Module):
 
     def forward(self, x, rope: RopeCache, position_ids=None):
         B, S, _ = x.shape
-        qkv = self.qkv_proj(x).view(B, S, self.nq + 2 * self.nkv, self.d)
         spg = _sp_group() if self.cfg.sequence_parallel else None
+        if not self.cfg.fpdt_chunk_size and spg is None:
+            # QKV projection + attention as one node: its weight gradient runs on token-minor
+            # operands (ops/attention.py _QKVProjAttn)
+            o = qkv_proj_attention(x, self.qkv_proj, self.nq, self.nkv, rope, position_ids, causal=True)
+            return self.o_proj(o.reshape(B, S, self.nq * self.d))
+        qkv = self.qkv_proj(x).view(B, S, self.nq + 2 * self.nkv, self.d)
         if self.cfg.fpdt_chunk_size:
             from ..sequence.fpdt_layer import fpdt_attention
             from .. import comm as dist

@@ -202,6 +202,72 @@ def attention_qkv_rope(qkv, nq, nkv, rope=None, position_ids=None, causal=True, 
     return attention(q, k, v, causal, scale)
 
 
+QKV_TN = os.environ.get("SXE_QKV_TN", "1") == "1"
+
+
+class _QKVProjAttn(torch.autograd.Function):
+    """QKV projection + RoPE + attention as ONE autograd node (GPU bf16 training). It keeps x^T
+    (token-minor) instead of x and transposes dqkv in the backward, so the QKV weight gradient runs
+    as hipBLASLt's TN fp32-out GEMM (0.62 ms at 16k tokens x 6144 x 4096) instead of the token-major
+    NT one (0.84 ms); the two transposes cost ~0.13 ms (profiles/r06/wgrad_variants_16k.log)."""
+
+    @staticmethod
+    def forward(ctx, x, w, cos, sin, nq, nkv, causal, scale, pos):
+        B, S, H = x.shape
+        x2 = x.reshape(-1, H)
+        qkv = F.linear(x2, w).view(B, S, nq + 2 * nkv, -1)
+        if cos is not None:
+            torch.ops.sxe.rope_(qkv[:, :, :nq + nkv], cos, sin, pos, S, 0, False)
+        q, k, v = qkv[:, :, :nq], qkv[:, :, nq:nq + nkv], qkv[:, :, nq + nkv:]
+        o, lse = torch.ops.sxe.flash_attn_fwd(q, k, v, bool(causal), float(scale))
+        xT = torch.ops.sxe.transpose16(x2) if ctx.needs_input_grad[1] else None
+        ctx.save_for_backward(xT, qkv, o, lse, cos, sin, pos, w)
+        ctx.meta = (nq, nkv, causal, scale, x.shape)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        xT, qkv, o, lse, cos, sin, pos, w = ctx.saved_tensors
+        nq, nkv, causal, scale, x_shape = ctx.meta
+        dqkv = torch.empty_like(qkv)
+        q, k, v = qkv[:, :, :nq], qkv[:, :, nq:nq + nkv], qkv[:, :, nq + nkv:]
+        dq, dk, dv = dqkv[:, :, :nq], dqkv[:, :, nq:nq + nkv], dqkv[:, :, nq + nkv:]
+        torch.ops.sxe.flash_attn_bwd(do.contiguous(), q, k, v, o, lse, dq, dk, dv, bool(causal), float(scale))
+        del q, k, v, o, lse, qkv
+        if cos is not None:
+            torch.ops.sxe.rope_(dqkv[:, :, :nq + nkv], cos, sin, pos, dqkv.shape[1], 0, True)
+        d2 = dqkv.view(-1, w.shape[0])
+        from .linear import data_grad
+        from .mlp import weight_grad_tn
+        dx = data_grad(d2, w).view(x_shape) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = weight_grad_tn(w, torch.ops.sxe.transpose16(d2), xT, fp32_out=True)
+        return dx, dw, None, None, None, None, None, None, None
+
+
+def qkv_proj_attention(x, qkv_proj, nq, nkv, rope=None, position_ids=None, causal=True, softmax_scale=None):
+    """``attention_qkv_rope(qkv_proj(x))`` for x [B, S, H]; one fused autograd node (``_QKVProjAttn``)
+    when the shapes, dtypes and the plain bias-free projection allow, else the two-step path."""
+    B, S, H = x.shape
+    w = getattr(qkv_proj, "weight", None)
+    from .mlp import _plain
+    N = (nq + 2 * nkv)
+    if (QKV_TN and x.is_cuda and x.dtype == torch.bfloat16 and torch.is_grad_enabled() and _plain(qkv_proj)
+            and (w.requires_grad or x.requires_grad) and (B * S) % 64 == 0 and H % 64 == 0 and w.shape[1] == H
+            and w.shape[0] % (64 * N) == 0 and native.use_hip(x)):
+        D = w.shape[0] // N
+        # hip_supported() for the q / k / v views of a fresh contiguous [B, S, N, D] projection
+        if D in HEAD_DIMS and S % TILE == 0 and nq % nkv == 0 and os.environ.get("SXE_ATTN_BACKEND") != "sdpa":
+            scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(D)
+            pos = position_ids.reshape(-1).contiguous().long() if position_ids is not None else None
+            cos = rope.cos if rope is not None else None
+            sin = rope.sin if rope is not None else None
+            return _QKVProjAttn.apply(x, w, cos, sin, nq, nkv, causal, scale, pos)
+    qkv = qkv_proj(x).view(B, S, N, -1)
+    return attention_qkv_rope(qkv, nq, nkv, rope, position_ids, causal, softmax_scale)
+
+
 def attention_with_lse(q, k, v, causal=True, softmax_scale=None):
     """Forward-only attention returning (out [B,S,H,D], lse [B,H,S]) for chunk merging (FPDT)."""
     scale = softmax_scale if softmax_scale is not None else 1.0 / math.sqrt(q.shape[-1])

@@ -6,8 +6,13 @@ buffer is overwritten in place with d(loss)/d(logits) during the forward (loss i
 terminal node, so the gradient is known up to the scalar upstream factor), the backward is just two
 GEMMs. Peak memory is one bf16 [T, V] buffer instead of logits + fp32 softmax + grad, and
 ``chunk_tokens`` bounds even that (ALST's TiledLoss, reference
-runtime/sequence_parallel/ulysses_sp.py:915, plays the same role).
+runtime/sequence_parallel/ulysses_sp.py:915, plays the same role). On bf16 GPU training steps whose
+shapes fit its tile, the gradient is instead written in the backward by ``xent_grad_dual``
+(token-major over the logits + vocab-major copy for the TN weight-gradient GEMM, upstream scalar
+folded in).
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -46,6 +51,17 @@ def cross_entropy(logits, target, ignore_index=-100, reduction="mean"):
     return per_tok.sum() / n
 
 
+DUAL = os.environ.get("SXE_XENT_DUAL", "1") == "1"
+
+
+def _dual_ok(h2, weight):
+    """The dual-layout gradient path applies: bf16 GPU operands, tokens % 64, vocab % 256, hidden % 64
+    (the kernel's tile and the transpose kernel's)."""
+    return (DUAL and h2.is_cuda and h2.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+            and weight.dim() == 2 and h2.shape[0] % 64 == 0 and h2.shape[0] > 0 and weight.shape[0] % 256 == 0
+            and h2.shape[1] % 64 == 0 and h2.is_contiguous() and native.use_hip(h2))
+
+
 class _FusedLinearXEnt(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, weight, target, ignore_index, chunk_tokens, reduction="mean"):
@@ -60,6 +76,17 @@ class _FusedLinearXEnt(torch.autograd.Function):
         inv_n = (1.0 / n_valid).reshape(1)
         need_grad = torch.is_grad_enabled() or h.requires_grad or weight.requires_grad
         chunk = T if not chunk_tokens else min(int(chunk_tokens), T)
+        if chunk == T and need_grad and _dual_ok(h2, weight):
+            # dual layout: the forward computes only loss + lse; the backward writes the scaled
+            # gradient over the logits AND its vocab-major transpose in one pass (xent_grad_dual),
+            # so the LM-head weight gradient is a TN GEMM with no transpose of the 4 GB gradient
+            logits = torch.matmul(h2, weight.t())
+            loss, lse = torch.ops.sxe.xent_fwd(logits, tgt, int(ignore_index), False, None, 1.0)
+            ctx.save_for_backward(logits, lse, tgt, inv_n, h2, weight)
+            ctx.mode = "dual"
+            ctx.ignore_index = int(ignore_index)
+            ctx.hshape = h.shape
+            return loss.sum() / n_valid
         if chunk == T:
             # unchunked: keep d(loss)/d(logits) (written over the logits) and do both GEMMs in
             # backward, where the weight-grad GEMM can land directly in the optimizer's buffer
@@ -93,6 +120,18 @@ class _FusedLinearXEnt(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gout):
+        if ctx.mode == "dual":
+            logits, lse, tgt, inv_n, h2, weight = ctx.saved_tensors
+            gT = torch.ops.sxe.xent_grad_dual(logits, tgt, lse, ctx.ignore_index, inv_n,
+                                              gout.detach().float().reshape(1).contiguous())
+            from .linear import data_grad
+            from .mlp import weight_grad_tn
+            dh = data_grad(logits, weight).view(ctx.hshape)  # logits now hold the gradient
+            del logits
+            dW = None
+            if ctx.needs_input_grad[1]:
+                dW = weight_grad_tn(weight, gT, torch.ops.sxe.transpose16(h2))
+            return dh, dW, None, None, None, None
         if ctx.mode == "dlogits":
             dl, h2, weight = ctx.saved_tensors
             dl.mul_(gout.to(dl.dtype))  # upstream scalar (1/GAS, loss scale, ...), in place

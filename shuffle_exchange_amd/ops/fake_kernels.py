@@ -90,6 +90,11 @@ def _xent_bwd(logits, target, lse, dloss, ignore_index, inplace):
     return torch.empty_like(logits)
 
 
+@_reg("sxe::xent_grad_dual")
+def _xent_grad_dual(logits, target, lse, ignore_index, scale_a, scale_b):
+    return logits.new_empty((logits.shape[1], logits.shape[0]))
+
+
 @_reg("sxe::transpose16")
 def _transpose16(x):
     return x.new_empty((x.shape[1], x.shape[0]))

@@ -1,0 +1,116 @@
+"""Dual-layout backward paths (GPU): the LM-head gradient kernel that writes g and g^T
+(xent_grad_dual), the fused LM-head loss on that path, and the fused QKV projection + attention
+node whose weight gradient runs as a TN GEMM -- each against a plain fp32 PyTorch reference."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    from shuffle_exchange_amd.ops import native
+    native.require_hip()
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def test_xent_grad_dual_kernel():
+    torch.manual_seed(0)
+    T, V = 192, 1280
+    logits = (torch.randn(T, V, device="cuda") * 3).to(torch.bfloat16)
+    tgt = torch.randint(0, V, (T,), device="cuda")
+    tgt[5] = -100
+    tgt[100] = V - 1
+    ref_in = logits.float()
+    lse = torch.logsumexp(ref_in, dim=-1)
+    sa = torch.tensor([0.25], device="cuda")
+    sb = torch.tensor([3.0], device="cuda")
+    ref = torch.softmax(ref_in, dim=-1)
+    ref[torch.arange(T, device="cuda")[tgt >= 0], tgt[tgt >= 0]] -= 1.0
+    ref *= 0.75
+    ref[tgt < 0] = 0
+    buf = logits.clone()
+    gT = torch.ops.sxe.xent_grad_dual(buf, tgt, lse, -100, sa, sb)
+    assert gT.shape == (V, T)
+    assert _rel(buf, ref) < 1e-2
+    assert torch.equal(gT, buf.t().contiguous())
+    assert buf[5].abs().max().item() == 0.0
+
+
+def test_fused_linear_xent_dual_path_matches_reference():
+    from shuffle_exchange_amd.ops import cross_entropy as CE
+    torch.manual_seed(1)
+    T, H, V = 256, 128, 2048
+    h = (torch.randn(T, H, device="cuda") * 0.5).to(torch.bfloat16).requires_grad_()
+    W = (torch.randn(V, H, device="cuda") * 0.05).to(torch.bfloat16).requires_grad_()
+    tgt = torch.randint(0, V, (T,), device="cuda")
+    tgt[:9] = -100
+    assert CE._dual_ok(h, W)
+    loss = CE.fused_linear_cross_entropy(h, W, tgt)
+    (loss * 0.5).backward()
+    h2, W2 = h.detach().float().requires_grad_(), W.detach().float().requires_grad_()
+    ref = F.cross_entropy(h2 @ W2.t(), tgt, ignore_index=-100)
+    (ref * 0.5).backward()
+    assert abs(loss.item() - ref.item()) < 1e-2 * abs(ref.item())
+    assert _rel(h.grad, h2.grad) < 3e-2 and _rel(W.grad, W2.grad) < 3e-2
+
+
+def test_fused_linear_xent_dual_writes_grad_target():
+    """The LM-head weight gradient lands in the optimizer's fp32 accumulator (accumulate on)."""
+    from shuffle_exchange_amd.ops import cross_entropy as CE
+    torch.manual_seed(2)
+    T, H, V = 128, 128, 1024
+    h = (torch.randn(T, H, device="cuda") * 0.5).to(torch.bfloat16).requires_grad_()
+    W = torch.nn.Parameter((torch.randn(V, H, device="cuda") * 0.05).to(torch.bfloat16))
+    buf = torch.full((V, H), 1.0, device="cuda")
+    done = []
+    W._sxe_grad_target = lambda p: (buf, True)
+    W._sxe_grad_done = lambda p: done.append(1)
+    tgt = torch.randint(0, V, (T,), device="cuda")
+    CE.fused_linear_cross_entropy(h, W, tgt).backward()
+    assert W.grad is None and done == [1]
+    W2 = W.detach().float().requires_grad_()
+    F.cross_entropy(h.detach().float() @ W2.t(), tgt).backward()
+    assert _rel(buf - 1.0, W2.grad) < 3e-2
+
+
+@pytest.mark.parametrize("target", [False, True])
+def test_qkv_proj_attention_matches_unfused(target):
+    from shuffle_exchange_amd.ops.attention import _QKVProjAttn, qkv_proj_attention, reference_attention
+    from shuffle_exchange_amd.ops.linear import Linear
+    from shuffle_exchange_amd.ops.rope import RopeCache, _ref_rope
+    torch.manual_seed(3)
+    B, S, H, nq, nkv, D = 2, 256, 512, 4, 2, 128
+    cache = RopeCache(D, 512, 500000.0, device="cuda")
+    proj = Linear(H, (nq + 2 * nkv) * D, bias=False, init_std=0.02).to(device="cuda", dtype=torch.bfloat16)
+    x = (torch.randn(B, S, H, device="cuda") * 0.5).to(torch.bfloat16).requires_grad_()
+    buf = torch.zeros(proj.weight.shape, device="cuda")
+    if target:
+        proj.weight._sxe_grad_target = lambda p: (buf, True)
+        proj.weight._sxe_grad_done = lambda p: None
+    seen = []
+    orig = _QKVProjAttn.apply
+    _QKVProjAttn.apply = lambda *a: (seen.append(1), orig(*a))[1]
+    try:
+        o = qkv_proj_attention(x, proj, nq, nkv, cache)
+    finally:
+        _QKVProjAttn.apply = orig
+    assert seen == [1], "fused node not taken"
+    x2 = x.detach().float().requires_grad_()
+    w2 = proj.weight.detach().float().requires_grad_()
+    qkv = (x2 @ w2.t()).view(B, S, nq + 2 * nkv, D)
+    pos = torch.arange(S, device="cuda").repeat(B)
+    rot = _ref_rope(qkv[:, :, :nq + nkv].reshape(B * S, nq + nkv, D), cache.cos, cache.sin, pos).view(B, S, nq + nkv, D)
+    o2 = reference_attention(rot[:, :, :nq], rot[:, :, nq:], qkv[:, :, nq + nkv:], causal=True)
+    assert _rel(o, o2) < 2e-2
+    do = torch.randn_like(o2)
+    (o.float() * do).sum().backward()
+    (o2 * do).sum().backward()
+    assert _rel(x.grad, x2.grad) < 3e-2
+    dw = buf if target else proj.weight.grad
+    assert proj.weight.grad is None if target else True
+    assert _rel(dw, w2.grad) < 3e-2
