@@ -43,6 +43,33 @@ def dual_variant(inter):
     return 4 if inter % 256 == 0 else 1 if inter % 128 == 0 else 0
 
 
+STASH = os.environ.get("SXE_WGRAD_STASH", "1") == "1"
+
+
+def _may_stash(w, gyT):
+    """The optimizer lets this micro-step's weight gradient be written late (``_sxe_grad_defer``:
+    before the accumulation boundary, single-rank fp32 accumulator) and the pair kernel applies."""
+    defer = getattr(w, "_sxe_grad_defer", None)
+    return STASH and defer is not None and gyT.is_cuda and gyT.dtype == torch.bfloat16 and defer(w)
+
+
+def flush_stashed_wgrad(w):
+    """Write a stashed bf16 weight gradient that no later micro-step consumed (the parameter got no
+    gradient at the accumulation boundary) into the optimizer's target."""
+    stash = w.__dict__.pop("_sxe_bstash", None)
+    if stash is None:
+        return
+    buf, accumulate = w._sxe_grad_target(w)
+    b2 = buf.view(w.shape)
+    b2.add_(stash) if accumulate else b2.copy_(stash)
+    w._sxe_grad_done(w)
+
+
+def drop_stashed_wgrad(w):
+    """zero_grad before the boundary: the partial accumulation is discarded with the rest."""
+    w.__dict__.pop("_sxe_bstash", None)
+
+
 def weight_grad_tn(w, gyT, xT, fp32_out=False):
     """dW = gyT @ xT^T (gyT [N, T], xT [K, T], both token-minor): written into the optimizer's
     target for ``w`` when it has one (returns None), else returned. ``fp32_out``: an fp32
@@ -53,7 +80,24 @@ def weight_grad_tn(w, gyT, xT, fp32_out=False):
     dw = None
     if tgt is None:
         return torch.mm(gyT, xT.t())
+    stash = w.__dict__.pop("_sxe_bstash", None)
+    if stash is None and not fp32_out and _may_stash(w, gyT):
+        # before the accumulation boundary of a single-rank unit: keep this micro-step's bf16 product
+        # and fold it into the accumulator together with the next one (acc2_bf16_: one fp32 pass
+        # for the pair instead of one per micro-step); _sxe_grad_done runs with that write
+        w.__dict__["_sxe_bstash"] = torch.mm(gyT, xT.t())
+        return None
     buf, accumulate = tgt(w)
+    if stash is not None:
+        dw = torch.mm(gyT, xT.t())
+        if buf.dtype == torch.float32 and buf.is_contiguous():
+            torch.ops.sxe.acc2_bf16_(buf, stash, dw.view_as(stash), bool(accumulate))
+        else:
+            b2 = buf.view(w.shape)
+            b2.add_(stash) if accumulate else b2.copy_(stash)
+            b2.add_(dw)
+        w._sxe_grad_done(w)
+        return None
     if buf.dtype == gyT.dtype and not accumulate and buf.is_contiguous():
         torch.mm(gyT, xT.t(), out=buf.view(w.shape))  # bf16 reduce-scatter slot of a multi-rank unit
     elif fp32_out and buf.dtype == torch.float32 and buf.is_contiguous():

@@ -266,9 +266,12 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         and, for ZeRO-1 at the boundary, everything still pending."""
         if self.micro_step_boundary:
             from ...moe.experts import flush_deferred_wgrad
+            from ...ops.mlp import flush_stashed_wgrad
             for p in self.param_unit:
                 if p.__dict__.get("_sxe_wstash"):  # deferred weight grads no boundary backward consumed
                     flush_deferred_wgrad(p)
+                if p.__dict__.get("_sxe_bstash") is not None:  # held bf16 weight grads (ops/mlp.py)
+                    flush_stashed_wgrad(p)
         if self.stage == 1 and not self.micro_step_boundary:
             if self.fp32_accum:  # the fp32 staging sums carry into the next micro-step
                 for units in self.units:
@@ -317,6 +320,8 @@ class ZeroStage12Optimizer(ZeroOptimizerBase):
         memset: each slot's first write of the next step overwrites and the slots no gradient
         reached are zeroed right before the update (_zero_stale). Units that reduce-scatter into
         their accumulator (add_) are zeroed as before."""
+        for p in self.param_unit:
+            p.__dict__.pop("_sxe_bstash", None)  # a partial accumulation goes with the rest
         multi = [u for units in self.units for u in units if u.topo.S > 1]
         if len(multi) == sum(len(us) for us in self.units):
             return super().zero_grad_buffers()

@@ -425,6 +425,14 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             # fused weight-grad GEMMs (ops/linear.py) write straight into the unit's buffers
             p._sxe_grad_target = self._grad_target
             p._sxe_grad_done = self._grad_done
+            p._sxe_grad_defer = self._grad_defer
+
+    def _grad_defer(self, p):
+        """May a weight-gradient producer hold this micro-step's contribution and write it with a
+        later one (ops/mlp.py weight_grad_tn)? Before the accumulation boundary, for a persistent
+        single-rank unit: its fp32 accumulator is read by nothing until the optimizer step."""
+        u = self.param_unit.get(p)
+        return not self._boundary and u is not None and u.persistent and self.S == 1
 
     # ---------------------------------------------------------------------- FX graph mode
     def enter_graph_mode(self):
@@ -833,6 +841,8 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
             for u in units:
                 u.acc_valid = [False] * len(u.params)
                 u.rs_valid = False
+                for p in u.params:
+                    p.__dict__.pop("_sxe_bstash", None)  # a partial accumulation goes with the rest
 
     def _zero_stale(self):
         if self.host_step is not None:
@@ -896,6 +906,11 @@ class ZeroStage3Optimizer(ZeroOptimizerBase):
         self._boundary = bool(flag)
 
     def reduce_gradients(self, pipeline_parallel=False):
+        if self._boundary:
+            from ...ops.mlp import flush_stashed_wgrad
+            for p in self.param_unit:
+                if p.__dict__.get("_sxe_bstash") is not None:  # held weight grads the boundary did not consume
+                    flush_stashed_wgrad(p)
         for units in self.units:
             for u in units:
                 if u.pending > 0:

@@ -114,3 +114,54 @@ def test_qkv_proj_attention_matches_unfused(target):
     dw = buf if target else proj.weight.grad
     assert proj.weight.grad is None if target else True
     assert _rel(dw, w2.grad) < 3e-2
+
+
+def _train(stage, gas, stash, steps=2):
+    import shuffle_exchange_amd as sxe
+    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+    from shuffle_exchange_amd.ops import mlp
+    torch.manual_seed(0)
+    cfg = llama_config("llama-tiny", hidden_size=256, intermediate_size=512, num_attention_heads=4,
+                       num_key_value_heads=2, vocab_size=1024, num_hidden_layers=2)
+    model = LlamaForCausalLM(cfg).to(device="cuda", dtype=torch.bfloat16)
+    ds = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": gas, "bf16": {"enabled": True},
+          "zero_optimization": {"stage": stage}, "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}},
+          "gradient_clipping": 1.0}
+    engine, _, _, _ = sxe.initialize(model=model, config=ds)
+    calls = []
+    orig = mlp._may_stash
+    mlp.STASH = stash
+    mlp._may_stash = lambda w, g: calls.append(orig(w, g)) or calls[-1]
+    try:
+        g = torch.Generator(device="cuda").manual_seed(1)
+        for _ in range(steps * gas):
+            ids = torch.randint(0, cfg.vocab_size, (2, 128), device="cuda", generator=g)
+            loss = engine(ids, labels=ids)
+            engine.backward(loss)
+            engine.step()
+    finally:
+        mlp._may_stash, mlp.STASH = orig, True
+    torch.cuda.synchronize()
+    return [p.detach().float().clone() for p in engine.module.parameters()], calls
+
+
+@pytest.mark.parametrize("stage,gas", [(3, 2), (3, 3), (2, 2)])
+def test_wgrad_stash_bit_identical(stage, gas):
+    """Holding a micro-step's bf16 weight gradient and folding it with the next one (acc2_bf16_)
+    is the same fp32 sum as writing every micro-step: parameters after two steps are identical."""
+    on, calls = _train(stage, gas, True)
+    off, _ = _train(stage, gas, False)
+    assert any(calls), "no weight gradient was held"
+    assert all(torch.equal(a, b) for a, b in zip(on, off))
+
+
+def test_acc2_bf16_kernel():
+    n = 1000003
+    a = torch.randn(n, device="cuda").to(torch.bfloat16)
+    b = torch.randn(n, device="cuda").to(torch.bfloat16)
+    d = torch.randn(n, device="cuda")
+    ref = d + a.float() + b.float()
+    torch.ops.sxe.acc2_bf16_(d, a, b, True)
+    assert torch.equal(d, ref)
+    torch.ops.sxe.acc2_bf16_(d, a, b, False)
+    assert torch.equal(d, a.float() + b.float())
