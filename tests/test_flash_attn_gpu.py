@@ -297,27 +297,6 @@ def test_flash_fwd_variants(dma, waves, causal, B, Sq, Sk, H, Hk, D, monkeypatch
     assert (lse - lse2).abs().max().item() < 2e-2
 
 
-@pytest.mark.parametrize("causal", [True, False])
-@pytest.mark.parametrize("B,Sq,Sk,H,Hk,D", [(2, 256, 256, 4, 4, 128), (1, 512, 512, 8, 2, 128),
-                                            (2, 256, 256, 4, 2, 64), (1, 256, 768, 4, 1, 128),
-                                            (1, 512, 1024, 4, 2, 64), (1, 1024, 1024, 2, 2, 128),
-                                            (1, 768, 768, 2, 1, 128), (1, 4096, 4096, 2, 1, 128)])
-def test_flash_fwd_skew(causal, B, Sq, Sk, H, Hk, D, monkeypatch):
-    """The skewed 8-wave forward (SXE_FA_FWD_SKEW=1: waves 4-7 half a tile behind over a 3-slot K/V
-    ring) against the fp32 oracle, including tile counts of every residue mod 3 and q_len != kv_len."""
-    A = _no_sdpa(monkeypatch)
-    monkeypatch.setenv("SXE_FA_FWD_WAVES", "8")
-    monkeypatch.setenv("SXE_FA_FWD_SKEW", "1")
-    torch.manual_seed(3)
-    q = torch.randn(B, Sq, H, D, device="cuda", dtype=torch.bfloat16)
-    k = torch.randn(B, Sk, Hk, D, device="cuda", dtype=torch.bfloat16)
-    v = torch.randn(B, Sk, Hk, D, device="cuda", dtype=torch.bfloat16)
-    o, lse = A.attention_with_lse(q, k, v, causal=causal)
-    o2, lse2 = A.reference_attention(q.float(), k.float(), v.float(), causal=causal, return_lse=True)
-    assert _rel(o, o2) < 1e-2
-    assert (lse - lse2).abs().max().item() < 2e-2
-
-
 def _chunked_reference(q, k, v, do, causal, chunk=1024):
     """fp32 attention output and gradients for long sequences, one query block at a time (the full
     score matrix of S = 16k would not be materialised at once). q [B, S, H, D], k/v [B, S, Hk, D]."""
