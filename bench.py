@@ -94,20 +94,29 @@ def zero_knobs(c, cfg, stage):
 ACT_BYTES_PER_TOKEN_LAYER = {"none": 170e3, "mlp": 55e3}
 
 
-def auto_ac_policy(model_name, layers, tokens_per_gpu, world, stage, hbm_bytes=288e9, budget=0.75):
-    """The least recompute that fits: no checkpointing if the saved activations and the ZeRO states
-    fit `budget` of HBM, else the MLP-only policy (attention outputs kept: the flash forward is not
-    re-run), else full-layer checkpointing. 288 GB per MI355X makes 'none' the answer for
-    Llama-3-8B at 32k tokens from 2 GPUs up."""
+def auto_ac_policy(model_name, layers, tokens_per_gpu, world, stage, hbm_bytes=288e9, budget=0.75,
+                   partial_budget=0.80):
+    """The least recompute that fits, as (policy, checkpointed layers or None = all): no
+    checkpointing if the saved activations and the ZeRO states fit `budget` of HBM; else the MLP-only
+    policy (attention outputs kept: the flash forward is not re-run) on as FEW layers as keep the
+    modelled bytes within `partial_budget` (the other layers keep their MLP activations: 288 GB holds
+    part of them -- at Llama-3-8B 32k tokens on one GPU, MLP recompute in every layer peaks at 204 GB
+    measured, ~18 GB above this model); else full-layer checkpointing. 288 GB per MI355X makes
+    'none' the answer for Llama-3-8B at 32k tokens from 2 GPUs up."""
     from shuffle_exchange_amd.models import llama_config
     cfg = llama_config(model_name, **({"num_hidden_layers": layers} if layers else {}))
     states = 16.0 * cfg.num_params() / (world if stage == 3 else 1)
     scale = (cfg.hidden_size / 4096 + cfg.intermediate_size / 14336) / 2
-    for policy in ("none", "mlp"):
-        acts = ACT_BYTES_PER_TOKEN_LAYER[policy] * scale * tokens_per_gpu * cfg.num_hidden_layers
-        if states + acts <= budget * hbm_bytes:
-            return policy
-    return "full"
+    L = cfg.num_hidden_layers
+    per = {k: v * scale * tokens_per_gpu for k, v in ACT_BYTES_PER_TOKEN_LAYER.items()}
+    if states + per["none"] * L <= budget * hbm_bytes:
+        return "none", None
+    if states + per["mlp"] * L <= budget * hbm_bytes:
+        for n in range(L + 1):  # fewest MLP-checkpointed layers within the partial budget
+            if states + per["mlp"] * n + per["none"] * (L - n) <= partial_budget * hbm_bytes:
+                return ("none", None) if n == 0 else ("mlp", None if n == L else n)
+        return "mlp", None
+    return "full", None
 
 
 def comm_model(opt, world, stage, knobs, gas, elem_bytes=2):
@@ -215,6 +224,8 @@ def main():
     ap.add_argument("--ac-policy", default=None, choices=["full", "mlp", "none", "auto"],
                     help="what activation checkpointing recomputes (default: the config's; auto = the "
                          "least recompute whose saved activations fit the HBM budget)")
+    ap.add_argument("--ac-layers", type=int, default=None,
+                    help="checkpoint only the first N decoder layers (default: all, or auto's choice)")
     ap.add_argument("--layers", type=int, default=None, help="override layer count (a cut model: not the metric)")
     ap.add_argument("--offload-ratio", type=float, default=None,
                     help="offload configs: Twin-Flow offload_optimizer.ratio (share of the optimizer on the "
@@ -250,13 +261,18 @@ def main():
     layers = args.layers if args.layers is not None else default_layers(args.config, world)
     ac = args.ac or bool(c.get("ac"))
     policy = args.ac_policy or c.get("ac_policy") or ("full" if ac else "none")
+    ac_layers = None
     if policy == "auto":
-        policy = auto_ac_policy(model_name, layers, seq // sp * mbs, world, stage)
+        policy, ac_layers = auto_ac_policy(model_name, layers, seq // sp * mbs, world, stage)
+    if args.ac_layers is not None:
+        ac_layers = args.ac_layers
     ac = policy != "none"
     torch.manual_seed(1234)
     over = {"activation_checkpointing": ac, "max_position_embeddings": max(8192, seq)}
     if c["family"] == "llama" and policy == "mlp":
         over["ac_policy"] = "mlp"
+    if ac and ac_layers is not None:
+        over["ac_layers"] = ac_layers
     if layers:
         over["num_hidden_layers"] = layers
     if sp > 1:
@@ -397,7 +413,7 @@ def main():
             "data": "synthetic",
             "config": {"name": args.config, "model": model_tag, "global_batch": dp * mbs * gas, "seq_len": seq,
                        "micro_batch_per_gpu": mbs, "grad_accum": gas, "parallelism": "-".join(par),
-                       "params": n_params, "activation_checkpointing": policy if ac else False,
+                       "params": n_params, "activation_checkpointing": (f"{policy}:{ac_layers}" if ac_layers is not None else policy) if ac else False,
                        "optimizer": "AdamW(fp32 master, " + ("C++ CPU Adam on host" if c.get("offload") else
                                                              "fused HIP") + ")",
                        "zero_knobs": c["knobs"], "zero_optimization": zero,

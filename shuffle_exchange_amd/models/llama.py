@@ -58,6 +58,9 @@ class LlamaConfig:
     # included); "mlp" = only the MLP sub-block (its gate_up / SwiGLU activations, ~70 % of a
     # layer's saved bytes, are recomputed by GEMMs; the flash-attention forward is NOT re-run)
     ac_policy: str = "full"
+    # how many decoder layers (the first N) the checkpoint policy covers; None = all of them. 288 GB
+    # of HBM often fits the activations of SOME layers: recomputing only the rest is faster
+    ac_layers: Optional[int] = None
     loss_chunk_tokens: Optional[int] = None
     sequence_parallel: bool = False  # Ulysses: inputs are [B, S/sp] chunks of the SP group
     sp_mode: str = "ulysses"         # "ring" / "ring_zigzag": ring attention (context parallelism) over
@@ -223,12 +226,19 @@ class LMHeadLoss(nn.Module):
         return s / n.clamp_min(1.0).squeeze(0)
 
 
+def _ac_covers(cfg, i):
+    """Layer i is under the activation-checkpoint policy (``ac_layers``: the first N layers only)."""
+    return cfg.ac_layers is None or i < cfg.ac_layers
+
+
 class LlamaForCausalLM(nn.Module):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
         self.cfg = cfg
         self.embed_tokens = Embedding(cfg.vocab_size, cfg.hidden_size, init_std=cfg.initializer_range)
         self.layers = nn.ModuleList([LlamaDecoderLayer(cfg) for _ in range(cfg.num_hidden_layers)])
+        for i, layer in enumerate(self.layers):
+            layer.ckpt_mlp = layer.ckpt_mlp and _ac_covers(cfg, i)
         self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         self.lm_head = LMHeadLoss(cfg, self.embed_tokens.weight if cfg.tie_word_embeddings else None)
         self._rope = None
@@ -265,9 +275,9 @@ class LlamaForCausalLM(nn.Module):
         x = self.embed_tokens(input_ids)
         rope = self.rope(x.device)
         res = None
-        for layer in self.layers:
+        for i, layer in enumerate(self.layers):
             if (self.cfg.activation_checkpointing and self.cfg.ac_policy == "full" and self.training
-                    and torch.is_grad_enabled()):
+                    and torch.is_grad_enabled() and _ac_covers(self.cfg, i)):
                 x, res = checkpoint(layer, x, res, rope, position_ids)
             else:
                 x, res = layer(x, res, rope, position_ids)

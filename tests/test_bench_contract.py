@@ -134,3 +134,24 @@ def test_bench_configs_wide_cpu(tmp_path, config, world):
     assert model_, out
     for op, b in model_.items():
         assert meas[op]["bytes_per_step"] == b, (op, meas[op], b)
+
+
+def test_auto_ac_policy_partial_mlp_layers():
+    """288 GB: Llama-3-8B at 32k tokens on one GPU checkpoints the MLP of only part of the layers;
+    from 2 GPUs (16k tokens each) nothing is recomputed."""
+    import bench
+    pol, n = bench.auto_ac_policy("llama3-8b", None, 32768, 1, 3)
+    assert pol == "mlp" and 0 < n < 32
+    assert bench.auto_ac_policy("llama3-8b", None, 16384, 2, 3) == ("none", None)
+    assert bench.auto_ac_policy("llama3-8b", None, 16384, 1, 3)[0] == "none"
+
+
+def test_llama_ac_layers_covers_first_layers():
+    import torch
+    from shuffle_exchange_amd.models import LlamaForCausalLM, llama_config
+    cfg = llama_config("llama-tiny", num_hidden_layers=4, activation_checkpointing=True, ac_policy="mlp", ac_layers=3)
+    m = LlamaForCausalLM(cfg)
+    assert [layer.ckpt_mlp for layer in m.layers] == [True, True, True, False]
+    ids = torch.randint(0, cfg.vocab_size, (2, 16))
+    m(ids, labels=ids).backward()
+    assert all(p.grad is not None for p in m.parameters() if p.requires_grad)
