@@ -20,7 +20,8 @@ architecture (no network access for checkpoints/datasets).
                       MoE layer), ZeRO-2 (the reference asserts MoE off at stage 3, engine.py:1760),
                       seq 2048; min(32, 8N) layers so the experts per GPU stay fixed (full 32 at N >= 4)
   llama70b-infinity   Llama-3-70B, ZeRO-3 + ZeRO-Infinity optimizer offload to pinned host DRAM
-                      (C++ AVX-512 Adam), activation checkpointing, seq 2048; 10N layers up to the
+                      (C++ AVX-512 Adam), activation checkpointing by HBM budget (auto_ac_policy:
+                      none while 10N layers' activations fit), seq 2048; 10N layers up to the
                       full 80 (host DRAM of one node bounds the fp32 state: 12 B/param)
   llama8b-sp32k       Llama-3-8B, Ulysses sequence parallel over all N GPUs, seq 32768, ZeRO-3; one 32k
                       sequence per SP group (strong scaling); activation checkpointing by HBM budget
@@ -49,7 +50,7 @@ CONFIGS = {
     "mixtral-ep": dict(family="mixtral", model="mixtral-8x7b", seq=2048, mbs=2, gas=2, stage=2, knobs="tuned",
                        ep=True, metric="tokens/sec Mixtral-8x7B expert-parallel bf16 (training, whole job)"),
     "llama70b-infinity": dict(family="llama", model="llama3-70b", seq=2048, mbs=2, gas=2, stage=3, knobs="reference",
-                              offload=True, ac=True,
+                              offload=True, ac=True, ac_policy="auto",
                               metric="tokens/sec Llama-3-70B ZeRO-3 + ZeRO-Infinity host offload bf16 "
                                      "(training, whole job)"),
     "llama8b-sp32k": dict(family="llama", model="llama3-8b", seq=32768, mbs=1, gas=1, stage=3, knobs="tuned", sp=True,
@@ -95,7 +96,7 @@ ACT_BYTES_PER_TOKEN_LAYER = {"none": 170e3, "mlp": 55e3}
 
 
 def auto_ac_policy(model_name, layers, tokens_per_gpu, world, stage, hbm_bytes=288e9, budget=0.75,
-                   partial_budget=0.80):
+                   partial_budget=0.80, state_bytes=16.0):
     """The least recompute that fits, as (policy, checkpointed layers or None = all): no
     checkpointing if the saved activations and the ZeRO states fit `budget` of HBM; else the MLP-only
     policy (attention outputs kept: the flash forward is not re-run) on as FEW layers as keep the
@@ -105,7 +106,9 @@ def auto_ac_policy(model_name, layers, tokens_per_gpu, world, stage, hbm_bytes=2
     'none' the answer for Llama-3-8B at 32k tokens from 2 GPUs up."""
     from shuffle_exchange_amd.models import llama_config
     cfg = llama_config(model_name, **({"num_hidden_layers": layers} if layers else {}))
-    states = 16.0 * cfg.num_params() / (world if stage == 3 else 1)
+    # HBM bytes per parameter of the ZeRO states: 16 (bf16 param, fp32 grad, master, moments), 6 with
+    # the optimizer offloaded to the host (bf16 param + fp32 gradient accumulator)
+    states = state_bytes * cfg.num_params() / (world if stage == 3 else 1)
     scale = (cfg.hidden_size / 4096 + cfg.intermediate_size / 14336) / 2
     L = cfg.num_hidden_layers
     per = {k: v * scale * tokens_per_gpu for k, v in ACT_BYTES_PER_TOKEN_LAYER.items()}
@@ -263,7 +266,8 @@ def main():
     policy = args.ac_policy or c.get("ac_policy") or ("full" if ac else "none")
     ac_layers = None
     if policy == "auto":
-        policy, ac_layers = auto_ac_policy(model_name, layers, seq // sp * mbs, world, stage)
+        policy, ac_layers = auto_ac_policy(model_name, layers, seq // sp * mbs, world, stage,
+                                           state_bytes=6.0 if c.get("offload") else 16.0)
     if args.ac_layers is not None:
         ac_layers = args.ac_layers
     ac = policy != "none"

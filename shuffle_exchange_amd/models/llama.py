@@ -59,7 +59,9 @@ class LlamaConfig:
     # layer's saved bytes, are recomputed by GEMMs; the flash-attention forward is NOT re-run)
     ac_policy: str = "full"
     # how many decoder layers (the first N) the checkpoint policy covers; None = all of them. 288 GB
-    # of HBM often fits the activations of SOME layers: recomputing only the rest is faster
+    # of HBM often fits the activations of SOME layers: recomputing only the rest is faster (the
+    # model-side analogue of activation_checkpointing.number_checkpoints, reference
+    # runtime/activation_checkpointing/checkpointing.py:1007)
     ac_layers: Optional[int] = None
     loss_chunk_tokens: Optional[int] = None
     sequence_parallel: bool = False  # Ulysses: inputs are [B, S/sp] chunks of the SP group
