@@ -96,13 +96,15 @@ ACT_BYTES_PER_TOKEN_LAYER = {"none": 170e3, "mlp": 55e3}
 
 
 def auto_ac_policy(model_name, layers, tokens_per_gpu, world, stage, hbm_bytes=288e9, budget=0.75,
-                   partial_budget=0.80, state_bytes=16.0):
+                   partial_budget=0.90, state_bytes=16.0):
     """The least recompute that fits, as (policy, checkpointed layers or None = all): no
     checkpointing if the saved activations and the ZeRO states fit `budget` of HBM; else the MLP-only
     policy (attention outputs kept: the flash forward is not re-run) on as FEW layers as keep the
     modelled bytes within `partial_budget` (the other layers keep their MLP activations: 288 GB holds
     part of them -- at Llama-3-8B 32k tokens on one GPU, MLP recompute in every layer peaks at 204 GB
-    measured, ~18 GB above this model); else full-layer checkpointing. 288 GB per MI355X makes
+    measured, ~18 GB above this model, and each layer left whole adds 2.6 GB measured vs 3.8 modelled:
+    21 checkpointed layers peaked at 234 GB, 15 at 249 GB, profiles/r06/sp32k/); else full-layer
+    checkpointing. 288 GB per MI355X makes
     'none' the answer for Llama-3-8B at 32k tokens from 2 GPUs up."""
     from shuffle_exchange_amd.models import llama_config
     cfg = llama_config(model_name, **({"num_hidden_layers": layers} if layers else {}))
