@@ -32,7 +32,7 @@ def main():
         tf = timeit(lambda: torch.ops.sxe.gated_act_fwd_dual(gu, 3, v))
         tb = timeit(lambda: torch.ops.sxe.gated_act_bwd_dual(dout, gu, 3, v))
         bf = (2 * T * I * 2 + 2 * T * I * 2) / tf
-        bb = (2 * T * I * 2 + T * I * 2 + 2 * 2 * T * 2 * I * 2) / tb
+        bb = (2 * T * I * 2 + T * I * 2 + 2 * T * 2 * I * 2) / tb  # gu + dout in, dgu + dgu^T out
         print(f"variant {v} ({nm:7s}) fwd {tf * 1e3:.3f} ms {bf / 1e12:.2f} TB/s | bwd {tb * 1e3:.3f} ms {bb / 1e12:.2f} TB/s",
               flush=True)
 
