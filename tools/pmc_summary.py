@@ -25,7 +25,7 @@ def main():
                 cv = r.get("Counter_Value") or r.get("Counter-Value")
                 if name and cn and cv:
                     vals[short(name)][cn].append(float(cv))
-    keep = [k for k in vals if any(s in k for s in ("fa::", "mx_gemm", "skinny", "paged_attn", "norm_fwd", "adam", "wgrad", "Cijk", "gated_dual", "grouped_gemm"))]
+    keep = [k for k in vals if any(s in k for s in ("fa::", "mx_gemm", "skinny", "paged_attn", "norm_fwd", "adam", "wgrad", "Cijk", "gated_dual", "grouped_gemm", "xent", "acc2", "transpose16"))]
     cols = sorted({c for k in keep for c in vals[k]})
     print("| kernel | " + " | ".join(cols) + " | derived |")
     print("|---|" + "---:|" * len(cols) + "---|")
