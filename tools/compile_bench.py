@@ -8,6 +8,7 @@ by in-graph reduce nodes -- against the eager engine with its autograd hooks. Th
 gather / release / prefetch placement itself is pinned by the gloo tests
 (tests/test_compile_fx.py).
   python tools/compile_bench.py [--layers 4] [--seq 2048] [--mbs 2] [--stages 1,2,3] [--steps 5] [--offload-param]
+                                [--only eager|compiled]
 """
 import argparse
 import gc
@@ -81,10 +82,15 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--offload-param", action="store_true", help="ZeRO-3 with offload_param cpu")
+    ap.add_argument("--only", choices=["eager", "compiled"], default=None,
+                    help="run one arm (per-arm kernel traces)")
     a = ap.parse_args()
     import shuffle_exchange_amd as sxe
     sxe.init_distributed(verbose=False)
     for s in (int(x) for x in a.stages.split(",")):
+        if a.only:
+            print(json.dumps(run(s, a.only == "compiled", a)), flush=True)
+            continue
         e = run(s, False, a)
         print(json.dumps(e), flush=True)
         c = run(s, True, a)
